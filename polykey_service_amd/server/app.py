@@ -1,0 +1,154 @@
+"""L1 transport / process entry (reference ``cmd/polykey/main.go:54-121``).
+
+Startup sequence mirrors the reference: JSON logger on stdout → listen on ``LISTEN_ADDR``
+(default ``:50051``) → gRPC server with keepalive + logging interceptor → reflection →
+health (SERVING for ``polykey.v2.PolykeyService`` and ``""``) → log every registered
+service and method → ``"server starting" {address}`` → wait for SIGINT/SIGTERM →
+``"server shutting down"`` → health NOT_SERVING → graceful stop → ``"server stopped"``.
+
+Transport parameters (``main.go:68-72``): MaxConnectionIdle 5 min, Time 2 h, Timeout 20 s.
+[NEW] a keepalive *enforcement* policy (min ping interval 5 s, pings allowed without
+streams): the reference's clients ping every 10 s with PermitWithoutStream while its server
+keeps grpc-go's 5 min default, which ends long-lived connections with GOAWAY
+``too_many_pings``.
+"""
+from __future__ import annotations
+
+import asyncio
+import signal
+from typing import List, Optional
+
+import grpc
+
+from .. import proto
+from ..utils import slog
+from .health import SERVING, HealthServicer
+from .interceptors import LoggingInterceptor
+from .reflection import ReflectionServicer
+from .rpc import SERVICE_METHODS, PolykeyServicer
+
+MIB = 1024 * 1024
+
+SERVER_OPTIONS = [
+    ("grpc.max_connection_idle_ms", 5 * 60 * 1000),
+    ("grpc.keepalive_time_ms", 2 * 3600 * 1000),
+    ("grpc.keepalive_timeout_ms", 20 * 1000),
+    ("grpc.keepalive_permit_without_calls", 1),
+    ("grpc.http2.min_recv_ping_interval_without_data_ms", 5 * 1000),
+    ("grpc.http2.max_ping_strikes", 0),
+    ("grpc.max_receive_message_length", 4 * MIB),
+    ("grpc.max_send_message_length", 64 * MIB),
+]
+
+
+def grpc_bind_address(addr: str) -> str:
+    """Go ``net.Listen`` style ``":50051"`` → ``"[::]:50051"``."""
+    if addr.startswith(":"):
+        return "[::]" + addr
+    return addr
+
+
+class PolykeyServer:
+    def __init__(self, service, logger: Optional[slog.Logger] = None, listen_addr: str = ":50051",
+                 metrics=None, extra_handlers: Optional[List] = None):
+        self.logger = logger or slog.Logger()
+        self.listen_addr = listen_addr
+        self.service = service
+        self.health = HealthServicer()
+        self.metrics = metrics
+        observer = metrics.observe_rpc if metrics is not None else None
+        self.server = grpc.aio.server(interceptors=[LoggingInterceptor(self.logger, observer)],
+                                      options=SERVER_OPTIONS)
+        self.port: Optional[int] = None
+        self._extra = extra_handlers or []
+        self._stopped = asyncio.Event()
+
+    async def start(self) -> int:
+        bind = grpc_bind_address(self.listen_addr)
+        try:
+            self.port = self.server.add_insecure_port(bind)
+        except RuntimeError as e:
+            self.logger.error("failed to listen", error=str(e))
+            raise
+        refl = [ReflectionServicer(SERVICE_METHODS.keys(), v) for v in ("v1alpha", "v1")]
+        handlers = [PolykeyServicer(self.service, self.logger).handler(), self.health.handler()]
+        handlers += [r.handler() for r in refl] + self._extra
+        self.server.add_generic_rpc_handlers(handlers)
+        self.health.set_serving_status(proto.POLYKEY_SERVICE, SERVING)
+        self.health.set_serving_status("", SERVING)
+
+        self.logger.info("Registered services:")
+        for name, methods in SERVICE_METHODS.items():
+            self.logger.info("Service registered", name=name, methods=len(methods))
+            for m in methods:
+                self.logger.info("Method available", service=name, method=m)
+
+        self.logger.info("server starting", address=self.listen_addr)
+        await self.server.start()
+        return self.port
+
+    async def stop(self, grace: float = 10.0) -> None:
+        self.logger.info("server shutting down")
+        self.health.shutdown()
+        await self.server.stop(grace)
+        close = getattr(self.service, "aclose", None)
+        if close is not None:
+            await close()
+        self.logger.info("server stopped")
+        self._stopped.set()
+
+    async def serve_until_signal(self, grace: float = 10.0) -> None:
+        loop = asyncio.get_running_loop()
+        quit_ev = asyncio.Event()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            try:
+                loop.add_signal_handler(sig, quit_ev.set)
+            except (NotImplementedError, RuntimeError):
+                pass
+        await quit_ev.wait()
+        await self.stop(grace)
+
+
+def build_service(cfg, logger: slog.Logger):
+    """Mock router, or router + on-node LLM backend (``cfg.backend == "local"``)."""
+    from ..service.router import ToolRouter
+    from ..adapters.security.secret_store import SecretStore
+
+    router = ToolRouter(secret_store=SecretStore.from_env())
+    if cfg.backend == "local":
+        from ..adapters.local_llm import attach_local_llm
+        attach_local_llm(router, cfg, logger)
+    elif cfg.backend != "mock":
+        raise ValueError(f"unknown backend {cfg.backend!r} (mock|local)")
+    return router
+
+
+async def amain(argv=None) -> int:
+    from ..config.server_config import load_server_config
+
+    cfg = load_server_config(argv)
+    logger = slog.Logger(level=slog.level_from_name(cfg.log_level))
+    slog.set_default(logger)
+    metrics = None
+    if cfg.metrics_addr:
+        from ..utils.metrics import Metrics
+        metrics = Metrics.start(cfg.metrics_addr)
+    service = build_service(cfg, logger)
+    srv = PolykeyServer(service, logger, cfg.listen_addr, metrics=metrics)
+    await srv.start()
+    http = None
+    if cfg.http_addr:
+        from ..api.openai import serve_openai
+        http = await serve_openai(service, cfg.http_addr, logger)
+    await srv.serve_until_signal(cfg.shutdown_grace)
+    if http is not None:
+        await http.shutdown()
+    return 0
+
+
+def main(argv=None) -> int:
+    return asyncio.run(amain(argv))
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

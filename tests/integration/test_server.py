@@ -1,0 +1,187 @@
+"""In-process grpc.aio server on an ephemeral port (config 1: dev_client example_tool vs mock, CPU)."""
+import asyncio
+import io
+import json
+import threading
+
+import grpc
+import pytest
+
+from polykey_service_amd import proto
+from polykey_service_amd.client import dev_client
+from polykey_service_amd.proto import schema
+from polykey_service_amd.server import NOT_SERVING, SERVING, PolykeyServer
+from polykey_service_amd.service import ToolError, ToolRouter
+from polykey_service_amd.utils import slog
+
+
+class ServerThread:
+    """Runs a PolykeyServer on its own event loop thread."""
+
+    def __init__(self, service=None):
+        self.log = io.StringIO()
+        self.service = service or ToolRouter()
+        self.loop = asyncio.new_event_loop()
+        self.ready = threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        asyncio.set_event_loop(self.loop)
+        self.srv = PolykeyServer(self.service, slog.Logger(self.log), "127.0.0.1:0")
+        self.port = self.loop.run_until_complete(self.srv.start())
+        self.ready.set()
+        self.loop.run_forever()
+
+    def __enter__(self):
+        self.t.start()
+        self.ready.wait(10)
+        self.addr = f"127.0.0.1:{self.port}"
+        return self
+
+    def stop(self, grace=1.0):
+        fut = asyncio.run_coroutine_threadsafe(self.srv.stop(grace), self.loop)
+        fut.result(10)
+
+    def __exit__(self, *a):
+        if not self.srv._stopped.is_set():
+            self.stop()
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.t.join(5)
+
+    def records(self, settle=0.2):
+        import time
+        time.sleep(settle)  # the "finished" line is written after the response is sent
+        return [json.loads(l) for l in self.log.getvalue().splitlines() if l.strip()]
+
+
+def unary(ch, method, req_cls, resp_cls):
+    return ch.unary_unary(method, request_serializer=req_cls.SerializeToString,
+                          response_deserializer=resp_cls.FromString)
+
+
+def test_execute_tool_and_interceptor_schema():
+    with ServerThread() as s, grpc.insecure_channel(s.addr) as ch:
+        call = unary(ch, proto.EXECUTE_TOOL, proto.ExecuteToolRequest, proto.ExecuteToolResponse)
+        r = call(dev_client.build_request("struct_tool"), timeout=5)
+        assert r.status.code == 200 and r.WhichOneof("output") == "struct_output"
+        hc = unary(ch, proto.HEALTH_CHECK, proto.HealthCheckRequest, proto.HealthCheckResponse)
+        assert hc(proto.HealthCheckRequest(service=""), timeout=5).status == SERVING
+        recs = s.records()
+    msgs = [r["msg"] for r in recs]
+    assert msgs[0] == "Registered services:" and "server starting" in msgs
+    methods = {(r["service"], r["method"]) for r in recs if r["msg"] == "Method available"}
+    assert ("polykey.v2.PolykeyService", "ExecuteTool") in methods
+    got = [r for r in recs if r["msg"].startswith("gRPC call")]
+    # Health/Check bypasses the interceptor (main.go:29-31)
+    assert [r["msg"] for r in got] == ["gRPC call received", "gRPC call finished"]
+    fin = got[1]
+    assert fin["method"] == "/polykey.v2.PolykeyService/ExecuteTool" and fin["code"] == "OK"
+    assert fin["level"] == "INFO" and fin["duration"].endswith("s")
+    called = [r for r in recs if r["msg"] == "ExecuteTool called"][0]
+    assert called == {**called, "tool_name": "struct_tool", "has_parameters": True, "has_secret_id": True,
+                      "has_metadata": True}
+
+
+class FailingService(ToolRouter):
+    async def execute_tool(self, ctx, tool_name, parameters=None, secret_id=None, metadata=None):
+        if tool_name == "raise":
+            raise RuntimeError("kaput")
+        raise ToolError("INVALID_ARGUMENT", "bad params")
+
+
+def test_errors_map_to_codes_and_error_logs():
+    with ServerThread(FailingService()) as s, grpc.insecure_channel(s.addr) as ch:
+        call = unary(ch, proto.EXECUTE_TOOL, proto.ExecuteToolRequest, proto.ExecuteToolResponse)
+        with pytest.raises(grpc.RpcError) as ei:
+            call(proto.ExecuteToolRequest(tool_name="raise"), timeout=5)
+        assert ei.value.code() == grpc.StatusCode.UNKNOWN and "kaput" in ei.value.details()
+        with pytest.raises(grpc.RpcError) as ei:
+            call(proto.ExecuteToolRequest(tool_name="x"), timeout=5)
+        assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        recs = s.records()
+    fins = [r for r in recs if r["msg"] == "gRPC call finished"]
+    assert [(r["level"], r["code"]) for r in fins] == [("ERROR", "Unknown"), ("ERROR", "InvalidArgument")]
+    assert any(r["msg"] == "Service ExecuteTool failed" and r["error"] == "kaput" for r in recs)
+
+
+def test_unimplemented_method():
+    with ServerThread() as s, grpc.insecure_channel(s.addr) as ch:
+        call = unary(ch, "/polykey.v2.PolykeyService/Nope", proto.ExecuteToolRequest, proto.ExecuteToolResponse)
+        with pytest.raises(grpc.RpcError) as ei:
+            call(proto.ExecuteToolRequest(), timeout=5)
+        assert ei.value.code() == grpc.StatusCode.UNIMPLEMENTED
+
+
+def test_streaming_rpc_mock():
+    with ServerThread() as s, grpc.insecure_channel(s.addr) as ch:
+        st = ch.unary_stream(proto.EXECUTE_TOOL_STREAM, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                             response_deserializer=proto.ExecuteToolResponse.FromString)
+        out = list(st(proto.ExecuteToolRequest(tool_name="file_tool"), timeout=5))
+        assert len(out) == 1 and out[0].file_output.content == b"This is mock file content"
+
+
+def test_health_unknown_watch_and_shutdown():
+    with ServerThread() as s, grpc.insecure_channel(s.addr) as ch:
+        hc = unary(ch, proto.HEALTH_CHECK, proto.HealthCheckRequest, proto.HealthCheckResponse)
+        assert hc(proto.HealthCheckRequest(service="polykey.v2.PolykeyService"), timeout=5).status == SERVING
+        with pytest.raises(grpc.RpcError) as ei:
+            hc(proto.HealthCheckRequest(service="nope"), timeout=5)
+        assert ei.value.code() == grpc.StatusCode.NOT_FOUND
+        watch = ch.unary_stream(proto.HEALTH_WATCH, request_serializer=proto.HealthCheckRequest.SerializeToString,
+                                response_deserializer=proto.HealthCheckResponse.FromString)
+        it = watch(proto.HealthCheckRequest(service=""), timeout=10)
+        assert next(it).status == SERVING
+        s.loop.call_soon_threadsafe(s.srv.health.shutdown)
+        assert next(it).status == NOT_SERVING
+        it.cancel()
+        s.stop(0.5)
+        msgs = [r["msg"] for r in s.records()]
+    assert msgs[-1] == "server stopped" and "server shutting down" in msgs
+
+
+def test_reflection_list_and_describe():
+    from google.protobuf import descriptor_pb2
+    Req = schema.message_class("grpc.reflection.v1alpha.ServerReflectionRequest")
+    Resp = schema.message_class("grpc.reflection.v1alpha.ServerReflectionResponse")
+    with ServerThread() as s, grpc.insecure_channel(s.addr) as ch:
+        rpc = ch.stream_stream("/grpc.reflection.v1alpha.ServerReflection/ServerReflectionInfo",
+                               request_serializer=Req.SerializeToString, response_deserializer=Resp.FromString)
+        reqs = [Req(list_services=""), Req(file_containing_symbol="polykey.v2.PolykeyService"),
+                Req(file_by_filename="common/v2/common.proto"), Req(file_containing_symbol="no.Such")]
+        out = list(rpc(iter(reqs), timeout=5))
+    names = [x.name for x in out[0].list_services_response.service]
+    assert "polykey.v2.PolykeyService" in names and "grpc.health.v1.Health" in names
+    files = [descriptor_pb2.FileDescriptorProto.FromString(b) for b in
+             out[1].file_descriptor_response.file_descriptor_proto]
+    fnames = [f.name for f in files]
+    assert fnames[0] == "polykey/v2/polykey.proto" and "google/protobuf/struct.proto" in fnames
+    assert "common/v2/common.proto" in fnames
+    svc = files[0].service[0]
+    assert [m.name for m in svc.method] == ["ExecuteTool", "ExecuteToolStream"]
+    assert out[2].file_descriptor_response.file_descriptor_proto
+    assert out[3].WhichOneof("message_response") == "error_response"
+
+
+def test_dev_client_end_to_end(monkeypatch):
+    with ServerThread() as s:
+        monkeypatch.setenv("POLYKEY_SERVER_ADDR", s.addr)
+        out = io.StringIO()
+        assert dev_client.main([], out=out) == 0
+        text = out.getvalue()
+    assert "All 4 checks passed" in text and "tool=example_tool" in text
+    assert "'Tool executed successfully'" in text
+
+
+def test_dev_client_fails_without_server(monkeypatch):
+    monkeypatch.setenv("POLYKEY_SERVER_ADDR", "127.0.0.1:1")
+    out = io.StringIO()
+    assert dev_client.main([], out=out) == 1
+    assert "Application Run" in out.getvalue() and "network test failed" in out.getvalue()
+
+
+def test_keepalive_enforcement_allows_10s_pings():
+    from polykey_service_amd.server import SERVER_OPTIONS
+    opts = dict(SERVER_OPTIONS)
+    assert opts["grpc.http2.min_recv_ping_interval_without_data_ms"] <= 10_000
+    assert opts["grpc.keepalive_permit_without_calls"] == 1
+    assert opts["grpc.max_connection_idle_ms"] == 300_000 and opts["grpc.keepalive_time_ms"] == 7_200_000
