@@ -1,0 +1,211 @@
+#!/usr/bin/env python
+"""Headline benchmark: output tokens/s via gRPC (+ p50 E2E latency), Llama-3-8B bf16.
+
+Metric/config from BASELINE.json ("output tokens/sec via gRPC + p50 E2E latency, Llama-3-8B
+TP=1 / 70B TP=8").  One process per GPU (torchrun); with ``--tp 1`` every rank is an
+independent Llama-3-8B replica (request-level data parallel → weak scaling: per-GPU work is
+fixed as N grows) that serves a real ``polykey.v2.PolykeyService`` gRPC server on
+127.0.0.1 and is driven by ``--concurrency`` concurrent ``ExecuteTool`` clients in the same
+process.  With ``--tp 8 --model llama3-70b`` the 8 ranks form one tensor-parallel replica
+(RCCL all-reduce over xGMI) and rank 0 serves the gRPC endpoint.
+
+A "step" is one wave of ``--concurrency`` requests per replica, each a synthetic
+``--prompt-len``-token prompt generating exactly ``--max-tokens`` tokens (``ignore_eos``,
+random-init weights, synthetic token ids — no network for checkpoints/datasets).
+W warmup waves run untimed; then K waves are timed between a barrier + device sync on both
+sides; elapsed = max over ranks; value = total output tokens of all replicas / elapsed.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import statistics
+import subprocess
+import sys
+import time
+
+METRIC = "output tokens/sec via gRPC + p50 E2E latency, Llama-3-8B TP=1 / 70B TP=8"
+MODEL_NAMES = {"llama3-8b": "Llama-3-8B", "llama3-70b": "Llama-3-70B", "mixtral-8x7b": "Mixtral-8x7B"}
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--concurrency", type=int, default=64, help="concurrent gRPC clients per replica")
+    ap.add_argument("--prompt-len", type=int, default=256)
+    ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--mode", choices=["unary", "stream"], default="unary")
+    ap.add_argument("--max-batched-tokens", type=int, default=8192)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--port-base", type=int, default=int(os.environ.get("POLYKEY_BENCH_PORT", "52100")))
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args(argv)
+
+
+def relaunch_with_torchrun(args) -> int:
+    """`python bench.py --gpus N` without torchrun: start torchrun as a child (no exec)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(29500 + random.randint(0, 999)),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+async def run_waves(args, engine, st, leaders_group):
+    import grpc
+    import torch
+    import torch.distributed as dist
+
+    from polykey_service_amd import proto
+    from polykey_service_amd.adapters.local_llm import attach_local_llm
+    from polykey_service_amd.config.server_config import ServerConfig
+    from polykey_service_amd.server import PolykeyServer
+    from polykey_service_amd.service import ToolRouter
+    from polykey_service_amd.utils import slog
+
+    logger = slog.Logger(open(os.devnull, "w"))
+    router = ToolRouter()
+    cfg = ServerConfig(model=args.model, backend="local")
+    attach_local_llm(router, cfg, logger, engine=engine)
+    port = args.port_base + st.rank
+    srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
+    await srv.start()
+    channel = grpc.aio.insecure_channel(f"127.0.0.1:{port}", options=[
+        ("grpc.max_receive_message_length", 64 << 20), ("grpc.max_send_message_length", 64 << 20)])
+    unary = channel.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                                response_deserializer=proto.ExecuteToolResponse.FromString)
+    stream = channel.unary_stream(proto.EXECUTE_TOOL_STREAM,
+                                  request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                                  response_deserializer=proto.ExecuteToolResponse.FromString)
+    V = engine.mcfg.vocab_size
+    rng = random.Random(args.seed * 1000 + st.rank)
+    tool = f"llm.generate:{args.model}"
+
+    async def one():
+        req = proto.ExecuteToolRequest(tool_name=tool)
+        req.parameters.update({"prompt_token_ids": [rng.randrange(0, V) for _ in range(args.prompt_len)],
+                               "max_tokens": args.max_tokens, "ignore_eos": True, "temperature": 0.0,
+                               "return": "struct"})
+        t0 = time.perf_counter()
+        if args.mode == "unary":
+            resp = await unary(req, timeout=600)
+        else:
+            resp = None
+            async for resp in stream(req, timeout=600):
+                pass
+        dt = time.perf_counter() - t0
+        usage = resp.struct_output.fields["usage"].struct_value.fields
+        return int(usage["completion_tokens"].number_value), dt
+
+    async def wave():
+        res = await asyncio.gather(*[one() for _ in range(args.concurrency)])
+        return sum(r[0] for r in res), [r[1] for r in res]
+
+    for _ in range(args.warmup):
+        await wave()
+    dev = engine.device
+    if dist.is_initialized():
+        dist.barrier(group=leaders_group)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    tokens, lats = 0, []
+    for _ in range(args.steps):
+        n, l = await wave()
+        tokens += n
+        lats += l
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    if dist.is_initialized():
+        dist.barrier(group=leaders_group)
+    elapsed = time.perf_counter() - t0
+    await channel.close()
+    await srv.server.stop(0)
+    return tokens, elapsed, lats
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world == 1:
+        return relaunch_with_torchrun(args)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import torch
+    import torch.distributed as dist
+
+    from polykey_service_amd.engine.llm_engine import EngineConfig, LLMEngine
+    from polykey_service_amd.parallel.state import init_parallel
+
+    st = init_parallel(tp=args.tp)
+    max_len = args.prompt_len + args.max_tokens + 32
+    max_len = (max_len + 511) // 512 * 512
+    ecfg = EngineConfig(model=args.model, seed=args.seed, max_num_seqs=max(args.concurrency, 1),
+                        max_num_batched_tokens=args.max_batched_tokens, max_model_len=max_len,
+                        hip_graphs=not args.no_graphs)
+    t_init = time.perf_counter()
+    engine = LLMEngine(ecfg, st)
+    init_s = time.perf_counter() - t_init
+    leaders = list(range(0, st.world_size, st.tp_size))
+    leaders_group = dist.new_group(leaders) if dist.is_initialized() else None
+    if st.tp_rank != 0:
+        engine.runner.worker_loop()
+        tokens, elapsed, lats = 0, 0.0, []
+    else:
+        tokens, elapsed, lats = asyncio.run(run_waves(args, engine, st, leaders_group))
+        engine.runner.stop_workers()
+
+    if dist.is_initialized():
+        # TP workers contribute (0 tokens, 0 s, no latencies); elapsed = max over ranks
+        allr = [None] * st.world_size
+        dist.all_gather_object(allr, (tokens, elapsed, lats))
+        tokens = sum(x[0] for x in allr)
+        elapsed = max(x[1] for x in allr)
+        lats = [l for x in allr for l in x[2]]
+    if st.rank == 0:
+        p50 = statistics.median(lats) if lats else None
+        value = tokens / elapsed if elapsed > 0 else 0.0
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "output_tokens/s",
+            "n_gpus": st.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / max(args.steps, 1) * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random prompt token ids, random-init weights, ignore_eos)",
+            "p50_e2e_latency_ms": round(p50 * 1000.0, 2) if p50 else None,
+            "config": {
+                "model": MODEL_NAMES.get(args.model, args.model),
+                "global_batch": args.concurrency * (st.world_size // st.tp_size),
+                "seq_len": args.prompt_len,
+                "output_len": args.max_tokens,
+                "parallelism": (f"tp{st.tp_size}" + (f"_dp{st.dp_size}" if st.dp_size > 1 else "")) if st.tp_size > 1
+                else f"dp{st.world_size}",
+                "concurrency_per_replica": args.concurrency,
+                "rpc": f"ExecuteTool ({args.mode})",
+                "hip_graphs": not args.no_graphs,
+                "init_s": round(init_s, 1),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

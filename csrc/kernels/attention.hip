@@ -1,0 +1,333 @@
+// Paged attention (decode + varlen causal prefill) for gfx950, head_dim = 128, bf16 KV.
+//
+// One wave computes 16 "columns" against a stream of 32-key steps with
+// mfma_f32_16x16x32_bf16.  A column is (query row, head): in DECODE the 16 columns are
+// the G query heads that share one KV head (GQA group, G <= 16, unused columns zero);
+// in PREFILL they are 16 consecutive query tokens of one head.  Per 32-key step:
+//
+//   S^T (32 keys x 16 cols) = K (A operand, rows = keys) . Q^T (B operand)    8 MFMAs
+//   online softmax on S^T in registers (per column: max over 8 regs + 2 xor-shuffles)
+//   O^T (128 d x 16 cols) += V^T (A, rows = d) . P^T (B, k = keys)             8 MFMAs
+//
+// Two permutations make every operand a single 16-byte-per-lane load with no LDS
+// transpose (guide §3 "accumulator tile as the next MFMA's operand"):
+//   * head-dim: lane group g = lane>>4 owns dims [32g, 32g+32) across the four k-steps, so a
+//     lane reads 64 contiguous bytes of its key row (K) and of its query row (Q);
+//   * keys: tile t, row r holds key 8*(r>>2) + 4t + (r&3), so after QK^T lane group g holds
+//     keys 8g..8g+7 of its column -- exactly the P^T B-fragment layout -- and the matching
+//     V^T A-fragment is 8 consecutive tokens of one channel: one 16-byte load from the
+//     transposed V cache [block][kv_head][d][block_size].
+// Softmax runs in base 2 with the 1/sqrt(d) scale folded into one multiply.  K/V go straight
+// from global memory to VGPRs (decode is HBM-bound: guide §5 "GEMV / M <= 16" row); waves of a
+// workgroup that read the same K/V tile hit the CU's L1.
+// Decode splits long contexts into partitions of kPart keys (flash-decoding) and merges them
+// in a second kernel; sequences that fit one partition are finished in place.
+#include "common.h"
+
+using namespace pk;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+constexpr int kHD = 128;
+constexpr int kStep = 32;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kNegBig = -1e30f;
+
+__device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+
+__device__ __forceinline__ bf16x8_t zero8() {
+  u32x4 z = {0u, 0u, 0u, 0u};
+  return __builtin_bit_cast(bf16x8_t, z);
+}
+
+__device__ __forceinline__ bf16x8_t pack_p(const float* p) {
+  u32x4 v;
+  v[0] = pack2(p[0], p[1]);
+  v[1] = pack2(p[2], p[3]);
+  v[2] = pack2(p[4], p[5]);
+  v[3] = pack2(p[6], p[7]);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+struct WaveState {
+  float m;        // running max (base-2 scaled) of this lane's column
+  float l;        // partial exp-sum of this lane's 8 keys per step (summed over lane groups at the end)
+  f32x4 o[8];     // O^T: o[dt][i] = O[col = lane&15][d = 16*dt + 4*g + i]
+};
+
+// Process keys [k_begin, k_end) in 32-key steps (k_begin multiple of 32), stride `k_stride`
+// between this wave's steps.  Keys >= n_valid or > col_limit are masked.
+__device__ __forceinline__ void attend(WaveState& st, const bf16x8_t (&qf)[4], const bf16_t* __restrict__ kc,
+                                       const bf16_t* __restrict__ vc, int64_t blk_stride, const int* __restrict__ bt,
+                                       int bs, int k_begin, int k_end, int k_stride, int n_valid, int col_limit,
+                                       float scale2) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  for (int s = k_begin; s < k_end; s += k_stride) {
+    // ---- issue K loads (2 tiles x 4 k-steps x 16 B) and V loads (8 d-tiles x 16 B)
+    bf16x8_t kf[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      int tok = s + 8 * (r >> 2) + 4 * t + (r & 3);
+      tok = min(tok, n_valid - 1);
+      const int blk = bt[tok / bs];
+      const bf16_t* p = kc + blk * blk_stride + (tok % bs) * kHD + 32 * g;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) kf[t][kk] = ld8(p + 8 * kk);
+    }
+    bf16x8_t vf[8];
+    {
+      int tok0 = s + 8 * g;
+      tok0 = min(tok0, ((n_valid - 1) >> 3) << 3);
+      const int blk = bt[tok0 / bs];
+      const bf16_t* p = vc + blk * blk_stride + r * bs + (tok0 % bs);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) vf[dt] = ld8(p + dt * 16 * bs);
+    }
+    // ---- S^T = K . Q^T
+    f32x4 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][kk], qf[kk], acc[t], 0, 0, 0);
+    }
+    // ---- online softmax over this step's 32 keys (8 per lane)
+    float sv[8];
+    float mx = kNegBig;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = s + 8 * g + 4 * t + i;
+        const bool ok = key < n_valid && key <= col_limit;
+        const float v = ok ? acc[t][i] * scale2 : -INFINITY;
+        sv[4 * t + i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(st.m, mx);
+    const float alpha = exp2f(st.m - m_new);
+    st.m = m_new;
+    float p[8];
+    float psum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      p[i] = exp2f(sv[i] - m_new);
+      psum += p[i];
+    }
+    st.l = st.l * alpha + psum;
+    const bf16x8_t pb = pack_p(p);
+    // ---- O^T += V^T . P^T
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      st.o[dt] *= alpha;
+      st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pb, st.o[dt], 0, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ void init_state(WaveState& st) {
+  st.m = kNegBig;
+  st.l = 0.f;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+__device__ __forceinline__ void load_q(bf16x8_t (&qf)[4], const bf16_t* q, bool valid) {
+  const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) qf[kk] = valid ? ld8(q + 32 * g + 8 * kk) : zero8();
+}
+
+// Total exp-sum of the lane's column (reduce the 4 lane groups).
+__device__ __forceinline__ float col_sum(float l) {
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  return l;
+}
+
+// ------------------------------------------------------------------------------ decode
+// grid (n_kv, n_seqs, n_parts), block 256 (4 waves).  LDS: 4 waves x 16 cols x 128 d fp32.
+template <int kPart>
+__global__ void __launch_bounds__(256) paged_decode_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int n_q, int n_kv, int bs, int max_blocks,
+    int q_stride, int out_stride, int n_parts, float scale2) {
+  __shared__ float o_lds[4][16][kHD + 4];
+  __shared__ float ml_lds[4][16][2];
+  const int h = blockIdx.x, seq = blockIdx.y, part = blockIdx.z;
+  const int ctx = context_lens[seq];
+  const int begin = part * kPart;
+  if (begin >= ctx) return;
+  const int end = min(ctx, begin + kPart);
+  const int G = n_q / n_kv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
+
+  bf16x8_t qf[4];
+  load_q(qf, q + static_cast<int64_t>(seq) * q_stride + (h * G + r) * kHD, r < G);
+  WaveState st;
+  init_state(st);
+  attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs, blk_stride,
+         block_tables + static_cast<int64_t>(seq) * max_blocks, bs, begin + kStep * w, end, 4 * kStep, ctx, ctx - 1,
+         scale2);
+  const float lsum = col_sum(st.l);
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o_lds[w][r][16 * dt + 4 * g + i] = st.o[dt][i];
+  if (g == 0) {
+    ml_lds[w][r][0] = st.m;
+    ml_lds[w][r][1] = lsum;
+  }
+  __syncthreads();
+  const int n_used = (ctx + kPart - 1) / kPart;
+  for (int idx = threadIdx.x; idx < G * kHD; idx += 256) {
+    const int c = idx / kHD, d = idx % kHD;
+    float M = kNegBig;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
+    float O = 0.f, L = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = exp2f(ml_lds[ww][c][0] - M);
+      O += f * o_lds[ww][c][d];
+      L += f * ml_lds[ww][c][1];
+    }
+    const int hq = h * G + c;
+    if (n_used == 1) {
+      out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
+    } else {
+      const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + part;
+      part_o[pi * kHD + d] = O;
+      if (d == 0) {
+        part_ml[2 * pi] = M;
+        part_ml[2 * pi + 1] = L;
+      }
+    }
+  }
+}
+
+// grid (n_q, n_seqs), block 128: merge the partitions of sequences that used more than one.
+template <int kPart>
+__global__ void __launch_bounds__(128) paged_decode_reduce_kernel(bf16_t* __restrict__ out,
+                                                                  const float* __restrict__ part_o,
+                                                                  const float* __restrict__ part_ml,
+                                                                  const int* __restrict__ context_lens, int n_q,
+                                                                  int out_stride, int n_parts) {
+  const int hq = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
+  const int ctx = context_lens[seq];
+  const int n_used = (ctx + kPart - 1) / kPart;
+  bf16_t* o = out + static_cast<int64_t>(seq) * out_stride + hq * kHD;
+  if (ctx <= 0) {
+    o[d] = 0;
+    return;
+  }
+  if (n_used <= 1) return;
+  const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
+  float M = kNegBig;
+  for (int p = 0; p < n_used; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
+  float O = 0.f, L = 0.f;
+  for (int p = 0; p < n_used; ++p) {
+    const float f = exp2f(part_ml[2 * (base + p)] - M);
+    O += f * part_o[(base + p) * kHD + d];
+    L += f * part_ml[2 * (base + p) + 1];
+  }
+  o[d] = f2bf(L > 0.f ? O / L : 0.f);
+}
+
+// ----------------------------------------------------------------------------- prefill
+// grid (max_q_blocks, n_seqs, n_kv * head_groups), block 64*W with W = min(G, 8) waves:
+// wave w = query head h*G + sub*W + w, 16 query tokens per workgroup.  cu_q: query offsets
+// (relative to q/out), ctx: total keys per seq.  At most 8 waves keeps the VGPR cap at 256.
+__global__ void __launch_bounds__(512) paged_prefill_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
+    const int* __restrict__ cu_q, int n_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride,
+    float scale2) {
+  const int qb = blockIdx.x, seq = blockIdx.y;
+  const int q0 = cu_q[seq], L = cu_q[seq + 1] - q0;
+  if (qb * 16 >= L) return;
+  const int ctx = context_lens[seq];
+  const int G = n_q / n_kv;
+  const int W = blockDim.x >> 6;
+  const int h = blockIdx.z / (G / W), sub = blockIdx.z % (G / W);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int hq = h * G + sub * W + w;
+  const int qi = qb * 16 + r;
+  const bool valid = qi < L;
+  const int qpos = ctx - L + qi;
+  const int last_q = min(L - 1, qb * 16 + 15);
+  const int k_end = min(ctx, ctx - L + last_q + 1);
+  bf16x8_t qf[4];
+  load_q(qf, q + static_cast<int64_t>(q0 + (valid ? qi : 0)) * q_stride + hq * kHD, valid);
+  WaveState st;
+  init_state(st);
+  attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs,
+         static_cast<int64_t>(n_kv) * bs * kHD, block_tables + static_cast<int64_t>(seq) * max_blocks, bs, 0, k_end,
+         kStep, ctx, valid ? qpos : -1, scale2);
+  const float lsum = col_sum(st.l);
+  if (!valid) return;
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  bf16_t* o = out + static_cast<int64_t>(q0 + qi) * out_stride + hq * kHD;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    uint2 v;
+    v.x = pack2(st.o[dt][0] * inv, st.o[dt][1] * inv);
+    v.y = pack2(st.o[dt][2] * inv, st.o[dt][3] * inv);
+    *reinterpret_cast<uint2*>(o + 16 * dt + 4 * g) = v;
+  }
+}
+
+constexpr int kDecodePart = 512;
+
+}  // namespace
+
+// Workspace for decode: part_o [n_seqs, n_q, n_parts, 128] fp32, part_ml [n_seqs, n_q, n_parts, 2] fp32.
+PK_EXPORT int pk_decode_num_parts(int max_context) { return (max_context + kDecodePart - 1) / kDecodePart; }
+
+PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
+                              const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
+                              int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride,
+                              float scale, hipStream_t stream) {
+  if (n_seqs <= 0) return 0;
+  if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
+  const int n_parts = (max_blocks * bs + kDecodePart - 1) / kDecodePart;
+  if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
+  dim3 grid(n_kv, n_seqs, n_parts);
+  paged_decode_kernel<kDecodePart><<<grid, 256, 0, stream>>>(
+      static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
+      static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables), static_cast<const int*>(context_lens),
+      static_cast<float*>(part_o), static_cast<float*>(part_ml), n_q, n_kv, bs, max_blocks, q_stride, out_stride,
+      n_parts, scale * kLog2e);
+  int rc = PK_CHECK_LAUNCH();
+  if (rc) return rc;
+  dim3 g2(n_q, n_seqs);
+  paged_decode_reduce_kernel<kDecodePart><<<g2, 128, 0, stream>>>(
+      static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
+      static_cast<const int*>(context_lens), n_q, out_stride, n_parts);
+  return PK_CHECK_LAUNCH();
+}
+
+PK_EXPORT int pk_paged_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,
+                               const void* block_tables, const void* context_lens, const void* cu_q, void* unused,
+                               int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride,
+                               int max_q_len, float scale, hipStream_t stream) {
+  if (n_seqs <= 0 || max_q_len <= 0) return 0;
+  if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
+  const int G = n_q / n_kv;
+  const int W = G > 8 ? 8 : G;
+  if (G % W) return -1;
+  dim3 grid((max_q_len + 15) / 16, n_seqs, n_kv * (G / W));
+  paged_prefill_kernel<<<grid, 64 * W, 0, stream>>>(
+      static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
+      static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables), static_cast<const int*>(context_lens),
+      static_cast<const int*>(cu_q), n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale * kLog2e);
+  return PK_CHECK_LAUNCH();
+}

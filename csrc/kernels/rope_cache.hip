@@ -1,0 +1,77 @@
+// Fused RoPE (neox / HF rotate_half) on q and k + paged KV-cache write, gfx950.
+//
+// Input is the fused QKV projection output [T, (nq + 2*nkv) * 128] (row stride q_stride).
+// q and k are rotated in place (fp32 math, fp32 cos/sin table [max_pos, 128] = cos | sin);
+// rotated k is also written to the K cache [block][kv_head][slot][128] and v to the
+// transposed V cache [block][kv_head][128][block_size].  One workgroup per token; a lane
+// rotates 8 channel pairs (i, i+64) with two 16-byte loads and two 16-byte stores.
+// slot_mapping[t] < 0 marks a padding row: it is rotated but nothing is cached.
+#include "common.h"
+
+using namespace pk;
+
+namespace {
+
+constexpr int kHD = 128;
+constexpr int kHalf = 64;
+
+__global__ void __launch_bounds__(256) rope_and_cache_kernel(bf16_t* __restrict__ qkv, const int* __restrict__ positions,
+                                                             const float* __restrict__ cos_sin, bf16_t* __restrict__ kc,
+                                                             bf16_t* __restrict__ vc, const int* __restrict__ slots,
+                                                             int nq, int nkv, int bs, int q_stride) {
+  const int t = blockIdx.x;
+  const int pos = positions[t];
+  const int slot = slots ? slots[t] : -1;
+  bf16_t* row = qkv + static_cast<int64_t>(t) * q_stride;
+  const float* cs = cos_sin + static_cast<int64_t>(pos) * kHD;
+  const int n_rot = (nq + nkv) * 8;  // 8 lanes x 8 pairs per head
+  for (int u = threadIdx.x; u < n_rot; u += blockDim.x) {
+    const int head = u >> 3, c = (u & 7) * 8;
+    bf16_t* x = row + head * kHD;
+    float a[8], b[8], co[8], si[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + c), a);
+    unpack8(*reinterpret_cast<const u32x4*>(x + c + kHalf), b);
+    const float4* cp = reinterpret_cast<const float4*>(cs + c);
+    const float4* sp = reinterpret_cast<const float4*>(cs + kHalf + c);
+    float4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+    co[0] = c0.x; co[1] = c0.y; co[2] = c0.z; co[3] = c0.w; co[4] = c1.x; co[5] = c1.y; co[6] = c1.z; co[7] = c1.w;
+    si[0] = s0.x; si[1] = s0.y; si[2] = s0.z; si[3] = s0.w; si[4] = s1.x; si[5] = s1.y; si[6] = s1.z; si[7] = s1.w;
+    float ra[8], rb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ra[j] = a[j] * co[j] - b[j] * si[j];
+      rb[j] = b[j] * co[j] + a[j] * si[j];
+    }
+    const u32x4 va = pack8(ra), vb = pack8(rb);
+    *reinterpret_cast<u32x4*>(x + c) = va;
+    *reinterpret_cast<u32x4*>(x + c + kHalf) = vb;
+    if (head >= nq && slot >= 0) {
+      const int kh = head - nq;
+      bf16_t* dst = kc + ((static_cast<int64_t>(slot / bs) * nkv + kh) * bs + slot % bs) * kHD;
+      *reinterpret_cast<u32x4*>(dst + c) = va;
+      *reinterpret_cast<u32x4*>(dst + c + kHalf) = vb;
+    }
+  }
+  if (slot < 0) return;
+  // V: nkv heads x 128 channels, scattered into the transposed cache (2-byte stores).
+  const int n_v = nkv * kHD;
+  const bf16_t* v = row + (nq + nkv) * kHD;
+  for (int u = threadIdx.x; u < n_v; u += blockDim.x) {
+    const int kh = u / kHD, d = u % kHD;
+    vc[((static_cast<int64_t>(slot / bs) * nkv + kh) * kHD + d) * bs + slot % bs] = v[u];
+  }
+}
+
+}  // namespace
+
+PK_EXPORT int pk_rope_and_cache(void* qkv, const void* positions, const void* cos_sin, void* k_cache, void* v_cache,
+                                const void* slot_mapping, int T, int nq, int nkv, int hd, int bs, int q_stride,
+                                int unused, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (hd != kHD || (bs % 8) != 0) return -1;
+  rope_and_cache_kernel<<<T, 256, 0, stream>>>(static_cast<bf16_t*>(qkv), static_cast<const int*>(positions),
+                                               static_cast<const float*>(cos_sin), static_cast<bf16_t*>(k_cache),
+                                               static_cast<bf16_t*>(v_cache), static_cast<const int*>(slot_mapping), nq,
+                                               nkv, bs, q_stride);
+  return PK_CHECK_LAUNCH();
+}

@@ -1,0 +1,155 @@
+"""On-node LLM adapter: the replacement for the reference's (absent) third-party HTTP
+provider layer (``internal/adapters``).
+
+Registers model tools on the :class:`ToolRouter`:
+
+* ``llm.generate:<model>`` — ``parameters = {prompt | prompt_token_ids, max_tokens, temperature,
+  top_p, top_k, min_p, seed, ignore_eos, stop, stop_token_ids, return: "text"|"struct"}``
+* ``llm.chat:<model>``     — same with ``messages = [{role, content}, ...]``
+
+Unary ``ExecuteTool`` returns the completion as ``string_output`` (what the reference's dev
+client logs), or a ``struct_output`` ``{text, finish_reason, usage, metrics}`` when
+``return == "struct"``.  ``ExecuteToolStream`` yields ``string_output`` deltas (tokens that
+arrived together are coalesced into one message) and ends with the struct summary.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+from .. import proto
+from ..engine.sequence import SamplingParams
+from ..service.base import RequestContext, ToolError, ok_status
+
+
+def _status():
+    return ok_status()
+
+
+class LLMTool:
+    requires_secret = False
+
+    def __init__(self, name: str, model_name: str, llm, chat: bool):
+        self.name = name
+        self.model_name = model_name
+        self.llm = llm
+        self.chat = chat
+        self.tok = llm.tokenizer
+
+    # ------------------------------------------------------------- params
+    def _prompt(self, params: dict) -> List[int]:
+        if "prompt_token_ids" in params:
+            return [int(x) for x in params["prompt_token_ids"]]
+        if self.chat:
+            msgs = params.get("messages")
+            if not isinstance(msgs, list) or not msgs:
+                raise ToolError("INVALID_ARGUMENT", "llm.chat requires a non-empty 'messages' list")
+            text = self.tok.apply_chat_template(msgs)
+        else:
+            text = params.get("prompt")
+            if not isinstance(text, str) or not text:
+                raise ToolError("INVALID_ARGUMENT", "llm.generate requires 'prompt' (string) or 'prompt_token_ids'")
+        return self.tok.encode(text)
+
+    def _sampling(self, params: dict) -> SamplingParams:
+        try:
+            sp = SamplingParams.from_dict(params)
+            sp.validate(1 << 30)
+        except (ValueError, TypeError) as e:
+            raise ToolError("INVALID_ARGUMENT", str(e))
+        return sp
+
+    def _summary(self, text: str, n_prompt: int, toks: List[int], last, t0: float) -> dict:
+        m = (last.metrics or {}) if last is not None else {}
+        return {
+            "model": self.model_name,
+            "text": text,
+            "finish_reason": last.finish_reason if last is not None else "abort",
+            "usage": {"prompt_tokens": n_prompt, "completion_tokens": len(toks),
+                      "total_tokens": n_prompt + len(toks)},
+            "metrics": {k: v for k, v in {**m, "server_e2e_s": time.monotonic() - t0}.items() if v is not None},
+        }
+
+    @staticmethod
+    def _stop_hit(text: str, stops) -> Optional[int]:
+        for s in stops or ():
+            i = text.find(s)
+            if i >= 0:
+                return i
+        return None
+
+    # ------------------------------------------------------------- tool API
+    async def run(self, ctx: RequestContext, params: dict, secret, metadata: Dict[str, str]):
+        t0 = time.monotonic()
+        prompt = self._prompt(params)
+        sp = self._sampling(params)
+        toks: List[int] = []
+        last = None
+        text = ""
+        async for out in self.llm.generate(prompt, sp, request_id=ctx.request_id):
+            toks.extend(out.new_token_ids)
+            last = out
+            if sp.stop:
+                text = self.tok.decode(toks)
+                cut = self._stop_hit(text, sp.stop)
+                if cut is not None:
+                    text = text[:cut]
+                    break
+        if not sp.stop:
+            text = self.tok.decode(toks)
+        resp = proto.ExecuteToolResponse(status=_status())
+        if params.get("return") == "struct":
+            resp.struct_output.update(self._summary(text, len(prompt), toks, last, t0))
+        else:
+            resp.string_output = text
+        return resp
+
+    async def stream(self, ctx: RequestContext, params: dict, secret, metadata: Dict[str, str]):
+        t0 = time.monotonic()
+        prompt = self._prompt(params)
+        sp = self._sampling(params)
+        toks: List[int] = []
+        sent = 0
+        last = None
+        text = ""
+        agen = self.llm.generate(prompt, sp, request_id=ctx.request_id)
+        try:
+            async for out in agen:
+                toks.extend(out.new_token_ids)
+                last = out
+                text = self.tok.decode(toks)
+                cut = self._stop_hit(text, sp.stop) if sp.stop else None
+                if cut is not None:
+                    text = text[:cut]
+                if len(text) > sent and not text.endswith("�"):
+                    yield proto.ExecuteToolResponse(string_output=text[sent:])
+                    sent = len(text)
+                if cut is not None:
+                    break
+        finally:
+            await agen.aclose()
+        final = proto.ExecuteToolResponse(status=_status())
+        final.struct_output.update(self._summary(text, len(prompt), toks, last, t0))
+        yield final
+
+
+def attach_local_llm(router, cfg, logger, engine=None):
+    """Build (or reuse) the engine for ``cfg.model`` and register its tools."""
+    from ..engine.async_llm import AsyncLLM
+    from ..engine.llm_engine import EngineConfig, LLMEngine
+    from ..parallel.state import init_parallel
+
+    if engine is None:
+        st = init_parallel(tp=cfg.tp, ep=cfg.ep)
+        engine = LLMEngine(EngineConfig.from_server_config(cfg), st)
+        if st.tp_rank != 0:
+            engine.runner.worker_loop()  # never returns until the leader stops
+            raise SystemExit(0)
+    llm = AsyncLLM(engine)
+    name = cfg.model if isinstance(cfg.model, str) else "model"
+    router.register_model_tool("llm.generate", name, LLMTool("llm.generate", name, llm, chat=False))
+    router.register_model_tool("llm.chat", name, LLMTool("llm.chat", name, llm, chat=True))
+    router.llm = llm
+    logger.info("local LLM backend ready", model=name, kv_blocks=engine.runner.num_blocks,
+                block_size=engine.cfg.block_size, tp=engine.st.tp_size)
+    return llm

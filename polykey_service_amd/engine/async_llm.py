@@ -1,0 +1,169 @@
+"""Async face of the engine: the continuous-batching loop runs on its own thread; gRPC
+handlers on the asyncio loop submit requests and consume per-request token streams.
+
+Thread → loop hand-off is batched: one ``call_soon_threadsafe`` per engine step delivers
+every request's new tokens (64 streams × 1 token each would otherwise be 64 self-pipe
+wake-ups per step).  A request whose consumer goes away (client cancelled / disconnected)
+is aborted on the engine thread, which frees its KV blocks.  If the engine
+loop dies, every open stream receives the error and ``on_fatal`` fires (the server flips
+health to NOT_SERVING).
+"""
+from __future__ import annotations
+
+import asyncio
+import collections
+import threading
+import time
+import traceback
+import uuid
+from typing import AsyncIterator, Callable, Deque, Dict, List, Optional, Tuple
+
+from .llm_engine import LLMEngine
+from .sequence import RequestOutput, SamplingParams
+
+
+class EngineDeadError(RuntimeError):
+    pass
+
+
+class AsyncLLM:
+    def __init__(self, engine: LLMEngine, on_fatal: Optional[Callable[[BaseException], None]] = None,
+                 watchdog_s: float = 0.0):
+        self.engine = engine
+        self.tokenizer = engine.tokenizer
+        self.on_fatal = on_fatal
+        self._cmds: Deque[Tuple[str, object]] = collections.deque()
+        self._wake = threading.Event()
+        self._streams: Dict[str, Tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
+        self._lock = threading.Lock()
+        self._stop = False
+        self.dead: Optional[BaseException] = None
+        self.last_step_time = time.monotonic()
+        self.watchdog_s = watchdog_s
+        self.stats = {"steps": 0, "requests": 0, "output_tokens": 0, "step_time_s": 0.0}
+        self._thread = threading.Thread(target=self._run, name="polykey-engine", daemon=True)
+        self._thread.start()
+
+    # ---------------------------------------------------------------- client side
+    async def generate(self, prompt_ids: List[int], params: SamplingParams,
+                       request_id: Optional[str] = None) -> AsyncIterator[RequestOutput]:
+        if self.dead is not None:
+            raise EngineDeadError(f"engine is dead: {self.dead}")
+        rid = request_id or uuid.uuid4().hex
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        with self._lock:
+            if rid in self._streams:
+                raise ValueError(f"duplicate request id {rid}")
+            self._streams[rid] = (loop, q)
+            self._cmds.append(("add", (rid, prompt_ids, params)))
+        self._wake.set()
+        finished = False
+        try:
+            while True:
+                item = await q.get()
+                if isinstance(item, BaseException):
+                    finished = True
+                    raise item
+                yield item
+                if item.finished:
+                    finished = True
+                    return
+        finally:
+            with self._lock:
+                self._streams.pop(rid, None)
+                if not finished:
+                    self._cmds.append(("abort", rid))
+            if not finished:
+                self._wake.set()
+
+    async def generate_all(self, prompt_ids: List[int], params: SamplingParams,
+                           request_id: Optional[str] = None) -> Tuple[List[int], RequestOutput]:
+        toks: List[int] = []
+        last = None
+        async for out in self.generate(prompt_ids, params, request_id):
+            toks.extend(out.new_token_ids)
+            last = out
+        return toks, last
+
+    def shutdown(self, timeout: float = 10.0) -> None:
+        self._stop = True
+        self._wake.set()
+        self._thread.join(timeout)
+        try:
+            self.engine.shutdown()
+        except Exception:
+            pass
+
+    async def aclose(self) -> None:
+        await asyncio.get_running_loop().run_in_executor(None, self.shutdown)
+
+    def healthy(self) -> bool:
+        if self.dead is not None:
+            return False
+        if self.watchdog_s and self.engine.has_unfinished():
+            return time.monotonic() - self.last_step_time < self.watchdog_s
+        return True
+
+    # ---------------------------------------------------------------- engine side
+    def _drain_cmds(self) -> None:
+        with self._lock:
+            cmds = list(self._cmds)
+            self._cmds.clear()
+        for kind, arg in cmds:
+            if kind == "add":
+                rid, prompt, params = arg
+                try:
+                    self.engine.add_request(prompt, params, rid)
+                    self.stats["requests"] += 1
+                except Exception as e:  # noqa: BLE001 - reported to that request only
+                    self._deliver([(rid, ValueError(str(e)))])
+            elif kind == "abort":
+                self.engine.abort(arg)
+
+    def _deliver(self, items) -> None:
+        by_loop: Dict[asyncio.AbstractEventLoop, list] = {}
+        with self._lock:
+            for rid, item in items:
+                ent = self._streams.get(rid)
+                if ent is not None:
+                    by_loop.setdefault(ent[0], []).append((ent[1], item))
+        for loop, batch in by_loop.items():
+            try:
+                loop.call_soon_threadsafe(_fanout, batch)
+            except RuntimeError:
+                pass  # loop closed
+
+    def _run(self) -> None:
+        eng = self.engine
+        try:
+            while not self._stop:
+                self._drain_cmds()
+                if not eng.has_unfinished():
+                    self._wake.wait(0.05)
+                    self._wake.clear()
+                    continue
+                t0 = time.perf_counter()
+                outs = eng.step()
+                self.stats["step_time_s"] += time.perf_counter() - t0
+                self.stats["steps"] += 1
+                self.last_step_time = time.monotonic()
+                if outs:
+                    self.stats["output_tokens"] += sum(len(o.new_token_ids) for o in outs)
+                    self._deliver([(o.request_id, o) for o in outs])
+        except BaseException as e:  # noqa: BLE001
+            self.dead = e
+            traceback.print_exc()
+            with self._lock:
+                rids = list(self._streams)
+            self._deliver([(r, EngineDeadError(f"engine loop failed: {e!r}")) for r in rids])
+            if self.on_fatal is not None:
+                try:
+                    self.on_fatal(e)
+                except Exception:
+                    pass
+
+
+def _fanout(batch) -> None:
+    for q, item in batch:
+        q.put_nowait(item)

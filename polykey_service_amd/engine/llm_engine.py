@@ -1,0 +1,140 @@
+"""Synchronous engine: add requests, ``step()`` until done (the L5 engine of SURVEY.md §3.6).
+
+``step()`` = schedule → model runner (pack, H2D, forward / graph replay, sample, D2H) →
+append tokens, detect stop conditions, free finished sequences → per-request outputs.
+The async/gRPC face is :mod:`polykey_service_amd.engine.async_llm`.
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+import uuid
+from typing import Dict, Iterable, List, Optional
+
+import torch
+
+from .._native.loader import load_extension
+from ..models import build_model
+from ..models.config import ModelConfig, get_config
+from ..parallel.state import ParallelState, get_state
+from .model_runner import ModelRunner, RunnerConfig
+from .scheduler import ScheduledBatch, Scheduler
+from .sequence import FinishReason, RequestOutput, SamplingParams, Sequence, seq_metrics
+from .tokenizer import get_tokenizer
+
+
+@dataclasses.dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    model_path: str = ""
+    tokenizer: str = ""
+    dtype: str = "bfloat16"
+    seed: int = 0
+    block_size: int = 32
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 8192
+    num_kv_blocks: int = 0
+    gpu_mem_fraction: float = 0.90
+    hip_graphs: bool = True
+    graph_batch_sizes: tuple = ()
+    watermark: float = 0.01
+    device: str = ""
+
+    @classmethod
+    def from_server_config(cls, sc) -> "EngineConfig":
+        return cls(model=sc.model, model_path=sc.model_path, tokenizer=sc.tokenizer, dtype=sc.dtype, seed=sc.seed,
+                   block_size=sc.kv_block_size, max_num_seqs=sc.max_num_seqs,
+                   max_num_batched_tokens=sc.max_num_batched_tokens, max_model_len=sc.max_model_len,
+                   num_kv_blocks=sc.num_kv_blocks, gpu_mem_fraction=sc.gpu_mem_fraction, hip_graphs=sc.hip_graphs)
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, st: Optional[ParallelState] = None, model=None):
+        self.cfg = cfg
+        self.st = st or get_state()
+        mcfg: ModelConfig = get_config(cfg.model_path or cfg.model)
+        if cfg.max_model_len > mcfg.max_position:
+            cfg = dataclasses.replace(cfg, max_model_len=mcfg.max_position)
+            self.cfg = cfg
+        self.mcfg = mcfg
+        dev = torch.device(cfg.device) if cfg.device else self.st.device
+        self.device = dev
+        dtype = getattr(torch, cfg.dtype)
+        if model is None:
+            model = build_model(mcfg, self.st, dtype, dev)
+            if cfg.model_path:
+                model.load_hf(cfg.model_path)
+            else:
+                model.init_random(cfg.seed)
+        self.model = model
+        self.tokenizer = get_tokenizer(cfg.tokenizer, mcfg.vocab_size, mcfg.bos_token_id, mcfg.eos_token_id)
+        rcfg = RunnerConfig(block_size=cfg.block_size, max_num_seqs=cfg.max_num_seqs,
+                            max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=cfg.max_model_len,
+                            num_kv_blocks=cfg.num_kv_blocks, gpu_mem_fraction=cfg.gpu_mem_fraction,
+                            hip_graphs=cfg.hip_graphs, graph_batch_sizes=tuple(cfg.graph_batch_sizes))
+        self.runner = ModelRunner(model, rcfg, dev)
+        nblocks = self.runner.allocate_kv_cache()
+        rt = load_extension("_pk_runtime")
+        self.bm = rt.BlockManager(nblocks, cfg.block_size, int(nblocks * cfg.watermark))
+        self.runner.bm = self.bm
+        self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
+        if cfg.hip_graphs and dev.type == "cuda":
+            self.runner.capture_graphs()
+        self.step_count = 0
+        self.total_output_tokens = 0
+
+    # ------------------------------------------------------------------ API
+    @property
+    def is_leader(self) -> bool:
+        return self.st.tp_rank == 0
+
+    def add_request(self, prompt_ids: List[int], params: SamplingParams, request_id: Optional[str] = None,
+                    user=None) -> Sequence:
+        params.validate(self.cfg.max_model_len)
+        if not prompt_ids:
+            raise ValueError("empty prompt")
+        if max(prompt_ids) >= self.mcfg.vocab_size or min(prompt_ids) < 0:
+            raise ValueError("prompt token id out of range")
+        seq = Sequence(request_id or uuid.uuid4().hex, prompt_ids, params, self.mcfg.eos_token_id, user)
+        self.scheduler.add(seq)
+        return seq
+
+    def abort(self, request_id: str) -> Optional[Sequence]:
+        return self.scheduler.abort(request_id)
+
+    def has_unfinished(self) -> bool:
+        return self.scheduler.has_work()
+
+    def step(self) -> List[RequestOutput]:
+        batch = self.scheduler.schedule()
+        if batch.empty:
+            return []
+        sampling = batch.sampling_seqs()
+        toks = self.runner.execute(batch)
+        now = time.monotonic()
+        outs: List[RequestOutput] = []
+        for s, n in batch.prefills:
+            s.num_computed += n
+        for s in batch.decodes:
+            s.num_computed += 1
+        for s, tok in zip(sampling, toks):
+            reason = s.append_token(int(tok), now)
+            if reason is not None:
+                self.scheduler.finish(s, reason)
+            outs.append(RequestOutput(s.request_id, [int(tok)], reason is not None,
+                                      reason.value if reason else None, len(s.prompt_ids), len(s.output_ids),
+                                      seq_metrics(s) if reason else None))
+        self.scheduler.remove_finished()
+        self.step_count += 1
+        self.total_output_tokens += len(toks)
+        return outs
+
+    def generate(self, prompts: List[List[int]], params: SamplingParams) -> List[List[int]]:
+        seqs = [self.add_request(p, dataclasses.replace(params)) for p in prompts]
+        while self.has_unfinished():
+            self.step()
+        return [s.output_ids for s in seqs]
+
+    def shutdown(self) -> None:
+        self.runner.stop_workers()

@@ -1,0 +1,320 @@
+"""Model runner: step inputs → device, forward, logits, sampling; HIP graphs for decode.
+
+Per step the CPU work is one native call (``BlockManager.pack_step`` writes token ids,
+positions, slot mapping, block tables, context lengths and query offsets into a pinned
+int32 staging buffer), one H2D copy of that buffer, the forward, and one D2H copy of the
+sampled ids.  The device-side copy of the staging buffer has fixed section offsets, so its
+views are stable and a decode step can be *captured once per batch-size bucket* and replayed
+with ``hipGraphLaunch`` (torch.cuda.CUDAGraph on ROCm) — the launch-bound decode loop of
+32–80 layers × ~10 kernels collapses into one graph launch (guide: "capture launch-bound
+inner loops in hipGraphs").
+
+KV cache: one allocation per layer pair, K ``[blocks, n_kv, bs, 128]`` and transposed V
+``[blocks, n_kv, 128, bs]`` (see ops/attention.py), sized from free HBM after weights and
+a measured activation peak — at 288 GB per MI355X an 8B model gets ~1.9 M cached tokens.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import time
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..ops import attention as attn_ops
+from ..ops import sampler as sampler_ops
+from .scheduler import ScheduledBatch
+from .sequence import Sequence
+
+
+@dataclasses.dataclass
+class RunnerConfig:
+    block_size: int = 32
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    max_model_len: int = 8192
+    num_kv_blocks: int = 0           # 0 → size from free memory
+    gpu_mem_fraction: float = 0.90
+    hip_graphs: bool = True
+    graph_batch_sizes: Tuple[int, ...] = ()
+
+
+class _Layout:
+    """Fixed offsets of every per-step int32 section inside one staging buffer."""
+
+    def __init__(self, max_tokens: int, max_seqs: int, max_blocks: int):
+        self.max_tokens, self.max_seqs, self.max_blocks = max_tokens, max_seqs, max_blocks
+        off = 0
+        self.sections = {}
+        for name, n in (("header", 16), ("input_ids", max_tokens), ("positions", max_tokens), ("slots", max_tokens),
+                        ("context_lens", max_seqs), ("cu_q", max_seqs + 1), ("cu_rel", max_seqs + 1), ("sample_idx", max_seqs),
+                        ("temperature", max_seqs), ("top_k", max_seqs), ("top_p", max_seqs), ("min_p", max_seqs),
+                        ("seeds", max_seqs), ("offsets", max_seqs), ("block_tables", max_seqs * max_blocks)):
+            self.sections[name] = (off, n)
+            off += (n + 15) // 16 * 16  # 64-byte aligned sections
+        self.size = off
+
+    def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        off, n = self.sections[name]
+        v = buf[off:off + n]
+        if name in ("temperature", "top_p", "min_p"):
+            v = v.view(torch.float32)
+        if name == "block_tables":
+            v = v.view(self.max_seqs, self.max_blocks)
+        return v
+
+
+class ModelRunner:
+    def __init__(self, model, cfg: RunnerConfig, device: torch.device, block_manager=None):
+        self.model = model
+        self.bm = block_manager
+        self.mcfg = model.cfg
+        self.cfg = cfg
+        self.device = device
+        self.bs = cfg.block_size
+        self.max_blocks = (cfg.max_model_len + self.bs - 1) // self.bs
+        self.layout = _Layout(cfg.max_num_batched_tokens, cfg.max_num_seqs, self.max_blocks)
+        pin = device.type == "cuda"
+        self.host_buf = torch.zeros(self.layout.size, dtype=torch.int32, pin_memory=pin)
+        self.dev_buf = torch.zeros(self.layout.size, dtype=torch.int32, device=device)
+        self.h = {k: self.layout.view(self.host_buf, k).numpy() for k in self.layout.sections}
+        self.d = {k: self.layout.view(self.dev_buf, k) for k in self.layout.sections}
+        self.tok_host = torch.zeros(cfg.max_num_seqs, dtype=torch.int32, pin_memory=pin)
+        self.kv_caches: List[Tuple[torch.Tensor, torch.Tensor]] = []
+        self.num_blocks = 0
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_out: Dict[int, torch.Tensor] = {}
+        self.graph_pool = None
+        nq_local = model.layers[0].attn.nq
+        self.part_o, self.part_ml = attn_ops.decode_workspace(cfg.max_num_seqs, nq_local, self.max_blocks, self.bs,
+                                                              device)
+        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0}
+
+    # ---------------------------------------------------------------- KV cache
+    def kv_bytes_per_block(self) -> int:
+        a = self.model.layers[0].attn
+        return 2 * len(self.model.layers) * a.nkv * self.bs * a.hd * 2
+
+    def allocate_kv_cache(self, num_blocks: int = 0) -> int:
+        a = self.model.layers[0].attn
+        if num_blocks <= 0:
+            num_blocks = self.cfg.num_kv_blocks
+        if num_blocks <= 0:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+                free, total = torch.cuda.mem_get_info(self.device)
+                reserve = self.activation_reserve_bytes()
+                usable = free - (1.0 - self.cfg.gpu_mem_fraction) * total - reserve
+                num_blocks = int(max(usable, 0) // self.kv_bytes_per_block())
+                cap = self.cfg.max_num_seqs * self.max_blocks + 16
+                num_blocks = max(16, min(num_blocks, cap))
+            else:
+                num_blocks = max(16, min(self.cfg.max_num_seqs * self.max_blocks, 4096))
+        self.num_blocks = num_blocks
+        self.kv_caches = []
+        for _ in self.model.layers:
+            k = torch.zeros((num_blocks, a.nkv, self.bs, a.hd), dtype=self.model.dtype, device=self.device)
+            v = torch.zeros((num_blocks, a.nkv, a.hd, self.bs), dtype=self.model.dtype, device=self.device)
+            self.kv_caches.append((k, v))
+        return num_blocks
+
+    def activation_reserve_bytes(self) -> int:
+        m = self.mcfg
+        T = self.cfg.max_num_batched_tokens
+        tp = self.model.st.tp_size
+        per_tok = 2 * (m.hidden_size * 4 + (m.q_size + 2 * m.kv_size) // tp + 3 * m.intermediate_size // tp)
+        logits = self.cfg.max_num_seqs * m.vocab_size * 4 * 2
+        return int(T * per_tok * 1.5 + logits + (1 << 30))
+
+    # ------------------------------------------------------------------ inputs
+    def _pack(self, batch: ScheduledBatch, sampling: List[Sequence]):
+        decodes, prefills = batch.decodes, batch.prefills
+        seqs = decodes + [s for s, _ in prefills]
+        n = len(seqs)
+        nnew = np.empty(n, dtype=np.int32)
+        ncomp = np.empty(n, dtype=np.int32)
+        sids = np.empty(n, dtype=np.int64)
+        toks: List[int] = []
+        for i, s in enumerate(decodes):
+            sids[i], ncomp[i], nnew[i] = s.seq_id, s.num_computed, 1
+            toks.append(s.output_ids[-1] if s.output_ids else s.prompt_ids[-1])
+        for j, (s, c) in enumerate(prefills):
+            i = len(decodes) + j
+            sids[i], ncomp[i], nnew[i] = s.seq_id, s.num_computed, c
+            toks.extend(s.token_slice(s.num_computed, s.num_computed + c))
+        tok_arr = np.asarray(toks, dtype=np.int32)
+        h = self.h
+        T = self.bm.pack_step(sids, ncomp, nnew, tok_arr, h["input_ids"], h["positions"], h["slots"],
+                              h["block_tables"], self.max_blocks, h["context_lens"], h["cu_q"])
+        # sampling rows: hidden-state row index of each sampling sequence
+        pos_of = {s.seq_id: int(h["cu_q"][i + 1]) - 1 for i, s in enumerate(seqs)}
+        for r, s in enumerate(sampling):
+            p = s.params
+            h["sample_idx"][r] = pos_of[s.seq_id]
+            h["temperature"][r] = p.temperature
+            h["top_k"][r] = p.top_k
+            h["top_p"][r] = p.top_p
+            h["min_p"][r] = p.min_p
+            h["seeds"][r] = s.seed
+            h["offsets"][r] = len(s.output_ids)
+        return T, n
+
+    def _metadata(self, nd: int, n: int, T: int, max_q: int) -> attn_ops.AttnMetadata:
+        d = self.d
+        npf = n - nd
+        md = attn_ops.AttnMetadata(
+            num_decode=nd, num_prefill=npf, num_prefill_tokens=T - nd, max_prefill_q_len=max_q,
+            slot_mapping=d["slots"][:T],
+            decode_block_tables=d["block_tables"][:nd] if nd else None,
+            decode_context_lens=d["context_lens"][:nd] if nd else None,
+            decode_part_o=self.part_o, decode_part_ml=self.part_ml)
+        if npf:
+            md.prefill_block_tables = d["block_tables"][nd:n]
+            md.prefill_context_lens = d["context_lens"][nd:n]
+            # query offsets relative to the first prefill token
+            md.prefill_cu_q = d["cu_rel"][:npf + 1]
+        return md
+
+    # ----------------------------------------------------------------- execute
+    # header words (section "header"): mode, T, n, nd, ns, max_q, graph bucket
+    MODE_IDLE, MODE_RUN, MODE_STOP = 0, 1, 2
+
+    @torch.inference_mode()
+    def execute(self, batch: ScheduledBatch) -> List[int]:
+        """TP leader / single rank: pack, publish, run.  Returns the sampled token ids of
+        ``batch.sampling_seqs()`` in order."""
+        sampling = batch.sampling_seqs()
+        T, n = self._pack(batch, sampling)
+        nd = len(batch.decodes)
+        ns = len(sampling)
+        h = self.h
+        max_q = 0
+        g = 0
+        if batch.prefills:
+            rel = h["cu_q"][nd:n + 1] - h["cu_q"][nd]
+            h["cu_rel"][:n - nd + 1] = rel
+            max_q = int(np.max(np.diff(rel)))
+        elif self.graphs:
+            g = self._graph_bucket(nd) or 0
+            if g:
+                self._pad_decode(nd, g)
+        h["header"][:7] = (self.MODE_RUN, T, n, nd, ns, max_q, g)
+        self._publish()
+        toks = self._run(T, n, nd, ns, max_q, g)
+        return self._fetch(toks, ns)
+
+    def _publish(self) -> None:
+        self.dev_buf.copy_(self.host_buf, non_blocking=True)
+        if self.model.st.tp_size > 1:
+            from ..parallel import comm
+            comm.tp_broadcast_tensor(self.dev_buf)
+
+    def worker_loop(self) -> None:
+        """Non-leader TP ranks: receive each step's inputs and run the same forward."""
+        from ..parallel import comm
+        while True:
+            comm.tp_broadcast_tensor(self.dev_buf)
+            hdr = self.d["header"][:7].tolist()
+            mode, T, n, nd, ns, max_q, g = hdr
+            if mode == self.MODE_STOP:
+                return
+            if mode == self.MODE_RUN:
+                with torch.inference_mode():
+                    self._run(T, n, nd, ns, max_q, g)
+
+    def stop_workers(self) -> None:
+        if self.model.st.tp_size > 1:
+            self.h["header"][0] = self.MODE_STOP
+            self._publish()
+
+    def _run(self, T: int, n: int, nd: int, ns: int, max_q: int, g: int):
+        d = self.d
+        if g:
+            self.graphs[g].replay()
+            self.stats["graph_steps"] += 1
+            return self.graph_out[g]
+        md = self._metadata(nd, n, T, max_q)
+        hidden = self.model(d["input_ids"][:T], d["positions"][:T], md, self.kv_caches)
+        if ns == 0:
+            return None
+        rows = hidden if ns == T else hidden.index_select(0, d["sample_idx"][:ns].long())
+        logits = self.model.compute_logits(rows)
+        return sampler_ops.sample(logits, d["temperature"][:ns], d["top_k"][:ns], d["top_p"][:ns],
+                                  d["min_p"][:ns], d["seeds"][:ns], d["offsets"][:ns])
+
+    def _fetch(self, toks, ns: int) -> List[int]:
+        self.stats["steps"] += 1
+        if ns == 0 or toks is None:
+            return []
+        if toks.is_cuda:
+            self.tok_host[:ns].copy_(toks[:ns], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            return self.tok_host[:ns].tolist()
+        return toks[:ns].tolist()
+
+    # ------------------------------------------------------------------ graphs
+    def _graph_bucket(self, nd: int) -> Optional[int]:
+        for b in sorted(self.graphs):
+            if b >= nd:
+                return b
+        return None
+
+    def _pad_decode(self, nd: int, g: int) -> None:
+        h = self.h
+        if g > nd:
+            h["input_ids"][nd:g] = 0
+            h["positions"][nd:g] = 0
+            h["slots"][nd:g] = -1
+            h["context_lens"][nd:g] = 0
+            h["sample_idx"][nd:g] = np.arange(nd, g, dtype=np.int32)
+            h["temperature"][nd:g] = 0.0
+            h["top_k"][nd:g] = 0
+            h["top_p"][nd:g] = 1.0
+            h["min_p"][nd:g] = 0.0
+
+    def default_graph_sizes(self) -> List[int]:
+        if self.cfg.graph_batch_sizes:
+            sizes = list(self.cfg.graph_batch_sizes)
+        else:
+            sizes = [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512]
+        return [s for s in sizes if s <= self.cfg.max_num_seqs]
+
+    @torch.inference_mode()
+    def capture_graphs(self, sizes: Optional[List[int]] = None) -> None:
+        if self.device.type != "cuda" or not self.cfg.hip_graphs:
+            return
+        sizes = sizes or self.default_graph_sizes()
+        d = self.d
+        # a valid dummy decode state: every row points at block 0, context 1, no cache writes
+        self.host_buf.zero_()
+        self.h["slots"][:] = -1
+        self.h["context_lens"][: self.cfg.max_num_seqs] = 1
+        self.h["top_p"][:] = 1.0
+        self.h["sample_idx"][: self.cfg.max_num_seqs] = np.arange(self.cfg.max_num_seqs, dtype=np.int32)
+        self.dev_buf.copy_(self.host_buf)
+        torch.cuda.synchronize(self.device)
+        stream = torch.cuda.Stream(self.device)
+        for g in sorted(sizes, reverse=True):
+            md = self._metadata(g, g, g, 0)
+
+            def run():
+                hidden = self.model(d["input_ids"][:g], d["positions"][:g], md, self.kv_caches)
+                logits = self.model.compute_logits(hidden)
+                return sampler_ops.sample(logits, d["temperature"][:g], d["top_k"][:g], d["top_p"][:g],
+                                          d["min_p"][:g], d["seeds"][:g], d["offsets"][:g])
+
+            # warm up on a side stream (allocator + library handles), then capture
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(stream):
+                run()
+            torch.cuda.current_stream(self.device).wait_stream(stream)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, pool=self.graph_pool):
+                out = run()
+            if self.graph_pool is None:
+                self.graph_pool = graph.pool()
+            self.graphs[g] = graph
+            self.graph_out[g] = out
+        torch.cuda.synchronize(self.device)

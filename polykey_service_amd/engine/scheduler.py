@@ -1,0 +1,185 @@
+"""Continuous-batching scheduler (the L3 "Scheduler" of SURVEY.md §1.2 / §3.6).
+
+Every engine step builds one batch under a token budget (``max_num_batched_tokens``) and a
+sequence cap (``max_num_seqs``):
+
+1. running sequences first, oldest first: a decode costs 1 token; a sequence still in a
+   chunked prefill takes ``min(pending, budget)`` tokens.  If the KV pool cannot grow a
+   running sequence, the *youngest* running sequence is preempted (blocks freed, state reset
+   to recompute) and the step retries — the oldest requests keep their latency;
+2. then waiting sequences in FIFO order, admitted only when their (chunked) prefill fits
+   both the budget and the KV pool minus a watermark reserve; the first one that does not fit
+   blocks the queue (no overtaking → no starvation).
+
+KV bookkeeping lives in the native :class:`_pk_runtime.BlockManager` (``csrc/runtime``).
+"""
+from __future__ import annotations
+
+import collections
+import dataclasses
+import time
+from typing import Deque, Dict, List, Optional, Tuple
+
+from .sequence import FinishReason, Sequence, SeqStatus
+
+
+@dataclasses.dataclass
+class ScheduledBatch:
+    decodes: List[Sequence]
+    prefills: List[Tuple[Sequence, int]]   # (seq, chunk length)
+    preempted: List[Sequence]
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self.decodes) + sum(n for _, n in self.prefills)
+
+    @property
+    def empty(self) -> bool:
+        return not self.decodes and not self.prefills
+
+    def sampling_seqs(self) -> List[Sequence]:
+        """Sequences that produce a token this step (decodes + prefills that finish their prompt)."""
+        out = list(self.decodes)
+        out += [s for s, n in self.prefills if s.num_computed + n == s.num_tokens]
+        return out
+
+
+class Scheduler:
+    def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
+                 max_model_len: int = 8192, max_prefill_chunk: Optional[int] = None):
+        self.bm = block_manager
+        self.max_num_seqs = max_num_seqs
+        self.max_num_batched_tokens = max_num_batched_tokens
+        self.max_model_len = max_model_len
+        self.max_prefill_chunk = max_prefill_chunk or max_num_batched_tokens
+        self.waiting: Deque[Sequence] = collections.deque()
+        self.running: List[Sequence] = []
+        self.by_request: Dict[str, Sequence] = {}
+        self.num_preemptions = 0
+
+    # --------------------------------------------------------------- queue ops
+    def add(self, seq: Sequence) -> None:
+        if seq.num_tokens + seq.params.max_tokens > self.max_model_len + 1:
+            # fail fast instead of overflowing the block table mid-generation
+            room = self.max_model_len - seq.num_tokens
+            if room < 1:
+                raise ValueError(f"prompt of {seq.num_tokens} tokens exceeds max_model_len {self.max_model_len}")
+            seq.params = dataclasses.replace(seq.params, max_tokens=room)
+        if self.bm.blocks_for(seq.num_tokens + 1) > self.bm.num_blocks:
+            raise ValueError("request can never fit in the KV cache")
+        cap = self.bm.num_blocks * self.bm.block_size - seq.num_tokens
+        if seq.params.max_tokens > cap:
+            # a lone sequence must always be able to finish, or preemption would livelock
+            seq.params = dataclasses.replace(seq.params, max_tokens=cap)
+        self.waiting.append(seq)
+        self.by_request[seq.request_id] = seq
+
+    def abort(self, request_id: str) -> Optional[Sequence]:
+        seq = self.by_request.pop(request_id, None)
+        if seq is None:
+            return None
+        if seq in self.running:
+            self.running.remove(seq)
+        else:
+            try:
+                self.waiting.remove(seq)
+            except ValueError:
+                pass
+        self.bm.free_seq(seq.seq_id)
+        seq.status = SeqStatus.FINISHED
+        seq.finish_reason = FinishReason.ABORT
+        seq.finish_time = time.monotonic()
+        return seq
+
+    def finish(self, seq: Sequence, reason: FinishReason) -> None:
+        seq.status = SeqStatus.FINISHED
+        seq.finish_reason = reason
+        seq.finish_time = time.monotonic()
+        self.bm.free_seq(seq.seq_id)
+        self.by_request.pop(seq.request_id, None)
+
+    def remove_finished(self) -> None:
+        self.running = [s for s in self.running if s.status != SeqStatus.FINISHED]
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def num_unfinished(self) -> int:
+        return len(self.waiting) + len(self.running)
+
+    # ------------------------------------------------------------------ policy
+    def _preempt_youngest(self, protect: Sequence) -> Optional[Sequence]:
+        for cand in reversed(self.running):
+            if cand is not protect:
+                self.running.remove(cand)
+                self.bm.free_seq(cand.seq_id)
+                cand.num_computed = 0
+                cand.status = SeqStatus.WAITING
+                cand.num_preemptions += 1
+                self.num_preemptions += 1
+                self.waiting.appendleft(cand)
+                return cand
+        return None
+
+    def schedule(self) -> ScheduledBatch:
+        budget = self.max_num_batched_tokens
+        decodes: List[Sequence] = []
+        prefills: List[Tuple[Sequence, int]] = []
+        preempted: List[Sequence] = []
+        scheduled = set()
+
+        i = 0
+        while i < len(self.running) and budget > 0:
+            seq = self.running[i]
+            pending = seq.num_pending
+            n = 1 if pending == 1 else min(pending, budget, self.max_prefill_chunk)
+            while not self.bm.allocate(seq.seq_id, seq.num_computed + n):
+                victim = self._preempt_youngest(protect=seq)
+                if victim is None:
+                    break
+                preempted.append(victim)
+            else:
+                if pending == 1:
+                    decodes.append(seq)
+                else:
+                    prefills.append((seq, n))
+                scheduled.add(seq.seq_id)
+                budget -= n
+                i = self.running.index(seq) + 1  # preemption may have removed earlier entries
+                continue
+            # could not even fit this sequence alone: preempt it too
+            i = self.running.index(seq)
+            self.running.remove(seq)
+            self.bm.free_seq(seq.seq_id)
+            seq.num_computed = 0
+            seq.status = SeqStatus.WAITING
+            seq.num_preemptions += 1
+            self.num_preemptions += 1
+            self.waiting.appendleft(seq)
+            preempted.append(seq)
+
+        # preempted sequences that were already scheduled this step are dropped from it
+        if preempted:
+            gone = {s.seq_id for s in preempted}
+            decodes = [s for s in decodes if s.seq_id not in gone]
+            prefills = [(s, n) for s, n in prefills if s.seq_id not in gone]
+
+        while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
+            seq = self.waiting[0]
+            if seq.seq_id in {s.seq_id for s in preempted}:
+                break  # do not thrash: re-admit preempted sequences next step
+            n = min(seq.num_pending, budget, self.max_prefill_chunk)
+            if not self.bm.can_allocate(seq.seq_id, seq.num_computed + n, True):
+                break
+            self.bm.allocate(seq.seq_id, seq.num_computed + n)
+            self.waiting.popleft()
+            seq.status = SeqStatus.RUNNING
+            if seq.first_scheduled is None:
+                seq.first_scheduled = time.monotonic()
+            self.running.append(seq)
+            if seq.num_pending == 1 and n == 1:
+                decodes.append(seq)
+            else:
+                prefills.append((seq, n))
+            budget -= n
+        return ScheduledBatch(decodes, prefills, preempted)

@@ -1,0 +1,73 @@
+"""Tokenizers.
+
+No network: a real Llama-3 / Mixtral ``tokenizer.json`` is used when a local path is given
+(HF ``tokenizers`` is installed); otherwise :class:`ByteTokenizer` maps UTF-8 bytes to ids
+``[offset, offset+256)`` so prompts round-trip and random-weight outputs decode to text.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, List, Optional
+
+
+class ByteTokenizer:
+    def __init__(self, vocab_size: int, bos_token_id: int = 1, eos_token_id: int = 2, offset: int = 3):
+        self.vocab_size = vocab_size
+        self.bos_token_id = bos_token_id
+        self.eos_token_id = eos_token_id
+        self.offset = offset
+
+    def encode(self, text: str, add_bos: bool = True) -> List[int]:
+        ids = [b + self.offset for b in text.encode("utf-8")]
+        return ([self.bos_token_id] if add_bos else []) + ids
+
+    def decode(self, ids: List[int]) -> str:
+        out = bytearray()
+        for i in ids:
+            b = i - self.offset
+            if 0 <= b < 256:
+                out.append(b)
+            elif i not in (self.bos_token_id, self.eos_token_id):
+                # random-weight models emit ids outside the byte range: render deterministically
+                out.extend(b"\xc2\xb7")  # '·'
+        return out.decode("utf-8", errors="replace")
+
+    def apply_chat_template(self, messages: List[Dict[str, str]]) -> str:
+        return format_chat(messages)
+
+
+class HFTokenizer:
+    def __init__(self, path: str, bos_token_id: int, eos_token_id: int):
+        from tokenizers import Tokenizer
+        self.tok = Tokenizer.from_file(path)
+        self.bos_token_id = bos_token_id
+        self.eos_token_id = eos_token_id
+        self.vocab_size = self.tok.get_vocab_size()
+
+    def encode(self, text: str, add_bos: bool = True) -> List[int]:
+        ids = self.tok.encode(text, add_special_tokens=False).ids
+        return ([self.bos_token_id] if add_bos else []) + ids
+
+    def decode(self, ids: List[int]) -> str:
+        return self.tok.decode(ids, skip_special_tokens=True)
+
+    def apply_chat_template(self, messages: List[Dict[str, str]]) -> str:
+        return format_chat(messages)
+
+
+def format_chat(messages: List[Dict[str, str]]) -> str:
+    """Llama-3 style chat markup (header/eot markers as plain text for the byte tokenizer)."""
+    parts = []
+    for m in messages:
+        parts.append(f"<|start_header_id|>{m.get('role', 'user')}<|end_header_id|>\n\n{m.get('content', '')}<|eot_id|>")
+    parts.append("<|start_header_id|>assistant<|end_header_id|>\n\n")
+    return "".join(parts)
+
+
+def get_tokenizer(path: str, vocab_size: int, bos_token_id: int, eos_token_id: int):
+    if path:
+        if os.path.isdir(path):
+            path = os.path.join(path, "tokenizer.json")
+        return HFTokenizer(path, bos_token_id, eos_token_id)
+    return ByteTokenizer(vocab_size, bos_token_id, eos_token_id, offset=3 if bos_token_id < 3 else 0)

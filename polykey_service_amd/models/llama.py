@@ -1,0 +1,206 @@
+"""Llama-3 family decoder (8B / 70B; also the attention half of Mixtral), TP-aware.
+
+Per layer on one rank (TP degree ``tp``; shapes for 8B TP1 / 70B TP8 in SURVEY.md §2.3):
+
+    x, res = fused_add_rmsnorm(x, res)                       HIP  (csrc/kernels/norm_act.hip)
+    qkv    = x @ Wqkv^T          column-parallel by heads     hipBLASLt
+    rope_and_cache(qkv)          rotate q,k in place, write paged K / V^T cache   HIP
+    a      = paged_attention(q)  decode split-K / varlen causal prefill          HIP (MFMA)
+    o      = a @ Wo^T            row-parallel → all-reduce (RCCL over xGMI)
+    x, res = fused_add_rmsnorm(o, res)                       HIP
+    h      = silu_and_mul(x @ Wgu^T)                         hipBLASLt + HIP
+    x      = h @ Wdown^T         row-parallel → all-reduce
+
+Fused projections (q|k|v, gate|up) halve the GEMM launches of a decode step; the residual
+stream stays bf16 and is updated in place by the fused norm.  Vocab-parallel embedding and
+LM head for TP>1 (logits all-gathered for sampling).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .. import ops
+from ..ops import attention as attn_ops
+from ..ops import reference
+from ..parallel import comm
+from ..parallel.state import ParallelState, get_state
+from .config import ModelConfig
+from .weights import SafetensorsIndex, random_full, shard_cols, shard_rows
+
+
+def _p(t: torch.Tensor) -> nn.Parameter:
+    return nn.Parameter(t, requires_grad=False)
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, cfg: ModelConfig, st: ParallelState):
+        super().__init__()
+        self.hd = cfg.head_dim
+        self.nq = cfg.num_heads // st.tp_size
+        self.nkv = cfg.num_kv_heads // st.tp_size
+        assert self.nkv >= 1, "tp larger than the number of KV heads is not supported"
+        self.scale = 1.0 / math.sqrt(self.hd)
+        self.qkv = None
+        self.o = None
+
+    def forward(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
+                kv: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
+        T = x.shape[0]
+        qkv = F.linear(x, self.qkv)
+        k_cache, v_cache = kv
+        attn_ops.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq, self.nkv, self.hd)
+        q = qkv.view(T, self.nq + 2 * self.nkv, self.hd)[:, :self.nq]
+        a = attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
+        return comm.tp_all_reduce(F.linear(a, self.o))
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.gate_up = None
+        self.down = None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = ops.silu_and_mul(F.linear(x, self.gate_up))
+        return comm.tp_all_reduce(F.linear(h, self.down))
+
+
+class LlamaLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, st: ParallelState, mlp: nn.Module):
+        super().__init__()
+        self.attn = LlamaAttention(cfg, st)
+        self.mlp = mlp
+        self.ln1 = None
+        self.ln2 = None
+        self.eps = cfg.rms_eps
+
+
+class LlamaForCausalLM(nn.Module):
+    """Dense Llama; :class:`~polykey_service_amd.models.mixtral.MixtralForCausalLM` swaps the MLP."""
+
+    def __init__(self, cfg: ModelConfig, st: Optional[ParallelState] = None, dtype=torch.bfloat16,
+                 device: Optional[torch.device] = None):
+        super().__init__()
+        self.cfg = cfg
+        self.st = st or get_state()
+        self.dtype = dtype
+        self.device = device or self.st.device
+        tp = self.st.tp_size
+        assert cfg.num_heads % tp == 0 and cfg.num_kv_heads % tp == 0 and cfg.intermediate_size % tp == 0
+        self.vocab_local = (cfg.vocab_size + tp - 1) // tp
+        self.vocab_start = self.st.tp_rank * self.vocab_local
+        self.layers = nn.ModuleList([LlamaLayer(cfg, self.st, self._make_mlp(i)) for i in range(cfg.num_layers)])
+        self.embed = None
+        self.norm = None
+        self.lm_head = None
+        self.register_buffer("cos_sin", reference.rope_cos_sin_cache(cfg.max_position, cfg.head_dim, cfg.rope_theta,
+                                                                      cfg.rope_scaling, device=self.device),
+                             persistent=False)
+
+    def _make_mlp(self, layer: int) -> nn.Module:
+        return LlamaMLP()
+
+    # ------------------------------------------------------------------ weights
+    def _vocab_pad(self, t: torch.Tensor) -> torch.Tensor:
+        tp = self.st.tp_size
+        pad = self.vocab_local * tp - t.shape[0]
+        return torch.cat([t, t.new_zeros((pad,) + t.shape[1:])]) if pad else t
+
+    def init_random(self, seed: int = 0) -> "LlamaForCausalLM":
+        cfg, st, dev, dt = self.cfg, self.st, self.device, self.dtype
+        H, hd, std = cfg.hidden_size, cfg.head_dim, cfg.init_std
+        tp, r = st.tp_size, st.tp_rank
+        rnd = lambda name, shape: random_full(name, shape, std, seed, dev, dt)
+        self.embed = _p(shard_rows(self._vocab_pad(rnd("embed", (cfg.vocab_size, H))), r, tp).contiguous())
+        self.norm = _p(torch.ones(H, dtype=dt, device=dev))
+        if cfg.tie_embeddings:
+            self.lm_head = self.embed
+        else:
+            self.lm_head = _p(shard_rows(self._vocab_pad(rnd("lm_head", (cfg.vocab_size, H))), r, tp).contiguous())
+        for i, layer in enumerate(self.layers):
+            q = rnd(f"l{i}.q", (cfg.num_heads * hd, H))
+            k = rnd(f"l{i}.k", (cfg.num_kv_heads * hd, H))
+            v = rnd(f"l{i}.v", (cfg.num_kv_heads * hd, H))
+            layer.attn.qkv = _p(torch.cat([shard_rows(q, r, tp), shard_rows(k, r, tp), shard_rows(v, r, tp)]).contiguous())
+            del q, k, v
+            layer.attn.o = _p(shard_cols(rnd(f"l{i}.o", (H, cfg.num_heads * hd)), r, tp).contiguous())
+            layer.ln1 = _p(torch.ones(H, dtype=dt, device=dev))
+            layer.ln2 = _p(torch.ones(H, dtype=dt, device=dev))
+            self._init_mlp_random(i, layer.mlp, rnd)
+        return self
+
+    def _init_mlp_random(self, i: int, mlp: nn.Module, rnd) -> None:
+        cfg, tp, r = self.cfg, self.st.tp_size, self.st.tp_rank
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        g = shard_rows(rnd(f"l{i}.gate", (I, H)), r, tp)
+        u = shard_rows(rnd(f"l{i}.up", (I, H)), r, tp)
+        mlp.gate_up = _p(torch.cat([g, u]).contiguous())
+        mlp.down = _p(shard_cols(rnd(f"l{i}.down", (H, I)), r, tp).contiguous())
+
+    def load_hf(self, path: str) -> "LlamaForCausalLM":
+        idx = SafetensorsIndex(path)
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        tp, r = self.st.tp_size, self.st.tp_rank
+        get = lambda n: idx.get(n).to(device=dev, dtype=dt)
+        self.embed = _p(shard_rows(self._vocab_pad(get("model.embed_tokens.weight")), r, tp).contiguous())
+        self.norm = _p(get("model.norm.weight"))
+        if idx.has("lm_head.weight") and not cfg.tie_embeddings:
+            self.lm_head = _p(shard_rows(self._vocab_pad(get("lm_head.weight")), r, tp).contiguous())
+        else:
+            self.lm_head = self.embed
+        for i, layer in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            q, k, v = (shard_rows(get(p + f"self_attn.{n}_proj.weight"), r, tp) for n in "qkv")
+            layer.attn.qkv = _p(torch.cat([q, k, v]).contiguous())
+            layer.attn.o = _p(shard_cols(get(p + "self_attn.o_proj.weight"), r, tp).contiguous())
+            layer.ln1 = _p(get(p + "input_layernorm.weight"))
+            layer.ln2 = _p(get(p + "post_attention_layernorm.weight"))
+            self._load_mlp_hf(i, layer.mlp, get, p)
+        return self
+
+    def _load_mlp_hf(self, i, mlp, get, p) -> None:
+        tp, r = self.st.tp_size, self.st.tp_rank
+        g = shard_rows(get(p + "mlp.gate_proj.weight"), r, tp)
+        u = shard_rows(get(p + "mlp.up_proj.weight"), r, tp)
+        mlp.gate_up = _p(torch.cat([g, u]).contiguous())
+        mlp.down = _p(shard_cols(get(p + "mlp.down_proj.weight"), r, tp).contiguous())
+
+    # ------------------------------------------------------------------ forward
+    def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
+        if self.st.tp_size == 1:
+            return F.embedding(ids, self.embed)
+        local = ids - self.vocab_start
+        mask = (local >= 0) & (local < self.vocab_local)
+        x = F.embedding(torch.where(mask, local, torch.zeros_like(local)), self.embed)
+        x = x * mask.unsqueeze(-1).to(x.dtype)
+        return comm.tp_all_reduce(x)
+
+    def forward(self, input_ids: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata,
+                kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        """Returns the final-normed hidden states [T, H]."""
+        x = self.embed_tokens(input_ids)
+        residual = None
+        for i, layer in enumerate(self.layers):
+            if residual is None:
+                residual = x
+                x = ops.rms_norm(x, layer.ln1, layer.eps)
+            else:
+                x, residual = ops.fused_add_rms_norm(x, residual, layer.ln1, layer.eps)
+            x = layer.attn(x, positions, md, self.cos_sin, kv_caches[i])
+            x, residual = ops.fused_add_rms_norm(x, residual, layer.ln2, layer.eps)
+            x = layer.mlp(x)
+        x, _ = ops.fused_add_rms_norm(x, residual, self.norm, self.cfg.rms_eps)
+        return x
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """hidden [B, H] → logits [B, vocab] (bf16; all-gathered across TP)."""
+        logits = F.linear(hidden, self.lm_head)
+        logits = comm.tp_all_gather_last(logits)
+        if logits.shape[-1] != self.cfg.vocab_size:
+            logits = logits[..., :self.cfg.vocab_size]
+        return logits

@@ -1,0 +1,99 @@
+"""Process-group bootstrap: one process per GPU, ``torch.distributed`` over RCCL ("nccl"
+on ROCm) between GPUs of one node, gloo for CPU tests and for the CPU-side control plane.
+
+Layout of a job with ``world`` ranks and tensor-parallel degree ``tp``:
+``dp = world // tp`` independent replicas (request-level data parallel, SURVEY.md §2.3 "DP"),
+each a TP group of consecutive ranks (``[r*tp, (r+1)*tp)``) so a TP group stays inside one
+xGMI-connected node.  Expert parallelism reuses the TP group (Mixtral EP=8 with attention
+TP=8, SURVEY.md §2.3 "EP").
+"""
+from __future__ import annotations
+
+import dataclasses
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclasses.dataclass
+class ParallelState:
+    world_size: int = 1
+    rank: int = 0
+    local_rank: int = 0
+    tp_size: int = 1
+    tp_rank: int = 0
+    dp_size: int = 1
+    dp_rank: int = 0
+    ep_size: int = 1
+    ep_rank: int = 0
+    tp_group: Optional[object] = None      # device collectives (RCCL / gloo on CPU)
+    tp_cpu_group: Optional[object] = None  # gloo: control-plane broadcast of step metadata
+    backend: str = "none"
+    device: torch.device = dataclasses.field(default_factory=lambda: torch.device("cpu"))
+
+    @property
+    def is_tp_leader(self) -> bool:
+        return self.tp_rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_STATE = ParallelState()
+
+
+def get_state() -> ParallelState:
+    return _STATE
+
+
+def set_state(st: ParallelState) -> None:
+    global _STATE
+    _STATE = st
+
+
+def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backend: Optional[str] = None,
+                  timeout_s: float = 600.0) -> ParallelState:
+    """Initialise from torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).
+    Without WORLD_SIZE (or WORLD_SIZE=1) returns a single-process state and creates no group."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device is None:
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    dev = torch.device(f"cuda:{local}") if device == "cuda" else torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    if world % tp:
+        raise ValueError(f"world size {world} not divisible by tp={tp}")
+    if ep not in (1, tp):
+        raise ValueError("expert parallelism must be 1 or equal to tp (EP reuses the TP group)")
+    st = ParallelState(world_size=world, rank=rank, local_rank=local, tp_size=tp, tp_rank=rank % tp,
+                       dp_size=world // tp, dp_rank=rank // tp, ep_size=ep, ep_rank=(rank % tp) if ep > 1 else 0,
+                       device=dev)
+    if world > 1:
+        be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not dist.is_initialized():
+            kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
+            if be == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+        st.backend = be
+        for r in range(world // tp):
+            ranks = list(range(r * tp, (r + 1) * tp))
+            g = dist.new_group(ranks) if tp < world else dist.group.WORLD
+            gc = dist.new_group(ranks, backend="gloo") if be != "gloo" else g
+            if rank in ranks:
+                st.tp_group, st.tp_cpu_group = g, gc
+    set_state(st)
+    return st
+
+
+def destroy_parallel() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    set_state(ParallelState())

@@ -92,6 +92,11 @@ class ToolRouter:
             return models[model]
         return None
 
+    async def aclose(self) -> None:
+        llm = getattr(self, "llm", None)
+        if llm is not None:
+            await llm.aclose()
+
     # ----------------------------------------------------------------- execution
     def _prepare(self, tool_name, parameters, secret_id, metadata):
         params = proto.struct_to_dict(parameters) if parameters is not None else {}

@@ -1,0 +1,136 @@
+"""Paged decode / prefill attention and fused RoPE+cache kernels vs fp32 references."""
+import math
+
+import pytest
+import torch
+
+from polykey_service_amd.ops import attention as A
+from polykey_service_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+HD = 128
+
+
+def make_cache(num_blocks, nkv, bs, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    k = torch.randn(num_blocks, nkv, bs, HD, generator=g).to(torch.bfloat16)
+    v = torch.randn(num_blocks, nkv, HD, bs, generator=g).to(torch.bfloat16)
+    return k, v
+
+
+def block_tables_for(ctxs, bs, num_blocks, max_blocks, seed=0):
+    g = torch.Generator().manual_seed(seed + 7)
+    perm = torch.randperm(num_blocks, generator=g).tolist()
+    bt = torch.zeros(len(ctxs), max_blocks, dtype=torch.int32)
+    i = 0
+    for s, c in enumerate(ctxs):
+        nb = (c + bs - 1) // bs
+        bt[s, :nb] = torch.tensor(perm[i:i + nb], dtype=torch.int32)
+        i += nb
+    return bt
+
+
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 32), (32, 8, 16), (4, 4, 32), (16, 1, 64)])
+@pytest.mark.parametrize("ctxs", [[1, 5, 32, 33, 100], [512, 513, 1200, 7], [2048, 1]])
+def test_decode(nq, nkv, bs, ctxs):
+    max_blocks = (max(ctxs) + bs - 1) // bs + 3
+    nb = sum((c + bs - 1) // bs for c in ctxs) + 4
+    kc, vc = make_cache(nb, nkv, bs)
+    bt = block_tables_for(ctxs, bs, nb, max_blocks)
+    B = len(ctxs)
+    qkv = torch.randn(B, (nq + 2 * nkv) * HD).to(torch.bfloat16)
+    q = qkv.view(B, nq + 2 * nkv, HD)[:, :nq]
+    cl = torch.tensor(ctxs, dtype=torch.int32)
+    scale = 1 / math.sqrt(HD)
+    exp = ref.paged_attention(q.contiguous(), kc, vc, bt, cl, torch.arange(B + 1, dtype=torch.int32), scale)
+    d = "cuda"
+    qkv_d = qkv.to(d)
+    q_d = qkv_d.view(B, nq + 2 * nkv, HD)[:, :nq]
+    po, pml = A.decode_workspace(B, nq, max_blocks, bs, d)
+    md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0,
+                        slot_mapping=torch.zeros(B, dtype=torch.int32, device=d),
+                        decode_block_tables=bt.to(d), decode_context_lens=cl.to(d), decode_part_o=po, decode_part_ml=pml)
+    out = A.paged_attention(q_d, kc.to(d), vc.to(d), md, scale)
+    torch.testing.assert_close(out.cpu().view(B, nq, HD).float(), exp.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_decode_zero_context_rows_are_zero():
+    nq, nkv, bs = 8, 2, 32
+    kc, vc = make_cache(8, nkv, bs)
+    bt = torch.zeros(3, 4, dtype=torch.int32)
+    cl = torch.tensor([0, 40, 0], dtype=torch.int32)
+    bt[1, :2] = torch.tensor([3, 5])
+    q = torch.randn(3, nq, HD).to(torch.bfloat16)
+    md = A.AttnMetadata(3, 0, 0, 0, torch.zeros(3, dtype=torch.int32, device="cuda"), bt.cuda(), cl.cuda())
+    out = A.paged_attention(q.cuda(), kc.cuda(), vc.cuda(), md, 0.1).cpu().view(3, nq, HD)
+    assert torch.all(out[0] == 0) and torch.all(out[2] == 0)
+    exp = ref.paged_attention(q[1:2], kc, vc, bt[1:2], cl[1:2], torch.tensor([0, 1], dtype=torch.int32), 0.1)
+    torch.testing.assert_close(out[1:2].float(), exp.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 32), (4, 1, 16), (16, 1, 32)])
+@pytest.mark.parametrize("qlens,ctxs", [([7, 16, 33], [7, 16, 33]), ([1, 20, 64], [100, 20, 300]),
+                                        ([130], [130]), ([5, 1], [70, 1])])
+def test_prefill_with_prefix(nq, nkv, bs, qlens, ctxs):
+    max_blocks = (max(ctxs) + bs - 1) // bs
+    nb = sum((c + bs - 1) // bs for c in ctxs) + 2
+    kc, vc = make_cache(nb, nkv, bs, seed=3)
+    bt = block_tables_for(ctxs, bs, nb, max_blocks, seed=3)
+    T = sum(qlens)
+    qkv = torch.randn(T, (nq + 2 * nkv) * HD).to(torch.bfloat16)
+    q = qkv.view(T, nq + 2 * nkv, HD)[:, :nq]
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32)
+    cl = torch.tensor(ctxs, dtype=torch.int32)
+    scale = 1 / math.sqrt(HD)
+    exp = ref.paged_attention(q.contiguous(), kc, vc, bt, cl, cu, scale)
+    d = "cuda"
+    md = A.AttnMetadata(0, len(qlens), T, max(qlens), torch.zeros(T, dtype=torch.int32, device=d),
+                        prefill_block_tables=bt.to(d), prefill_context_lens=cl.to(d), prefill_cu_q=cu.to(d))
+    qkv_d = qkv.to(d)
+    out = A.paged_attention(qkv_d.view(T, nq + 2 * nkv, HD)[:, :nq], kc.to(d), vc.to(d), md, scale)
+    torch.testing.assert_close(out.cpu().view(T, nq, HD).float(), exp.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_mixed_decode_and_prefill():
+    nq, nkv, bs = 16, 4, 32
+    dctx, qlens, pctx = [40, 600], [9, 30], [9, 75]
+    ctxs = dctx + pctx
+    max_blocks = 24
+    nb = 64
+    kc, vc = make_cache(nb, nkv, bs, seed=5)
+    bt = block_tables_for(ctxs, bs, nb, max_blocks, seed=5)
+    T = 2 + sum(qlens)
+    q = torch.randn(T, nq, HD).to(torch.bfloat16)
+    scale = 0.09
+    cu = torch.tensor([0, 9, 39], dtype=torch.int32)
+    exp_d = ref.paged_attention(q[:2], kc, vc, bt[:2], torch.tensor(dctx), torch.arange(3, dtype=torch.int32), scale)
+    exp_p = ref.paged_attention(q[2:], kc, vc, bt[2:], torch.tensor(pctx), cu, scale)
+    d = "cuda"
+    po, pml = A.decode_workspace(2, nq, max_blocks, bs, d)
+    md = A.AttnMetadata(2, 2, sum(qlens), 30, torch.zeros(T, dtype=torch.int32, device=d),
+                        bt[:2].to(d), torch.tensor(dctx, dtype=torch.int32, device=d), bt[2:].to(d),
+                        torch.tensor(pctx, dtype=torch.int32, device=d), cu.to(d), po, pml)
+    out = A.paged_attention(q.to(d), kc.to(d), vc.to(d), md, scale).cpu().view(T, nq, HD)
+    torch.testing.assert_close(out[:2].float(), exp_d.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(out[2:].float(), exp_p.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 16), (4, 2, 64)])
+def test_rope_and_cache(nq, nkv, bs):
+    T = 37
+    qkv = torch.randn(T, (nq + 2 * nkv) * HD).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32)
+    cs = ref.rope_cos_sin_cache(4096, HD, 500000.0)
+    nb = 8 + T // bs * 2
+    slots = torch.randperm(nb * bs)[:T].to(torch.int32)
+    slots[3] = -1
+    kc = torch.zeros(nb, nkv, bs, HD, dtype=torch.bfloat16)
+    vc = torch.zeros(nb, nkv, HD, bs, dtype=torch.bfloat16)
+    qkv_r, kc_r, vc_r = qkv.clone(), kc.clone(), vc.clone()
+    ref.rope_and_cache(qkv_r, pos, cs, kc_r, vc_r, slots, nq, nkv, HD)
+    d = "cuda"
+    qkv_d, kc_d, vc_d = qkv.to(d), kc.to(d), vc.to(d)
+    A.rope_and_cache(qkv_d, pos.to(d), cs.to(d), kc_d, vc_d, slots.to(d), nq, nkv, HD)
+    torch.testing.assert_close(qkv_d.cpu().float(), qkv_r.float(), atol=1.6e-2, rtol=1e-2)
+    torch.testing.assert_close(kc_d.cpu().float(), kc_r.float(), atol=1.6e-2, rtol=1e-2)
+    assert torch.equal(vc_d.cpu(), vc_r)

@@ -1,0 +1,67 @@
+"""Sampler kernel: greedy exact, RNG bit-exact vs reference, survivors within the top-k/top-p set."""
+import numpy as np
+import pytest
+import torch
+
+from polykey_service_amd.ops import reference as ref
+from polykey_service_amd.ops import sampler
+
+pytestmark = pytest.mark.gpu
+
+
+def params(B, temp=0.0, k=0, p=1.0, mp=0.0, seed=0, off=0, device="cuda"):
+    f = lambda v, dt: torch.full((B,), v, dtype=dt, device=device)
+    return (f(temp, torch.float32), f(k, torch.int32), f(p, torch.float32), f(mp, torch.float32),
+            torch.arange(B, dtype=torch.int32, device=device) + seed, f(off, torch.int32))
+
+
+@pytest.mark.parametrize("V,dtype", [(128256, torch.bfloat16), (32000, torch.float32), (1024, torch.bfloat16)])
+def test_greedy(V, dtype):
+    x = torch.randn(64, V, device="cuda").to(dtype)
+    x[5, 17] = 100.0
+    x[6, :] = 1.0  # ties → lowest index
+    out = sampler.sample(x, *params(64))
+    exp = torch.argmax(x.float(), -1)
+    exp[6] = 0
+    assert torch.equal(out.long().cpu(), exp.cpu())
+    assert torch.equal(sampler.greedy(x).long().cpu(), exp.cpu())
+
+
+def test_top_k_1_is_greedy_and_rng_matches_reference():
+    V, B = 4096, 16
+    x = torch.randn(B, V, device="cuda") * 3
+    out = sampler.sample(x, *params(B, temp=1.0, k=1))
+    assert torch.equal(out.long().cpu(), torch.argmax(x, -1).cpu())
+    # plain temperature sampling: bit-exact RNG → identical tokens (up to fp rounding ties)
+    t, k, p, mp, seeds, offs = params(B, temp=0.8, off=11)
+    out = sampler.sample(x, t, k, p, mp, seeds, offs).long().cpu()
+    exp = ref.sample(x.cpu(), t.cpu(), k.cpu(), p.cpu(), mp.cpu(), seeds.cpu(), offs.cpu())
+    assert (out == exp).float().mean() >= 0.9
+
+
+@pytest.mark.parametrize("k,p,mp", [(50, 1.0, 0.0), (0, 0.9, 0.0), (40, 0.5, 0.0), (0, 1.0, 0.1), (7, 0.95, 0.05)])
+def test_survivor_sets(k, p, mp):
+    V, B = 32000, 8
+    torch.manual_seed(0)
+    x = torch.randn(B, V, device="cuda") * 2
+    for trial in range(20):
+        t, kk, pp, mpp, seeds, offs = params(B, temp=0.7, k=k, p=p, mp=mp, seed=trial * 100, off=trial)
+        out = sampler.sample(x, t, kk, pp, mpp, seeds, offs).long().cpu()
+        for b in range(B):
+            allowed = ref.sampling_mask(x[b:b + 1].cpu(), 0.7, k, p, mp)[0]
+            assert allowed[out[b]], (b, k, p, mp)
+
+
+def test_distribution_chi2():
+    V = 8
+    logits = torch.tensor([[2.0, 1.0, 0.5, 0.0, -1.0, -2.0, 0.3, 1.5]], device="cuda").repeat(4096, 1)
+    B = logits.shape[0]
+    t, k, p, mp, seeds, offs = params(B, temp=1.0)
+    counts = np.zeros(V)
+    for it in range(4):
+        out = sampler.sample(logits, t, k, p, mp, seeds + it * B, offs).cpu().numpy()
+        counts += np.bincount(out, minlength=V)
+    probs = torch.softmax(logits[0].cpu(), -1).numpy()
+    expct = probs * counts.sum()
+    chi2 = ((counts - expct) ** 2 / expct).sum()
+    assert chi2 < 30, (chi2, counts, expct)  # 7 dof, p≈1e-4
