@@ -1,0 +1,178 @@
+"""OpenAI-compatible HTTP route (config 4 of BASELINE.json: "70B TP=8, OpenAI-compatible chat
+route").  No reference counterpart (no HTTP/OpenAI route in polykey).
+
+Endpoints: ``POST /v1/chat/completions`` and ``POST /v1/completions`` (``stream: true`` →
+server-sent events ending with ``data: [DONE]``), ``GET /v1/models``, ``GET /health``.
+Requests are served by the same :class:`ToolRouter` model tools as gRPC, so both fronts share
+one continuous-batching engine; ``model`` selects the backend like ``llm.chat:<model>``.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import time
+import uuid
+from typing import Any, Dict, List, Optional
+
+from ..engine.sequence import SamplingParams
+from ..service.base import ToolError
+
+_SAMPLING_KEYS = ("max_tokens", "temperature", "top_p", "top_k", "min_p", "seed", "stop", "ignore_eos",
+                  "stop_token_ids")
+
+
+def _llm(router, model: Optional[str]):
+    llm = getattr(router, "llm", None)
+    if llm is None:
+        raise ToolError("UNAVAILABLE", "no local LLM backend attached")
+    models = router.models("llm.chat")
+    if model and models and model not in models:
+        raise ToolError("NOT_FOUND", f"model {model!r} not served; available: {models}")
+    return llm, (model or (models[0] if models else "model"))
+
+
+def _params(body: Dict[str, Any]) -> SamplingParams:
+    d = {k: body[k] for k in _SAMPLING_KEYS if k in body and body[k] is not None}
+    if "max_completion_tokens" in body and "max_tokens" not in d:
+        d["max_tokens"] = body["max_completion_tokens"]
+    d.setdefault("max_tokens", 256)
+    d.setdefault("temperature", 1.0)
+    sp = SamplingParams.from_dict(d)
+    sp.validate(1 << 30)
+    return sp
+
+
+def create_app(router):
+    from fastapi import FastAPI, Request
+    from fastapi.responses import JSONResponse, StreamingResponse
+
+    app = FastAPI(title="polykey OpenAI-compatible API")
+
+    def err(status: int, msg: str, typ: str = "invalid_request_error"):
+        return JSONResponse({"error": {"message": msg, "type": typ}}, status_code=status)
+
+    @app.get("/health")
+    async def health():
+        llm = getattr(router, "llm", None)
+        ok = llm is None or llm.healthy()
+        return JSONResponse({"status": "ok" if ok else "unhealthy"}, status_code=200 if ok else 503)
+
+    @app.get("/v1/models")
+    async def models():
+        now = int(time.time())
+        return {"object": "list", "data": [{"id": m, "object": "model", "created": now, "owned_by": "polykey"}
+                                           for m in router.models("llm.chat")]}
+
+    async def _run(body: Dict[str, Any], chat: bool):
+        try:
+            llm, model = _llm(router, body.get("model"))
+            sp = _params(body)
+        except ToolError as e:
+            return err(404 if e.code == "NOT_FOUND" else 503, e.message)
+        except (ValueError, TypeError) as e:
+            return err(400, str(e))
+        tok = llm.tokenizer
+        if chat:
+            msgs = body.get("messages")
+            if not isinstance(msgs, list) or not msgs:
+                return err(400, "'messages' must be a non-empty list")
+            prompt_ids = tok.encode(tok.apply_chat_template(msgs))
+        else:
+            p = body.get("prompt")
+            if isinstance(p, list) and p and isinstance(p[0], int):
+                prompt_ids = [int(x) for x in p]
+            elif isinstance(p, str) and p:
+                prompt_ids = tok.encode(p)
+            else:
+                return err(400, "'prompt' must be a non-empty string or token id list")
+        rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex[:24]
+        created = int(time.time())
+        obj = "chat.completion" if chat else "text_completion"
+
+        if body.get("stream"):
+            async def sse():
+                toks: List[int] = []
+                sent = 0
+                finish = None
+                if chat:
+                    first = {"id": rid, "object": "chat.completion.chunk", "created": created, "model": model,
+                             "choices": [{"index": 0, "delta": {"role": "assistant"}, "finish_reason": None}]}
+                    yield f"data: {json.dumps(first)}\n\n"
+                agen = llm.generate(prompt_ids, sp, request_id=rid)
+                try:
+                    async for out in agen:
+                        toks.extend(out.new_token_ids)
+                        finish = out.finish_reason
+                        text = tok.decode(toks)
+                        if len(text) > sent and not text.endswith("�"):
+                            delta = text[sent:]
+                            sent = len(text)
+                            choice = ({"index": 0, "delta": {"content": delta}, "finish_reason": None} if chat
+                                      else {"index": 0, "text": delta, "finish_reason": None})
+                            ch = {"id": rid, "object": obj + (".chunk" if chat else ""), "created": created,
+                                  "model": model, "choices": [choice]}
+                            yield f"data: {json.dumps(ch)}\n\n"
+                finally:
+                    await agen.aclose()
+                last_choice = ({"index": 0, "delta": {}, "finish_reason": finish} if chat
+                               else {"index": 0, "text": "", "finish_reason": finish})
+                last = {"id": rid, "object": obj + (".chunk" if chat else ""), "created": created, "model": model,
+                        "choices": [last_choice],
+                        "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": len(toks),
+                                  "total_tokens": len(prompt_ids) + len(toks)}}
+                yield f"data: {json.dumps(last)}\n\n"
+                yield "data: [DONE]\n\n"
+
+            return StreamingResponse(sse(), media_type="text/event-stream")
+
+        toks, last = await llm.generate_all(prompt_ids, sp, request_id=rid)
+        text = tok.decode(toks)
+        if sp.stop:
+            cuts = [text.find(s) for s in sp.stop if text.find(s) >= 0]
+            if cuts:
+                text = text[:min(cuts)]
+        choice = ({"index": 0, "message": {"role": "assistant", "content": text},
+                   "finish_reason": last.finish_reason if last else None} if chat
+                  else {"index": 0, "text": text, "finish_reason": last.finish_reason if last else None})
+        return {"id": rid, "object": obj, "created": created, "model": model, "choices": [choice],
+                "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": len(toks),
+                          "total_tokens": len(prompt_ids) + len(toks)}}
+
+    @app.post("/v1/chat/completions")
+    async def chat_completions(request: Request):
+        try:
+            body = await request.json()
+        except json.JSONDecodeError:
+            return err(400, "invalid JSON")
+        return await _run(body, chat=True)
+
+    @app.post("/v1/completions")
+    async def completions(request: Request):
+        try:
+            body = await request.json()
+        except json.JSONDecodeError:
+            return err(400, "invalid JSON")
+        return await _run(body, chat=False)
+
+    return app
+
+
+class _HttpHandle:
+    def __init__(self, server, task):
+        self.server = server
+        self.task = task
+
+    async def shutdown(self):
+        self.server.should_exit = True
+        await self.task
+
+
+async def serve_openai(router, addr: str, logger):
+    import uvicorn
+    host, _, port = addr.rpartition(":")
+    cfg = uvicorn.Config(create_app(router), host=host or "0.0.0.0", port=int(port), log_level="warning",
+                         lifespan="off")
+    server = uvicorn.Server(cfg)
+    task = asyncio.create_task(server.serve())
+    logger.info("openai route listening", address=addr)
+    return _HttpHandle(server, task)
