@@ -94,6 +94,23 @@ __global__ void __launch_bounds__(256) silu_and_mul_kernel(bf16_t* __restrict__ 
   reinterpret_cast<u32x4*>(out + static_cast<int64_t>(row) * I)[c] = pack8(y);
 }
 
+// in: [T, 2*I] with gate/up interleaved in blocks of 16 columns, out: [T, I].
+// Each lane handles 8 outputs (half a 16-block): gate at 32*b + h*8, up at 32*b + 16 + h*8.
+__global__ void __launch_bounds__(256) silu_and_mul_il_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ in,
+                                                              int I) {
+  const int row = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;  // output vector index (8 columns)
+  if (c * 8 >= I) return;
+  const int b = c >> 1, h = c & 1;
+  const bf16_t* base = in + static_cast<int64_t>(row) * 2 * I + 32 * b + 8 * h;
+  float a[8], u[8], y[8];
+  unpack8(*reinterpret_cast<const u32x4*>(base), a);
+  unpack8(*reinterpret_cast<const u32x4*>(base + 16), u);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) y[j] = bf2f(f2bf(silu(a[j]))) * u[j];
+  reinterpret_cast<u32x4*>(out + static_cast<int64_t>(row) * I)[c] = pack8(y);
+}
+
 int pick_vpt(int H, int* threads) {
   const int vecs = H / 8;
   for (int vpt : {1, 2, 4, 8}) {
@@ -150,6 +167,15 @@ PK_EXPORT int pk_silu_and_mul(void* out, const void* in, int T, int I, hipStream
   const int vecs = I / 8;
   dim3 grid((vecs + 255) / 256, T);
   silu_and_mul_kernel<<<grid, 256, 0, stream>>>(static_cast<bf16_t*>(out), static_cast<const bf16_t*>(in), I);
+  return PK_CHECK_LAUNCH();
+}
+
+PK_EXPORT int pk_silu_and_mul_il(void* out, const void* in, int T, int I, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (I % 16) return -1;
+  const int vecs = I / 8;
+  dim3 grid((vecs + 255) / 256, T);
+  silu_and_mul_il_kernel<<<grid, 256, 0, stream>>>(static_cast<bf16_t*>(out), static_cast<const bf16_t*>(in), I);
   return PK_CHECK_LAUNCH();
 }
 

@@ -91,6 +91,8 @@ class ModelRunner:
         self.part_o, self.part_ml = attn_ops.decode_workspace(cfg.max_num_seqs, nq_local, self.max_blocks, self.bs,
                                                               device)
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0}
+        self.keep_logits = False  # tests: keep the last eager step's logits
+        self.last_logits = None
 
     # ---------------------------------------------------------------- KV cache
     def kv_bytes_per_block(self) -> int:
@@ -241,6 +243,8 @@ class ModelRunner:
             return None
         rows = hidden if ns == T else hidden.index_select(0, d["sample_idx"][:ns].long())
         logits = self.model.compute_logits(rows)
+        if self.keep_logits:
+            self.last_logits = logits
         return sampler_ops.sample(logits, d["temperature"][:ns], d["top_k"][:ns], d["top_p"][:ns],
                                   d["min_p"][:ns], d["seeds"][:ns], d["offsets"][:ns])
 

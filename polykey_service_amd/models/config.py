@@ -67,7 +67,7 @@ PRESETS: Dict[str, ModelConfig] = {
                               bos_token_id=1, eos_token_id=2),
     "tiny-llama-gqa4": ModelConfig("tiny-llama-gqa4", 1024, 1024, 2048, 2, 8, 2, max_position=2048,
                                    init_std=0.05, bos_token_id=1, eos_token_id=2),
-    "tiny-mixtral": ModelConfig("tiny-mixtral", 1024, 512, 768, 2, 4, 1, rope_theta=1e6, max_position=2048,
+    "tiny-mixtral": ModelConfig("tiny-mixtral", 1024, 512, 768, 2, 8, 2, rope_theta=1e6, max_position=2048,
                                 num_experts=4, experts_per_token=2, init_std=0.05, bos_token_id=1,
                                 eos_token_id=2),
     "small-llama": ModelConfig("small-llama", 32000, 2048, 5632, 8, 16, 4, init_std=0.02,

@@ -26,6 +26,7 @@ from torch import nn
 
 from .. import ops
 from ..ops import attention as attn_ops
+from ..ops import gemm
 from ..ops import reference
 from ..parallel import comm
 from ..parallel.state import ParallelState, get_state
@@ -35,6 +36,32 @@ from .weights import SafetensorsIndex, random_full, shard_cols, shard_rows
 
 def _p(t: torch.Tensor) -> nn.Parameter:
     return nn.Parameter(t, requires_grad=False)
+
+
+def _proj(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor]) -> torch.Tensor:
+    """Column-parallel projection → bf16 (skinny split-K + reduce for decode-sized M)."""
+    if ws is not None and gemm.skinny_ok(x, w):
+        S = gemm.choose_split(w.shape[0], x.shape[1], x.shape[0])
+        if S > 1 and ws.numel() >= S * x.shape[0] * w.shape[0]:
+            return gemm.reduce_partial(gemm.linear_partial(x, w, ws, S))
+    return gemm.linear(x, w)
+
+
+def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor]):
+    """Row-parallel projection feeding a residual add + RMSNorm.  TP=1 decode returns the
+    split-K partial slabs unreduced (the norm kernel sums them); TP>1 all-reduces bf16."""
+    if get_state().tp_size == 1 and ws is not None and gemm.skinny_ok(x, w) and gemm.norm_fusable(w.shape[0]):
+        S = gemm.choose_split(w.shape[0], x.shape[1], x.shape[0])
+        if ws.numel() >= S * x.shape[0] * w.shape[0]:
+            return gemm.linear_partial(x, w, ws, S)
+    return comm.tp_all_reduce(_proj(x, w, ws))
+
+
+def add_norm(pending, residual: torch.Tensor, w: torch.Tensor, eps: float):
+    """residual += pending; x = rms_norm(residual) * w → (x, residual)."""
+    if isinstance(pending, gemm.Partial):
+        return gemm.partial_add_rms_norm(pending, residual, w, eps)
+    return ops.fused_add_rms_norm(pending, residual, w, eps)
 
 
 class LlamaAttention(nn.Module):
@@ -49,14 +76,16 @@ class LlamaAttention(nn.Module):
         self.o = None
 
     def forward(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
-                kv: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
+                kv: Tuple[torch.Tensor, torch.Tensor], ws: Optional[torch.Tensor] = None):
+        """Returns the o-projection output: a bf16 tensor, or (decode, TP=1) an unreduced
+        split-K :class:`~polykey_service_amd.ops.gemm.Partial` consumed by the next norm."""
         T = x.shape[0]
-        qkv = F.linear(x, self.qkv)
+        qkv = _proj(x, self.qkv, ws)
         k_cache, v_cache = kv
         attn_ops.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq, self.nkv, self.hd)
         q = qkv.view(T, self.nq + 2 * self.nkv, self.hd)[:, :self.nq]
         a = attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
-        return comm.tp_all_reduce(F.linear(a, self.o))
+        return _proj_out(a, self.o, ws)
 
 
 class LlamaMLP(nn.Module):
@@ -65,9 +94,9 @@ class LlamaMLP(nn.Module):
         self.gate_up = None
         self.down = None
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = ops.silu_and_mul(F.linear(x, self.gate_up))
-        return comm.tp_all_reduce(F.linear(h, self.down))
+    def forward(self, x: torch.Tensor, ws: Optional[torch.Tensor] = None):
+        h = gemm.linear_silu(x, self.gate_up, ws)  # gate/up rows interleaved in blocks of 16
+        return _proj_out(h, self.down, ws)
 
 
 class LlamaLayer(nn.Module):
@@ -139,7 +168,7 @@ class LlamaForCausalLM(nn.Module):
         H, I = cfg.hidden_size, cfg.intermediate_size
         g = shard_rows(rnd(f"l{i}.gate", (I, H)), r, tp)
         u = shard_rows(rnd(f"l{i}.up", (I, H)), r, tp)
-        mlp.gate_up = _p(torch.cat([g, u]).contiguous())
+        mlp.gate_up = _p(gemm.interleave_gate_up(g, u).contiguous())
         mlp.down = _p(shard_cols(rnd(f"l{i}.down", (H, I)), r, tp).contiguous())
 
     def load_hf(self, path: str) -> "LlamaForCausalLM":
@@ -167,7 +196,7 @@ class LlamaForCausalLM(nn.Module):
         tp, r = self.st.tp_size, self.st.tp_rank
         g = shard_rows(get(p + "mlp.gate_proj.weight"), r, tp)
         u = shard_rows(get(p + "mlp.up_proj.weight"), r, tp)
-        mlp.gate_up = _p(torch.cat([g, u]).contiguous())
+        mlp.gate_up = _p(gemm.interleave_gate_up(g, u).contiguous())
         mlp.down = _p(shard_cols(get(p + "mlp.down_proj.weight"), r, tp).contiguous())
 
     # ------------------------------------------------------------------ forward
@@ -184,21 +213,43 @@ class LlamaForCausalLM(nn.Module):
                 kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Returns the final-normed hidden states [T, H]."""
         x = self.embed_tokens(input_ids)
+        ws = self.workspace(x.shape[0])
         residual = None
         for i, layer in enumerate(self.layers):
             if residual is None:
                 residual = x
                 x = ops.rms_norm(x, layer.ln1, layer.eps)
             else:
-                x, residual = ops.fused_add_rms_norm(x, residual, layer.ln1, layer.eps)
-            x = layer.attn(x, positions, md, self.cos_sin, kv_caches[i])
-            x, residual = ops.fused_add_rms_norm(x, residual, layer.ln2, layer.eps)
-            x = layer.mlp(x)
-        x, _ = ops.fused_add_rms_norm(x, residual, self.norm, self.cfg.rms_eps)
+                x, residual = add_norm(x, residual, layer.ln1, layer.eps)
+            x = layer.attn(x, positions, md, self.cos_sin, kv_caches[i], ws)
+            x, residual = add_norm(x, residual, layer.ln2, layer.eps)
+            x = layer.mlp(x, ws)
+        x, _ = add_norm(x, residual, self.norm, self.cfg.rms_eps)
         return x
+
+    def workspace(self, M: int) -> Optional[torch.Tensor]:
+        """fp32 split-K slab buffer for decode-sized batches (fixed address: graph-safe)."""
+        if self.device.type != "cuda" or M > gemm.SKINNY_MAX_M:
+            return None
+        if getattr(self, "_ws", None) is None:
+            self._ws = torch.empty(self._workspace_elems(), dtype=torch.float32, device=self.device)
+        return self._ws
+
+    def _workspace_elems(self) -> int:
+        M = gemm.SKINNY_MAX_M
+        shapes = []
+        l0 = self.layers[0]
+        for w in (l0.attn.qkv, l0.attn.o) + self._mlp_weights(l0.mlp):
+            if w is not None:
+                shapes.append(gemm.choose_split(w.shape[0], w.shape[1], M) * M * w.shape[0])
+        return max(shapes + [1])
+
+    def _mlp_weights(self, mlp) -> tuple:
+        return (mlp.gate_up, mlp.down)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """hidden [B, H] → logits [B, vocab] (bf16; all-gathered across TP)."""
+        # hipBLASLt streams the 1 GB vocab projection faster than the skinny kernel (bench_gemm.py)
         logits = F.linear(hidden, self.lm_head)
         logits = comm.tp_all_gather_last(logits)
         if logits.shape[-1] != self.cfg.vocab_size:

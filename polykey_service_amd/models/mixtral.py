@@ -1,0 +1,86 @@
+"""Mixtral-8x7B: Llama attention + sparse top-2 MoE MLP (config 5 of BASELINE.json).
+
+Expert placement on a TP group of size ``tp``:
+
+* ``ep == 1``  — every rank holds all 8 experts with the intermediate dim sharded by ``tp``
+  (tensor-parallel experts; output all-reduced like the dense MLP);
+* ``ep == tp`` — expert parallel: rank r holds experts ``[r*E/ep, (r+1)*E/ep)`` unsharded.
+  Tokens are already replicated on every rank by the TP attention, so each rank routes all
+  tokens, computes only its local experts (a rank whose experts received no token reads no
+  expert weights at all) and the combine is one all-reduce; :mod:`..parallel.ep` has the
+  all-to-all dispatch/combine used when tokens are *not* replicated.
+
+Mixtral bf16 (~93 GB) also fits a single 288 GB MI355X (``tp = ep = 1``).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+
+from ..ops import gemm, moe
+from ..parallel import comm
+from .llama import LlamaForCausalLM, _p
+from .weights import shard_cols, shard_rows
+
+
+class MixtralMoE(nn.Module):
+    def __init__(self, num_experts: int, top_k: int, e_lo: int, e_hi: int):
+        super().__init__()
+        self.E = num_experts
+        self.k = top_k
+        self.e_lo, self.e_hi = e_lo, e_hi
+        self.router = None
+        self.w13 = None  # [E_local, 2*I_local, H], gate/up rows interleaved by 16
+        self.w2 = None   # [E_local, H, I_local]
+
+    def forward(self, x: torch.Tensor, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+        y = moe.fused_moe(x, self.router, self.w13, self.w2, self.k, self.e_lo, self.e_hi)
+        return comm.tp_all_reduce(y)
+
+
+class MixtralForCausalLM(LlamaForCausalLM):
+    def _make_mlp(self, layer: int) -> nn.Module:
+        cfg, st = self.cfg, self.st
+        ep = st.ep_size
+        per = cfg.num_experts // ep
+        e_lo = st.ep_rank * per if ep > 1 else 0
+        return MixtralMoE(cfg.num_experts, cfg.experts_per_token, e_lo, e_lo + per)
+
+    def _mlp_weights(self, mlp) -> tuple:
+        return ()
+
+    def _init_mlp_random(self, i: int, mlp: MixtralMoE, rnd) -> None:
+        cfg, st = self.cfg, self.st
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        tp_shard = st.ep_size == 1 and st.tp_size > 1
+        mlp.router = _p(rnd(f"l{i}.router", (cfg.num_experts, H)).contiguous())
+        w13, w2 = [], []
+        for e in range(mlp.e_lo, mlp.e_hi):
+            g, u, d = rnd(f"l{i}.e{e}.w1", (I, H)), rnd(f"l{i}.e{e}.w3", (I, H)), rnd(f"l{i}.e{e}.w2", (H, I))
+            if tp_shard:
+                g, u, d = shard_rows(g, st.tp_rank, st.tp_size), shard_rows(u, st.tp_rank, st.tp_size), \
+                    shard_cols(d, st.tp_rank, st.tp_size)
+            w13.append(gemm.interleave_gate_up(g, u))
+            w2.append(d.contiguous())
+        mlp.w13 = _p(torch.stack(w13).contiguous())
+        mlp.w2 = _p(torch.stack(w2).contiguous())
+
+    def _load_mlp_hf(self, i, mlp: MixtralMoE, get, p) -> None:
+        st = self.st
+        tp_shard = st.ep_size == 1 and st.tp_size > 1
+        base = p + "block_sparse_moe."
+        mlp.router = _p(get(base + "gate.weight").contiguous())
+        w13, w2 = [], []
+        for e in range(mlp.e_lo, mlp.e_hi):
+            g = get(base + f"experts.{e}.w1.weight")
+            u = get(base + f"experts.{e}.w3.weight")
+            d = get(base + f"experts.{e}.w2.weight")
+            if tp_shard:
+                g, u, d = shard_rows(g, st.tp_rank, st.tp_size), shard_rows(u, st.tp_rank, st.tp_size), \
+                    shard_cols(d, st.tp_rank, st.tp_size)
+            w13.append(gemm.interleave_gate_up(g, u))
+            w2.append(d.contiguous())
+        mlp.w13 = _p(torch.stack(w13).contiguous())
+        mlp.w2 = _p(torch.stack(w2).contiguous())

@@ -1,0 +1,145 @@
+"""Projection GEMMs: hand-written weight-streaming kernel for decode-sized M, hipBLASLt otherwise.
+
+``y = x @ W^T`` with ``W`` in PyTorch ``[N, K]`` layout.  For ``M <= 64`` on the GPU the HIP
+kernel in ``csrc/kernels/gemm_skinny.hip`` streams ``W`` once at (near) HBM rate and can
+(a) emit fp32 split-K partial slabs that the *consumer* reduces (``Partial``), or (b) apply
+SiLU(gate)*up in its epilogue when the gate/up rows are interleaved in blocks of 16
+(:func:`interleave_gate_up`).  Prefill-sized M goes to ``F.linear`` (hipBLASLt), whose tuned
+MFMA kernels are the right tool for compute-bound shapes.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import native, reference
+
+import os
+
+SKINNY_MAX_M = 64
+_TARGET_WGS = 192   # measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
+_ROWS_PER_WG = 128
+_KCHUNK = 256
+# The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see
+# tools/bench_gemm.py and profiles/); POLYKEY_SKINNY_GEMM=0/1 forces it off/on.
+SKINNY_ENABLED = os.environ.get("POLYKEY_SKINNY_GEMM", "1") == "1"
+
+
+@dataclasses.dataclass
+class Partial:
+    """fp32 split-K slabs ``buf[:S*M*N]`` viewed as [S, M, N] (not yet summed)."""
+    buf: torch.Tensor
+    S: int
+    M: int
+    N: int
+
+    def view(self) -> torch.Tensor:
+        return self.buf[: self.S * self.M * self.N].view(self.S, self.M, self.N)
+
+
+def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor, block: int = 16) -> torch.Tensor:
+    """[I, K] gate, [I, K] up → [2I, K] with rows [g0..g15, u0..u15, g16.., u16.., ...]."""
+    I, K = gate.shape
+    assert I % block == 0
+    return torch.stack([gate.view(I // block, block, K), up.view(I // block, block, K)], dim=1).reshape(2 * I, K)
+
+
+def deinterleave_gate_up(w: torch.Tensor, block: int = 16):
+    I2, K = w.shape
+    v = w.view(I2 // (2 * block), 2, block, K)
+    return v[:, 0].reshape(I2 // 2, K), v[:, 1].reshape(I2 // 2, K)
+
+
+def choose_split(N: int, K: int, M: int, target: int = _TARGET_WGS) -> int:
+    """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows each)."""
+    blocks = N // _ROWS_PER_WG
+    s = 1
+    while blocks * s < target and s < 16 and K % (_KCHUNK * s * 2) == 0:
+        s *= 2
+    return s
+
+
+def skinny_ok(x: torch.Tensor, w: torch.Tensor, force: bool = False) -> bool:
+    if not (SKINNY_ENABLED or force) or not x.is_cuda or x.dtype != torch.bfloat16:
+        return False
+    M, K = x.shape
+    N = w.shape[0]
+    return (0 < M <= SKINNY_MAX_M and N % _ROWS_PER_WG == 0 and K % _KCHUNK == 0 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0)
+
+
+def norm_fusable(H: int) -> bool:
+    """Hidden sizes the split-K + residual + RMSNorm kernel handles."""
+    return H % 1024 == 0 and H <= 8192
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 out [M, N]."""
+    if not skinny_ok(x, w):
+        return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0), out.stride(0),
+                1, 0, native.stream_ptr())
+    return out
+
+
+def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Optional[int] = None) -> Partial:
+    """Split-K fp32 slabs into workspace ``ws`` (fp32, >= S*M*N)."""
+    M, K = x.shape
+    N = w.shape[0]
+    S = S or choose_split(N, K, M)
+    assert ws.numel() >= S * M * N, "split-K workspace too small"
+    native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0), N, S, 1,
+                native.stream_ptr())
+    return Partial(ws, S, M, N)
+
+
+def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(x @ Wg^T) * (x @ Wu^T) with interleaved gate/up rows → [M, I]."""
+    if not skinny_ok(x, w_gu_interleaved):
+        return silu_and_mul_interleaved(linear(x, w_gu_interleaved))
+    M, K = x.shape
+    N = w_gu_interleaved.shape[0]
+    out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
+    S = choose_split(N, K, M)
+    if S == 1 or ws is None or ws.numel() < S * M * N:
+        native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), w_gu_interleaved.data_ptr(), M, N, K,
+                    x.stride(0), out.stride(0), 1, 2, native.stream_ptr())
+    else:
+        p = linear_partial(x, w_gu_interleaved, ws, S)
+        native.call("pk_splitk_reduce", out.data_ptr(), ws.data_ptr(), S, M, N, out.stride(0), 1, native.stream_ptr())
+    return out
+
+
+def reduce_partial(p: Partial, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if out is None:
+        out = torch.empty((p.M, p.N), dtype=torch.bfloat16, device=p.buf.device)
+    native.call("pk_splitk_reduce", out.data_ptr(), p.buf.data_ptr(), p.S, p.M, p.N, out.stride(0), 0,
+                native.stream_ptr())
+    return out
+
+
+def partial_add_rms_norm(p: Partial, residual: torch.Tensor, weight: torch.Tensor, eps: float,
+                         out: Optional[torch.Tensor] = None):
+    """residual += sum(p) (bf16), x = rms_norm(residual) * w.  Returns (x, residual)."""
+    if out is None:
+        out = torch.empty_like(residual)
+    native.call("pk_splitk_add_rmsnorm", out.data_ptr(), residual.data_ptr(), p.buf.data_ptr(), weight.data_ptr(),
+                p.S, p.M, p.N, float(eps), native.stream_ptr())
+    return out, residual
+
+
+def silu_and_mul_interleaved(x: torch.Tensor) -> torch.Tensor:
+    if not x.is_cuda:
+        return reference.silu_and_mul_interleaved(x)
+    I2 = x.shape[-1]
+    T = x.numel() // I2
+    out = torch.empty(x.shape[:-1] + (I2 // 2,), dtype=x.dtype, device=x.device)
+    native.call("pk_silu_and_mul_il", out.data_ptr(), x.data_ptr(), T, I2 // 2, native.stream_ptr())
+    return out

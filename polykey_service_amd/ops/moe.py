@@ -1,0 +1,148 @@
+"""Mixture-of-experts dispatch (Mixtral): routing, expert grouping, grouped GEMM, combine.
+
+Decode (T <= 64 tokens): everything stays on the device and is graph-capturable —
+``topk_softmax`` → ``align`` (stable counting sort by expert) → ``permute`` → grouped skinny
+GEMM for w13 with the fused SiLU epilogue → grouped skinny GEMM for w2 → weighted
+``unpermute``.  An expert that received no token is skipped without reading its weights.
+
+Prefill (T > 64): the same routing kernels, then one hipBLASLt GEMM per expert over its
+contiguous rows (expert row counts are read back once per layer; prefill is not graphed).
+
+Expert parallelism: with ``e_lo, e_hi`` this rank only computes experts ``[e_lo, e_hi)``;
+slots routed elsewhere get ``inv = -1`` and contribute zero, and the caller all-reduces the
+combined output across the EP group (tokens are replicated by TP attention, so the combine is
+the same all-reduce the dense MLP already does — see parallel/ep.py for the all-to-all form).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import native, reference
+from .gemm import silu_and_mul_interleaved
+
+
+def topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    T, E = router_logits.shape
+    if not router_logits.is_cuda:
+        p = torch.softmax(router_logits.float(), -1)
+        w, ids = torch.topk(p, k, dim=-1)
+        if renorm:
+            w = w / w.sum(-1, keepdim=True)
+        return ids.to(torch.int32), w
+    ids = torch.empty((T, k), dtype=torch.int32, device=router_logits.device)
+    w = torch.empty((T, k), dtype=torch.float32, device=router_logits.device)
+    native.call("pk_moe_topk_softmax", ids.data_ptr(), w.data_ptr(), router_logits.data_ptr(), T, E, k,
+                router_logits.stride(0), int(renorm), native.stream_ptr())
+    return ids, w
+
+
+def align(ids: torch.Tensor, E: int, e_lo: int, e_hi: int):
+    """→ offsets [E_local+1], sorted slots [n], inverse positions [n] (int32; -1 = not local)."""
+    n = ids.numel()
+    El = e_hi - e_lo
+    dev = ids.device
+    if not ids.is_cuda:
+        flat = ids.reshape(-1).long()
+        local = (flat >= e_lo) & (flat < e_hi)
+        key = torch.where(local, flat - e_lo, torch.full_like(flat, El))
+        order = torch.sort(key, stable=True).indices
+        counts = torch.bincount(key, minlength=El + 1)[:El]
+        offsets = torch.zeros(El + 1, dtype=torch.int32)
+        offsets[1:] = torch.cumsum(counts, 0)
+        m = int(offsets[-1])
+        sorted_ = order[:m].to(torch.int32)
+        inv = torch.full((n,), -1, dtype=torch.int32)
+        inv[order[:m]] = torch.arange(m, dtype=torch.int32)
+        return offsets, sorted_, inv
+    offsets = torch.empty(El + 1, dtype=torch.int32, device=dev)
+    sorted_ = torch.empty(n, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    native.call("pk_moe_align", ids.data_ptr(), offsets.data_ptr(), sorted_.data_ptr(), inv.data_ptr(), n, E, e_lo,
+                e_hi, native.stream_ptr())
+    return offsets, sorted_, inv
+
+
+def permute(x: torch.Tensor, sorted_: torch.Tensor, offsets: torch.Tensor, k: int) -> torch.Tensor:
+    n = sorted_.numel()
+    H = x.shape[-1]
+    if not x.is_cuda:
+        m = int(offsets[-1])
+        return x[(sorted_[:m].long() // k)]
+    out = torch.empty((n, H), dtype=x.dtype, device=x.device)
+    native.call("pk_moe_permute", out.data_ptr(), x.data_ptr(), sorted_.data_ptr(), offsets.data_ptr(), n,
+                offsets.numel() - 1, k, H, native.stream_ptr())
+    return out
+
+
+def unpermute(y: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, T: int, k: int) -> torch.Tensor:
+    H = y.shape[-1]
+    if not y.is_cuda:
+        out = torch.zeros((T, H), dtype=torch.float32)
+        invl = inv.view(T, k).long()
+        for j in range(k):
+            valid = invl[:, j] >= 0
+            idx = invl[:, j].clamp(min=0)
+            out += torch.where(valid[:, None], y[idx].float() * w[:, j:j + 1].float(), torch.zeros(()))
+        return out.to(y.dtype)
+    out = torch.empty((T, H), dtype=y.dtype, device=y.device)
+    native.call("pk_moe_unpermute", out.data_ptr(), y.data_ptr(), inv.data_ptr(), w.data_ptr(), T, k, H,
+                native.stream_ptr())
+    return out
+
+
+def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_rows: int, silu: bool) -> torch.Tensor:
+    """Rows of expert e = a[offsets[e]:offsets[e+1]] times w[e]^T (w: [E_local, N, K])."""
+    E_local, N, K = w.shape
+    n_out = N // 2 if silu else N
+    out = torch.empty((a.shape[0], n_out), dtype=a.dtype, device=a.device)
+    if a.is_cuda and max_rows <= 64:
+        native.call("pk_moe_gemm", out.data_ptr(), a.data_ptr(), w.data_ptr(), offsets.data_ptr(), max_rows, N, K,
+                    out.stride(0), E_local, 2 if silu else 0, native.stream_ptr())
+        return out
+    offs = offsets.tolist()  # prefill: one read-back per layer, then a library GEMM per expert
+    for e in range(E_local):
+        lo, hi = offs[e], offs[e + 1]
+        if hi > lo:
+            y = F.linear(a[lo:hi], w[e])
+            out[lo:hi] = silu_and_mul_interleaved(y) if silu else y
+    return out
+
+
+def fused_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, k: int,
+              e_lo: int = 0, e_hi: Optional[int] = None) -> torch.Tensor:
+    """Mixtral sparse MLP for this rank's experts.  x [T, H]; router_w [E, H]; w13 [E_l, 2I, H]
+    (gate/up interleaved by 16); w2 [E_l, H, I].  Returns the (partial, if EP) combined output."""
+    T = x.shape[0]
+    E = router_w.shape[0]
+    e_hi = E if e_hi is None else e_hi
+    logits = F.linear(x, router_w)
+    ids, wts = topk_softmax(logits, k)
+    offsets, sorted_, inv = align(ids, E, e_lo, e_hi)
+    xs = permute(x, sorted_, offsets, k)
+    h = grouped_gemm(xs, w13, offsets, T, silu=True)
+    y = grouped_gemm(h, w2, offsets, T, silu=False)
+    return unpermute(y, inv, wts, T, k)
+
+
+def fused_moe_reference(x, router_w, w13, w2, k, e_lo=0, e_hi=None):
+    """Loop-over-experts oracle with fp32 GEMMs and the kernels' bf16 rounding points
+    (projection outputs, SiLU and h are bf16 tensors in the fused path)."""
+    E = router_w.shape[0]
+    e_hi = E if e_hi is None else e_hi
+    bf = lambda t: t.to(torch.bfloat16).float()
+    p = torch.softmax(bf(x.float() @ router_w.float().t()), -1)
+    w, ids = torch.topk(p, k, -1)
+    w = w / w.sum(-1, keepdim=True)
+    out = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+    H = x.shape[1]
+    for e in range(e_lo, e_hi):
+        v = w13[e - e_lo].float().view(-1, 2, 16, H)
+        g, u = v[:, 0].reshape(-1, H), v[:, 1].reshape(-1, H)
+        h = bf(bf(torch.nn.functional.silu(bf(x.float() @ g.t()))) * bf(x.float() @ u.t()))
+        y = bf(h @ w2[e - e_lo].float().t())
+        sel = (ids == e).float() * w
+        out += sel.sum(-1, keepdim=True) * y
+    return out

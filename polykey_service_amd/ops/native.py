@@ -39,12 +39,16 @@ SIGNATURES = {
     "pk_paged_prefill": [P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, F32, P],
     "pk_sample": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, P],
     "pk_embedding": [P, P, P, I32, I32, I32, I32, P],
-    "pk_moe_topk_softmax": [P, P, P, I32, I32, I32, I32, P],
-    "pk_moe_align": [P, P, P, P, P, I32, I32, I32, I32, P],
-    "pk_moe_permute": [P, P, P, I32, I32, P],
+    "pk_moe_topk_softmax": [P, P, P, I32, I32, I32, I32, I32, P],
+    "pk_moe_align": [P, P, P, P, I32, I32, I32, I32, P],
+    "pk_moe_permute": [P, P, P, P, I32, I32, I32, I32, P],
     "pk_moe_unpermute": [P, P, P, P, I32, I32, I32, P],
-    "pk_grouped_gemm": [P, P, P, P, P, I32, I32, I32, I32, I32, P],
+    "pk_moe_gemm": [P, P, P, P, I32, I32, I32, I32, I32, I32, P],
     "pk_argmax": [P, P, I32, I32, I32, P],
+    "pk_silu_and_mul_il": [P, P, I32, I32, P],
+    "pk_skinny_gemm": [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P],
+    "pk_splitk_reduce": [P, P, I32, I32, I32, I32, I32, P],
+    "pk_splitk_add_rmsnorm": [P, P, P, P, I32, I32, I32, F32, P],
 }
 
 

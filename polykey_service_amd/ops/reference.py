@@ -37,6 +37,14 @@ def silu_and_mul(x: torch.Tensor) -> torch.Tensor:
     return (torch.nn.functional.silu(g).to(x.dtype).float() * u).to(x.dtype)
 
 
+def silu_and_mul_interleaved(x: torch.Tensor, block: int = 16) -> torch.Tensor:
+    """x: [T, 2I] with gate/up interleaved in blocks of ``block`` columns."""
+    T, I2 = x.shape[0], x.shape[-1]
+    v = x.reshape(-1, I2 // (2 * block), 2, block)
+    g, u = v[:, :, 0].reshape(-1, I2 // 2).float(), v[:, :, 1].reshape(-1, I2 // 2).float()
+    return (torch.nn.functional.silu(g).to(x.dtype).float() * u).to(x.dtype).view(x.shape[:-1] + (I2 // 2,))
+
+
 # ------------------------------------------------------------------------------ rope
 def rope_inv_freq(head_dim: int, theta: float, scaling: Optional[dict] = None) -> torch.Tensor:
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))

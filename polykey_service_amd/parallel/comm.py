@@ -31,8 +31,9 @@ def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:
     if st.tp_size == 1:
         return x
     x = x.contiguous()
-    out = torch.empty((st.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    out = torch.empty((st.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x, group=st.tp_group)
+    out = out.view((st.tp_size,) + tuple(x.shape))
     return out.movedim(0, -2).reshape(*x.shape[:-1], x.shape[-1] * st.tp_size)
 
 

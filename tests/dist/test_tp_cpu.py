@@ -1,0 +1,122 @@
+"""Tensor / expert parallel correctness on CPU with gloo (world size 2): the sharded model must
+reproduce the single-rank model (same random-init weights, shards sliced from the full tensors)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+PROMPTS = [[1, 5, 6, 7, 8, 9], [1] + list(range(20, 60)), [1, 2]]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _engine(model, st, **kw):
+    from polykey_service_amd.engine import EngineConfig, LLMEngine
+    return LLMEngine(EngineConfig(model=model, max_num_seqs=8, max_num_batched_tokens=128, max_model_len=256,
+                                  hip_graphs=False, device="cpu", **kw), st)
+
+
+def _first_step_logits_and_tokens(eng):
+    from polykey_service_amd.engine import SamplingParams
+    eng.runner.keep_logits = True
+    seqs = [eng.add_request(p, SamplingParams(max_tokens=4)) for p in PROMPTS]
+    eng.step()
+    logits = eng.runner.last_logits.float().clone()
+    while eng.has_unfinished():
+        eng.step()
+    return logits, [s.output_ids for s in seqs]
+
+
+def _worker(rank, world, port, model, ep, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    st = init_parallel(tp=world, ep=ep, device="cpu", backend="gloo")
+    eng = _engine(model, st)
+    if st.tp_rank == 0:
+        logits, toks = _first_step_logits_and_tokens(eng)
+        eng.runner.stop_workers()
+        torch.save({"logits": logits, "tokens": toks}, out_path)
+    else:
+        eng.runner.worker_loop()
+    destroy_parallel()
+
+
+@pytest.mark.parametrize("model,ep", [("tiny-llama-gqa4", 1), ("tiny-mixtral", 1), ("tiny-mixtral", 2)])
+def test_tp2_matches_tp1(tmp_path, model, ep):
+    from polykey_service_amd.parallel.state import ParallelState
+    ref_logits, ref_toks = _first_step_logits_and_tokens(_engine(model, ParallelState()))
+    out = str(tmp_path / "tp.pt")
+    mp.start_processes(_worker, args=(2, _free_port(), model, ep, out), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    # bf16 row-parallel partials are rounded per rank before the all-reduce: ~1 bf16 ulp noise
+    torch.testing.assert_close(got["logits"], ref_logits, atol=1e-1, rtol=5e-2)
+    assert [t[0] for t in got["tokens"]] == [t[0] for t in ref_toks]
+
+
+def _comm_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from polykey_service_amd.parallel import comm
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    init_parallel(tp=world, device="cpu", backend="gloo")
+    x = torch.full((2, 3), float(rank + 1))
+    ar = comm.tp_all_reduce(x.clone())
+    ag = comm.tp_all_gather_last(torch.arange(3, dtype=torch.float32).view(1, 3) + 10 * rank)
+    # all-to-all: rank r sends (r+1) rows to every peer
+    send = torch.full((world * (rank + 1), 2), float(rank))
+    cnt = comm.tp_all_to_all_counts(torch.full((world,), rank + 1, dtype=torch.int64))
+    recv = comm.tp_all_to_all(send, cnt.tolist(), [rank + 1] * world)
+    obj = comm.tp_broadcast_object({"step": 7} if rank == 0 else None)
+    torch.save({"ar": ar, "ag": ag, "recv": recv, "obj": obj}, f"{out_path}.{rank}")
+    destroy_parallel()
+
+
+def test_collectives_gloo(tmp_path):
+    out = str(tmp_path / "c")
+    mp.start_processes(_comm_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        d = torch.load(f"{out}.{r}", weights_only=False)
+        assert torch.equal(d["ar"], torch.full((2, 3), 3.0))
+        assert d["ag"].tolist() == [[0.0, 1.0, 2.0, 10.0, 11.0, 12.0]]
+        assert d["recv"][:, 0].tolist() == [0.0] * 1 + [1.0] * 2
+        assert d["obj"] == {"step": 7}
+
+
+def _a2a_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from polykey_service_amd.ops import gemm
+    from polykey_service_amd.parallel.ep import moe_all_to_all
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    init_parallel(tp=world, ep=world, device="cpu", backend="gloo")
+    g = torch.Generator().manual_seed(1)
+    E, H, I, k = 4, 256, 256, 2
+    router = (torch.randn(E, H, generator=g) * 0.2).to(torch.bfloat16)
+    w13 = torch.stack([gemm.interleave_gate_up((torch.randn(I, H, generator=g) * 0.05).to(torch.bfloat16),
+                                               (torch.randn(I, H, generator=g) * 0.05).to(torch.bfloat16))
+                       for _ in range(E)])
+    w2 = (torch.randn(E, H, I, generator=g) * 0.05).to(torch.bfloat16)
+    x = torch.randn(12, H, generator=g).to(torch.bfloat16)
+    per = E // world
+    mine = x[rank * 6:(rank + 1) * 6]
+    y = moe_all_to_all(mine, router, w13[rank * per:(rank + 1) * per], w2[rank * per:(rank + 1) * per], k)
+    torch.save({"y": y, "x": x, "router": router, "w13": w13, "w2": w2}, f"{out_path}.{rank}")
+    destroy_parallel()
+
+
+def test_moe_all_to_all_matches_dense(tmp_path):
+    from polykey_service_amd.ops.moe import fused_moe_reference
+    out = str(tmp_path / "a2a")
+    mp.start_processes(_a2a_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    d0, d1 = torch.load(f"{out}.0", weights_only=True), torch.load(f"{out}.1", weights_only=True)
+    y = torch.cat([d0["y"], d1["y"]]).float()
+    ref = fused_moe_reference(d0["x"], d0["router"], d0["w13"], d0["w2"], 2)
+    torch.testing.assert_close(y, ref, atol=3e-2, rtol=3e-2)

@@ -1,0 +1,65 @@
+"""Weight-streaming decode GEMM (csrc/kernels/gemm_skinny.hip) vs fp32 matmul references."""
+import pytest
+import torch
+
+from polykey_service_amd.ops import gemm
+from polykey_service_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1280, 8192), (128256, 4096), (64, 256)])
+def test_linear_bf16(M, N, K):
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    y = gemm.linear(x, w)
+    exp = (x.float() @ w.float().t())
+    torch.testing.assert_close(y.float(), exp, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [3, 64])
+@pytest.mark.parametrize("N,K,S", [(4096, 4096, 8), (4096, 14336, 8), (6144, 4096, 4), (512, 1024, 2)])
+def test_partial_and_reduce(M, N, K, S):
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    ws = torch.empty(S * M * N, dtype=torch.float32, device="cuda")
+    p = gemm.linear_partial(x, w, ws, S)
+    exp = x.float() @ w.float().t()
+    torch.testing.assert_close(p.view().sum(0), exp, atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(gemm.reduce_partial(p).float(), exp, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,I,K", [(5, 14336, 4096), (64, 3584, 8192), (1, 512, 256)])
+def test_fused_silu_epilogue(M, I, K):
+    x = rnd(M, K)
+    g, u = rnd(I, K, scale=0.05), rnd(I, K, scale=0.05)
+    w = gemm.interleave_gate_up(g, u)
+    exp = ref.silu_and_mul(torch.cat([(x.float() @ g.float().t()), (x.float() @ u.float().t())], -1).to(torch.bfloat16))
+    ws = torch.empty(64 * 2 * I * 16, dtype=torch.float32, device="cuda")
+    y = gemm.linear_silu(x, w, ws)
+    torch.testing.assert_close(y.float(), exp.float(), atol=3e-2, rtol=3e-2)
+    # prefill path: hipBLASLt + interleaved SiLU kernel
+    y2 = gemm.silu_and_mul_interleaved(torch.nn.functional.linear(x, w))
+    torch.testing.assert_close(y2.float(), exp.float(), atol=3e-2, rtol=3e-2)
+    g2, u2 = gemm.deinterleave_gate_up(w)
+    assert torch.equal(g2, g) and torch.equal(u2, u)
+
+
+@pytest.mark.parametrize("M,H,S", [(64, 4096, 8), (3, 8192, 4), (17, 1024, 2)])
+def test_partial_add_rmsnorm(M, H, S):
+    K = 256 * S
+    x, w = rnd(M, K), rnd(H, K, scale=0.05)
+    res = rnd(M, H)
+    nw = rnd(H)
+    ws = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
+    p = gemm.linear_partial(x, w, ws, S)
+    proj = (x.float() @ w.float().t()).to(torch.bfloat16)
+    res_ref, x_ref = res.clone().cpu(), proj.clone().cpu()
+    ref.fused_add_rms_norm(x_ref, res_ref, nw.cpu(), 1e-5)
+    out, res2 = gemm.partial_add_rms_norm(p, res, nw, 1e-5)
+    torch.testing.assert_close(res2.cpu().float(), res_ref.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(out.cpu().float(), x_ref.float(), atol=5e-2, rtol=3e-2)
