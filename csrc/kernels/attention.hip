@@ -155,16 +155,21 @@ template <int kPart>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int n_q, int n_kv, int bs, int max_blocks,
-    int q_stride, int out_stride, int n_parts, float scale2) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int n_q, int n_kv, int bs,
+    int max_blocks, int q_stride, int out_stride, int n_parts, float scale2) {
   __shared__ float o_lds[4][16][kHD + 4];
   __shared__ float ml_lds[4][16][2];
   const int h = blockIdx.x, seq = blockIdx.y, part = blockIdx.z;
   const int ctx = context_lens[seq];
   const int begin = part * kPart;
-  if (begin >= ctx) return;
-  const int end = min(ctx, begin + kPart);
   const int G = n_q / n_kv;
+  if (begin >= ctx) {
+    if (part == 0)  // ctx == 0: a padded (graph) row -> zeros
+      for (int idx = threadIdx.x; idx < G * kHD; idx += 256)
+        out[static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD] = 0;
+    return;
+  }
+  const int end = min(ctx, begin + kPart);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
@@ -210,6 +215,41 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
         part_ml[2 * pi + 1] = L;
       }
     }
+  }
+  if (n_used == 1 || counters == nullptr) return;
+  // ---- in-launch split-K merge: the last partition to arrive combines all of them
+  // (guide §5 "In-launch split-K reduction": plain slab stores, every wave drains, one agent
+  // release + ticket; the last arriver acquires, merges and re-arms the counter).
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* ctr = counters + seq * n_kv + h;
+    const int t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == n_used - 1);
+    if (last) {
+      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int idx = threadIdx.x; idx < G * kHD; idx += 256) {
+    const int c = idx / kHD, d = idx % kHD;
+    const int hq = h * G + c;
+    const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
+    float M = kNegBig;
+    for (int p = 0; p < n_used; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
+    float O = 0.f, L = 0.f;
+    for (int p = 0; p < n_used; ++p) {
+      const float f = exp2f(part_ml[2 * (base + p)] - M);
+      O += f * part_o[(base + p) * kHD + d];
+      L += f * part_ml[2 * (base + p) + 1];
+    }
+    out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
   }
 }
 
@@ -292,10 +332,12 @@ constexpr int kDecodePart = 512;
 // Workspace for decode: part_o [n_seqs, n_q, n_parts, 128] fp32, part_ml [n_seqs, n_q, n_parts, 2] fp32.
 PK_EXPORT int pk_decode_num_parts(int max_context) { return (max_context + kDecodePart - 1) / kDecodePart; }
 
+// counters: [n_seqs, n_kv] int32, zero-initialised once (the merging workgroup re-arms its
+// counter); with counters == null the partitions are merged by a second kernel instead.
 PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
                               const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
-                              int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride,
-                              float scale, hipStream_t stream) {
+                              void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
+                              int out_stride, float scale, hipStream_t stream) {
   if (n_seqs <= 0) return 0;
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
   const int n_parts = (max_blocks * bs + kDecodePart - 1) / kDecodePart;
@@ -304,10 +346,10 @@ PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, con
   paged_decode_kernel<kDecodePart><<<grid, 256, 0, stream>>>(
       static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
       static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables), static_cast<const int*>(context_lens),
-      static_cast<float*>(part_o), static_cast<float*>(part_ml), n_q, n_kv, bs, max_blocks, q_stride, out_stride,
-      n_parts, scale * kLog2e);
+      static_cast<float*>(part_o), static_cast<float*>(part_ml), static_cast<int*>(counters), n_q, n_kv, bs,
+      max_blocks, q_stride, out_stride, n_parts, scale * kLog2e);
   int rc = PK_CHECK_LAUNCH();
-  if (rc) return rc;
+  if (rc || counters != nullptr || n_parts == 1) return rc;
   dim3 g2(n_q, n_seqs);
   paged_decode_reduce_kernel<kDecodePart><<<g2, 128, 0, stream>>>(
       static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),

@@ -205,25 +205,29 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
   }
 }
 
-// residual = bf16(residual + sum_s partial[s]); x = rmsnorm(residual) * w.  One row per block,
-// H / 4 threads... handled as VPT float4 groups per thread (blockDim = 256).
+// residual = bf16(residual + bf16(sum_s partial[s])); x = rmsnorm(residual) * w.
+// One row per workgroup of H/4 (<= 1024) threads, PER float4 column groups per thread; the S
+// slab loads of a group are independent and issued back to back (latency, not bandwidth, is
+// what a 64-row reduction fights).
 template <int PER>
-__global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
-                                                                 const float* __restrict__ partial,
-                                                                 const bf16_t* __restrict__ w, int S, int M, int H,
-                                                                 float eps) {
+__global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
+                                                                  const float* __restrict__ partial,
+                                                                  const bf16_t* __restrict__ w, int S, int M, int H,
+                                                                  float eps) {
   __shared__ float red[16];
   const int m = blockIdx.x;
-  constexpr int per = PER;  // float4 groups per thread (H = 4096 -> 4)
   float v[PER][4];
   float ss = 0.f;
   bf16_t* res = residual + static_cast<int64_t>(m) * H;
+  const int64_t slab = static_cast<int64_t>(M) * H;
+  const float* base = partial + static_cast<int64_t>(m) * H;
 #pragma unroll
-  for (int i = 0; i < per; ++i) {
+  for (int i = 0; i < PER; ++i) {
     const int c = 4 * (threadIdx.x + i * blockDim.x);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = 0; s < S; ++s) {
-      const float4 p = *reinterpret_cast<const float4*>(partial + (static_cast<int64_t>(s) * M + m) * H + c);
+    float4 acc = *reinterpret_cast<const float4*>(base + c);
+#pragma unroll 8
+    for (int s = 1; s < S; ++s) {
+      const float4 p = *reinterpret_cast<const float4*>(base + s * slab + c);
       acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
     }
     const uint2 rr = *reinterpret_cast<const uint2*>(res + c);
@@ -241,7 +245,7 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(bf16_t* __restr
   const float rinv = rsqrtf(block_sum(ss, red) / H + eps);
   bf16_t* xo = x + static_cast<int64_t>(m) * H;
 #pragma unroll
-  for (int i = 0; i < per; ++i) {
+  for (int i = 0; i < PER; ++i) {
     const int c = 4 * (threadIdx.x + i * blockDim.x);
     const uint2 ww = *reinterpret_cast<const uint2*>(w + c);
     float y[4];
@@ -253,6 +257,77 @@ __global__ void __launch_bounds__(256) splitk_add_rmsnorm_kernel(bf16_t* __restr
     o.x = pack2(y[0], y[1]);
     o.y = pack2(y[2], y[3]);
     *reinterpret_cast<uint2*>(xo + c) = o;
+  }
+}
+
+// Split-K QKV epilogue fused with RoPE and the paged KV write: per token, sum the S fp32 slabs
+// of the fused q|k|v projection, round to bf16 (the unfused GEMM output), rotate q and k
+// (neox, fp32 cos|sin table), write q to q_out [M, nq*128], k to the K cache and v to the
+// transposed V cache (slot < 0: padding row, nothing cached).  Replaces reduce + rope_and_cache.
+__global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
+    bf16_t* __restrict__ q_out, const float* __restrict__ partial, int S, int M, int nq, int nkv,
+    const int* __restrict__ positions, const float* __restrict__ cos_sin, bf16_t* __restrict__ kc,
+    bf16_t* __restrict__ vc, const int* __restrict__ slots, int bs) {
+  const int m = blockIdx.x;
+  const int N = (nq + 2 * nkv) * 128;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  const float* base = partial + static_cast<int64_t>(m) * N;
+  const int pos = positions[m];
+  const int slot = slots[m];
+  const float* cs = cos_sin + static_cast<int64_t>(pos) * 128;
+  const int n_rot = (nq + nkv) * 16;  // (head, 4-pair group)
+  const int n_items = n_rot + nkv * 32;
+  for (int it = threadIdx.x; it < n_items; it += blockDim.x) {
+    if (it < n_rot) {
+      const int h = it >> 4, j = (it & 15) * 4;
+      const int c = h * 128 + j;
+      float4 a = *reinterpret_cast<const float4*>(base + c);
+      float4 b = *reinterpret_cast<const float4*>(base + c + 64);
+      for (int s = 1; s < S; ++s) {
+        const float4 pa = *reinterpret_cast<const float4*>(base + s * slab + c);
+        const float4 pb = *reinterpret_cast<const float4*>(base + s * slab + c + 64);
+        a.x += pa.x; a.y += pa.y; a.z += pa.z; a.w += pa.w;
+        b.x += pb.x; b.y += pb.y; b.z += pb.z; b.w += pb.w;
+      }
+      const float av[4] = {bf2f(f2bf(a.x)), bf2f(f2bf(a.y)), bf2f(f2bf(a.z)), bf2f(f2bf(a.w))};
+      const float bv[4] = {bf2f(f2bf(b.x)), bf2f(f2bf(b.y)), bf2f(f2bf(b.z)), bf2f(f2bf(b.w))};
+      const float4 co = *reinterpret_cast<const float4*>(cs + j);
+      const float4 si = *reinterpret_cast<const float4*>(cs + 64 + j);
+      const float cc[4] = {co.x, co.y, co.z, co.w}, ss[4] = {si.x, si.y, si.z, si.w};
+      float ra[4], rb[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ra[q] = av[q] * cc[q] - bv[q] * ss[q];
+        rb[q] = bv[q] * cc[q] + av[q] * ss[q];
+      }
+      uint2 va, vb;
+      va.x = pack2(ra[0], ra[1]);
+      va.y = pack2(ra[2], ra[3]);
+      vb.x = pack2(rb[0], rb[1]);
+      vb.y = pack2(rb[2], rb[3]);
+      if (h < nq) {
+        bf16_t* o = q_out + static_cast<int64_t>(m) * nq * 128 + h * 128 + j;
+        *reinterpret_cast<uint2*>(o) = va;
+        *reinterpret_cast<uint2*>(o + 64) = vb;
+      } else if (slot >= 0) {
+        bf16_t* d = kc + ((static_cast<int64_t>(slot / bs) * nkv + (h - nq)) * bs + slot % bs) * 128 + j;
+        *reinterpret_cast<uint2*>(d) = va;
+        *reinterpret_cast<uint2*>(d + 64) = vb;
+      }
+    } else if (slot >= 0) {
+      const int u = it - n_rot;
+      const int kh = u >> 5, d0 = (u & 31) * 4;
+      const int c = (nq + nkv) * 128 + kh * 128 + d0;
+      float4 a = *reinterpret_cast<const float4*>(base + c);
+      for (int s = 1; s < S; ++s) {
+        const float4 pa = *reinterpret_cast<const float4*>(base + s * slab + c);
+        a.x += pa.x; a.y += pa.y; a.z += pa.z; a.w += pa.w;
+      }
+      const float av[4] = {a.x, a.y, a.z, a.w};
+      bf16_t* d = vc + ((static_cast<int64_t>(slot / bs) * nkv + kh) * 128 + d0) * bs + slot % bs;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q * bs] = f2bf(av[q]);
+    }
   }
 }
 
@@ -312,12 +387,23 @@ PK_EXPORT int pk_splitk_add_rmsnorm(void* x, void* residual, const void* partial
   auto rr = static_cast<bf16_t*>(residual);
   auto pp = static_cast<const float*>(partial);
   auto ww = static_cast<const bf16_t*>(w);
-  switch (H / 1024) {
-    case 1: splitk_add_rmsnorm_kernel<1><<<M, 256, 0, stream>>>(xx, rr, pp, ww, S, M, H, eps); break;
-    case 2: splitk_add_rmsnorm_kernel<2><<<M, 256, 0, stream>>>(xx, rr, pp, ww, S, M, H, eps); break;
-    case 4: splitk_add_rmsnorm_kernel<4><<<M, 256, 0, stream>>>(xx, rr, pp, ww, S, M, H, eps); break;
-    case 8: splitk_add_rmsnorm_kernel<8><<<M, 256, 0, stream>>>(xx, rr, pp, ww, S, M, H, eps); break;
+  const int threads = H / 4 > 1024 ? 1024 : H / 4;
+  switch (H / (4 * threads)) {
+    case 1: splitk_add_rmsnorm_kernel<1><<<M, threads, 0, stream>>>(xx, rr, pp, ww, S, M, H, eps); break;
+    case 2: splitk_add_rmsnorm_kernel<2><<<M, threads, 0, stream>>>(xx, rr, pp, ww, S, M, H, eps); break;
     default: return -1;
   }
+  return PK_CHECK_LAUNCH();
+}
+
+PK_EXPORT int pk_qkv_reduce_rope_cache(void* q_out, const void* partial, int S, int M, int nq, int nkv,
+                                       const void* positions, const void* cos_sin, void* k_cache, void* v_cache,
+                                       const void* slots, int bs, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (bs % 8) return -1;
+  qkv_reduce_rope_cache_kernel<<<M, 256, 0, stream>>>(
+      static_cast<bf16_t*>(q_out), static_cast<const float*>(partial), S, M, nq, nkv,
+      static_cast<const int*>(positions), static_cast<const float*>(cos_sin), static_cast<bf16_t*>(k_cache),
+      static_cast<bf16_t*>(v_cache), static_cast<const int*>(slots), bs);
   return PK_CHECK_LAUNCH();
 }

@@ -1,4 +1,4 @@
 set -e
-R=$GRAFT_REPO_ROOT
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof2 -o run -- python3 $R/bench.py --steps 1 --warmup 1 > $R/gpurun_out/prof2.log 2>&1
+cd $GRAFT_REPO_ROOT
+timeout -k 10 900 python -m pytest tests -m gpu -q -x 2>&1 | tail -30
+timeout -k 10 900 python bench.py --steps 2 --warmup 1 2>&1 | tail -3

@@ -87,9 +87,9 @@ class ModelRunner:
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_out: Dict[int, torch.Tensor] = {}
         self.graph_pool = None
-        nq_local = model.layers[0].attn.nq
-        self.part_o, self.part_ml = attn_ops.decode_workspace(cfg.max_num_seqs, nq_local, self.max_blocks, self.bs,
-                                                              device)
+        a0 = model.layers[0].attn
+        self.part_o, self.part_ml, self.part_ctr = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks,
+                                                                             self.bs, device, n_kv=a0.nkv)
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0}
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None
@@ -171,7 +171,7 @@ class ModelRunner:
             slot_mapping=d["slots"][:T],
             decode_block_tables=d["block_tables"][:nd] if nd else None,
             decode_context_lens=d["context_lens"][:nd] if nd else None,
-            decode_part_o=self.part_o, decode_part_ml=self.part_ml)
+            decode_part_o=self.part_o, decode_part_ml=self.part_ml, decode_counters=self.part_ctr)
         if npf:
             md.prefill_block_tables = d["block_tables"][nd:n]
             md.prefill_context_lens = d["context_lens"][nd:n]

@@ -80,10 +80,17 @@ class LlamaAttention(nn.Module):
         """Returns the o-projection output: a bf16 tensor, or (decode, TP=1) an unreduced
         split-K :class:`~polykey_service_amd.ops.gemm.Partial` consumed by the next norm."""
         T = x.shape[0]
-        qkv = _proj(x, self.qkv, ws)
         k_cache, v_cache = kv
-        attn_ops.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq, self.nkv, self.hd)
-        q = qkv.view(T, self.nq + 2 * self.nkv, self.hd)[:, :self.nq]
+        S = gemm.choose_split(self.qkv.shape[0], x.shape[1], T)
+        if ws is not None and gemm.skinny_ok(x, self.qkv) and S > 1 and ws.numel() >= S * T * self.qkv.shape[0]:
+            # decode: split-K QKV whose epilogue kernel also applies RoPE and writes the KV cache
+            q = gemm.qkv_reduce_rope_cache(gemm.linear_partial(x, self.qkv, ws, S), positions, cos_sin, k_cache,
+                                           v_cache, md.slot_mapping, self.nq, self.nkv)
+        else:
+            qkv = gemm.linear(x, self.qkv)
+            attn_ops.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq, self.nkv,
+                                    self.hd)
+            q = qkv.view(T, self.nq + 2 * self.nkv, self.hd)[:, :self.nq]
         a = attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
         return _proj_out(a, self.o, ws)
 

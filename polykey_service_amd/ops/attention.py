@@ -31,6 +31,7 @@ class AttnMetadata:
     prefill_cu_q: Optional[torch.Tensor] = None          # [np+1] int32, relative to the first prefill token
     decode_part_o: Optional[torch.Tensor] = None         # split-K workspace
     decode_part_ml: Optional[torch.Tensor] = None
+    decode_counters: Optional[torch.Tensor] = None       # [n_seqs, n_kv] int32, zero-initialised
 
     @property
     def num_tokens(self) -> int:
@@ -40,12 +41,15 @@ class AttnMetadata:
 _PART = 512  # must match kDecodePart in csrc/kernels/attention.hip
 
 
-def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, device) -> tuple:
+def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, device, n_kv: int = 0) -> tuple:
+    """Partition slabs (+ arrival counters when ``n_kv``) for split-K decode attention."""
     n_parts = (max_blocks * block_size + _PART - 1) // _PART
     if n_parts <= 1:
-        return None, None
+        return (None, None, None) if n_kv else (None, None)
     o = torch.empty((n_seqs, n_q, n_parts, 128), dtype=torch.float32, device=device)
     ml = torch.empty((n_seqs, n_q, n_parts, 2), dtype=torch.float32, device=device)
+    if n_kv:
+        return o, ml, torch.zeros((n_seqs, n_kv), dtype=torch.int32, device=device)
     return o, ml
 
 
@@ -83,7 +87,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         native.call("pk_paged_decode", out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                     bt.data_ptr(), md.decode_context_lens.data_ptr(),
                     native.ptr(md.decode_part_o) or 0, native.ptr(md.decode_part_ml) or 0,
-                    nd, nq, nkv, bs, bt.shape[1], q.stride(0), out.stride(0), float(scale), stream)
+                    native.ptr(md.decode_counters) or 0, nd, nq, nkv, bs, bt.shape[1], q.stride(0), out.stride(0), float(scale), stream)
     if md.num_prefill > 0:
         bt = md.prefill_block_tables
         qp = q[nd:]

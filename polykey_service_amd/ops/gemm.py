@@ -143,3 +143,13 @@ def silu_and_mul_interleaved(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty(x.shape[:-1] + (I2 // 2,), dtype=x.dtype, device=x.device)
     native.call("pk_silu_and_mul_il", out.data_ptr(), x.data_ptr(), T, I2 // 2, native.stream_ptr())
     return out
+
+
+def qkv_reduce_rope_cache(p: Partial, positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor,
+                          v_cache: torch.Tensor, slots: torch.Tensor, nq: int, nkv: int) -> torch.Tensor:
+    """Split-K QKV epilogue: sum slabs, RoPE q/k, write k/v to the paged cache → q [M, nq, 128]."""
+    q = torch.empty((p.M, nq, 128), dtype=torch.bfloat16, device=p.buf.device)
+    native.call("pk_qkv_reduce_rope_cache", q.data_ptr(), p.buf.data_ptr(), p.S, p.M, nq, nkv, positions.data_ptr(),
+                cos_sin.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), slots.data_ptr(), k_cache.shape[2],
+                native.stream_ptr())
+    return q

@@ -35,7 +35,7 @@ SIGNATURES = {
     "pk_fused_add_rmsnorm": [P, P, P, I32, I32, F32, P],
     "pk_silu_and_mul": [P, P, I32, I32, P],
     "pk_rope_and_cache": [P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P],
-    "pk_paged_decode": [P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, F32, P],
+    "pk_paged_decode": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, F32, P],
     "pk_paged_prefill": [P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, F32, P],
     "pk_sample": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, P],
     "pk_embedding": [P, P, P, I32, I32, I32, I32, P],
@@ -49,6 +49,7 @@ SIGNATURES = {
     "pk_skinny_gemm": [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P],
     "pk_splitk_reduce": [P, P, I32, I32, I32, I32, I32, P],
     "pk_splitk_add_rmsnorm": [P, P, P, P, I32, I32, I32, F32, P],
+    "pk_qkv_reduce_rope_cache": [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, P],
 }
 
 

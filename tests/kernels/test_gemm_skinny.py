@@ -63,3 +63,26 @@ def test_partial_add_rmsnorm(M, H, S):
     out, res2 = gemm.partial_add_rms_norm(p, res, nw, 1e-5)
     torch.testing.assert_close(res2.cpu().float(), res_ref.float(), atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(out.cpu().float(), x_ref.float(), atol=5e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("nq,nkv,bs,M", [(32, 8, 32, 64), (8, 1, 16, 5)])
+def test_qkv_reduce_rope_cache(nq, nkv, bs, M):
+    from polykey_service_amd.ops import attention as A
+    K, S = 1024, 4
+    N = (nq + 2 * nkv) * 128
+    x, w = rnd(M, K), rnd(N, K, scale=0.05)
+    ws = torch.empty(S * M * N, dtype=torch.float32, device="cuda")
+    pos = torch.randint(0, 2000, (M,), dtype=torch.int32, device="cuda")
+    cs = ref.rope_cos_sin_cache(2048, 128, 500000.0).cuda()
+    nb = M // bs + 4
+    slots = torch.randperm(nb * bs, device="cuda")[:M].to(torch.int32)
+    slots[0] = -1
+    kc = torch.zeros(nb, nkv, bs, 128, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros(nb, nkv, 128, bs, dtype=torch.bfloat16, device="cuda")
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = gemm.qkv_reduce_rope_cache(gemm.linear_partial(x, w, ws, S), pos, cs, kc, vc, slots, nq, nkv)
+    qkv = (x.float() @ w.float().t()).to(torch.bfloat16)
+    A.rope_and_cache(qkv, pos, cs, kc2, vc2, slots, nq, nkv)
+    torch.testing.assert_close(q.float(), qkv.view(M, -1, 128)[:, :nq].float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(kc.float(), kc2.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(vc.float(), vc2.float(), atol=3e-2, rtol=2e-2)
