@@ -1,0 +1,70 @@
+# polykey (MI355X-native) — developer targets, mirroring the reference's Makefile
+# (build / run-server / run-test-client / test / test-integration / compose-*) plus the
+# GPU-side targets (kernels, gpu tests, bench, profiling).
+.DEFAULT_GOAL := help
+PY        ?= python3
+SERVER_ADDR ?= localhost:50051
+PORT      ?= 50051
+
+.PHONY: help build clean run-server run-llm-server run-test-client test test-gpu test-dist test-integration \
+        bench bench-gpu8 prof compose-up compose-down compose-logs lint ci-check kill-local-server
+
+help: ## show targets
+	@grep -E '^[a-zA-Z0-9_-]+:.*## ' $(MAKEFILE_LIST) | awk -F':.*## ' '{printf "  \033[36m%-18s\033[0m %s\n", $$1, $$2}'
+
+build: ## compile HIP kernels (gfx950), comm lib and C++ runtime/crypto extensions in-tree
+	PYTORCH_ROCM_ARCH=gfx950 $(PY) -m polykey_service_amd._native.build -j 8
+
+clean: ## remove native build artefacts
+	$(PY) -m polykey_service_amd._native.build --clean
+
+run-server: build ## run the gRPC server with the mock backend (reference behaviour)
+	LISTEN_ADDR=:$(PORT) $(PY) -m polykey_service_amd.server
+
+run-llm-server: build ## run the gRPC + OpenAI server with the on-node Llama-3-8B backend (random init)
+	LISTEN_ADDR=:$(PORT) POLYKEY_BACKEND=local POLYKEY_HTTP_ADDR=:8000 POLYKEY_METRICS_ADDR=:9100 \
+	  $(PY) -m polykey_service_amd.server
+
+run-llm-server-tp8: build ## 70B TP=8 server (one process per GPU over RCCL; rank 0 serves)
+	$(PY) -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 -m polykey_service_amd.server \
+	  -backend local -model llama3-70b -tp 8 -http-addr :8000
+
+run-test-client: ## dev client against $(SERVER_ADDR) with the Jest-style report
+	POLYKEY_SERVER_ADDR=$(SERVER_ADDR) $(PY) -m polykey_service_amd.client
+
+test: build ## CPU test suite (unit + integration + gloo multi-process) with a Jest-style summary
+	$(PY) -m pytest tests -q -m "not gpu" -p polykey_service_amd.report.pytest_plugin --jest-json=.jest.jsonl; \
+	  rc=$$?; $(PY) -m polykey_service_amd.report jest < .jest.jsonl; exit $$rc
+
+test-gpu: build ## kernel numerics + GPU engine tests (needs an MI355X)
+	$(PY) -m pytest tests -q -m gpu
+
+test-dist: ## multi-process TP/EP tests on gloo (CPU)
+	$(PY) -m pytest tests/dist -q
+
+test-integration: build ## in-process server + dev client, health, reflection, LLM tools
+	$(PY) -m pytest tests/integration -q
+
+bench: build ## headline benchmark on 1 GPU (output tokens/s via gRPC, Llama-3-8B)
+	$(PY) bench.py --gpus 1
+
+bench-gpu8: build ## 1/2/4/8-GPU weak-scaling curve
+	for n in 1 2 4 8; do $(PY) bench.py --gpus $$n --steps 3 --warmup 1; done
+
+prof: build ## rocprofv3 kernel trace + stats of a short bench run into gpurun_out/prof
+	cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv -d $(CURDIR)/gpurun_out/prof -o run \
+	  -- $(PY) $(CURDIR)/bench.py --steps 1 --warmup 1
+
+compose-up: ## docker compose up (server image)
+	docker compose -f compose.yml up -d --build
+
+compose-down: ## docker compose down
+	docker compose -f compose.yml down
+
+compose-logs: ## follow server logs through the Jest-style beautifier
+	docker compose -f compose.yml logs -f | $(PY) -m polykey_service_amd.report
+
+kill-local-server: ## kill whatever listens on $(PORT)
+	@pid=$$(lsof -t -i :$(PORT) 2>/dev/null); if [ -n "$$pid" ]; then kill $$pid; fi
+
+ci-check: build test ## what CI runs on a CPU runner

@@ -6,7 +6,7 @@ server-sent events ending with ``data: [DONE]``), ``GET /v1/models``, ``GET /hea
 Requests are served by the same :class:`ToolRouter` model tools as gRPC, so both fronts share
 one continuous-batching engine; ``model`` selects the backend like ``llm.chat:<model>``.
 """
-from __future__ import annotations
+
 
 import asyncio
 import json
@@ -22,13 +22,14 @@ _SAMPLING_KEYS = ("max_tokens", "temperature", "top_p", "top_k", "min_p", "seed"
 
 
 def _llm(router, model: Optional[str]):
-    llm = getattr(router, "llm", None)
-    if llm is None:
-        raise ToolError("UNAVAILABLE", "no local LLM backend attached")
+    """The AsyncLLM serving ``model`` (the ``llm.chat`` tool registered for it)."""
     models = router.models("llm.chat")
-    if model and models and model not in models:
+    if not models:
+        raise ToolError("UNAVAILABLE", "no local LLM backend attached")
+    if model and model not in models:
         raise ToolError("NOT_FOUND", f"model {model!r} not served; available: {models}")
-    return llm, (model or (models[0] if models else "model"))
+    tool = router.resolve("llm.chat" + (f":{model}" if model else ""), {})
+    return tool.llm, tool.model_name
 
 
 def _params(body: Dict[str, Any]) -> SamplingParams:

@@ -28,8 +28,10 @@ class EngineDeadError(RuntimeError):
 
 class AsyncLLM:
     def __init__(self, engine: LLMEngine, on_fatal: Optional[Callable[[BaseException], None]] = None,
-                 watchdog_s: float = 0.0):
+                 watchdog_s: float = 0.0, metrics=None):
+        from ..utils import metrics as _m
         self.engine = engine
+        self.metrics = metrics if metrics is not None else _m.current()
         self.tokenizer = engine.tokenizer
         self.on_fatal = on_fatal
         self._cmds: Deque[Tuple[str, object]] = collections.deque()
@@ -145,7 +147,10 @@ class AsyncLLM:
                     continue
                 t0 = time.perf_counter()
                 outs = eng.step()
-                self.stats["step_time_s"] += time.perf_counter() - t0
+                dt = time.perf_counter() - t0
+                self.stats["step_time_s"] += dt
+                if self.metrics is not None:
+                    self.metrics.observe_step(eng, dt, outs)
                 self.stats["steps"] += 1
                 self.last_step_time = time.monotonic()
                 if outs:

@@ -50,7 +50,7 @@ def grpc_bind_address(addr: str) -> str:
 
 class PolykeyServer:
     def __init__(self, service, logger: Optional[slog.Logger] = None, listen_addr: str = ":50051",
-                 metrics=None, extra_handlers: Optional[List] = None):
+                 metrics=None, extra_handlers: Optional[List] = None, own_service: bool = True):
         self.logger = logger or slog.Logger()
         self.listen_addr = listen_addr
         self.service = service
@@ -61,6 +61,7 @@ class PolykeyServer:
                                       options=SERVER_OPTIONS)
         self.port: Optional[int] = None
         self._extra = extra_handlers or []
+        self.own_service = own_service  # stop() also closes the service (engine thread)
         self._stopped = asyncio.Event()
 
     async def start(self) -> int:
@@ -89,13 +90,42 @@ class PolykeyServer:
 
     async def stop(self, grace: float = 10.0) -> None:
         self.logger.info("server shutting down")
+        w = getattr(self, "_watch", None)
+        if w is not None:
+            w.cancel()
         self.health.shutdown()
         await self.server.stop(grace)
-        close = getattr(self.service, "aclose", None)
+        close = getattr(self.service, "aclose", None) if self.own_service else None
         if close is not None:
             await close()
         self.logger.info("server stopped")
         self._stopped.set()
+
+    def watch_backend(self, llm, interval: float = 1.0) -> "asyncio.Task":
+        """Failure detection: the health status follows the engine — NOT_SERVING
+        as soon as its loop dies (``on_fatal``) or its watchdog says a step has stalled."""
+        from .health import NOT_SERVING
+        loop = asyncio.get_running_loop()
+
+        def fatal(exc):
+            self.logger.error("engine loop died", error=repr(exc))
+            loop.call_soon_threadsafe(self.health.set_serving_status, proto.POLYKEY_SERVICE, NOT_SERVING)
+            loop.call_soon_threadsafe(self.health.set_serving_status, "", NOT_SERVING)
+
+        llm.on_fatal = fatal
+
+        async def poll():
+            while True:
+                await asyncio.sleep(interval)
+                ok = llm.healthy()
+                st = SERVING if ok else NOT_SERVING
+                if self.health.get(proto.POLYKEY_SERVICE) != st:
+                    self.logger.warn("backend health changed", serving=ok)
+                    self.health.set_serving_status(proto.POLYKEY_SERVICE, st)
+                    self.health.set_serving_status("", st)
+
+        self._watch = asyncio.create_task(poll())
+        return self._watch
 
     async def serve_until_signal(self, grace: float = 10.0) -> None:
         loop = asyncio.get_running_loop()
@@ -136,6 +166,9 @@ async def amain(argv=None) -> int:
     service = build_service(cfg, logger)
     srv = PolykeyServer(service, logger, cfg.listen_addr, metrics=metrics)
     await srv.start()
+    if getattr(service, "llm", None) is not None:
+        service.llm.watchdog_s = 60.0
+        srv.watch_backend(service.llm)
     http = None
     if cfg.http_addr:
         from ..api.openai import serve_openai

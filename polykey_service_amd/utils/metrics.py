@@ -1,0 +1,81 @@
+"""Prometheus metrics (``prometheus_client``) on a side port.
+
+The reference only recommends Prometheus (``test/README.md:61-70``); here the server exports
+RPC latency/count by method and code (fed by the logging interceptor's observer), and the
+engine exports request TTFT / inter-token latency / end-to-end latency histograms, output
+token and request counters, queue depth, running batch size and KV-block utilisation
+(SURVEY.md §5.5).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, start_http_server
+
+_LAT_BUCKETS = (.001, .0025, .005, .01, .025, .05, .1, .25, .5, 1, 2.5, 5, 10, 30, 60, 120)
+_TOK_BUCKETS = (.002, .004, .006, .008, .01, .015, .02, .03, .05, .1, .25, .5, 1)
+
+_current: Optional["Metrics"] = None
+
+
+class Metrics:
+    def __init__(self, registry: Optional[CollectorRegistry] = None):
+        self.registry = registry or CollectorRegistry()
+        r = self.registry
+        self.rpc_latency = Histogram("polykey_rpc_latency_seconds", "gRPC call latency", ["method", "code"],
+                                     buckets=_LAT_BUCKETS, registry=r)
+        self.requests = Counter("polykey_llm_requests_total", "finished LLM requests", ["finish_reason"], registry=r)
+        self.output_tokens = Counter("polykey_llm_output_tokens_total", "generated tokens", registry=r)
+        self.ttft = Histogram("polykey_llm_ttft_seconds", "time to first token", buckets=_LAT_BUCKETS, registry=r)
+        self.itl = Histogram("polykey_llm_inter_token_seconds", "mean inter-token latency per request",
+                             buckets=_TOK_BUCKETS, registry=r)
+        self.e2e = Histogram("polykey_llm_e2e_seconds", "request end-to-end latency", buckets=_LAT_BUCKETS,
+                             registry=r)
+        self.running = Gauge("polykey_engine_running_seqs", "sequences in the running batch", registry=r)
+        self.waiting = Gauge("polykey_engine_waiting_seqs", "queued sequences", registry=r)
+        self.kv_util = Gauge("polykey_engine_kv_utilization", "fraction of KV blocks in use", registry=r)
+        self.step_seconds = Histogram("polykey_engine_step_seconds", "engine step wall time", buckets=_TOK_BUCKETS,
+                                      registry=r)
+        self.preemptions = Gauge("polykey_engine_preemptions", "preemptions so far", registry=r)
+
+    @classmethod
+    def start(cls, addr: str) -> "Metrics":
+        m = cls()
+        host, _, port = addr.rpartition(":")
+        start_http_server(int(port), addr=host or "0.0.0.0", registry=m.registry)
+        set_current(m)
+        return m
+
+    def observe_rpc(self, method: str, seconds: float, code: str) -> None:
+        self.rpc_latency.labels(method, code).observe(seconds)
+
+    def observe_step(self, engine, seconds: float, outputs) -> None:
+        sch = engine.scheduler
+        self.step_seconds.observe(seconds)
+        self.running.set(len(sch.running))
+        self.waiting.set(len(sch.waiting))
+        bm = engine.bm
+        self.kv_util.set(1.0 - bm.num_free / max(bm.num_blocks, 1))
+        self.preemptions.set(sch.num_preemptions)
+        n = 0
+        for o in outputs:
+            n += len(o.new_token_ids)
+            if o.finished:
+                self.requests.labels(o.finish_reason or "unknown").inc()
+                m = o.metrics or {}
+                if m.get("ttft_s") is not None:
+                    self.ttft.observe(m["ttft_s"])
+                if m.get("mean_itl_s") is not None:
+                    self.itl.observe(m["mean_itl_s"])
+                if m.get("e2e_s") is not None:
+                    self.e2e.observe(m["e2e_s"])
+        self.output_tokens.inc(n)
+
+
+def current() -> Optional[Metrics]:
+    return _current
+
+
+def set_current(m: Optional[Metrics]) -> None:
+    global _current
+    _current = m

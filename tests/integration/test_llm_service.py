@@ -1,0 +1,163 @@
+"""LLM tools end to end on CPU (tiny Llama/Mixtral, reference ops): gRPC unary + streaming,
+cancellation frees KV, OpenAI-compatible HTTP route, model routing (config 5 tool-call path)."""
+import asyncio
+import json
+import threading
+import time
+
+import grpc
+import pytest
+
+from polykey_service_amd import proto
+from polykey_service_amd.adapters.local_llm import LLMTool, attach_local_llm
+from polykey_service_amd.config.server_config import ServerConfig
+from polykey_service_amd.engine import EngineConfig, LLMEngine
+from polykey_service_amd.engine.async_llm import AsyncLLM
+from polykey_service_amd.parallel.state import ParallelState
+from polykey_service_amd.service import ToolRouter
+from polykey_service_amd.utils import slog
+
+from tests.helpers import ServerThread
+
+
+def make_engine(model="tiny-llama", **kw):
+    return LLMEngine(EngineConfig(model=model, max_num_seqs=8, max_num_batched_tokens=128, max_model_len=512,
+                                  hip_graphs=False, device="cpu", **kw), ParallelState())
+
+
+@pytest.fixture(scope="module")
+def router():
+    r = ToolRouter()
+    log = slog.Logger(open("/dev/null", "w"))
+    attach_local_llm(r, ServerConfig(model="tiny-llama", backend="local"), log, engine=make_engine())
+    # a second backend to exercise model routing ("llm.chat:<model>")
+    mix = AsyncLLM(make_engine("tiny-mixtral"))
+    r.register_model_tool("llm.chat", "tiny-mixtral", LLMTool("llm.chat", "tiny-mixtral", mix, chat=True))
+    r.register_model_tool("llm.generate", "tiny-mixtral", LLMTool("llm.generate", "tiny-mixtral", mix, chat=False))
+    yield r
+    r.llm.shutdown()
+    mix.shutdown()
+
+
+def req(tool, **params):
+    r = proto.ExecuteToolRequest(tool_name=tool)
+    r.parameters.update(params)
+    return r
+
+
+def test_unary_generate_text_and_struct(router):
+    with ServerThread(router) as s, grpc.insecure_channel(s.addr) as ch:
+        call = ch.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                              response_deserializer=proto.ExecuteToolResponse.FromString)
+        r = call(req("llm.generate", prompt="hello", max_tokens=5, ignore_eos=True), timeout=60)
+        assert r.status.code == 200 and r.WhichOneof("output") == "string_output"
+        r = call(req("llm.generate", prompt_token_ids=[1, 5, 6], max_tokens=7, ignore_eos=True, **{"return": "struct"}),
+                 timeout=60)
+        d = proto.struct_to_dict(r.struct_output)
+        assert d["usage"] == {"prompt_tokens": 3.0, "completion_tokens": 7.0, "total_tokens": 10.0}
+        assert d["finish_reason"] == "length" and d["model"] == "tiny-llama"
+        # mock tools still behave exactly like the reference next to the model tools
+        assert call(req("example_tool"), timeout=5).string_output.startswith("Mock execution of example_tool at ")
+        with pytest.raises(grpc.RpcError) as ei:
+            call(req("llm.generate", max_tokens=3), timeout=10)
+        assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+
+
+def test_greedy_is_deterministic_and_batch_invariant(router):
+    with ServerThread(router) as s, grpc.insecure_channel(s.addr) as ch:
+        call = ch.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                              response_deserializer=proto.ExecuteToolResponse.FromString)
+        one = call(req("llm.generate", prompt="same prompt", max_tokens=8, ignore_eos=True), timeout=60).string_output
+        futs = [call.future(req("llm.generate", prompt="same prompt", max_tokens=8, ignore_eos=True), timeout=60)
+                for _ in range(6)]
+        assert all(f.result().string_output == one for f in futs)
+
+
+def test_streaming_chunks_and_final_usage(router):
+    with ServerThread(router) as s, grpc.insecure_channel(s.addr) as ch:
+        st = ch.unary_stream(proto.EXECUTE_TOOL_STREAM, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                             response_deserializer=proto.ExecuteToolResponse.FromString)
+        chunks = list(st(req("llm.chat", messages=[{"role": "user", "content": "hi"}], max_tokens=12,
+                             ignore_eos=True), timeout=60))
+        assert len(chunks) >= 2
+        final = proto.struct_to_dict(chunks[-1].struct_output)
+        text = "".join(c.string_output for c in chunks[:-1])
+        assert final["usage"]["completion_tokens"] == 12 and final["text"] == text
+        assert chunks[-1].status.code == 200
+
+
+def test_model_routing_to_mixtral(router):
+    with ServerThread(router) as s, grpc.insecure_channel(s.addr) as ch:
+        call = ch.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                              response_deserializer=proto.ExecuteToolResponse.FromString)
+        r = call(req("llm.chat:tiny-mixtral", messages=[{"role": "user", "content": "route me"}], max_tokens=4,
+                     ignore_eos=True, **{"return": "struct"}), timeout=60)
+        assert proto.struct_to_dict(r.struct_output)["model"] == "tiny-mixtral"
+        with pytest.raises(grpc.RpcError) as ei:
+            call(req("llm.chat:nope", messages=[{"role": "user", "content": "x"}]), timeout=10)
+        assert ei.value.code() == grpc.StatusCode.NOT_FOUND
+
+
+def test_cancellation_frees_kv(router):
+    eng = router.llm.engine
+    free0 = eng.bm.num_free
+    with ServerThread(router) as s, grpc.insecure_channel(s.addr) as ch:
+        st = ch.unary_stream(proto.EXECUTE_TOOL_STREAM, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                             response_deserializer=proto.ExecuteToolResponse.FromString)
+        it = st(req("llm.generate", prompt="long " * 20, max_tokens=400, ignore_eos=True), timeout=60)
+        next(it)
+        it.cancel()
+        deadline = time.time() + 20
+        while time.time() < deadline and (eng.has_unfinished() or eng.bm.num_free != free0):
+            time.sleep(0.05)
+    assert not eng.has_unfinished() and eng.bm.num_free == free0
+
+
+def test_concurrent_streams_interleave(router):
+    async def run():
+        async with grpc.aio.insecure_channel(addr) as ch:
+            st = ch.unary_stream(proto.EXECUTE_TOOL_STREAM,
+                                 request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                                 response_deserializer=proto.ExecuteToolResponse.FromString)
+
+            async def one(i):
+                n = 0
+                async for c in st(req("llm.generate", prompt_token_ids=[1, 3 + i], max_tokens=6, ignore_eos=True),
+                                  timeout=60):
+                    if c.HasField("struct_output"):
+                        n = int(c.struct_output["usage"]["completion_tokens"])
+                return n
+
+            return await asyncio.gather(*[one(i) for i in range(16)])
+
+    with ServerThread(router) as s:
+        addr = s.addr
+        assert asyncio.run(run()) == [6] * 16
+
+
+def test_openai_routes(router):
+    from fastapi.testclient import TestClient
+
+    from polykey_service_amd.api.openai import create_app
+    c = TestClient(create_app(router))
+    assert c.get("/health").json() == {"status": "ok"}
+    models = [m["id"] for m in c.get("/v1/models").json()["data"]]
+    assert "tiny-llama" in models and "tiny-mixtral" in models
+    r = c.post("/v1/chat/completions", json={"model": "tiny-llama", "max_tokens": 5, "ignore_eos": True,
+                                             "temperature": 0, "messages": [{"role": "user", "content": "hey"}]})
+    body = r.json()
+    assert r.status_code == 200 and body["object"] == "chat.completion"
+    assert body["usage"]["completion_tokens"] == 5 and body["choices"][0]["message"]["role"] == "assistant"
+    r = c.post("/v1/completions", json={"model": "tiny-llama", "prompt": [1, 4, 5], "max_tokens": 3,
+                                        "ignore_eos": True})
+    assert r.json()["usage"] == {"prompt_tokens": 3, "completion_tokens": 3, "total_tokens": 6}
+    with c.stream("POST", "/v1/chat/completions", json={"model": "tiny-llama", "stream": True, "max_tokens": 6,
+                                                        "ignore_eos": True,
+                                                        "messages": [{"role": "user", "content": "s"}]}) as resp:
+        lines = [l for l in resp.iter_lines() if l]
+    assert lines[-1] == "data: [DONE]"
+    last = json.loads(lines[-2][len("data: "):])
+    assert last["usage"]["completion_tokens"] == 6 and last["choices"][0]["finish_reason"] == "length"
+    assert c.post("/v1/chat/completions", json={"model": "nope", "messages": [{"role": "user", "content": "x"}]}
+                  ).status_code == 404
+    assert c.post("/v1/chat/completions", json={"messages": []}).status_code == 400

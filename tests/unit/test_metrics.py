@@ -1,0 +1,31 @@
+"""Prometheus metrics wiring (RPC observer + engine step observer)."""
+from prometheus_client import generate_latest
+
+from polykey_service_amd.engine.sequence import RequestOutput
+from polykey_service_amd.utils.metrics import Metrics
+
+
+class _BM:
+    num_free, num_blocks = 30, 40
+
+
+class _Sch:
+    running, waiting, num_preemptions = [1, 2], [3], 2
+
+
+class _Eng:
+    bm, scheduler = _BM(), _Sch()
+
+
+def test_metrics_export():
+    m = Metrics()
+    m.observe_rpc("/polykey.v2.PolykeyService/ExecuteTool", 0.01, "OK")
+    outs = [RequestOutput("a", [5], False), RequestOutput("b", [6], True, "length", 3, 4,
+                                                          {"ttft_s": 0.1, "mean_itl_s": 0.01, "e2e_s": 0.2})]
+    m.observe_step(_Eng(), 0.005, outs)
+    text = generate_latest(m.registry).decode()
+    assert 'polykey_rpc_latency_seconds_count{code="OK",method="/polykey.v2.PolykeyService/ExecuteTool"} 1.0' in text
+    assert "polykey_llm_output_tokens_total 2.0" in text
+    assert 'polykey_llm_requests_total{finish_reason="length"} 1.0' in text
+    assert "polykey_engine_kv_utilization 0.25" in text
+    assert "polykey_engine_running_seqs 2.0" in text and "polykey_llm_ttft_seconds_count 1.0" in text
