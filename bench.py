@@ -182,7 +182,7 @@ def main(argv=None) -> int:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / max(args.steps, 1) * 1000.0, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if st.tp_size > 1 and st.dp_size == 1 else "weak",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (random prompt token ids, random-init weights, ignore_eos)",

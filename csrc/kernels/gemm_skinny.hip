@@ -28,6 +28,10 @@ constexpr int kR = 2;        // 16-row W tiles per wave
 enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2 };
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+// weights are streamed once per step: non-temporal loads skip L2 retention (guide: nt-weights)
+__device__ __forceinline__ bf16x8_t ld8_nt(const bf16_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(p));
+}
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
@@ -40,7 +44,7 @@ __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); 
 constexpr int kKC = 256;           // k per LDS chunk
 constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows shift one 16-B slot)
 
-template <int MT, int MODE>
+template <int MT, int MODE, bool NT>
 __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(bf16_t* __restrict__ out, float* __restrict__ partial,
                                                              const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                              int M, int N, int K, int lda, int ldo, int S, int n_blocks) {
@@ -90,7 +94,7 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(bf16_t* __restrict_
 #pragma unroll
     for (int t = 0; t < kR; ++t)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) dst[t][s] = ld8(wp[t] + k + 32 * s);
+      for (int s = 0; s < 4; ++s) dst[t][s] = NT ? ld8_nt(wp[t] + k + 32 * s) : ld8(wp[t] + k + 32 * s);
   };
   auto mma_step = [&](const bf16x8_t (&wf)[kR][4], int buf, int kk) {
 #pragma unroll
@@ -331,16 +335,16 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
   }
 }
 
-template <int MODE>
+template <int MODE, bool NT>
 int launch(int MT, bf16_t* out, float* partial, const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldo,
            int S, hipStream_t stream) {
   const int n_blocks = N / 128;
   const int grid = n_blocks * S;
   switch (MT) {
-    case 1: skinny_gemm_kernel<1, MODE><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 2: skinny_gemm_kernel<2, MODE><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 3: skinny_gemm_kernel<3, MODE><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 4: skinny_gemm_kernel<4, MODE><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+    case 1: skinny_gemm_kernel<1, MODE, NT><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+    case 2: skinny_gemm_kernel<2, MODE, NT><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+    case 3: skinny_gemm_kernel<3, MODE, NT><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+    case 4: skinny_gemm_kernel<4, MODE, NT><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
@@ -359,10 +363,19 @@ PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void
   auto p = static_cast<float*>(partial);
   auto a = static_cast<const bf16_t*>(A);
   auto w = static_cast<const bf16_t*>(W);
-  switch (mode) {
-    case kBF16: return S == 1 ? launch<kBF16>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream) : -1;
-    case kPartial: return launch<kPartial>(MT, o, p, a, w, M, N, K, lda, ldo, S, stream);
-    case kSiluMul: return S == 1 ? launch<kSiluMul>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream) : -1;
+  const bool nt = (mode & 8) != 0;  // bit 3: non-temporal weight loads
+  switch (mode & 7) {
+    case kBF16:
+      if (S != 1) return -1;
+      return nt ? launch<kBF16, true>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream)
+                : launch<kBF16, false>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream);
+    case kPartial:
+      return nt ? launch<kPartial, true>(MT, o, p, a, w, M, N, K, lda, ldo, S, stream)
+                : launch<kPartial, false>(MT, o, p, a, w, M, N, K, lda, ldo, S, stream);
+    case kSiluMul:
+      if (S != 1) return -1;
+      return nt ? launch<kSiluMul, true>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream)
+                : launch<kSiluMul, false>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream);
     default: return -1;
   }
 }

@@ -1,4 +1,3 @@
 set -e
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -m pytest tests -m gpu -q -x 2>&1 | tail -30
-timeout -k 10 900 python bench.py --steps 2 --warmup 1 2>&1 | tail -3
+timeout -k 10 300 python tools/bench_gemm.py 64 2>&1 | tail -12

@@ -19,6 +19,7 @@ from typing import Dict, List, Optional
 
 from .. import proto
 from ..engine.sequence import SamplingParams
+from ..engine.tokenizer import IncrementalDetokenizer
 from ..service.base import RequestContext, ToolError, ok_status
 
 
@@ -109,25 +110,30 @@ class LLMTool:
         prompt = self._prompt(params)
         sp = self._sampling(params)
         toks: List[int] = []
-        sent = 0
         last = None
-        text = ""
+        detok = IncrementalDetokenizer(self.tok)
         agen = self.llm.generate(prompt, sp, request_id=ctx.request_id)
         try:
             async for out in agen:
                 toks.extend(out.new_token_ids)
                 last = out
-                text = self.tok.decode(toks)
-                cut = self._stop_hit(text, sp.stop) if sp.stop else None
+                before = len(detok.text)
+                delta = detok.push(out.new_token_ids)
+                cut = self._stop_hit(detok.text, sp.stop) if sp.stop else None
                 if cut is not None:
-                    text = text[:cut]
-                if len(text) > sent and not text.endswith("�"):
-                    yield proto.ExecuteToolResponse(string_output=text[sent:])
-                    sent = len(text)
+                    delta = detok.text[before:cut] if cut > before else ""
+                    detok.text = detok.text[:cut]
+                if delta:
+                    yield proto.ExecuteToolResponse(string_output=delta)
                 if cut is not None:
                     break
+            else:
+                tail = detok.flush()
+                if tail:
+                    yield proto.ExecuteToolResponse(string_output=tail)
         finally:
             await agen.aclose()
+        text = detok.text
         final = proto.ExecuteToolResponse(status=_status())
         final.struct_output.update(self._summary(text, len(prompt), toks, last, t0))
         yield final

@@ -92,8 +92,9 @@ def create_app(router):
 
         if body.get("stream"):
             async def sse():
+                from ..engine.tokenizer import IncrementalDetokenizer
                 toks: List[int] = []
-                sent = 0
+                detok = IncrementalDetokenizer(tok)
                 finish = None
                 if chat:
                     first = {"id": rid, "object": "chat.completion.chunk", "created": created, "model": model,
@@ -104,10 +105,8 @@ def create_app(router):
                     async for out in agen:
                         toks.extend(out.new_token_ids)
                         finish = out.finish_reason
-                        text = tok.decode(toks)
-                        if len(text) > sent and not text.endswith("�"):
-                            delta = text[sent:]
-                            sent = len(text)
+                        delta = detok.push(out.new_token_ids)
+                        if delta:
                             choice = ({"index": 0, "delta": {"content": delta}, "finish_reason": None} if chat
                                       else {"index": 0, "text": delta, "finish_reason": None})
                             ch = {"id": rid, "object": obj + (".chunk" if chat else ""), "created": created,

@@ -64,6 +64,16 @@ class AsyncLLM:
         try:
             while True:
                 item = await q.get()
+                # coalesce whatever else already arrived: a lagging consumer gets one message
+                # carrying several tokens instead of one message per engine step
+                while not isinstance(item, BaseException) and not item.finished and not q.empty():
+                    nxt = q.get_nowait()
+                    if isinstance(nxt, BaseException):
+                        item = nxt
+                        break
+                    item = RequestOutput(item.request_id, item.new_token_ids + nxt.new_token_ids, nxt.finished,
+                                         nxt.finish_reason, nxt.num_prompt_tokens, nxt.num_output_tokens,
+                                         nxt.metrics)
                 if isinstance(item, BaseException):
                     finished = True
                     raise item

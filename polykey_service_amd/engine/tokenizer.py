@@ -56,6 +56,36 @@ class HFTokenizer:
         return format_chat(messages)
 
 
+class IncrementalDetokenizer:
+    """Streaming detokenization in O(window) per step (decode the tail since the last emitted
+    boundary, diff against its already-emitted prefix, hold back incomplete UTF-8)."""
+
+    def __init__(self, tok):
+        self.tok = tok
+        self.ids: List[int] = []
+        self.prefix = 0
+        self.read = 0
+        self.text = ""
+
+    def push(self, new_ids: List[int]) -> str:
+        self.ids.extend(new_ids)
+        prefix_text = self.tok.decode(self.ids[self.prefix:self.read])
+        new_text = self.tok.decode(self.ids[self.prefix:])
+        if len(new_text) > len(prefix_text) and not new_text.endswith("\ufffd"):
+            delta = new_text[len(prefix_text):]
+            self.prefix, self.read = self.read, len(self.ids)
+            self.text += delta
+            return delta
+        return ""
+
+    def flush(self) -> str:
+        """Whatever is still held back (e.g. a trailing incomplete UTF-8 sequence)."""
+        rest = self.tok.decode(self.ids[self.prefix:])[len(self.tok.decode(self.ids[self.prefix:self.read])):]
+        self.prefix = self.read = len(self.ids)
+        self.text += rest
+        return rest
+
+
 def format_chat(messages: List[Dict[str, str]]) -> str:
     """Llama-3 style chat markup (header/eot markers as plain text for the byte tokenizer)."""
     parts = []

@@ -26,6 +26,8 @@ _KCHUNK = 256
 # The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see
 # tools/bench_gemm.py and profiles/); POLYKEY_SKINNY_GEMM=0/1 forces it off/on.
 SKINNY_ENABLED = os.environ.get("POLYKEY_SKINNY_GEMM", "1") == "1"
+# non-temporal weight loads (mode bit 3); measured per shape by tools/bench_gemm.py
+NT = 8 if os.environ.get("POLYKEY_SKINNY_NT", "0") == "1" else 0
 
 
 @dataclasses.dataclass
@@ -85,7 +87,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     if out is None:
         out = torch.empty((M, N), dtype=x.dtype, device=x.device)
     native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0), out.stride(0),
-                1, 0, native.stream_ptr())
+                1, 0 | NT, native.stream_ptr())
     return out
 
 
@@ -95,7 +97,7 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
     N = w.shape[0]
     S = S or choose_split(N, K, M)
     assert ws.numel() >= S * M * N, "split-K workspace too small"
-    native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0), N, S, 1,
+    native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0), N, S, 1 | NT,
                 native.stream_ptr())
     return Partial(ws, S, M, N)
 
@@ -110,7 +112,7 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
     S = choose_split(N, K, M)
     if S == 1 or ws is None or ws.numel() < S * M * N:
         native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), w_gu_interleaved.data_ptr(), M, N, K,
-                    x.stride(0), out.stride(0), 1, 2, native.stream_ptr())
+                    x.stride(0), out.stride(0), 1, 2 | NT, native.stream_ptr())
     else:
         p = linear_partial(x, w_gu_interleaved, ws, S)
         native.call("pk_splitk_reduce", out.data_ptr(), ws.data_ptr(), S, M, N, out.stride(0), 1, native.stream_ptr())
