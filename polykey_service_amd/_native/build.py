@@ -57,7 +57,7 @@ def targets() -> List[Target]:
     return [
         Target("libpk_kernels", "hip", _g("csrc/kernels/*.hip"), _g("csrc/kernels/*.h") + _g("csrc/kernels/*.cuh")),
         Target("libpk_comm", "hip", _g("csrc/comm/*.hip"), _g("csrc/comm/*.h")),
-        Target("_pk_aesgcm", "pybind", _g("csrc/security/*.cpp"), [], ["crypto"]),
+        Target("_pk_aesgcm", "pybind", _g("csrc/security/*.cpp"), _g("csrc/security/*.h"), ["crypto"]),
         Target("_pk_runtime", "pybind", _g("csrc/runtime/*.cpp"), _g("csrc/runtime/*.h")),
     ]
 

@@ -139,23 +139,78 @@ class LLMTool:
         yield final
 
 
+class ReplicaPool:
+    """Request-level data parallelism inside one server process (SURVEY.md §2.3 "DP"):
+    one engine per GPU (each on its own thread and HIP device), every request goes to the
+    replica with the fewest unfinished sequences.  Duck-types :class:`AsyncLLM`."""
+
+    def __init__(self, replicas):
+        self.replicas = list(replicas)
+        self.tokenizer = self.replicas[0].tokenizer
+        self.engine = self.replicas[0].engine
+        self.on_fatal = None
+        self.watchdog_s = 0.0
+
+    def _pick(self):
+        return min(self.replicas, key=lambda r: r.engine.scheduler.num_unfinished() + len(r._cmds))
+
+    def generate(self, prompt_ids, params, request_id=None):
+        return self._pick().generate(prompt_ids, params, request_id)
+
+    async def generate_all(self, prompt_ids, params, request_id=None):
+        return await self._pick().generate_all(prompt_ids, params, request_id)
+
+    def healthy(self) -> bool:
+        return all(r.healthy() for r in self.replicas)
+
+    def __setattr__(self, k, v):
+        object.__setattr__(self, k, v)
+        if k in ("on_fatal", "watchdog_s") and "replicas" in self.__dict__:
+            for r in self.replicas:
+                setattr(r, k, v)
+
+    def shutdown(self, timeout: float = 10.0) -> None:
+        for r in self.replicas:
+            r.shutdown(timeout)
+
+    async def aclose(self) -> None:
+        for r in self.replicas:
+            await r.aclose()
+
+
 def attach_local_llm(router, cfg, logger, engine=None):
     """Build (or reuse) the engine for ``cfg.model`` and register its tools."""
     from ..engine.async_llm import AsyncLLM
     from ..engine.llm_engine import EngineConfig, LLMEngine
     from ..parallel.state import init_parallel
 
-    if engine is None:
-        st = init_parallel(tp=cfg.tp, ep=cfg.ep)
-        engine = LLMEngine(EngineConfig.from_server_config(cfg), st)
-        if st.tp_rank != 0:
-            engine.runner.worker_loop()  # never returns until the leader stops
-            raise SystemExit(0)
-    llm = AsyncLLM(engine)
+    if engine is None and getattr(cfg, "replicas", 1) > 1 and cfg.tp == 1:
+        import dataclasses as _dc
+
+        import torch
+
+        from ..parallel.state import ParallelState
+        n = cfg.replicas
+        engines = []
+        for i in range(n):
+            dev = torch.device(f"cuda:{i}") if torch.cuda.is_available() else torch.device("cpu")
+            ecfg = _dc.replace(EngineConfig.from_server_config(cfg), device=str(dev))
+            engines.append(LLMEngine(ecfg, ParallelState(device=dev)))
+        llm = ReplicaPool([AsyncLLM(e) for e in engines])
+        engine = engines[0]
+    else:
+        if engine is None:
+            st = init_parallel(tp=cfg.tp, ep=cfg.ep)
+            engine = LLMEngine(EngineConfig.from_server_config(cfg), st)
+            if st.tp_rank != 0:
+                engine.runner.worker_loop()  # never returns until the leader stops
+                raise SystemExit(0)
+        llm = AsyncLLM(engine)
     name = cfg.model if isinstance(cfg.model, str) else "model"
     router.register_model_tool("llm.generate", name, LLMTool("llm.generate", name, llm, chat=False))
     router.register_model_tool("llm.chat", name, LLMTool("llm.chat", name, llm, chat=True))
     router.llm = llm
     logger.info("local LLM backend ready", model=name, kv_blocks=engine.runner.num_blocks,
-                block_size=engine.cfg.block_size, tp=engine.st.tp_size)
+                block_size=engine.cfg.block_size, tp=engine.st.tp_size,
+                replicas=len(getattr(llm, "replicas", [llm])))
     return llm

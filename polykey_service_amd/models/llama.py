@@ -206,6 +206,50 @@ class LlamaForCausalLM(nn.Module):
         mlp.gate_up = _p(gemm.interleave_gate_up(g, u).contiguous())
         mlp.down = _p(shard_cols(get(p + "mlp.down_proj.weight"), r, tp).contiguous())
 
+    def hf_state_dict(self) -> dict:
+        """Weights under HF Llama/Mixtral names (unfused q/k/v, gate/up; TP=1 only)."""
+        assert self.st.tp_size == 1, "export a TP=1 model"
+        cfg = self.cfg
+        q_sz, kv_sz = cfg.q_size, cfg.kv_size
+        out = {"model.embed_tokens.weight": self.embed[:cfg.vocab_size], "model.norm.weight": self.norm}
+        if self.lm_head is not self.embed:
+            out["lm_head.weight"] = self.lm_head[:cfg.vocab_size]
+        for i, layer in enumerate(self.layers):
+            p = f"model.layers.{i}."
+            q, k, v = layer.attn.qkv.split([q_sz, kv_sz, kv_sz])
+            out.update({p + "self_attn.q_proj.weight": q, p + "self_attn.k_proj.weight": k,
+                        p + "self_attn.v_proj.weight": v, p + "self_attn.o_proj.weight": layer.attn.o,
+                        p + "input_layernorm.weight": layer.ln1, p + "post_attention_layernorm.weight": layer.ln2})
+            out.update(self._mlp_hf_state(p, layer.mlp))
+        return {k: v.detach().contiguous().cpu() for k, v in out.items()}
+
+    def _mlp_hf_state(self, p: str, mlp) -> dict:
+        g, u = gemm.deinterleave_gate_up(mlp.gate_up)
+        return {p + "mlp.gate_proj.weight": g, p + "mlp.up_proj.weight": u, p + "mlp.down_proj.weight": mlp.down}
+
+    def save_hf(self, path: str) -> None:
+        """Write ``config.json`` + ``model.safetensors`` (checkpoint / export; reload with ``load_hf``)."""
+        import json
+        import os
+
+        from safetensors.torch import save_file
+        os.makedirs(path, exist_ok=True)
+        cfg = self.cfg
+        hf = {"architectures": ["MixtralForCausalLM" if cfg.is_moe else "LlamaForCausalLM"],
+              "vocab_size": cfg.vocab_size, "hidden_size": cfg.hidden_size,
+              "intermediate_size": cfg.intermediate_size, "num_hidden_layers": cfg.num_layers,
+              "num_attention_heads": cfg.num_heads, "num_key_value_heads": cfg.num_kv_heads,
+              "head_dim": cfg.head_dim, "rope_theta": cfg.rope_theta, "rms_norm_eps": cfg.rms_eps,
+              "max_position_embeddings": cfg.max_position, "tie_word_embeddings": cfg.tie_embeddings,
+              "bos_token_id": cfg.bos_token_id, "eos_token_id": cfg.eos_token_id, "_name_or_path": cfg.name}
+        if cfg.is_moe:
+            hf.update(num_local_experts=cfg.num_experts, num_experts_per_tok=cfg.experts_per_token)
+        if cfg.rope_scaling:
+            hf["rope_scaling"] = cfg.rope_scaling
+        with open(os.path.join(path, "config.json"), "w") as f:
+            json.dump(hf, f, indent=1)
+        save_file(self.hf_state_dict(), os.path.join(path, "model.safetensors"))
+
     # ------------------------------------------------------------------ forward
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
         if self.st.tp_size == 1:

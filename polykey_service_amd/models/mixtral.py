@@ -67,6 +67,14 @@ class MixtralForCausalLM(LlamaForCausalLM):
         mlp.w13 = _p(torch.stack(w13).contiguous())
         mlp.w2 = _p(torch.stack(w2).contiguous())
 
+    def _mlp_hf_state(self, p: str, mlp: MixtralMoE) -> dict:
+        out = {p + "block_sparse_moe.gate.weight": mlp.router}
+        for j, e in enumerate(range(mlp.e_lo, mlp.e_hi)):
+            g, u = gemm.deinterleave_gate_up(mlp.w13[j])
+            q = p + f"block_sparse_moe.experts.{e}."
+            out.update({q + "w1.weight": g, q + "w3.weight": u, q + "w2.weight": mlp.w2[j]})
+        return out
+
     def _load_mlp_hf(self, i, mlp: MixtralMoE, get, p) -> None:
         st = self.st
         tp_shard = st.ep_size == 1 and st.tp_size > 1

@@ -161,3 +161,26 @@ def test_openai_routes(router):
     assert c.post("/v1/chat/completions", json={"model": "nope", "messages": [{"role": "user", "content": "x"}]}
                   ).status_code == 404
     assert c.post("/v1/chat/completions", json={"messages": []}).status_code == 400
+
+
+def test_replica_pool_balances_requests():
+    from polykey_service_amd.adapters.local_llm import ReplicaPool
+    pool = ReplicaPool([AsyncLLM(make_engine()), AsyncLLM(make_engine())])
+    r = ToolRouter()
+    r.register_model_tool("llm.generate", "tiny-llama", LLMTool("llm.generate", "tiny-llama", pool, chat=False))
+    r.llm = pool
+
+    async def run():
+        async with grpc.aio.insecure_channel(addr) as ch:
+            call = ch.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                                  response_deserializer=proto.ExecuteToolResponse.FromString)
+            outs = await asyncio.gather(*[call(req("llm.generate", prompt="balance", max_tokens=6, ignore_eos=True),
+                                               timeout=60) for _ in range(12)])
+            return [o.string_output for o in outs]
+
+    with ServerThread(r) as s:
+        addr = s.addr
+        outs = asyncio.run(run())
+    assert len(set(outs)) == 1  # same weights (same seed) on both replicas → same greedy text
+    assert all(rep.stats["requests"] > 0 for rep in pool.replicas)
+    pool.shutdown()
