@@ -28,7 +28,8 @@ def topk_softmax(router_logits: torch.Tensor, k: int, renorm: bool = True) -> Tu
     T, E = router_logits.shape
     if not router_logits.is_cuda:
         p = torch.softmax(router_logits.float(), -1)
-        w, ids = torch.topk(p, k, dim=-1)
+        w, ids = torch.sort(p, dim=-1, descending=True, stable=True)  # ties → lower expert id, as the kernel
+        w, ids = w[:, :k], ids[:, :k]
         if renorm:
             w = w / w.sum(-1, keepdim=True)
         return ids.to(torch.int32), w

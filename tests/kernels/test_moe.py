@@ -18,10 +18,14 @@ def weights(E, H, I, dev="cuda"):
 
 
 def test_topk_softmax():
-    x = torch.randn(100, 8, device="cuda").to(torch.bfloat16)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(100, 8, generator=g).to(torch.bfloat16)
+    x[0, 3] = x[0, 5] = 4.0  # exact tie: the kernel picks the lower expert id
+    x = x.cuda()
     ids, w = moe.topk_softmax(x, 2)
     p = torch.softmax(x.float(), -1)
-    ew, eids = torch.topk(p, 2, -1)
+    ew, eids = torch.sort(p, dim=-1, descending=True, stable=True)
+    ew, eids = ew[:, :2], eids[:, :2]
     assert torch.equal(ids.long().cpu(), eids.cpu())
     torch.testing.assert_close(w.cpu(), (ew / ew.sum(-1, keepdim=True)).cpu(), atol=1e-5, rtol=1e-5)
 
