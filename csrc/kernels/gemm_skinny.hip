@@ -15,6 +15,8 @@
 //     RMSNorm), so a split costs no extra launch on the hot path;
 //   * epilogues: bf16 store, fp32 partial store, or fused SiLU(gate)*up when W's gate/up rows
 //     are interleaved in blocks of 16 (then one wave holds gate and up of the same columns).
+#include <type_traits>
+
 #include "common.h"
 
 using namespace pk;
@@ -28,10 +30,6 @@ constexpr int kR = 2;        // 16-row W tiles per wave
 enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2 };
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
-// weights are streamed once per step: non-temporal loads skip L2 retention (guide: nt-weights)
-__device__ __forceinline__ bf16x8_t ld8_nt(const bf16_t* p) {
-  return __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(p));
-}
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
@@ -44,8 +42,8 @@ __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); 
 constexpr int kKC = 256;           // k per LDS chunk
 constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows shift one 16-B slot)
 
-template <int MT, int MODE, bool NT>
-__global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(bf16_t* __restrict__ out, float* __restrict__ partial,
+template <int MT, int MODE, int D, bool PK>
+__global__ void __launch_bounds__(256, D == 2 ? 2 : 1) skinny_gemm_kernel(bf16_t* __restrict__ out, float* __restrict__ partial,
                                                              const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                              int M, int N, int K, int lda, int ldo, int S, int n_blocks) {
   __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kAStride];
@@ -59,7 +57,9 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(bf16_t* __restrict_
 
   const bf16_t* wp[kR];
 #pragma unroll
-  for (int t = 0; t < kR; ++t) wp[t] = W + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;
+  for (int t = 0; t < kR; ++t)
+    wp[t] = PK ? W + (static_cast<int64_t>((n0 >> 4) + t) * (K >> 5)) * 512 + 8 * lane   // fragment-packed
+               : W + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                // row-major [N, K]
 
   // A staging: MT*16 rows x 256 cols = MT*512 16-byte pieces over 256 threads
   constexpr int kPieces = (16 * MT * kKC / 8 + 255) / 256;
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(bf16_t* __restrict_
 #pragma unroll
     for (int t = 0; t < kR; ++t)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) dst[t][s] = NT ? ld8_nt(wp[t] + k + 32 * s) : ld8(wp[t] + k + 32 * s);
+      for (int s = 0; s < 4; ++s) dst[t][s] = PK ? ld8(wp[t] + static_cast<int64_t>((k >> 5) + s) * 512) : ld8(wp[t] + k + 32 * s);
   };
   auto mma_step = [&](const bf16x8_t (&wf)[kR][4], int buf, int kk) {
 #pragma unroll
@@ -117,24 +117,56 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(bf16_t* __restrict_
   const int nchunks = kper / kKC;
   const int rot = (nb * 5) % nchunks;
   auto chunk_k = [&](int c) { return k0 + ((c + rot) % nchunks) * kKC; };
-  load_a(chunk_k(0));
-  load_w(wa, chunk_k(0));
-  load_w(wb, chunk_k(0) + 128);
-  store_a(0);
-  int buf = 0;
-  for (int c = 0; c < nchunks; ++c) {
-    const bool more = c + 1 < nchunks;
-    const int kn = more ? chunk_k(c + 1) : 0;
-    if (more) load_a(kn);
-    __syncthreads();  // chunk c visible in a_lds[buf]
-    mma_step(wa, buf, 0);
-    if (more) load_w(wa, kn);
-    mma_step(wb, buf, 128);
-    if (more) {
+  // Every load in the loop is unconditional (past the last chunk the address is clamped to it
+  // and the data is dropped): a load behind a branch makes the compiler's vmcnt bookkeeping
+  // assume it was not issued, so it then drains ALL loads (vmcnt(0)) before the next MFMAs and
+  // the W stream stalls once per chunk (measured: ~26 GB/s per workgroup).
+  auto ck = [&](int c) { return chunk_k(min(c, nchunks - 1)); };
+  if constexpr (D == 2) {
+    // ring of 2 k-steps: W for the current chunk's two 128-steps in flight
+    load_a(ck(0));
+    load_w(wa, ck(0));
+    load_w(wb, ck(0) + 128);
+    store_a(0);
+    int buf = 0;
+    for (int c = 0; c < nchunks; ++c) {
+      const int kn = ck(c + 1);
+      load_a(kn);
+      __syncthreads();  // chunk c visible in a_lds[buf]; every wave is done with a_lds[buf^1]
+      mma_step(wa, buf, 0);
+      load_w(wa, kn);
+      mma_step(wb, buf, 128);
       load_w(wb, kn + 128);
-      store_a(buf ^ 1);  // last read of buf^1 was before this iteration's barrier
+      store_a(buf ^ 1);
+      buf ^= 1;
     }
-    buf ^= 1;
+  } else {
+    // ring of 4 k-steps (two chunks, ~32 KB per wave in flight); the loop is unrolled over a
+    // chunk pair so every ring slot and LDS buffer index is static.
+    bf16x8_t wc[kR][4], wd[kR][4];
+    load_a(ck(0));
+    load_w(wa, ck(0));
+    load_w(wb, ck(0) + 128);
+    load_w(wc, ck(1));
+    load_w(wd, ck(1) + 128);
+    store_a(0);
+    for (int c = 0; c < nchunks; c += 2) {
+      load_a(ck(c + 1));
+      __syncthreads();  // chunk c visible in a_lds[0]; every wave is done with a_lds[1]
+      mma_step(wa, 0, 0);
+      load_w(wa, ck(c + 2));
+      mma_step(wb, 0, 128);
+      load_w(wb, ck(c + 2) + 128);
+      store_a(1);
+      if (c + 1 >= nchunks) break;  // uniform
+      load_a(ck(c + 2));
+      __syncthreads();  // chunk c+1 visible in a_lds[1]; every wave is done with a_lds[0]
+      mma_step(wc, 1, 0);
+      load_w(wc, ck(c + 3));
+      mma_step(wd, 1, 128);
+      load_w(wd, ck(c + 3) + 128);
+      store_a(0);
+    }
   }
 
   // C^T tile: rows = W rows (n), cols = m:  acc[t][mt][i] = C[m = 16*mt + r][n = n0 + 16*t + 4*g + i]
@@ -335,16 +367,16 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
   }
 }
 
-template <int MODE, bool NT>
+template <int MODE, int D, bool PK>
 int launch(int MT, bf16_t* out, float* partial, const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldo,
            int S, hipStream_t stream) {
   const int n_blocks = N / 128;
   const int grid = n_blocks * S;
   switch (MT) {
-    case 1: skinny_gemm_kernel<1, MODE, NT><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 2: skinny_gemm_kernel<2, MODE, NT><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 3: skinny_gemm_kernel<3, MODE, NT><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 4: skinny_gemm_kernel<4, MODE, NT><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+    case 1: skinny_gemm_kernel<1, MODE, D, PK><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+    case 2: skinny_gemm_kernel<2, MODE, D, PK><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+    case 3: skinny_gemm_kernel<3, MODE, D, PK><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+    case 4: skinny_gemm_kernel<4, MODE, D, PK><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
@@ -363,19 +395,25 @@ PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void
   auto p = static_cast<float*>(partial);
   auto a = static_cast<const bf16_t*>(A);
   auto w = static_cast<const bf16_t*>(W);
-  const bool nt = (mode & 8) != 0;  // bit 3: non-temporal weight loads
+  const bool deep = (mode & 8) != 0;     // bit 3: 4-step W register ring instead of 2
+  const bool packed = (mode & 16) != 0;  // bit 4: W in fragment-packed layout (pk_pack_weight)
+  auto go = [&](auto mode_c) -> int {
+    constexpr int MD = decltype(mode_c)::value;
+    const int s_ = MD == kPartial ? S : 1;
+    if (packed) return deep ? launch<MD, 4, true>(MT, o, p, a, w, M, N, K, lda, ldo, s_, stream)
+                            : launch<MD, 2, true>(MT, o, p, a, w, M, N, K, lda, ldo, s_, stream);
+    return deep ? launch<MD, 4, false>(MT, o, p, a, w, M, N, K, lda, ldo, s_, stream)
+                : launch<MD, 2, false>(MT, o, p, a, w, M, N, K, lda, ldo, s_, stream);
+  };
   switch (mode & 7) {
     case kBF16:
       if (S != 1) return -1;
-      return nt ? launch<kBF16, true>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream)
-                : launch<kBF16, false>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream);
+      return go(std::integral_constant<int, kBF16>{});
     case kPartial:
-      return nt ? launch<kPartial, true>(MT, o, p, a, w, M, N, K, lda, ldo, S, stream)
-                : launch<kPartial, false>(MT, o, p, a, w, M, N, K, lda, ldo, S, stream);
+      return go(std::integral_constant<int, kPartial>{});
     case kSiluMul:
       if (S != 1) return -1;
-      return nt ? launch<kSiluMul, true>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream)
-                : launch<kSiluMul, false>(MT, o, p, a, w, M, N, K, lda, ldo, 1, stream);
+      return go(std::integral_constant<int, kSiluMul>{});
     default: return -1;
   }
 }

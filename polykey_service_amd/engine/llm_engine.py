@@ -68,6 +68,8 @@ class LLMEngine:
             else:
                 model.init_random(cfg.seed)
         self.model = model
+        if hasattr(model, "pack_decode_weights"):
+            model.pack_decode_weights()
         self.tokenizer = get_tokenizer(cfg.tokenizer, mcfg.vocab_size, mcfg.bos_token_id, mcfg.eos_token_id)
         rcfg = RunnerConfig(block_size=cfg.block_size, max_num_seqs=cfg.max_num_seqs,
                             max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=cfg.max_model_len,

@@ -18,6 +18,7 @@ LM head for TP>1 (logits all-gathered for sampling).
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -38,23 +39,25 @@ def _p(t: torch.Tensor) -> nn.Parameter:
     return nn.Parameter(t, requires_grad=False)
 
 
-def _proj(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor]) -> torch.Tensor:
-    """Column-parallel projection → bf16 (skinny split-K + reduce for decode-sized M)."""
+def _proj(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor],
+          wp: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Column-parallel projection → bf16 (skinny split-K + reduce for decode-sized M).
+    ``wp``: the fragment-packed copy of ``w`` streamed by the decode GEMM (None: row-major)."""
     if ws is not None and gemm.skinny_ok(x, w):
         S = gemm.choose_split(w.shape[0], x.shape[1], x.shape[0])
         if S > 1 and ws.numel() >= S * x.shape[0] * w.shape[0]:
-            return gemm.reduce_partial(gemm.linear_partial(x, w, ws, S))
-    return gemm.linear(x, w)
+            return gemm.reduce_partial(gemm.linear_partial(x, w, ws, S, packed=wp))
+    return gemm.linear(x, w, packed=wp)
 
 
-def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor]):
+def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: Optional[torch.Tensor] = None):
     """Row-parallel projection feeding a residual add + RMSNorm.  TP=1 decode returns the
     split-K partial slabs unreduced (the norm kernel sums them); TP>1 all-reduces bf16."""
     if get_state().tp_size == 1 and ws is not None and gemm.skinny_ok(x, w) and gemm.norm_fusable(w.shape[0]):
         S = gemm.choose_split(w.shape[0], x.shape[1], x.shape[0])
         if ws.numel() >= S * x.shape[0] * w.shape[0]:
-            return gemm.linear_partial(x, w, ws, S)
-    return comm.tp_all_reduce(_proj(x, w, ws))
+            return gemm.linear_partial(x, w, ws, S, packed=wp)
+    return comm.tp_all_reduce(_proj(x, w, ws, wp))
 
 
 def add_norm(pending, residual: torch.Tensor, w: torch.Tensor, eps: float):
@@ -74,6 +77,8 @@ class LlamaAttention(nn.Module):
         self.scale = 1.0 / math.sqrt(self.hd)
         self.qkv = None
         self.o = None
+        self.qkv_p = None  # fragment-packed decode copies (LlamaForCausalLM.pack_decode_weights)
+        self.o_p = None
 
     def forward(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
                 kv: Tuple[torch.Tensor, torch.Tensor], ws: Optional[torch.Tensor] = None):
@@ -84,15 +89,16 @@ class LlamaAttention(nn.Module):
         S = gemm.choose_split(self.qkv.shape[0], x.shape[1], T)
         if ws is not None and gemm.skinny_ok(x, self.qkv) and S > 1 and ws.numel() >= S * T * self.qkv.shape[0]:
             # decode: split-K QKV whose epilogue kernel also applies RoPE and writes the KV cache
-            q = gemm.qkv_reduce_rope_cache(gemm.linear_partial(x, self.qkv, ws, S), positions, cos_sin, k_cache,
+            q = gemm.qkv_reduce_rope_cache(gemm.linear_partial(x, self.qkv, ws, S, packed=self.qkv_p), positions,
+                                           cos_sin, k_cache,
                                            v_cache, md.slot_mapping, self.nq, self.nkv)
         else:
-            qkv = gemm.linear(x, self.qkv)
+            qkv = gemm.linear(x, self.qkv, packed=self.qkv_p)
             attn_ops.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq, self.nkv,
                                     self.hd)
             q = qkv.view(T, self.nq + 2 * self.nkv, self.hd)[:, :self.nq]
         a = attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
-        return _proj_out(a, self.o, ws)
+        return _proj_out(a, self.o, ws, self.o_p)
 
 
 class LlamaMLP(nn.Module):
@@ -100,10 +106,12 @@ class LlamaMLP(nn.Module):
         super().__init__()
         self.gate_up = None
         self.down = None
+        self.gate_up_p = None
+        self.down_p = None
 
     def forward(self, x: torch.Tensor, ws: Optional[torch.Tensor] = None):
-        h = gemm.linear_silu(x, self.gate_up, ws)  # gate/up rows interleaved in blocks of 16
-        return _proj_out(h, self.down, ws)
+        h = gemm.linear_silu(x, self.gate_up, ws, packed=self.gate_up_p)  # gate/up rows interleaved by 16
+        return _proj_out(h, self.down, ws, self.down_p)
 
 
 class LlamaLayer(nn.Module):
@@ -297,6 +305,31 @@ class LlamaForCausalLM(nn.Module):
 
     def _mlp_weights(self, mlp) -> tuple:
         return (mlp.gate_up, mlp.down)
+
+    def pack_decode_weights(self, mode: Optional[str] = None) -> bool:
+        """Give every dense projection a fragment-packed copy (:func:`gemm.pack_weight`) for the
+        decode GEMM, which streams it ~1.2-1.35x faster than row-major (tools/bench_gemm.py).
+        Prefill keeps using the row-major weight through hipBLASLt, so this doubles projection
+        memory: ``auto`` packs only when both copies fit in 60 % of HBM (8B: +15 GB of 288 GB;
+        70B on one GPU: skipped).  ``POLYKEY_PACKED_WEIGHTS`` = auto | 1 | 0."""
+        mode = mode or os.environ.get("POLYKEY_PACKED_WEIGHTS", "auto")
+        if mode == "0" or self.device.type != "cuda" or not gemm.SKINNY_ENABLED:
+            return False
+        if mode == "auto":
+            total = torch.cuda.get_device_properties(self.device).total_memory
+            proj = sum(w.numel() * w.element_size() for layer in self.layers
+                       for w in (layer.attn.qkv, layer.attn.o) + self._mlp_weights(layer.mlp) if w is not None)
+            if 2 * proj + self.lm_head.numel() * self.lm_head.element_size() > 0.6 * total:
+                return False
+        for layer in self.layers:
+            layer.attn.qkv_p = gemm.pack_weight(layer.attn.qkv)
+            layer.attn.o_p = gemm.pack_weight(layer.attn.o)
+            self._pack_mlp(layer.mlp)
+        return True
+
+    def _pack_mlp(self, mlp) -> None:
+        mlp.gate_up_p = gemm.pack_weight(mlp.gate_up)
+        mlp.down_p = gemm.pack_weight(mlp.down)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """hidden [B, H] → logits [B, vocab] (bf16; all-gathered across TP)."""

@@ -67,6 +67,9 @@ class MixtralForCausalLM(LlamaForCausalLM):
         mlp.w13 = _p(torch.stack(w13).contiguous())
         mlp.w2 = _p(torch.stack(w2).contiguous())
 
+    def _pack_mlp(self, mlp) -> None:
+        pass  # experts are streamed by the grouped MoE kernel in their own layout
+
     def _mlp_hf_state(self, p: str, mlp: MixtralMoE) -> dict:
         out = {p + "block_sparse_moe.gate.weight": mlp.router}
         for j, e in enumerate(range(mlp.e_lo, mlp.e_hi)):

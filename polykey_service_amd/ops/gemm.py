@@ -26,8 +26,10 @@ _KCHUNK = 256
 # The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see
 # tools/bench_gemm.py and profiles/); POLYKEY_SKINNY_GEMM=0/1 forces it off/on.
 SKINNY_ENABLED = os.environ.get("POLYKEY_SKINNY_GEMM", "1") == "1"
-# non-temporal weight loads (mode bit 3); measured per shape by tools/bench_gemm.py
-NT = 8 if os.environ.get("POLYKEY_SKINNY_NT", "0") == "1" else 0
+# mode bit 3: 4-step (instead of 2-step) W register ring, ~32 KB per wave in flight;
+# measured per shape by tools/bench_gemm.py
+DEEP = 8 if os.environ.get("POLYKEY_SKINNY_DEEP", "0") == "1" else 0
+PACKED_BIT = 16
 
 
 @dataclasses.dataclass
@@ -78,31 +80,56 @@ def norm_fusable(H: int) -> bool:
     return H % 1024 == 0 and H <= 8192
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """bf16 out [M, N]."""
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """Row-major ``[N, K]`` → fragment-packed layout for the decode GEMM (same size).
+
+    Every (16-row tile, 32-k block) fragment is stored as 1 KiB in MFMA A-operand lane order
+    (lane l = 16*g + r holds row r, k = 8g..8g+7), so each wave load instruction reads 1 KiB
+    contiguous instead of 64 B from each of 16 rows."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 32 == 0
+    return w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+
+
+def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
+    N, K = wp.shape
+    return wp.view(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().view(N, K)
+
+
+def _wmode(packed: Optional[torch.Tensor]) -> int:
+    return DEEP | (PACKED_BIT if packed is not None else 0)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
+           packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 out [M, N]; ``packed`` = :func:`pack_weight` (w) streamed instead of ``w`` when given."""
     if not skinny_ok(x, w):
         return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
     M, K = x.shape
     N = w.shape[0]
     if out is None:
         out = torch.empty((M, N), dtype=x.dtype, device=x.device)
-    native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0), out.stride(0),
-                1, 0 | NT, native.stream_ptr())
+    src = packed if packed is not None else w
+    native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), src.data_ptr(), M, N, K, x.stride(0),
+                out.stride(0), 1, 0 | _wmode(packed), native.stream_ptr())
     return out
 
 
-def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Optional[int] = None) -> Partial:
+def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Optional[int] = None,
+                   packed: Optional[torch.Tensor] = None) -> Partial:
     """Split-K fp32 slabs into workspace ``ws`` (fp32, >= S*M*N)."""
     M, K = x.shape
     N = w.shape[0]
     S = S or choose_split(N, K, M)
     assert ws.numel() >= S * M * N, "split-K workspace too small"
-    native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0), N, S, 1 | NT,
-                native.stream_ptr())
+    src = packed if packed is not None else w
+    native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), src.data_ptr(), M, N, K, x.stride(0), N, S,
+                1 | _wmode(packed), native.stream_ptr())
     return Partial(ws, S, M, N)
 
 
-def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[torch.Tensor] = None,
+                packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     """silu(x @ Wg^T) * (x @ Wu^T) with interleaved gate/up rows → [M, I]."""
     if not skinny_ok(x, w_gu_interleaved):
         return silu_and_mul_interleaved(linear(x, w_gu_interleaved))
@@ -111,10 +138,11 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
     out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
     S = choose_split(N, K, M)
     if S == 1 or ws is None or ws.numel() < S * M * N:
-        native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), w_gu_interleaved.data_ptr(), M, N, K,
-                    x.stride(0), out.stride(0), 1, 2 | NT, native.stream_ptr())
+        src = packed if packed is not None else w_gu_interleaved
+        native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), src.data_ptr(), M, N, K,
+                    x.stride(0), out.stride(0), 1, 2 | _wmode(packed), native.stream_ptr())
     else:
-        p = linear_partial(x, w_gu_interleaved, ws, S)
+        p = linear_partial(x, w_gu_interleaved, ws, S, packed=packed)
         native.call("pk_splitk_reduce", out.data_ptr(), ws.data_ptr(), S, M, N, out.stride(0), 1, native.stream_ptr())
     return out
 

@@ -8,6 +8,13 @@ from polykey_service_amd.ops import reference as ref
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=[0, 8], ids=["ring2", "ring4"], autouse=True)
+def w_ring_depth(request):
+    """Every test runs with the 2-step and the 4-step W register ring (mode bit 3)."""
+    old = gemm.DEEP
+    gemm.DEEP = request.param
+    yield
+    gemm.DEEP = old
 
 def rnd(*shape, scale=1.0):
     return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
@@ -86,3 +93,28 @@ def test_qkv_reduce_rope_cache(nq, nkv, bs, M):
     torch.testing.assert_close(q.float(), qkv.view(M, -1, 128)[:, :nq].float(), atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(kc.float(), kc2.float(), atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(vc.float(), vc2.float(), atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("N,K,S", [(6144, 4096, 4), (4096, 14336, 8), (128, 256, 1)])
+def test_fragment_packed_weights(M, N, K, S):
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    wp = gemm.pack_weight(w)
+    assert torch.equal(gemm.unpack_weight(wp), w)
+    exp = x.float() @ w.float().t()
+    torch.testing.assert_close(gemm.linear(x, w, packed=wp).float(), exp, atol=2e-2, rtol=2e-2)
+    ws = torch.empty(max(S, 1) * M * N, dtype=torch.float32, device="cuda")
+    if S > 1:
+        p = gemm.linear_partial(x, w, ws, S, packed=wp)
+        torch.testing.assert_close(p.view().sum(0), exp, atol=1e-2, rtol=1e-2)
+
+
+def test_fragment_packed_silu():
+    M, I, K = 9, 3584, 4096
+    x = rnd(M, K)
+    g, u = rnd(I, K, scale=0.05), rnd(I, K, scale=0.05)
+    w = gemm.interleave_gate_up(g, u)
+    exp = ref.silu_and_mul(torch.cat([(x.float() @ g.float().t()), (x.float() @ u.float().t())], -1).to(torch.bfloat16))
+    ws = torch.empty(64 * 2 * I * 16, dtype=torch.float32, device="cuda")
+    y = gemm.linear_silu(x, w, ws, packed=gemm.pack_weight(w))
+    torch.testing.assert_close(y.float(), exp.float(), atol=3e-2, rtol=3e-2)

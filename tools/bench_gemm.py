@@ -52,12 +52,19 @@ for M in (int(a) for a in (sys.argv[1:] or ["64"])):
         if name == "gate_up" or name == "70b_gu":
             ts = timeit(lambda i: gemm.linear_silu(x, ws_list[i], ws), n)
             row += f" | silu {ts:6.1f}us {bytes_/ts/1e6:5.2f}"
-        S = gemm.choose_split(N, K, M)
-        if K % (256 * S) == 0 and N % 128 == 0:
-            gemm.NT = 8
-            tn = timeit(lambda i: gemm.linear_partial(x, ws_list[i], ws, S) if S > 1 else gemm.linear(x, ws_list[i]), n)
-            gemm.NT = 0
-            row += f" | NT(S{S}) {tn:6.1f}us {bytes_/tn/1e6:5.2f}"
+        wp_list = [gemm.pack_weight(w) for w in ws_list]
+        for S in (1, 2, 4, 8, 16):
+            if K % (256 * S) or N % 128:
+                continue
+            if S == 1:
+                tn = timeit(lambda i: gemm.linear(x, ws_list[i], packed=wp_list[i]), n)
+            else:
+                tn = timeit(lambda i: gemm.linear_partial(x, ws_list[i], ws, S, packed=wp_list[i]), n)
+            row += f" | PK-S{S} {tn:6.1f}us {bytes_/tn/1e6:5.2f}"
+        if name in ("gate_up", "70b_gu"):
+            tsd = timeit(lambda i: gemm.linear_silu(x, ws_list[i], ws, packed=wp_list[i]), n)
+            row += f" | PK-silu {tsd:6.1f}us {bytes_/tsd/1e6:5.2f}"
+        del wp_list
         print(row, flush=True)
         del ws_list
         torch.cuda.empty_cache()
