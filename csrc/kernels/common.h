@@ -20,16 +20,16 @@ __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
 
-// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<bf16_t>((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<bf16_t>(u >> 16);
-}
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+// round-to-nearest-even f32 -> bf16: gfx950's v_cvt_pk_bf16_f32 (one VALU op per pair, no
+// branches; a software RNE with a NaN test compiles to exec-mask branches per element)
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, static_cast<__bf16>(f)); }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return static_cast<uint32_t>(f2bf(a)) | (static_cast<uint32_t>(f2bf(b)) << 16);
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 __device__ __forceinline__ void unpack8(const u32x4& v, float* f) {

@@ -21,56 +21,234 @@
 
 using namespace pk;
 
+// kernel arguments of the decode GEMM (mirrored by ops/gemm.py GemmArgs, ctypes)
+struct GemmArgs {
+  bf16_t* out;               // kBF16 / kSiluMul: [M, ldo]; kQkvRope: q [M, nq * 128]
+  float* partial;            // fp32 slabs [S, M, N]
+  const bf16_t* A;           // [M, lda]; with the norm prologue: the residual stream
+  const bf16_t* W;           // [N, K] row-major or fragment-packed
+  int M, N, K, lda, ldo, S;
+  int* counters;             // [N / 128] zeroed once; the last arriver re-arms its counter
+  const float* nrm_parts;    // norm prologue: per-row sums of squares [nrm_nparts, M]
+  const bf16_t* nrm_w;       // [K]
+  int nrm_nparts;
+  float eps;
+  bf16_t* residual;          // kAddResNorm: [M, N], updated in place
+  float* sumsq_parts;        // kAddResNorm: [N / 128, M]
+  const int* positions;      // kQkvRope: [M]
+  const float* cos_sin;      // [max_pos, 128] = cos[64] | sin[64]
+  bf16_t* k_cache;           // [blocks, nkv, bs, 128]
+  bf16_t* v_cache;           // [blocks, nkv, 128, bs]
+  const int* slots;          // [M]
+  int nq, nkv, bs;
+};
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 
 constexpr int kR = 2;        // 16-row W tiles per wave
 
-enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2 };
+// Epilogues.  kAddResNorm / kQkvRope are split-K with an in-launch reduction: every split
+// stores its fp32 slab, the last workgroup of an n-block to arrive (agent-scope release /
+// ticket / acquire, guide §5 "In-launch split-K reduction") sums the slabs and applies:
+//   kAddResNorm: residual[m, n] += bf16(sum)   and writes the per-(n-block, row) sum of squares
+//                of the new residual, consumed by the next GEMM's RMSNorm prologue;
+//   kQkvRope:    128-column n-block = one head: RoPE (neox) for q / k heads, q -> out, k -> K
+//                cache, v -> transposed V cache at the token's slot (slot < 0: not cached).
+enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4 };
+
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+__device__ __forceinline__ float4 ld4f(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void add4(float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; }
+__device__ __forceinline__ float rbf(float x) { return bf2f(f2bf(x)); }
+
+// ---- split-K tile epilogues (run by the last arriving split of n-block nb) ----------------
+// Sum of the SS fp32 slabs of element group (m, c..c+3) / (m, c+64..c+67); SS == 0: runtime S.
+// The loads of a batch of rows are all issued before any add, so one reducer thread has
+// RB * SS 16-byte loads in flight instead of paying the slab latency serially.
+template <int SS>
+__device__ __forceinline__ float4 slab_sum(const float* src, int64_t slab, int S) {
+  if constexpr (SS == 0) {
+    float4 a = ld4f(src);
+    for (int s = 1; s < S; ++s) add4(a, ld4f(src + s * slab));
+    return a;
+  } else {
+    float4 v[SS];
+#pragma unroll
+    for (int s = 0; s < SS; ++s) v[s] = ld4f(src + s * slab);
+#pragma unroll
+    for (int s = 1; s < SS; ++s) add4(v[0], v[s]);
+    return v[0];
+  }
+}
+
+template <int MODE, int SS>
+__device__ void epilogue(const GemmArgs& args, int nb) {
+  const int M = args.M, N = args.N, S = args.S, tid = threadIdx.x;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  const int nbase = nb * 128;
+  constexpr int RB = (SS == 0 || SS >= 16) ? 1 : (SS == 8 ? 2 : 4);  // rows per thread per batch
+  if constexpr (MODE == kAddResNorm) {
+    // 32 threads (half a wave) per row, 4 columns each; 8 rows per pass of the workgroup
+    const int c = nbase + (tid & 31) * 4;
+    for (int m0 = tid >> 5; m0 < M; m0 += 8 * RB) {
+      float4 a[RB];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int m = min(m0 + 8 * i, M - 1);
+        a[i] = slab_sum<SS>(args.partial + static_cast<int64_t>(m) * N + c, slab, S);
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int m = m0 + 8 * i;
+        if (m >= M) break;  // uniform per half-wave
+        bf16_t* res = args.residual + static_cast<int64_t>(m) * N + c;
+        const uint2 rr = *reinterpret_cast<const uint2*>(res);
+        const float v0 = rbf(rbf(a[i].x) + bf2f(static_cast<bf16_t>(rr.x & 0xffff)));
+        const float v1 = rbf(rbf(a[i].y) + bf2f(static_cast<bf16_t>(rr.x >> 16)));
+        const float v2 = rbf(rbf(a[i].z) + bf2f(static_cast<bf16_t>(rr.y & 0xffff)));
+        const float v3 = rbf(rbf(a[i].w) + bf2f(static_cast<bf16_t>(rr.y >> 16)));
+        uint2 o;
+        o.x = pack2(v0, v1);
+        o.y = pack2(v2, v3);
+        *reinterpret_cast<uint2*>(res) = o;
+        float sq = v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) sq += __shfl_xor(sq, off, 32);
+        if ((tid & 31) == 0) args.sumsq_parts[static_cast<int64_t>(nb) * M + m] = sq;
+      }
+    }
+  } else {  // kQkvRope: n-block nb is head nb of q | k | v
+    const int nq = args.nq, nkv = args.nkv, bs = args.bs;
+    if (nb < nq + nkv) {
+      // 16 threads per row, 4 rotation pairs (j, j + 64) each; 16 rows per pass
+      const int j = (tid & 15) * 4;
+      for (int m0 = tid >> 4; m0 < M; m0 += 16 * RB) {
+        float4 a[RB], b[RB];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int m = min(m0 + 16 * i, M - 1);
+          const float* src = args.partial + static_cast<int64_t>(m) * N + nbase + j;
+          a[i] = slab_sum<SS>(src, slab, S);
+          b[i] = slab_sum<SS>(src + 64, slab, S);
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int m = m0 + 16 * i;
+          if (m >= M) break;
+          const float av[4] = {rbf(a[i].x), rbf(a[i].y), rbf(a[i].z), rbf(a[i].w)};
+          const float bv[4] = {rbf(b[i].x), rbf(b[i].y), rbf(b[i].z), rbf(b[i].w)};
+          const float* cs = args.cos_sin + static_cast<int64_t>(args.positions[m]) * 128;
+          const float4 co = ld4f(cs + j), si = ld4f(cs + 64 + j);
+          const float cc[4] = {co.x, co.y, co.z, co.w}, sn[4] = {si.x, si.y, si.z, si.w};
+          float ra[4], rb[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            ra[q] = av[q] * cc[q] - bv[q] * sn[q];
+            rb[q] = bv[q] * cc[q] + av[q] * sn[q];
+          }
+          uint2 va, vb;
+          va.x = pack2(ra[0], ra[1]);
+          va.y = pack2(ra[2], ra[3]);
+          vb.x = pack2(rb[0], rb[1]);
+          vb.y = pack2(rb[2], rb[3]);
+          bf16_t* d;
+          if (nb < nq) {
+            d = args.out + static_cast<int64_t>(m) * args.ldo + nb * 128 + j;
+          } else {
+            const int slot = args.slots[m];
+            if (slot < 0) continue;
+            d = args.k_cache + ((static_cast<int64_t>(slot / bs) * nkv + (nb - nq)) * bs + slot % bs) * 128 + j;
+          }
+          *reinterpret_cast<uint2*>(d) = va;
+          *reinterpret_cast<uint2*>(d + 64) = vb;
+        }
+      }
+    } else {
+      const int kh = nb - nq - nkv;
+      const int d0 = (tid & 31) * 4;
+      for (int m0 = tid >> 5; m0 < M; m0 += 8 * RB) {
+        float4 a[RB];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int m = min(m0 + 8 * i, M - 1);
+          a[i] = slab_sum<SS>(args.partial + static_cast<int64_t>(m) * N + nbase + d0, slab, S);
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int m = m0 + 8 * i;
+          if (m >= M) break;
+          const int slot = args.slots[m];
+          if (slot < 0) continue;
+          bf16_t* d = args.v_cache + ((static_cast<int64_t>(slot / bs) * nkv + kh) * 128 + d0) * bs + slot % bs;
+          d[0] = f2bf(a[i].x);
+          d[bs] = f2bf(a[i].y);
+          d[2 * bs] = f2bf(a[i].z);
+          d[3 * bs] = f2bf(a[i].w);
+        }
+      }
+    }
+  }
+}
+
 // grid: (n_blocks * S) workgroups of 4 waves; workgroup -> (128-row n-block, k-split) with the
 // split fastest.  Per 256-deep k-chunk the workgroup stages A[0:M, chunk] in LDS (double
 // buffered, register-staged: loads for chunk c+1 are issued before chunk c's MFMAs and written
 // after them), while each wave streams its own 32 W rows straight to VGPRs two 128-steps
-// ahead (~16 KB per wave in flight).  W fragments use the natural k order (lane group g reads
-// bytes [64s + 16g, +16) of a row in instruction s: 64 contiguous bytes per row).
+// ahead.  Row-major W: lane group g reads bytes [64s + 16g, +16) of a row in instruction s
+// (64 B from each of 16 rows); fragment-packed W (PK): one contiguous KiB per instruction.
+// NORM: A is the residual stream and the RMSNorm (x = bf16(bf16(v * rinv[m]) * w[k])) is
+// applied while staging A into LDS, rinv[m] from the producer's sum-of-squares parts.
 constexpr int kKC = 256;           // k per LDS chunk
 constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows shift one 16-B slot)
 
-template <int MT, int MODE, int D, bool PK>
-__global__ void __launch_bounds__(256, D == 2 ? 2 : 1) skinny_gemm_kernel(bf16_t* __restrict__ out, float* __restrict__ partial,
-                                                             const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-                                                             int M, int N, int K, int lda, int ldo, int S, int n_blocks) {
+template <int MT, int MODE, bool PK, bool NORM>
+__global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kAStride];
+  __shared__ float rinv_s[64];
+  __shared__ int last_s;
+  const int M = args.M, N = args.N, K = args.K, S = args.S;
+  const bf16_t* __restrict__ A = args.A;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
   const int nb = blockIdx.x / S, split = blockIdx.x % S;
   const int kper = K / S;
-  const int k0 = split * kper, k1 = k0 + kper;
+  const int k0 = split * kper;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = nb * 128 + w * 16 * kR;
+
+  if constexpr (NORM) {
+    if (tid < M) {
+      float ss = 0.f;
+      for (int q = 0; q < args.nrm_nparts; ++q) ss += args.nrm_parts[q * M + tid];
+      rinv_s[tid] = rsqrtf(ss / K + args.eps);
+    }
+    __syncthreads();
+  }
 
   const bf16_t* wp[kR];
 #pragma unroll
   for (int t = 0; t < kR; ++t)
-    wp[t] = PK ? W + (static_cast<int64_t>((n0 >> 4) + t) * (K >> 5)) * 512 + 8 * lane   // fragment-packed
-               : W + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                // row-major [N, K]
+    wp[t] = PK ? args.W + (static_cast<int64_t>((n0 >> 4) + t) * (K >> 5)) * 512 + 8 * lane  // fragment-packed
+               : args.W + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                 // row-major [N, K]
 
   // A staging: MT*16 rows x 256 cols = MT*512 16-byte pieces over 256 threads
   constexpr int kPieces = (16 * MT * kKC / 8 + 255) / 256;
   u32x4 stage[kPieces];
+  u32x4 stage_w[NORM ? kPieces : 1];
   auto load_a = [&](int kc) {
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) {
       const int idx = tid + 256 * p;  // piece index
       const int row = idx >> 5, col = (idx & 31) * 8;
       const int src_row = min(row, M - 1);
-      stage[p] = *reinterpret_cast<const u32x4*>(A + static_cast<int64_t>(src_row) * lda + kc + col);
+      stage[p] = *reinterpret_cast<const u32x4*>(A + static_cast<int64_t>(src_row) * args.lda + kc + col);
+      if constexpr (NORM) stage_w[p] = *reinterpret_cast<const u32x4*>(args.nrm_w + kc + col);
     }
   };
   auto store_a = [&](int buf) {
@@ -78,7 +256,17 @@ __global__ void __launch_bounds__(256, D == 2 ? 2 : 1) skinny_gemm_kernel(bf16_t
     for (int p = 0; p < kPieces; ++p) {
       const int idx = tid + 256 * p;
       const int row = idx >> 5, col = (idx & 31) * 8;
-      *reinterpret_cast<u32x4*>(&a_lds[buf][row][col]) = stage[p];
+      u32x4 v = stage[p];
+      if constexpr (NORM) {
+        float x[8], wv[8];
+        unpack8(v, x);
+        unpack8(stage_w[p], wv);
+        const float ri = rinv_s[min(row, M - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = rbf(x[j] * ri) * wv[j];
+        v = pack8(x);
+      }
+      *reinterpret_cast<u32x4*>(&a_lds[buf][row][col]) = v;
     }
   };
 
@@ -88,13 +276,13 @@ __global__ void __launch_bounds__(256, D == 2 ? 2 : 1) skinny_gemm_kernel(bf16_t
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // W register ring: steps k, k+128 (current chunk) loaded ahead
   bf16x8_t wa[kR][4], wb[kR][4];
   auto load_w = [&](bf16x8_t (&dst)[kR][4], int k) {
 #pragma unroll
     for (int t = 0; t < kR; ++t)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) dst[t][s] = PK ? ld8(wp[t] + static_cast<int64_t>((k >> 5) + s) * 512) : ld8(wp[t] + k + 32 * s);
+      for (int s = 0; s < 4; ++s)
+        dst[t][s] = PK ? ld8(wp[t] + static_cast<int64_t>((k >> 5) + s) * 512) : ld8(wp[t] + k + 32 * s);
   };
   auto mma_step = [&](const bf16x8_t (&wf)[kR][4], int buf, int kk) {
 #pragma unroll
@@ -111,76 +299,43 @@ __global__ void __launch_bounds__(256, D == 2 ? 2 : 1) skinny_gemm_kernel(bf16_t
     }
   };
 
-  // Chunk order is rotated per n-block: at any instant concurrent workgroups read different
-  // column ranges of their rows, so the row-strided W stream spreads over all HBM channels
-  // instead of camping on the few that one (row stride mod interleave) offset maps to.
-  const int nchunks = kper / kKC;
-  const int rot = (nb * 5) % nchunks;
-  auto chunk_k = [&](int c) { return k0 + ((c + rot) % nchunks) * kKC; };
+  // Chunk order is rotated per n-block so concurrent workgroups read different column ranges.
   // Every load in the loop is unconditional (past the last chunk the address is clamped to it
   // and the data is dropped): a load behind a branch makes the compiler's vmcnt bookkeeping
-  // assume it was not issued, so it then drains ALL loads (vmcnt(0)) before the next MFMAs and
-  // the W stream stalls once per chunk (measured: ~26 GB/s per workgroup).
-  auto ck = [&](int c) { return chunk_k(min(c, nchunks - 1)); };
-  if constexpr (D == 2) {
-    // ring of 2 k-steps: W for the current chunk's two 128-steps in flight
-    load_a(ck(0));
-    load_w(wa, ck(0));
-    load_w(wb, ck(0) + 128);
-    store_a(0);
-    int buf = 0;
-    for (int c = 0; c < nchunks; ++c) {
-      const int kn = ck(c + 1);
-      load_a(kn);
-      __syncthreads();  // chunk c visible in a_lds[buf]; every wave is done with a_lds[buf^1]
-      mma_step(wa, buf, 0);
-      load_w(wa, kn);
-      mma_step(wb, buf, 128);
-      load_w(wb, kn + 128);
-      store_a(buf ^ 1);
-      buf ^= 1;
-    }
-  } else {
-    // ring of 4 k-steps (two chunks, ~32 KB per wave in flight); the loop is unrolled over a
-    // chunk pair so every ring slot and LDS buffer index is static.
-    bf16x8_t wc[kR][4], wd[kR][4];
-    load_a(ck(0));
-    load_w(wa, ck(0));
-    load_w(wb, ck(0) + 128);
-    load_w(wc, ck(1));
-    load_w(wd, ck(1) + 128);
-    store_a(0);
-    for (int c = 0; c < nchunks; c += 2) {
-      load_a(ck(c + 1));
-      __syncthreads();  // chunk c visible in a_lds[0]; every wave is done with a_lds[1]
-      mma_step(wa, 0, 0);
-      load_w(wa, ck(c + 2));
-      mma_step(wb, 0, 128);
-      load_w(wb, ck(c + 2) + 128);
-      store_a(1);
-      if (c + 1 >= nchunks) break;  // uniform
-      load_a(ck(c + 2));
-      __syncthreads();  // chunk c+1 visible in a_lds[1]; every wave is done with a_lds[0]
-      mma_step(wc, 1, 0);
-      load_w(wc, ck(c + 3));
-      mma_step(wd, 1, 128);
-      load_w(wd, ck(c + 3) + 128);
-      store_a(0);
-    }
+  // assume it was not issued, so it then drains ALL loads before the next MFMAs.
+  const int nchunks = kper / kKC;
+  const int rot = (nb * 5) % nchunks;
+  auto ck = [&](int c) { return k0 + ((min(c, nchunks - 1) + rot) % nchunks) * kKC; };
+  load_a(ck(0));
+  load_w(wa, ck(0));
+  load_w(wb, ck(0) + 128);
+  store_a(0);
+  int buf = 0;
+  for (int c = 0; c < nchunks; ++c) {
+    const int kn = ck(c + 1);
+    load_a(kn);
+    __syncthreads();  // chunk c visible in a_lds[buf]; every wave is done with a_lds[buf^1]
+    mma_step(wa, buf, 0);
+    load_w(wa, kn);
+    mma_step(wb, buf, 128);
+    load_w(wb, kn + 128);
+    store_a(buf ^ 1);
+    buf ^= 1;
   }
 
   // C^T tile: rows = W rows (n), cols = m:  acc[t][mt][i] = C[m = 16*mt + r][n = n0 + 16*t + 4*g + i]
+  constexpr bool kSlab = MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = 16 * mt + r;
     if (m >= M) continue;
-    if (MODE == kPartial) {
-      float* p = partial + (static_cast<int64_t>(split) * M + m) * N + n0 + 4 * g;
+    if constexpr (kSlab) {
+      float* p = args.partial + (static_cast<int64_t>(split) * M + m) * N + n0 + 4 * g;
 #pragma unroll
       for (int t = 0; t < kR; ++t) *reinterpret_cast<float4*>(p + 16 * t) =
           make_float4(acc[t][mt][0], acc[t][mt][1], acc[t][mt][2], acc[t][mt][3]);
-    } else if (MODE == kBF16) {
-      bf16_t* o = out + static_cast<int64_t>(m) * ldo + n0 + 4 * g;
+    } else if constexpr (MODE == kBF16) {
+      bf16_t* o = args.out + static_cast<int64_t>(m) * args.ldo + n0 + 4 * g;
 #pragma unroll
       for (int t = 0; t < kR; ++t) {
         uint2 v;
@@ -189,19 +344,64 @@ __global__ void __launch_bounds__(256, D == 2 ? 2 : 1) skinny_gemm_kernel(bf16_t
         *reinterpret_cast<uint2*>(o + 16 * t) = v;
       }
     } else {  // kSiluMul: tile 0 = gate, tile 1 = up of the same 16 columns
-      bf16_t* o = out + static_cast<int64_t>(m) * ldo + (n0 >> 1) + 4 * g;
+      bf16_t* o = args.out + static_cast<int64_t>(m) * args.ldo + (n0 >> 1) + 4 * g;
       float y[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float gt = bf2f(f2bf(acc[0][mt][i]));
-        const float up = bf2f(f2bf(acc[1][mt][i]));
-        y[i] = bf2f(f2bf(silu(gt))) * up;
-      }
+      for (int i = 0; i < 4; ++i) y[i] = rbf(silu(rbf(acc[0][mt][i]))) * rbf(acc[1][mt][i]);
       uint2 v;
       v.x = pack2(y[0], y[1]);
       v.y = pack2(y[2], y[3]);
       *reinterpret_cast<uint2*>(o) = v;
     }
+  }
+  if constexpr (MODE == kAddResNorm || MODE == kQkvRope) {
+    // ---- in-launch split-K reduction by the last split of this n-block to arrive
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      int last = 1;
+      if (S > 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(args.counters + nb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == S - 1;
+        if (last) __hip_atomic_store(args.counters + nb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      last_s = last;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    switch (S) {
+      case 1: epilogue<MODE, 1>(args, nb); break;
+      case 2: epilogue<MODE, 2>(args, nb); break;
+      case 4: epilogue<MODE, 4>(args, nb); break;
+      case 8: epilogue<MODE, 8>(args, nb); break;
+      case 16: epilogue<MODE, 16>(args, nb); break;
+      default: epilogue<MODE, 0>(args, nb); break;
+    }
+  }
+}
+
+// x[m] = bf16(bf16(residual[m] * rinv[m]) * w), rinv from the per-row sum-of-squares parts a
+// kAddResNorm epilogue wrote (the final RMSNorm of the fused decode chain).  One row per WG.
+__global__ void __launch_bounds__(256) norm_apply_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ residual,
+                                                         const float* __restrict__ parts, int nparts,
+                                                         const bf16_t* __restrict__ w, int M, int H, float eps) {
+  const int m = blockIdx.x;
+  float ss = 0.f;
+  for (int q = 0; q < nparts; ++q) ss += parts[q * M + m];
+  const float ri = rsqrtf(ss / H + eps);
+  for (int c = threadIdx.x * 8; c < H; c += 256 * 8) {
+    float v[8], wv[8];
+    unpack8(*reinterpret_cast<const u32x4*>(residual + static_cast<int64_t>(m) * H + c), v);
+    unpack8(*reinterpret_cast<const u32x4*>(w + c), wv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = rbf(v[j] * ri) * wv[j];
+    *reinterpret_cast<u32x4*>(x + static_cast<int64_t>(m) * H + c) = pack8(v);
   }
 }
 
@@ -245,7 +445,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
 // One row per workgroup of H/4 (<= 1024) threads, PER float4 column groups per thread; the S
 // slab loads of a group are independent and issued back to back (latency, not bandwidth, is
 // what a 64-row reduction fights).
-template <int PER>
+template <int PER, int SS>
 __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
                                                                   const float* __restrict__ partial,
                                                                   const bf16_t* __restrict__ w, int S, int M, int H,
@@ -260,11 +460,17 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __rest
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = 4 * (threadIdx.x + i * blockDim.x);
-    float4 acc = *reinterpret_cast<const float4*>(base + c);
-#pragma unroll 8
-    for (int s = 1; s < S; ++s) {
-      const float4 p = *reinterpret_cast<const float4*>(base + s * slab + c);
-      acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+    float4 acc;
+    if constexpr (SS > 0) {
+      float4 p[SS];  // all slab loads in flight before the first add
+#pragma unroll
+      for (int q = 0; q < SS; ++q) p[q] = ld4f(base + q * slab + c);
+      acc = p[0];
+#pragma unroll
+      for (int q = 1; q < SS; ++q) add4(acc, p[q]);
+    } else {
+      acc = ld4f(base + c);
+      for (int q = 1; q < S; ++q) add4(acc, ld4f(base + q * slab + c));
     }
     const uint2 rr = *reinterpret_cast<const uint2*>(res + c);
     // the projection output is rounded to bf16 first (as the unfused GEMM would store it)
@@ -296,127 +502,143 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __rest
   }
 }
 
-// Split-K QKV epilogue fused with RoPE and the paged KV write: per token, sum the S fp32 slabs
-// of the fused q|k|v projection, round to bf16 (the unfused GEMM output), rotate q and k
-// (neox, fp32 cos|sin table), write q to q_out [M, nq*128], k to the K cache and v to the
-// transposed V cache (slot < 0: padding row, nothing cached).  Replaces reduce + rope_and_cache.
+// Split-K QKV epilogue fused with RoPE and the paged KV write: sum the S fp32 slabs of the
+// fused q|k|v projection, round to bf16 (the unfused GEMM output), rotate q and k (neox, fp32
+// cos|sin table), write q to q_out [M, nq*128], k to the K cache and v to the transposed V
+// cache (slot < 0: padding row, nothing cached).  Replaces reduce + rope_and_cache.
+// One wave per (row, head) so M * (nq + 2 nkv) waves cover the chip and every lane issues its
+// 2 S slab loads back to back (a per-row workgroup walking heads serially was latency-bound).
+template <int SS>
 __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
     bf16_t* __restrict__ q_out, const float* __restrict__ partial, int S, int M, int nq, int nkv,
     const int* __restrict__ positions, const float* __restrict__ cos_sin, bf16_t* __restrict__ kc,
     bf16_t* __restrict__ vc, const int* __restrict__ slots, int bs) {
-  const int m = blockIdx.x;
-  const int N = (nq + 2 * nkv) * 128;
+  const int nh = nq + 2 * nkv;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= M * nh) return;
+  const int m = item / nh, h = item % nh;
+  const int lane = threadIdx.x & 63;
+  const int N = nh * 128;
   const int64_t slab = static_cast<int64_t>(M) * N;
-  const float* base = partial + static_cast<int64_t>(m) * N;
-  const int pos = positions[m];
+  const float* base = partial + static_cast<int64_t>(m) * N + h * 128;
   const int slot = slots[m];
-  const float* cs = cos_sin + static_cast<int64_t>(pos) * 128;
-  const int n_rot = (nq + nkv) * 16;  // (head, 4-pair group)
-  const int n_items = n_rot + nkv * 32;
-  for (int it = threadIdx.x; it < n_items; it += blockDim.x) {
-    if (it < n_rot) {
-      const int h = it >> 4, j = (it & 15) * 4;
-      const int c = h * 128 + j;
-      float4 a = *reinterpret_cast<const float4*>(base + c);
-      float4 b = *reinterpret_cast<const float4*>(base + c + 64);
-      for (int s = 1; s < S; ++s) {
-        const float4 pa = *reinterpret_cast<const float4*>(base + s * slab + c);
-        const float4 pb = *reinterpret_cast<const float4*>(base + s * slab + c + 64);
-        a.x += pa.x; a.y += pa.y; a.z += pa.z; a.w += pa.w;
-        b.x += pb.x; b.y += pb.y; b.z += pb.z; b.w += pb.w;
-      }
-      const float av[4] = {bf2f(f2bf(a.x)), bf2f(f2bf(a.y)), bf2f(f2bf(a.z)), bf2f(f2bf(a.w))};
-      const float bv[4] = {bf2f(f2bf(b.x)), bf2f(f2bf(b.y)), bf2f(f2bf(b.z)), bf2f(f2bf(b.w))};
-      const float4 co = *reinterpret_cast<const float4*>(cs + j);
-      const float4 si = *reinterpret_cast<const float4*>(cs + 64 + j);
-      const float cc[4] = {co.x, co.y, co.z, co.w}, ss[4] = {si.x, si.y, si.z, si.w};
-      float ra[4], rb[4];
+  if (h >= nq && slot < 0) return;
+  float a, b;
+  if constexpr (SS > 0) {
+    float va[SS], vb[SS];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ra[q] = av[q] * cc[q] - bv[q] * ss[q];
-        rb[q] = bv[q] * cc[q] + av[q] * ss[q];
-      }
-      uint2 va, vb;
-      va.x = pack2(ra[0], ra[1]);
-      va.y = pack2(ra[2], ra[3]);
-      vb.x = pack2(rb[0], rb[1]);
-      vb.y = pack2(rb[2], rb[3]);
-      if (h < nq) {
-        bf16_t* o = q_out + static_cast<int64_t>(m) * nq * 128 + h * 128 + j;
-        *reinterpret_cast<uint2*>(o) = va;
-        *reinterpret_cast<uint2*>(o + 64) = vb;
-      } else if (slot >= 0) {
-        bf16_t* d = kc + ((static_cast<int64_t>(slot / bs) * nkv + (h - nq)) * bs + slot % bs) * 128 + j;
-        *reinterpret_cast<uint2*>(d) = va;
-        *reinterpret_cast<uint2*>(d + 64) = vb;
-      }
-    } else if (slot >= 0) {
-      const int u = it - n_rot;
-      const int kh = u >> 5, d0 = (u & 31) * 4;
-      const int c = (nq + nkv) * 128 + kh * 128 + d0;
-      float4 a = *reinterpret_cast<const float4*>(base + c);
-      for (int s = 1; s < S; ++s) {
-        const float4 pa = *reinterpret_cast<const float4*>(base + s * slab + c);
-        a.x += pa.x; a.y += pa.y; a.z += pa.z; a.w += pa.w;
-      }
-      const float av[4] = {a.x, a.y, a.z, a.w};
-      bf16_t* d = vc + ((static_cast<int64_t>(slot / bs) * nkv + kh) * 128 + d0) * bs + slot % bs;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) d[q * bs] = f2bf(av[q]);
+    for (int s = 0; s < SS; ++s) {
+      va[s] = base[s * slab + lane];
+      vb[s] = base[s * slab + lane + 64];
     }
+    a = va[0];
+    b = vb[0];
+#pragma unroll
+    for (int s = 1; s < SS; ++s) {
+      a += va[s];
+      b += vb[s];
+    }
+  } else {
+    a = 0.f;
+    b = 0.f;
+    for (int s = 0; s < S; ++s) {
+      a += base[s * slab + lane];
+      b += base[s * slab + lane + 64];
+    }
+  }
+  if (h < nq + nkv) {
+    a = rbf(a);
+    b = rbf(b);
+    const float* cs = cos_sin + static_cast<int64_t>(positions[m]) * 128;
+    const float co = cs[lane], si = cs[64 + lane];
+    bf16_t* d = h < nq ? q_out + static_cast<int64_t>(m) * nq * 128 + h * 128
+                       : kc + ((static_cast<int64_t>(slot / bs) * nkv + (h - nq)) * bs + slot % bs) * 128;
+    d[lane] = f2bf(a * co - b * si);
+    d[lane + 64] = f2bf(b * co + a * si);
+  } else {
+    bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * nkv + (h - nq - nkv)) * 128 * bs + slot % bs;
+    d[static_cast<int64_t>(lane) * bs] = f2bf(a);
+    d[static_cast<int64_t>(lane + 64) * bs] = f2bf(b);
   }
 }
 
-template <int MODE, int D, bool PK>
-int launch(int MT, bf16_t* out, float* partial, const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldo,
-           int S, hipStream_t stream) {
-  const int n_blocks = N / 128;
-  const int grid = n_blocks * S;
-  switch (MT) {
-    case 1: skinny_gemm_kernel<1, MODE, D, PK><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 2: skinny_gemm_kernel<2, MODE, D, PK><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 3: skinny_gemm_kernel<3, MODE, D, PK><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
-    case 4: skinny_gemm_kernel<4, MODE, D, PK><<<grid, 256, 0, stream>>>(out, partial, A, W, M, N, K, lda, ldo, S, n_blocks); break;
+template <int MODE, bool PK, bool NORM>
+int launch(const GemmArgs& a, hipStream_t stream) {
+  const int grid = (a.N / 128) * a.S;
+  switch ((a.M + 15) / 16) {
+    case 1: skinny_gemm_kernel<1, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
+    case 2: skinny_gemm_kernel<2, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
+    case 3: skinny_gemm_kernel<3, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
+    case 4: skinny_gemm_kernel<4, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
 }
 
-}  // namespace
+template <int MODE, bool NORM>
+int launch_pk(const GemmArgs& a, bool packed, hipStream_t stream) {
+  return packed ? launch<MODE, true, NORM>(a, stream) : launch<MODE, false, NORM>(a, stream);
+}
 
-// mode 0: out bf16 [M, ldo] (S must be 1); 1: partial fp32 [S, M, N]; 2: SiLU-mul of interleaved
-// gate/up rows -> out bf16 [M, N/2] (S must be 1).  Requires M <= 64, N % 32 == 0, K % (128 S) == 0.
-PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void* W, int M, int N, int K, int lda,
-                             int ldo, int S, int mode, hipStream_t stream) {
-  if (M <= 0) return 0;
-  if (M > 64 || N % 128 || S < 1 || K % (kKC * S) || lda % 8) return -1;
-  const int MT = (M + 15) / 16;
-  auto o = static_cast<bf16_t*>(out);
-  auto p = static_cast<float*>(partial);
-  auto a = static_cast<const bf16_t*>(A);
-  auto w = static_cast<const bf16_t*>(W);
-  const bool deep = (mode & 8) != 0;     // bit 3: 4-step W register ring instead of 2
-  const bool packed = (mode & 16) != 0;  // bit 4: W in fragment-packed layout (pk_pack_weight)
-  auto go = [&](auto mode_c) -> int {
-    constexpr int MD = decltype(mode_c)::value;
-    const int s_ = MD == kPartial ? S : 1;
-    if (packed) return deep ? launch<MD, 4, true>(MT, o, p, a, w, M, N, K, lda, ldo, s_, stream)
-                            : launch<MD, 2, true>(MT, o, p, a, w, M, N, K, lda, ldo, s_, stream);
-    return deep ? launch<MD, 4, false>(MT, o, p, a, w, M, N, K, lda, ldo, s_, stream)
-                : launch<MD, 2, false>(MT, o, p, a, w, M, N, K, lda, ldo, s_, stream);
-  };
+int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
+  if (a.M <= 0) return 0;
+  if (a.M > 64 || a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;
+  const bool packed = (mode & 16) != 0;  // bit 4: W in fragment-packed layout
+  const bool norm = (mode & 32) != 0;    // bit 5: RMSNorm prologue on A
+  if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr || a.M > 64)) return -1;
   switch (mode & 7) {
     case kBF16:
-      if (S != 1) return -1;
-      return go(std::integral_constant<int, kBF16>{});
+      if (a.S != 1 || norm) return -1;
+      return launch_pk<kBF16, false>(a, packed, stream);
     case kPartial:
-      return go(std::integral_constant<int, kPartial>{});
+      if (norm) return -1;
+      return launch_pk<kPartial, false>(a, packed, stream);
     case kSiluMul:
-      if (S != 1) return -1;
-      return go(std::integral_constant<int, kSiluMul>{});
+      if (a.S != 1) return -1;
+      return norm ? launch_pk<kSiluMul, true>(a, packed, stream) : launch_pk<kSiluMul, false>(a, packed, stream);
+    case kAddResNorm:
+      if (norm || a.counters == nullptr || a.residual == nullptr || a.sumsq_parts == nullptr) return -1;
+      return launch_pk<kAddResNorm, false>(a, packed, stream);
+    case kQkvRope:
+      if (a.counters == nullptr || a.N != (a.nq + 2 * a.nkv) * 128 || a.bs <= 0) return -1;
+      return norm ? launch_pk<kQkvRope, true>(a, packed, stream) : launch_pk<kQkvRope, false>(a, packed, stream);
     default: return -1;
   }
 }
+
+}  // namespace
+
+// mode 0: out bf16 [M, ldo] (S must be 1); 1: partial fp32 [S, M, N]; 2: SiLU-mul of interleaved
+// gate/up rows -> out bf16 [M, N/2] (S must be 1); bit 4: fragment-packed W.
+// Requires M <= 64, N % 128 == 0, K % (256 S) == 0.
+PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void* W, int M, int N, int K, int lda,
+                             int ldo, int S, int mode, hipStream_t stream) {
+  GemmArgs a{};
+  a.out = static_cast<bf16_t*>(out);
+  a.partial = static_cast<float*>(partial);
+  a.A = static_cast<const bf16_t*>(A);
+  a.W = static_cast<const bf16_t*>(W);
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldo = ldo; a.S = S;
+  if ((mode & 7) > kSiluMul || (mode & 32)) return -1;
+  return dispatch(a, mode, stream);
+}
+
+// Full-featured entry: modes 0-4 (see Mode), bit 4 packed W, bit 5 RMSNorm prologue.
+PK_EXPORT int pk_skinny_gemm_ex(const GemmArgs* args, int mode, hipStream_t stream) {
+  return dispatch(*args, mode, stream);
+}
+
+PK_EXPORT int pk_norm_apply(void* x, const void* residual, const void* parts, int nparts, const void* w, int M,
+                            int H, float eps, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (H % 8) return -1;
+  norm_apply_kernel<<<M, 256, 0, stream>>>(static_cast<bf16_t*>(x), static_cast<const bf16_t*>(residual),
+                                           static_cast<const float*>(parts), nparts, static_cast<const bf16_t*>(w), M,
+                                           H, eps);
+  return PK_CHECK_LAUNCH();
+}
+
+PK_EXPORT int pk_gemm_args_size() { return static_cast<int>(sizeof(GemmArgs)); }
 
 PK_EXPORT int pk_splitk_reduce(void* out, const void* partial, int S, int M, int N, int ldo, int silu,
                                hipStream_t stream) {
@@ -439,9 +661,20 @@ PK_EXPORT int pk_splitk_add_rmsnorm(void* x, void* residual, const void* partial
   auto pp = static_cast<const float*>(partial);
   auto ww = static_cast<const bf16_t*>(w);
   const int threads = H / 4 > 1024 ? 1024 : H / 4;
+  auto go = [&](auto per, auto ss) {
+    splitk_add_rmsnorm_kernel<decltype(per)::value, decltype(ss)::value><<<M, threads, 0, stream>>>(
+        xx, rr, pp, ww, S, M, H, eps);
+  };
+  auto go_s = [&](auto per) {
+    switch (S) {
+      case 4: go(per, std::integral_constant<int, 4>{}); break;
+      case 8: go(per, std::integral_constant<int, 8>{}); break;
+      default: go(per, std::integral_constant<int, 0>{}); break;
+    }
+  };
   switch (H / (4 * threads)) {
-    case 1: splitk_add_rmsnorm_kernel<1><<<M, threads, 0, stream>>>(xx, rr, pp, ww, S, M, H, eps); break;
-    case 2: splitk_add_rmsnorm_kernel<2><<<M, threads, 0, stream>>>(xx, rr, pp, ww, S, M, H, eps); break;
+    case 1: go_s(std::integral_constant<int, 1>{}); break;
+    case 2: go_s(std::integral_constant<int, 2>{}); break;
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
@@ -451,10 +684,20 @@ PK_EXPORT int pk_qkv_reduce_rope_cache(void* q_out, const void* partial, int S, 
                                        const void* positions, const void* cos_sin, void* k_cache, void* v_cache,
                                        const void* slots, int bs, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (bs % 8) return -1;
-  qkv_reduce_rope_cache_kernel<<<M, 256, 0, stream>>>(
-      static_cast<bf16_t*>(q_out), static_cast<const float*>(partial), S, M, nq, nkv,
-      static_cast<const int*>(positions), static_cast<const float*>(cos_sin), static_cast<bf16_t*>(k_cache),
-      static_cast<bf16_t*>(v_cache), static_cast<const int*>(slots), bs);
+  if (bs <= 0 || S < 1) return -1;
+  const int grid = (M * (nq + 2 * nkv) + 3) / 4;
+  auto go = [&](auto ss) {
+    qkv_reduce_rope_cache_kernel<decltype(ss)::value><<<grid, 256, 0, stream>>>(
+        static_cast<bf16_t*>(q_out), static_cast<const float*>(partial), S, M, nq, nkv,
+        static_cast<const int*>(positions), static_cast<const float*>(cos_sin), static_cast<bf16_t*>(k_cache),
+        static_cast<bf16_t*>(v_cache), static_cast<const int*>(slots), bs);
+  };
+  switch (S) {
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 8: go(std::integral_constant<int, 8>{}); break;
+    case 16: go(std::integral_constant<int, 16>{}); break;
+    default: go(std::integral_constant<int, 0>{}); break;
+  }
   return PK_CHECK_LAUNCH();
 }

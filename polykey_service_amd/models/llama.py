@@ -273,6 +273,8 @@ class LlamaForCausalLM(nn.Module):
         """Returns the final-normed hidden states [T, H]."""
         x = self.embed_tokens(input_ids)
         ws = self.workspace(x.shape[0])
+        if ws is not None and self._fused_decode_ok(x):
+            return self._forward_fused(x, positions, md, kv_caches, ws)
         residual = None
         for i, layer in enumerate(self.layers):
             if residual is None:
@@ -285,6 +287,67 @@ class LlamaForCausalLM(nn.Module):
             x = layer.mlp(x, ws)
         x, _ = add_norm(x, residual, self.norm, self.cfg.rms_eps)
         return x
+
+    # ------------------------------------------------------------------ fused decode chain
+    # Off by default: measured slower on MI355X (tools/bench_gemm.py "fused decode chain": the
+    # last-arriver reduction of 256 KB of fp32 slabs per 128-column tile is serial, and the
+    # in-GEMM RMSNorm prologue re-normalises A in every workgroup) than GEMM + separate reduce.
+    FUSED_DECODE = os.environ.get("POLYKEY_FUSED_DECODE", "0") == "1"
+
+    def _fused_decode_ok(self, x: torch.Tensor) -> bool:
+        """TP=1 decode-sized batches run the 5-kernel-per-layer chain of :meth:`_forward_fused`."""
+        if not self.FUSED_DECODE or self.st.tp_size != 1 or self.cfg.head_dim != 128:
+            return False
+        l0 = self.layers[0]
+        if not isinstance(l0.mlp, LlamaMLP):
+            return False
+        H = self.cfg.hidden_size
+        return (H % 256 == 0 and gemm.skinny_ok(x, l0.attn.qkv) and gemm.skinny_ok(x, l0.mlp.gate_up)
+                and l0.attn.o.shape[1] % 256 == 0 and l0.mlp.down.shape[1] % 256 == 0)
+
+    def _fused_buffers(self):
+        """Fixed-address (graph-safe) split-K tickets and two sum-of-squares part buffers."""
+        if getattr(self, "_fbuf", None) is None:
+            H = self.cfg.hidden_size
+            n = (H // 128) * gemm.SKINNY_MAX_M
+            ctr = torch.zeros(4096, dtype=torch.int32, device=self.device)
+            self._fbuf = (ctr, torch.zeros(n, dtype=torch.float32, device=self.device),
+                          torch.zeros(n, dtype=torch.float32, device=self.device))
+        return self._fbuf
+
+    def _forward_fused(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata,
+                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]], ws: torch.Tensor) -> torch.Tensor:
+        """Decode step with every norm and split-K reduction folded into a GEMM:
+
+            qkv GEMM (prologue: RMSNorm(ln1); epilogue: reduce + RoPE + KV-cache write)
+            paged attention
+            o GEMM    (epilogue: reduce + residual add + row sum-of-squares parts)
+            gate_up   (prologue: RMSNorm(ln2); epilogue: SiLU(gate) * up)
+            down GEMM (epilogue: reduce + residual add + row sum-of-squares parts)
+
+        Layer 0's ln1 and the final norm are separate kernels.  The residual stream is updated
+        in place; a layer's norm weights are applied by the *consumer* GEMM from the producer's
+        per-(128-column block, row) sum-of-squares parts."""
+        T = x.shape[0]
+        H = self.cfg.hidden_size
+        ctr, pa, pb = self._fused_buffers()
+        parts_attn = pa[: (H // 128) * T].view(H // 128, T)  # written by o, read by gate_up
+        parts_mlp = pb[: (H // 128) * T].view(H // 128, T)   # written by down, read by next qkv
+        residual = x
+        h = ops.rms_norm(residual, self.layers[0].ln1, self.layers[0].eps)
+        for i, layer in enumerate(self.layers):
+            at, mlp = layer.attn, layer.mlp
+            kc, vc = kv_caches[i]
+            norm = None if i == 0 else gemm.NormIn(parts_mlp, layer.ln1, layer.eps)
+            q = gemm.linear_qkv_rope(residual if norm is not None else h, at.qkv, ws, ctr, positions,
+                                     self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv, packed=at.qkv_p,
+                                     norm=norm)
+            a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
+            gemm.linear_add_residual(a, at.o, ws, ctr, residual, parts_attn, packed=at.o_p)
+            h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_p,
+                                 norm=gemm.NormIn(parts_attn, layer.ln2, layer.eps))
+            gemm.linear_add_residual(h, mlp.down, ws, ctr, residual, parts_mlp, packed=mlp.down_p)
+        return gemm.norm_apply(residual, parts_mlp, self.norm, self.cfg.rms_eps)
 
     def workspace(self, M: int) -> Optional[torch.Tensor]:
         """fp32 split-K slab buffer for decode-sized batches (fixed address: graph-safe)."""

@@ -9,8 +9,9 @@ MFMA kernels are the right tool for compute-bound shapes.
 """
 from __future__ import annotations
 
+import ctypes
 import dataclasses
-from typing import Optional
+from typing import NamedTuple, Optional
 
 import torch
 import torch.nn.functional as F
@@ -26,10 +27,106 @@ _KCHUNK = 256
 # The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see
 # tools/bench_gemm.py and profiles/); POLYKEY_SKINNY_GEMM=0/1 forces it off/on.
 SKINNY_ENABLED = os.environ.get("POLYKEY_SKINNY_GEMM", "1") == "1"
-# mode bit 3: 4-step (instead of 2-step) W register ring, ~32 KB per wave in flight;
-# measured per shape by tools/bench_gemm.py
-DEEP = 8 if os.environ.get("POLYKEY_SKINNY_DEEP", "0") == "1" else 0
 PACKED_BIT = 16
+
+
+MODE_BF16, MODE_PARTIAL, MODE_SILU, MODE_ADD_RES_NORM, MODE_QKV_ROPE = 0, 1, 2, 3, 4
+NORM_BIT = 32
+
+
+class GemmArgs(ctypes.Structure):
+    """Mirror of ``struct GemmArgs`` in csrc/kernels/gemm_skinny.hip (checked against
+    ``pk_gemm_args_size`` on first use)."""
+    _fields_ = [("out", ctypes.c_void_p), ("partial", ctypes.c_void_p), ("A", ctypes.c_void_p),
+                ("W", ctypes.c_void_p), ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
+                ("lda", ctypes.c_int), ("ldo", ctypes.c_int), ("S", ctypes.c_int), ("counters", ctypes.c_void_p),
+                ("nrm_parts", ctypes.c_void_p), ("nrm_w", ctypes.c_void_p), ("nrm_nparts", ctypes.c_int),
+                ("eps", ctypes.c_float), ("residual", ctypes.c_void_p), ("sumsq_parts", ctypes.c_void_p),
+                ("positions", ctypes.c_void_p), ("cos_sin", ctypes.c_void_p), ("k_cache", ctypes.c_void_p),
+                ("v_cache", ctypes.c_void_p), ("slots", ctypes.c_void_p), ("nq", ctypes.c_int),
+                ("nkv", ctypes.c_int), ("bs", ctypes.c_int)]
+
+
+_ARGS_CHECKED = False
+
+
+class NormIn(NamedTuple):
+    """RMSNorm applied in a GEMM's A-staging prologue: A is the residual stream, ``parts`` the
+    per-row sum-of-squares parts [nparts, M] a MODE_ADD_RES_NORM epilogue produced."""
+    parts: torch.Tensor
+    weight: torch.Tensor
+    eps: float
+
+
+def _launch_ex(mode: int, x: torch.Tensor, w: torch.Tensor, packed: Optional[torch.Tensor], S: int,
+               out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+               counters: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None, **kw) -> None:
+    global _ARGS_CHECKED
+    if not _ARGS_CHECKED:
+        n = native.lib().pk_gemm_args_size()
+        assert n == ctypes.sizeof(GemmArgs), f"GemmArgs layout mismatch: C {n} vs ctypes {ctypes.sizeof(GemmArgs)}"
+        _ARGS_CHECKED = True
+    M, K = x.shape
+    N = w.shape[0]
+    a = GemmArgs()
+    a.out = native.ptr(out)
+    a.partial = native.ptr(ws)
+    a.A = x.data_ptr()
+    a.W = (packed if packed is not None else w).data_ptr()
+    a.M, a.N, a.K, a.lda, a.S = M, N, K, x.stride(0), S
+    a.ldo = out.stride(0) if out is not None else N
+    a.counters = native.ptr(counters)
+    if norm is not None:
+        mode |= NORM_BIT
+        a.nrm_parts = norm.parts.data_ptr()
+        a.nrm_nparts = norm.parts.shape[0]
+        a.nrm_w = norm.weight.data_ptr()
+        a.eps = float(norm.eps)
+    for k, v in kw.items():
+        setattr(a, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
+    if packed is not None:
+        mode |= PACKED_BIT
+    native.call("pk_skinny_gemm_ex", ctypes.byref(a), mode, native.stream_ptr())
+
+
+def linear_add_residual(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, counters: torch.Tensor,
+                        residual: torch.Tensor, sumsq_parts: torch.Tensor, S: Optional[int] = None,
+                        packed: Optional[torch.Tensor] = None) -> None:
+    """residual += x @ w^T (split-K reduced in-kernel) and sumsq_parts[N/128, M] = per-row
+    sums of squares of the new residual over each 128-column block (for the next NormIn)."""
+    M, K = x.shape
+    N = w.shape[0]
+    S = S or choose_split(N, K, M)
+    assert ws.numel() >= S * M * N and sumsq_parts.numel() >= (N // 128) * M and counters.numel() >= N // 128
+    _launch_ex(MODE_ADD_RES_NORM, x, w, packed, S, ws=ws, counters=counters, residual=residual,
+               sumsq_parts=sumsq_parts)
+
+
+def linear_qkv_rope(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, counters: torch.Tensor,
+                    positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                    slots: torch.Tensor, nq: int, nkv: int, S: Optional[int] = None,
+                    packed: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None) -> torch.Tensor:
+    """Fused QKV projection (split-K reduced in-kernel) + RoPE + paged KV write → q [M, nq, 128].
+    With ``norm``, ``x`` is the residual stream and the RMSNorm is applied on the fly."""
+    M, K = x.shape
+    N = w.shape[0]
+    assert N == (nq + 2 * nkv) * 128
+    S = S or choose_split(N, K, M)
+    assert ws.numel() >= S * M * N and counters.numel() >= N // 128
+    q = torch.empty((M, nq, 128), dtype=torch.bfloat16, device=x.device)
+    _launch_ex(MODE_QKV_ROPE, x, w, packed, S, out=q.view(M, nq * 128), ws=ws, counters=counters, norm=norm,
+               positions=positions, cos_sin=cos_sin, k_cache=k_cache, v_cache=v_cache, slots=slots, nq=nq,
+               nkv=nkv, bs=k_cache.shape[2])
+    return q
+
+
+def norm_apply(residual: torch.Tensor, parts: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
+    """rms_norm(residual) * weight using precomputed per-row sum-of-squares parts."""
+    M, H = residual.shape
+    x = torch.empty_like(residual)
+    native.call("pk_norm_apply", x.data_ptr(), residual.data_ptr(), parts.data_ptr(), parts.shape[0],
+                weight.data_ptr(), M, H, float(eps), native.stream_ptr())
+    return x
 
 
 @dataclasses.dataclass
@@ -97,7 +194,7 @@ def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
 
 
 def _wmode(packed: Optional[torch.Tensor]) -> int:
-    return DEEP | (PACKED_BIT if packed is not None else 0)
+    return PACKED_BIT if packed is not None else 0
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -129,8 +226,15 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
 
 
 def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[torch.Tensor] = None,
-                packed: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """silu(x @ Wg^T) * (x @ Wu^T) with interleaved gate/up rows → [M, I]."""
+                packed: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None) -> torch.Tensor:
+    """silu(x @ Wg^T) * (x @ Wu^T) with interleaved gate/up rows → [M, I].  With ``norm``,
+    ``x`` is the residual stream and the RMSNorm is applied in the kernel's prologue (S = 1)."""
+    if norm is not None:
+        M, K = x.shape
+        N = w_gu_interleaved.shape[0]
+        out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
+        _launch_ex(MODE_SILU, x, w_gu_interleaved, packed, 1, out=out, norm=norm)
+        return out
     if not skinny_ok(x, w_gu_interleaved):
         return silu_and_mul_interleaved(linear(x, w_gu_interleaved))
     M, K = x.shape

@@ -50,6 +50,9 @@ SIGNATURES = {
     "pk_splitk_reduce": [P, P, I32, I32, I32, I32, I32, P],
     "pk_splitk_add_rmsnorm": [P, P, P, P, I32, I32, I32, F32, P],
     "pk_qkv_reduce_rope_cache": [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, P],
+    "pk_skinny_gemm_ex": [P, I32, P],
+    "pk_gemm_args_size": [],
+    "pk_norm_apply": [P, P, P, I32, P, I32, I32, F32, P],
 }
 
 

@@ -8,13 +8,6 @@ from polykey_service_amd.ops import reference as ref
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 8], ids=["ring2", "ring4"], autouse=True)
-def w_ring_depth(request):
-    """Every test runs with the 2-step and the 4-step W register ring (mode bit 3)."""
-    old = gemm.DEEP
-    gemm.DEEP = request.param
-    yield
-    gemm.DEEP = old
 
 def rnd(*shape, scale=1.0):
     return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
@@ -118,3 +111,78 @@ def test_fragment_packed_silu():
     ws = torch.empty(64 * 2 * I * 16, dtype=torch.float32, device="cuda")
     y = gemm.linear_silu(x, w, ws, packed=gemm.pack_weight(w))
     torch.testing.assert_close(y.float(), exp.float(), atol=3e-2, rtol=3e-2)
+
+
+def _sumsq_parts(res: torch.Tensor) -> torch.Tensor:
+    M, H = res.shape
+    return res.float().view(M, H // 128, 128).pow(2).sum(-1).t().contiguous()
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("M,H,K,S", [(64, 4096, 4096, 8), (5, 4096, 14336, 8), (33, 1024, 512, 2), (1, 2048, 256, 1)])
+def test_add_residual_epilogue(M, H, K, S, packed):
+    """In-kernel split-K reduction + residual add + per-block sums of squares (mode 3)."""
+    x, w = rnd(M, K), rnd(H, K, scale=0.05)
+    res = rnd(M, H)
+    ws = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
+    ctr = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    parts = torch.full((H // 128, M), -1.0, device="cuda")
+    exp = ((x.float() @ w.float().t()).to(torch.bfloat16).float() + res.float()).to(torch.bfloat16)
+    for _ in range(2):  # second round checks the tickets re-armed
+        r = res.clone()
+        gemm.linear_add_residual(x, w, ws, ctr, r, parts, S, packed=gemm.pack_weight(w) if packed else None)
+        torch.testing.assert_close(r.float(), exp.float(), atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(parts, _sumsq_parts(r), atol=1e-2, rtol=1e-3)
+    assert int(ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("use_norm", [False, True])
+@pytest.mark.parametrize("nq,nkv,bs,M,S", [(32, 8, 32, 64, 4), (8, 1, 16, 5, 8), (4, 2, 32, 16, 1)])
+def test_qkv_rope_epilogue(nq, nkv, bs, M, S, use_norm):
+    """Fused QKV (mode 4, optional RMSNorm prologue) vs GEMM + rope_and_cache reference."""
+    from polykey_service_amd.ops import attention as A
+    K = 2048
+    N = (nq + 2 * nkv) * 128
+    res, w = rnd(M, K), rnd(N, K, scale=0.05)
+    nw = (1.0 + 0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    ws = torch.empty(S * M * N, dtype=torch.float32, device="cuda")
+    ctr = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    pos = torch.randint(0, 2000, (M,), dtype=torch.int32, device="cuda")
+    cs = ref.rope_cos_sin_cache(2048, 128, 500000.0).cuda()
+    nb = M // bs + 4
+    slots = torch.randperm(nb * bs, device="cuda")[:M].to(torch.int32)
+    slots[0] = -1
+    kc = torch.zeros(nb, nkv, bs, 128, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros(nb, nkv, 128, bs, dtype=torch.bfloat16, device="cuda")
+    kc2, vc2 = kc.clone(), vc.clone()
+    norm = gemm.NormIn(_sumsq_parts(res), nw, 1e-5) if use_norm else None
+    q = gemm.linear_qkv_rope(res, w, ws, ctr, pos, cs, kc, vc, slots, nq, nkv, S, norm=norm)
+    xin = ref.rms_norm(res, nw, 1e-5) if use_norm else res
+    qkv = (xin.float() @ w.float().t()).to(torch.bfloat16)
+    A.rope_and_cache(qkv, pos, cs, kc2, vc2, slots, nq, nkv)
+    torch.testing.assert_close(q.float(), qkv.view(M, -1, 128)[:, :nq].float(), atol=5e-2, rtol=3e-2)
+    torch.testing.assert_close(kc.float(), kc2.float(), atol=5e-2, rtol=3e-2)
+    torch.testing.assert_close(vc.float(), vc2.float(), atol=5e-2, rtol=3e-2)
+    assert int(ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_silu_norm_prologue(packed):
+    M, I, K = 40, 1792, 4096
+    res = rnd(M, K)
+    nw = (1.0 + 0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    g, u = rnd(I, K, scale=0.05), rnd(I, K, scale=0.05)
+    w = gemm.interleave_gate_up(g, u)
+    xin = ref.rms_norm(res, nw, 1e-5).float()
+    exp = ref.silu_and_mul(torch.cat([xin @ g.float().t(), xin @ u.float().t()], -1).to(torch.bfloat16))
+    y = gemm.linear_silu(res, w, packed=gemm.pack_weight(w) if packed else None,
+                         norm=gemm.NormIn(_sumsq_parts(res), nw, 1e-5))
+    torch.testing.assert_close(y.float(), exp.float(), atol=4e-2, rtol=4e-2)
+
+
+def test_norm_apply():
+    M, H = 64, 4096
+    res = rnd(M, H)
+    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    y = gemm.norm_apply(res, _sumsq_parts(res), nw, 1e-5)
+    torch.testing.assert_close(y.float(), ref.rms_norm(res, nw, 1e-5).float(), atol=2e-2, rtol=2e-2)

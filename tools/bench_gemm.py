@@ -68,3 +68,43 @@ for M in (int(a) for a in (sys.argv[1:] or ["64"])):
         print(row, flush=True)
         del ws_list
         torch.cuda.empty_cache()
+
+# ---- fused decode-chain modes (8B shapes, M = 64, packed weights) vs the unfused kernel pairs
+M, H, I, nq, nkv, bs = 64, 4096, 14336, 32, 8, 32
+ctr = torch.zeros(4096, dtype=torch.int32, device="cuda")
+res = torch.randn(M, H, device="cuda").to(torch.bfloat16)
+parts = res.float().view(M, H // 128, 128).pow(2).sum(-1).t().contiguous()
+nw = torch.ones(H, dtype=torch.bfloat16, device="cuda")
+pos = torch.arange(M, dtype=torch.int32, device="cuda") + 300
+cs = torch.randn(4096, 128, device="cuda")
+slots = torch.arange(M, dtype=torch.int32, device="cuda") * 3
+kc = torch.zeros(512, nkv, bs, 128, dtype=torch.bfloat16, device="cuda")
+vc = torch.zeros(512, nkv, 128, bs, dtype=torch.bfloat16, device="cuda")
+print("fused decode chain (us):", flush=True)
+for name, N, K in (("qkv", (nq + 2 * nkv) * 128, H), ("o", H, H), ("gate_up", 2 * I, H), ("down", H, I)):
+    n = max(2, (1 << 30) // (N * K * 2) + 1)
+    wl = [gemm.pack_weight((torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)) for _ in range(n)]
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    S = gemm.choose_split(N, K, M)
+    row = f"  {name:8s} S{S}"
+    if name == "qkv":
+        t0 = timeit(lambda i: gemm.qkv_reduce_rope_cache(gemm.linear_partial(x, wl[i], ws, S, packed=wl[i]), pos, cs,
+                                                         kc, vc, slots, nq, nkv), n)
+        t1 = timeit(lambda i: gemm.linear_qkv_rope(x, wl[i], ws, ctr, pos, cs, kc, vc, slots, nq, nkv, S,
+                                                   packed=wl[i]), n)
+        t2 = timeit(lambda i: gemm.linear_qkv_rope(res, wl[i], ws, ctr, pos, cs, kc, vc, slots, nq, nkv, S,
+                                                   packed=wl[i], norm=gemm.NormIn(parts, nw, 1e-5)), n)
+        row += f" partial+reduce_rope {t0:6.1f} | fused {t1:6.1f} | fused+norm {t2:6.1f}"
+    elif name in ("o", "down"):
+        r2 = res.clone()
+        p2 = torch.empty(H // 128 * M, device="cuda")
+        t0 = timeit(lambda i: gemm.partial_add_rms_norm(gemm.linear_partial(x, wl[i], ws, S, packed=wl[i]), r2, nw,
+                                                        1e-5), n)
+        t1 = timeit(lambda i: gemm.linear_add_residual(x, wl[i], ws, ctr, r2, p2, S, packed=wl[i]), n)
+        row += f" partial+add_rmsnorm {t0:6.1f} | fused {t1:6.1f}"
+    else:
+        t0 = timeit(lambda i: gemm.linear_silu(x, wl[i], ws, packed=wl[i]), n)
+        t1 = timeit(lambda i: gemm.linear_silu(res, wl[i], ws, packed=wl[i], norm=gemm.NormIn(parts, nw, 1e-5)), n)
+        row += f" silu {t0:6.1f} | silu+norm {t1:6.1f}"
+    print(row, flush=True)
+    del wl
