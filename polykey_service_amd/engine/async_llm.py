@@ -11,6 +11,7 @@ health to NOT_SERVING).
 from __future__ import annotations
 
 import asyncio
+import os
 import collections
 import threading
 import time
@@ -31,6 +32,8 @@ class AsyncLLM:
                  watchdog_s: float = 0.0, metrics=None):
         from ..utils import metrics as _m
         self.engine = engine
+        # pipelined steps: RequestOutputs are built / delivered while the GPU runs the next step
+        engine.overlap = os.environ.get("POLYKEY_OVERLAP_STEPS", "1") == "1"
         self.metrics = metrics if metrics is not None else _m.current()
         self.tokenizer = engine.tokenizer
         self.on_fatal = on_fatal

@@ -40,6 +40,7 @@ class EngineConfig:
     graph_batch_sizes: tuple = ()
     watermark: float = 0.01
     device: str = ""
+    overlap: bool = False  # pipelined steps (see LLMEngine.step); AsyncLLM turns it on
 
     @classmethod
     def from_server_config(cls, sc) -> "EngineConfig":
@@ -85,6 +86,8 @@ class LLMEngine:
             self.runner.capture_graphs()
         self.step_count = 0
         self.total_output_tokens = 0
+        self.overlap = cfg.overlap
+        self._inflight = None
 
     # ------------------------------------------------------------------ API
     @property
@@ -106,31 +109,53 @@ class LLMEngine:
         return self.scheduler.abort(request_id)
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.has_work()
+        return self.scheduler.has_work() or self._inflight is not None
 
     def step(self) -> List[RequestOutput]:
+        """One engine iteration.  With ``overlap`` the step is pipelined: the batch launched by
+        the previous call is completed (wait for its sampled ids, advance sequence state, free
+        finished sequences), the next batch is scheduled and launched, and only then are the
+        completed batch's :class:`RequestOutput` objects built and returned — so output
+        construction and the caller's delivery of them run while the GPU executes the next
+        step.  Without ``overlap`` each call launches and completes its own batch."""
+        done = None
+        if self._inflight is not None:
+            done = self._complete(*self._inflight)
+            self._inflight = None
         batch = self.scheduler.schedule()
-        if batch.empty:
-            return []
-        sampling = batch.sampling_seqs()
-        toks = self.runner.execute(batch)
+        if not batch.empty:
+            sampling = batch.sampling_seqs()
+            self._inflight = (batch, sampling, self.runner.launch(batch))
+            if not self.overlap:
+                done = self._complete(*self._inflight)
+                self._inflight = None
+        return self._outputs(done) if done else []
+
+    def _complete(self, batch, sampling, handle):
+        toks = self.runner.fetch(handle)
         now = time.monotonic()
-        outs: List[RequestOutput] = []
         for s, n in batch.prefills:
             s.num_computed += n
         for s in batch.decodes:
             s.num_computed += 1
+        done = []
         for s, tok in zip(sampling, toks):
-            reason = s.append_token(int(tok), now)
+            if s.is_finished():  # aborted while its step was in flight
+                continue
+            reason = s.append_token(tok, now)
             if reason is not None:
                 self.scheduler.finish(s, reason)
-            outs.append(RequestOutput(s.request_id, [int(tok)], reason is not None,
-                                      reason.value if reason else None, len(s.prompt_ids), len(s.output_ids),
-                                      seq_metrics(s) if reason else None))
+            done.append((s, tok, reason))
         self.scheduler.remove_finished()
         self.step_count += 1
         self.total_output_tokens += len(toks)
-        return outs
+        return done
+
+    @staticmethod
+    def _outputs(done) -> List[RequestOutput]:
+        return [RequestOutput(s.request_id, [tok], reason is not None, reason.value if reason else None,
+                              len(s.prompt_ids), len(s.output_ids), seq_metrics(s) if reason else None)
+                for s, tok, reason in done]
 
     def generate(self, prompts: List[List[int]], params: SamplingParams) -> List[List[int]]:
         seqs = [self.add_request(p, dataclasses.replace(params)) for p in prompts]

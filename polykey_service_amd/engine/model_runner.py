@@ -91,6 +91,7 @@ class ModelRunner:
         self.part_o, self.part_ml, self.part_ctr = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks,
                                                                              self.bs, device, n_kv=a0.nkv)
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0}
+        self._tok_event = None
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None
 
@@ -187,6 +188,11 @@ class ModelRunner:
     def execute(self, batch: ScheduledBatch) -> List[int]:
         """TP leader / single rank: pack, publish, run.  Returns the sampled token ids of
         ``batch.sampling_seqs()`` in order."""
+        return self.fetch(self.launch(batch))
+
+    def launch(self, batch: ScheduledBatch):
+        """Enqueue one step (pack → H2D → graph replay / eager forward → sample → async D2H of
+        the sampled ids) without waiting for the GPU; :meth:`fetch` returns the ids."""
         sampling = batch.sampling_seqs()
         T, n = self._pack(batch, sampling)
         nd = len(batch.decodes)
@@ -205,7 +211,24 @@ class ModelRunner:
         h["header"][:7] = (self.MODE_RUN, T, n, nd, ns, max_q, g)
         self._publish()
         toks = self._run(T, n, nd, ns, max_q, g)
-        return self._fetch(toks, ns)
+        self.stats["steps"] += 1
+        if ns == 0 or toks is None:
+            return None, 0
+        if toks.is_cuda:
+            self.tok_host[:ns].copy_(toks[:ns], non_blocking=True)
+            if self._tok_event is None:
+                self._tok_event = torch.cuda.Event()
+            self._tok_event.record(torch.cuda.current_stream(self.device))
+            return self.tok_host, ns
+        return toks, ns
+
+    def fetch(self, handle) -> List[int]:
+        toks, ns = handle
+        if ns == 0:
+            return []
+        if toks is self.tok_host and self._tok_event is not None:
+            self._tok_event.synchronize()
+        return toks[:ns].tolist()
 
     def _publish(self) -> None:
         self.dev_buf.copy_(self.host_buf, non_blocking=True)
@@ -247,16 +270,6 @@ class ModelRunner:
             self.last_logits = logits
         return sampler_ops.sample(logits, d["temperature"][:ns], d["top_k"][:ns], d["top_p"][:ns],
                                   d["min_p"][:ns], d["seeds"][:ns], d["offsets"][:ns])
-
-    def _fetch(self, toks, ns: int) -> List[int]:
-        self.stats["steps"] += 1
-        if ns == 0 or toks is None:
-            return []
-        if toks.is_cuda:
-            self.tok_host[:ns].copy_(toks[:ns], non_blocking=True)
-            torch.cuda.current_stream(self.device).synchronize()
-            return self.tok_host[:ns].tolist()
-        return toks[:ns].tolist()
 
     # ------------------------------------------------------------------ graphs
     def _graph_bucket(self, nd: int) -> Optional[int]:
