@@ -41,6 +41,10 @@ struct GemmArgs {
   bf16_t* v_cache;           // [blocks, nkv, 128, bs]
   const int* slots;          // [M]
   int nq, nkv, bs;
+  const int* row_offsets;    // grouped (MoE): rows of group e = [row_offsets[e], row_offsets[e+1]) of A /
+  long long w_stride;        //   out / slabs, W of group e at W + e * w_stride; group = blockIdx.y
+  int groups;                // number of groups (grid.y)
+  int max_group_rows;        // bound on any group's rows (<= 64): picks the M-tile count
 };
 
 namespace {
@@ -212,8 +216,17 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kAStride];
   __shared__ float rinv_s[64];
   __shared__ int last_s;
-  const int M = args.M, N = args.N, K = args.K, S = args.S;
-  const bf16_t* __restrict__ A = args.A;
+  const int N = args.N, K = args.K, S = args.S;
+  int M = args.M;  // rows of this workgroup's group (all rows when not grouped)
+  int row0 = 0;
+  const bf16_t* Wg = args.W;
+  if (args.row_offsets != nullptr) {
+    row0 = args.row_offsets[blockIdx.y];
+    M = min(args.row_offsets[blockIdx.y + 1] - row0, 16 * MT);
+    if (M <= 0) return;  // no tokens routed to this expert: its weights are never read
+    Wg += static_cast<int64_t>(blockIdx.y) * args.w_stride;
+  }
+  const bf16_t* __restrict__ A = args.A + static_cast<int64_t>(row0) * args.lda;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
   const int nb = blockIdx.x / S, split = blockIdx.x % S;
@@ -234,8 +247,8 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   const bf16_t* wp[kR];
 #pragma unroll
   for (int t = 0; t < kR; ++t)
-    wp[t] = PK ? args.W + (static_cast<int64_t>((n0 >> 4) + t) * (K >> 5)) * 512 + 8 * lane  // fragment-packed
-               : args.W + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                 // row-major [N, K]
+    wp[t] = PK ? Wg + (static_cast<int64_t>((n0 >> 4) + t) * (K >> 5)) * 512 + 8 * lane  // fragment-packed
+               : Wg + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                 // row-major [N, K]
 
   // A staging: MT*16 rows x 256 cols = MT*512 16-byte pieces over 256 threads
   constexpr int kPieces = (16 * MT * kKC / 8 + 255) / 256;
@@ -330,12 +343,12 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     const int m = 16 * mt + r;
     if (m >= M) continue;
     if constexpr (kSlab) {
-      float* p = args.partial + (static_cast<int64_t>(split) * M + m) * N + n0 + 4 * g;
+      float* p = args.partial + (static_cast<int64_t>(split) * args.M + row0 + m) * N + n0 + 4 * g;
 #pragma unroll
       for (int t = 0; t < kR; ++t) *reinterpret_cast<float4*>(p + 16 * t) =
           make_float4(acc[t][mt][0], acc[t][mt][1], acc[t][mt][2], acc[t][mt][3]);
     } else if constexpr (MODE == kBF16) {
-      bf16_t* o = args.out + static_cast<int64_t>(m) * args.ldo + n0 + 4 * g;
+      bf16_t* o = args.out + static_cast<int64_t>(row0 + m) * args.ldo + n0 + 4 * g;
 #pragma unroll
       for (int t = 0; t < kR; ++t) {
         uint2 v;
@@ -344,7 +357,7 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
         *reinterpret_cast<uint2*>(o + 16 * t) = v;
       }
     } else {  // kSiluMul: tile 0 = gate, tile 1 = up of the same 16 columns
-      bf16_t* o = args.out + static_cast<int64_t>(m) * args.ldo + (n0 >> 1) + 4 * g;
+      bf16_t* o = args.out + static_cast<int64_t>(row0 + m) * args.ldo + (n0 >> 1) + 4 * g;
       float y[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) y[i] = rbf(silu(rbf(acc[0][mt][i]))) * rbf(acc[1][mt][i]);
@@ -564,8 +577,8 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
 
 template <int MODE, bool PK, bool NORM>
 int launch(const GemmArgs& a, hipStream_t stream) {
-  const int grid = (a.N / 128) * a.S;
-  switch ((a.M + 15) / 16) {
+  const dim3 grid((a.N / 128) * a.S, a.row_offsets != nullptr ? a.groups : 1);
+  switch ((min(a.M, a.max_group_rows > 0 ? a.max_group_rows : a.M) + 15) / 16) {
     case 1: skinny_gemm_kernel<1, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
     case 2: skinny_gemm_kernel<2, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
     case 3: skinny_gemm_kernel<3, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
@@ -582,7 +595,11 @@ int launch_pk(const GemmArgs& a, bool packed, hipStream_t stream) {
 
 int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
   if (a.M <= 0) return 0;
-  if (a.M > 64 || a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;
+  const bool grouped = a.row_offsets != nullptr;
+  if (grouped && (a.groups <= 0 || a.max_group_rows <= 0 || a.max_group_rows > 64 || (mode & 7) > kSiluMul ||
+                  (mode & 32)))
+    return -1;
+  if ((!grouped && a.M > 64) || a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;
   const bool packed = (mode & 16) != 0;  // bit 4: W in fragment-packed layout
   const bool norm = (mode & 32) != 0;    // bit 5: RMSNorm prologue on A
   if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr || a.M > 64)) return -1;

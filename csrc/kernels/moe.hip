@@ -149,6 +149,37 @@ __global__ void unpermute_kernel(bf16_t* __restrict__ out, const bf16_t* __restr
   }
 }
 
+// Combine from split-K slabs of the w2 GEMM: y[p] = bf16(sum_s partial[s][p]) (the GEMM output
+// the unsplit kernel would store), out[t] = sum_j w[t,j] * y[inv[t,j]].  Saves the separate
+// reduce pass over [S, R, H].
+__global__ void unpermute_partial_kernel(bf16_t* __restrict__ out, const float* __restrict__ partial, int S, int R,
+                                         const int* __restrict__ inv, const float* __restrict__ w, int k, int H) {
+  const int t = blockIdx.x;
+  const int64_t slab = static_cast<int64_t>(R) * H;
+  for (int v = threadIdx.x; v < H / 4; v += blockDim.x) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const int p = inv[t * k + j];
+      if (p < 0) continue;
+      const float* src = partial + static_cast<int64_t>(p) * H + 4 * v;
+      float4 y = *reinterpret_cast<const float4*>(src);
+      for (int q = 1; q < S; ++q) {
+        const float4 z = *reinterpret_cast<const float4*>(src + q * slab);
+        y.x += z.x; y.y += z.y; y.z += z.z; y.w += z.w;
+      }
+      const float ww = w[t * k + j];
+      acc[0] += ww * bf2f(f2bf(y.x));
+      acc[1] += ww * bf2f(f2bf(y.y));
+      acc[2] += ww * bf2f(f2bf(y.z));
+      acc[3] += ww * bf2f(f2bf(y.w));
+    }
+    uint2 o;
+    o.x = pack2(acc[0], acc[1]);
+    o.y = pack2(acc[2], acc[3]);
+    reinterpret_cast<uint2*>(out + static_cast<int64_t>(t) * H)[v] = o;
+  }
+}
+
 // Grouped skinny GEMM.  Expert e's rows of A are [offsets[e], offsets[e+1]) (<= 16*MT rows);
 // W is [E_local, N, K].  MODE 0: bf16 out [rows, N]; MODE 2: SiLU-mul of interleaved gate/up
 // rows -> out [rows, N/2].  grid: (E_local * n_blocks * S / 4), block 256.
@@ -283,6 +314,15 @@ PK_EXPORT int pk_moe_unpermute(void* out, const void* y, const void* inv, const 
   if (H % 8) return -1;
   unpermute_kernel<<<T, 256, 0, stream>>>(static_cast<bf16_t*>(out), static_cast<const bf16_t*>(y),
                                           static_cast<const int*>(inv), static_cast<const float*>(w), k, H);
+  return PK_CHECK_LAUNCH();
+}
+
+PK_EXPORT int pk_moe_unpermute_partial(void* out, const void* partial, int S, int R, const void* inv, const void* w,
+                                       int T, int k, int H, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 4 || S < 1) return -1;
+  unpermute_partial_kernel<<<T, 256, 0, stream>>>(static_cast<bf16_t*>(out), static_cast<const float*>(partial), S, R,
+                                                  static_cast<const int*>(inv), static_cast<const float*>(w), k, H);
   return PK_CHECK_LAUNCH();
 }
 

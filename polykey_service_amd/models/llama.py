@@ -373,16 +373,15 @@ class LlamaForCausalLM(nn.Module):
         """Give every dense projection a fragment-packed copy (:func:`gemm.pack_weight`) for the
         decode GEMM, which streams it ~1.2-1.35x faster than row-major (tools/bench_gemm.py).
         Prefill keeps using the row-major weight through hipBLASLt, so this doubles projection
-        memory: ``auto`` packs only when both copies fit in 60 % of HBM (8B: +15 GB of 288 GB;
-        70B on one GPU: skipped).  ``POLYKEY_PACKED_WEIGHTS`` = auto | 1 | 0."""
+        memory: ``auto`` packs only when both copies fit in 75 % of HBM (8B: +15 GB of 288 GB;
+        Mixtral-8x7B: +90 GB; 70B on one GPU: skipped).  ``POLYKEY_PACKED_WEIGHTS`` = auto | 1 | 0."""
         mode = mode or os.environ.get("POLYKEY_PACKED_WEIGHTS", "auto")
         if mode == "0" or self.device.type != "cuda" or not gemm.SKINNY_ENABLED:
             return False
         if mode == "auto":
             total = torch.cuda.get_device_properties(self.device).total_memory
-            proj = sum(w.numel() * w.element_size() for layer in self.layers
-                       for w in (layer.attn.qkv, layer.attn.o) + self._mlp_weights(layer.mlp) if w is not None)
-            if 2 * proj + self.lm_head.numel() * self.lm_head.element_size() > 0.6 * total:
+            proj = sum(w.numel() * w.element_size() for w in self.layers.parameters())
+            if 2 * proj + self.lm_head.numel() * self.lm_head.element_size() > 0.75 * total:
                 return False
         for layer in self.layers:
             layer.attn.qkv_p = gemm.pack_weight(layer.attn.qkv)

@@ -34,9 +34,11 @@ class MixtralMoE(nn.Module):
         self.router = None
         self.w13 = None  # [E_local, 2*I_local, H], gate/up rows interleaved by 16
         self.w2 = None   # [E_local, H, I_local]
+        self.w13_p = None  # fragment-packed decode copies (MixtralForCausalLM._pack_mlp)
+        self.w2_p = None
 
     def forward(self, x: torch.Tensor, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-        y = moe.fused_moe(x, self.router, self.w13, self.w2, self.k, self.e_lo, self.e_hi)
+        y = moe.fused_moe(x, self.router, self.w13, self.w2, self.k, self.e_lo, self.e_hi, self.w13_p, self.w2_p)
         return comm.tp_all_reduce(y)
 
 
@@ -68,7 +70,10 @@ class MixtralForCausalLM(LlamaForCausalLM):
         mlp.w2 = _p(torch.stack(w2).contiguous())
 
     def _pack_mlp(self, mlp) -> None:
-        pass  # experts are streamed by the grouped MoE kernel in their own layout
+        E, N, K = mlp.w13.shape
+        mlp.w13_p = gemm.pack_weight(mlp.w13.view(E * N, K)).view(E, N, K)
+        E, N, K = mlp.w2.shape
+        mlp.w2_p = gemm.pack_weight(mlp.w2.view(E * N, K)).view(E, N, K)
 
     def _mlp_hf_state(self, p: str, mlp: MixtralMoE) -> dict:
         out = {p + "block_sparse_moe.gate.weight": mlp.router}

@@ -44,7 +44,8 @@ class GemmArgs(ctypes.Structure):
                 ("eps", ctypes.c_float), ("residual", ctypes.c_void_p), ("sumsq_parts", ctypes.c_void_p),
                 ("positions", ctypes.c_void_p), ("cos_sin", ctypes.c_void_p), ("k_cache", ctypes.c_void_p),
                 ("v_cache", ctypes.c_void_p), ("slots", ctypes.c_void_p), ("nq", ctypes.c_int),
-                ("nkv", ctypes.c_int), ("bs", ctypes.c_int)]
+                ("nkv", ctypes.c_int), ("bs", ctypes.c_int), ("row_offsets", ctypes.c_void_p),
+                ("w_stride", ctypes.c_longlong), ("groups", ctypes.c_int), ("max_group_rows", ctypes.c_int)]
 
 
 _ARGS_CHECKED = False
@@ -67,7 +68,9 @@ def _launch_ex(mode: int, x: torch.Tensor, w: torch.Tensor, packed: Optional[tor
         assert n == ctypes.sizeof(GemmArgs), f"GemmArgs layout mismatch: C {n} vs ctypes {ctypes.sizeof(GemmArgs)}"
         _ARGS_CHECKED = True
     M, K = x.shape
-    N = w.shape[0]
+    N = kw.pop("n_override", None) or w.shape[0]
+    if "groups" in kw:
+        N = w.shape[0] // kw["groups"]
     a = GemmArgs()
     a.out = native.ptr(out)
     a.partial = native.ptr(ws)
@@ -118,6 +121,26 @@ def linear_qkv_rope(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, counters
                positions=positions, cos_sin=cos_sin, k_cache=k_cache, v_cache=v_cache, slots=slots, nq=nq,
                nkv=nkv, bs=k_cache.shape[2])
     return q
+
+
+def grouped_linear(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_rows: int, silu: bool,
+                   packed: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+                   S: int = 1) -> torch.Tensor:
+    """Grouped decode GEMM (MoE experts): rows ``a[offsets[e]:offsets[e+1]]`` times ``w[e]^T``,
+    ``w`` [G, N, K] (``packed``: :func:`pack_weight` of ``w.view(G*N, K)``), every group <= 64
+    rows.  One launch; groups without rows read no weights.  ``silu``: interleaved gate/up →
+    [R, N/2] bf16.  Otherwise ``S`` > 1 returns fp32 split-K slabs [S, R, N] in ``ws``."""
+    G, N, K = w.shape
+    R = a.shape[0]
+    out = None
+    if silu or S == 1:
+        out = torch.empty((R, N // 2 if silu else N), dtype=a.dtype, device=a.device)
+    mode = MODE_SILU if silu else (MODE_BF16 if S == 1 else MODE_PARTIAL)
+    M2 = a  # A rows are addressed through the offsets
+    args = dict(row_offsets=offsets, w_stride=N * K, groups=G, max_group_rows=max_rows)
+    _launch_ex(mode, M2, w.view(G * N, K), None if packed is None else packed.view(G * N, K), S, out=out,
+               ws=ws if S > 1 else None, **args)
+    return out if out is not None else ws
 
 
 def norm_apply(residual: torch.Tensor, parts: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:

@@ -20,7 +20,7 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from . import native, reference
+from . import gemm, native, reference
 from .gemm import silu_and_mul_interleaved
 
 
@@ -94,10 +94,15 @@ def unpermute(y: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, T: int, k: in
     return out
 
 
-def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_rows: int, silu: bool) -> torch.Tensor:
-    """Rows of expert e = a[offsets[e]:offsets[e+1]] times w[e]^T (w: [E_local, N, K])."""
+def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_rows: int, silu: bool,
+                 packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Rows of expert e = a[offsets[e]:offsets[e+1]] times w[e]^T (w: [E_local, N, K]).
+    Decode-sized groups (<= 64 rows) run the weight-streaming decode GEMM of
+    csrc/kernels/gemm_skinny.hip in grouped mode (``packed``: fragment-packed experts)."""
     E_local, N, K = w.shape
     n_out = N // 2 if silu else N
+    if a.is_cuda and max_rows <= 64 and gemm.SKINNY_ENABLED and N % 128 == 0 and K % 256 == 0:
+        return gemm.grouped_linear(a, w, offsets, max_rows, silu, packed=packed)
     out = torch.empty((a.shape[0], n_out), dtype=a.dtype, device=a.device)
     if a.is_cuda and max_rows <= 64:
         native.call("pk_moe_gemm", out.data_ptr(), a.data_ptr(), w.data_ptr(), offsets.data_ptr(), max_rows, N, K,
@@ -113,7 +118,8 @@ def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_ro
 
 
 def fused_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, k: int,
-              e_lo: int = 0, e_hi: Optional[int] = None) -> torch.Tensor:
+              e_lo: int = 0, e_hi: Optional[int] = None, w13_p: Optional[torch.Tensor] = None,
+              w2_p: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Mixtral sparse MLP for this rank's experts.  x [T, H]; router_w [E, H]; w13 [E_l, 2I, H]
     (gate/up interleaved by 16); w2 [E_l, H, I].  Returns the (partial, if EP) combined output."""
     T = x.shape[0]
@@ -123,8 +129,8 @@ def fused_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: to
     ids, wts = topk_softmax(logits, k)
     offsets, sorted_, inv = align(ids, E, e_lo, e_hi)
     xs = permute(x, sorted_, offsets, k)
-    h = grouped_gemm(xs, w13, offsets, T, silu=True)
-    y = grouped_gemm(h, w2, offsets, T, silu=False)
+    h = grouped_gemm(xs, w13, offsets, T, silu=True, packed=w13_p)
+    y = grouped_gemm(h, w2, offsets, T, silu=False, packed=w2_p)
     return unpermute(y, inv, wts, T, k)
 
 

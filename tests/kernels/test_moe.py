@@ -51,3 +51,30 @@ def test_fused_moe(T, ep):
     y = moe.fused_moe(x, router, w13[lo:hi].contiguous(), w2[lo:hi].contiguous(), 2, lo, hi)
     ref = moe.fused_moe_reference(x, router, w13[lo:hi], w2[lo:hi], 2, lo, hi)
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("T", [1, 9, 64])
+def test_fused_moe_packed_experts(T):
+    """Decode MoE through the grouped weight-streaming GEMM with fragment-packed experts."""
+    E, H, I = 8, 512, 1024
+    router, w13, w2 = weights(E, H, I)
+    x = torch.randn(T, H, device="cuda").to(torch.bfloat16)
+    w13_p = gemm.pack_weight(w13.view(-1, H)).view(w13.shape)
+    w2_p = gemm.pack_weight(w2.view(-1, I)).view(w2.shape)
+    y = moe.fused_moe(x, router, w13, w2, 2, 0, E, w13_p, w2_p)
+    ref = moe.fused_moe_reference(x, router, w13, w2, 2, 0, E)
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+def test_grouped_linear_skips_empty_groups_and_splits():
+    G, N, K, R = 4, 256, 512, 40
+    a = torch.randn(R, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(G, N, K, device="cuda") * 0.05).to(torch.bfloat16)
+    offsets = torch.tensor([0, 17, 17, 40, 40], dtype=torch.int32, device="cuda")  # groups 1 and 3 empty
+    y = gemm.grouped_linear(a, w, offsets, 23, silu=False)
+    exp = torch.cat([a[:17].float() @ w[0].float().t(), a[17:40].float() @ w[2].float().t()])
+    torch.testing.assert_close(y.float(), exp, atol=2e-2, rtol=2e-2)
+    ws = torch.empty(2 * R * N, dtype=torch.float32, device="cuda")
+    p = gemm.grouped_linear(a, w, offsets, 23, silu=False, packed=gemm.pack_weight(w.view(-1, K)).view(w.shape),
+                            ws=ws, S=2)
+    torch.testing.assert_close(p[: 2 * R * N].view(2, R, N).sum(0), exp, atol=2e-2, rtol=2e-2)
