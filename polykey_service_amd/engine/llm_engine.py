@@ -88,6 +88,7 @@ class LLMEngine:
         self.total_output_tokens = 0
         self.overlap = cfg.overlap
         self._inflight = None
+        self.continuation_steps = 0
 
     # ------------------------------------------------------------------ API
     @property
@@ -120,8 +121,14 @@ class LLMEngine:
         step.  Without ``overlap`` each call launches and completes its own batch."""
         done = None
         if self._inflight is not None:
-            done = self._complete(*self._inflight)
+            batch, sampling, handle = self._inflight
+            nxt = self._continuation(batch, handle)
+            done = self._complete(batch, sampling, handle)
             self._inflight = None
+            if nxt is not None:
+                self._inflight = (batch, batch.decodes, nxt)
+                self.continuation_steps += 1
+                return self._outputs(done)
         batch = self.scheduler.schedule()
         if not batch.empty:
             sampling = batch.sampling_seqs()
@@ -130,6 +137,16 @@ class LLMEngine:
                 done = self._complete(*self._inflight)
                 self._inflight = None
         return self._outputs(done) if done else []
+
+    def _continuation(self, batch, handle):
+        """Launch the next decode step of ``batch`` before its current step has been read back
+        (see ModelRunner.launch_continuation) when nothing else could change the batch: pure
+        decode, every running sequence in it and alive, no request waiting for admission."""
+        sch = self.scheduler
+        if (not self.overlap or batch.prefills or sch.waiting or len(batch.decodes) != len(sch.running)
+                or any(s.is_finished() for s in batch.decodes)):
+            return None
+        return self.runner.launch_continuation(batch, handle)
 
     def _complete(self, batch, sampling, handle):
         toks = self.runner.fetch(handle)

@@ -77,11 +77,18 @@ class ModelRunner:
         self.max_blocks = (cfg.max_model_len + self.bs - 1) // self.bs
         self.layout = _Layout(cfg.max_num_batched_tokens, cfg.max_num_seqs, self.max_blocks)
         pin = device.type == "cuda"
-        self.host_buf = torch.zeros(self.layout.size, dtype=torch.int32, pin_memory=pin)
+        # two pinned staging buffers used alternately: a step may be packed while the previous
+        # step's H2D copy is still queued behind the GPU (continuation launches, LLMEngine.step)
+        self._host_bufs = [torch.zeros(self.layout.size, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._hs = [{k: self.layout.view(b, k).numpy() for k in self.layout.sections} for b in self._host_bufs]
+        self._h2d_events = [None, None]
+        self._cur = 0
+        self.host_buf, self.h = self._host_bufs[0], self._hs[0]
         self.dev_buf = torch.zeros(self.layout.size, dtype=torch.int32, device=device)
-        self.h = {k: self.layout.view(self.host_buf, k).numpy() for k in self.layout.sections}
         self.d = {k: self.layout.view(self.dev_buf, k) for k in self.layout.sections}
-        self.tok_host = torch.zeros(cfg.max_num_seqs, dtype=torch.int32, pin_memory=pin)
+        self._tok_hosts = [torch.zeros(cfg.max_num_seqs, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._tok_events = [None, None]
+        self._tok_i = 0
         self.kv_caches: List[Tuple[torch.Tensor, torch.Tensor]] = []
         self.num_blocks = 0
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
@@ -91,7 +98,6 @@ class ModelRunner:
         self.part_o, self.part_ml, self.part_ctr = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks,
                                                                              self.bs, device, n_kv=a0.nkv)
         self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0}
-        self._tok_event = None
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None
 
@@ -190,9 +196,17 @@ class ModelRunner:
         ``batch.sampling_seqs()`` in order."""
         return self.fetch(self.launch(batch))
 
+    def _next_staging(self) -> None:
+        self._cur ^= 1
+        ev = self._h2d_events[self._cur]
+        if ev is not None:
+            ev.synchronize()  # that buffer's last H2D copy has been consumed (normally long ago)
+        self.host_buf, self.h = self._host_bufs[self._cur], self._hs[self._cur]
+
     def launch(self, batch: ScheduledBatch):
         """Enqueue one step (pack → H2D → graph replay / eager forward → sample → async D2H of
         the sampled ids) without waiting for the GPU; :meth:`fetch` returns the ids."""
+        self._next_staging()
         sampling = batch.sampling_seqs()
         T, n = self._pack(batch, sampling)
         nd = len(batch.decodes)
@@ -211,27 +225,74 @@ class ModelRunner:
         h["header"][:7] = (self.MODE_RUN, T, n, nd, ns, max_q, g)
         self._publish()
         toks = self._run(T, n, nd, ns, max_q, g)
+        return self._handle(toks, ns)
+
+    def _handle(self, toks, ns: int):
         self.stats["steps"] += 1
         if ns == 0 or toks is None:
-            return None, 0
-        if toks.is_cuda:
-            self.tok_host[:ns].copy_(toks[:ns], non_blocking=True)
-            if self._tok_event is None:
-                self._tok_event = torch.cuda.Event()
-            self._tok_event.record(torch.cuda.current_stream(self.device))
-            return self.tok_host, ns
-        return toks, ns
+            return None, 0, None, None
+        if not toks.is_cuda:
+            return toks, ns, None, None
+        self._tok_i ^= 1
+        host = self._tok_hosts[self._tok_i]
+        host[:ns].copy_(toks[:ns], non_blocking=True)
+        ev = self._tok_events[self._tok_i]
+        if ev is None:
+            ev = self._tok_events[self._tok_i] = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return host, ns, ev, toks
 
     def fetch(self, handle) -> List[int]:
-        toks, ns = handle
+        toks, ns, ev, _ = handle
         if ns == 0:
             return []
-        if toks is self.tok_host and self._tok_event is not None:
-            self._tok_event.synchronize()
+        if ev is not None:
+            ev.synchronize()
         return toks[:ns].tolist()
+
+    def launch_continuation(self, batch: ScheduledBatch, prev) -> Optional[tuple]:
+        """Decode step k+1 of ``batch.decodes`` enqueued while step k (``prev``) may still run:
+        every sequence advances one position, and step k's sampled ids — still on the GPU —
+        are copied into this step's input ids on the stream, so the host never waits between
+        the two steps.  Needs a captured graph bucket; returns None (caller falls back to a
+        scheduled step) when a sequence cannot get the KV block for its next position."""
+        seqs = batch.decodes
+        n = len(seqs)
+        g = self._graph_bucket(n) if self.graphs else None
+        if not g or prev[3] is None or batch.prefills or self.model.st.tp_size > 1:
+            return None
+        for s in seqs:
+            if s.num_computed + 2 > self.cfg.max_model_len or not self.bm.allocate(s.seq_id, s.num_computed + 2):
+                return None
+        self._next_staging()
+        h = self.h
+        sids = np.fromiter((s.seq_id for s in seqs), dtype=np.int64, count=n)
+        ncomp = np.fromiter((s.num_computed + 1 for s in seqs), dtype=np.int32, count=n)
+        ones = np.ones(n, dtype=np.int32)
+        T = self.bm.pack_step(sids, ncomp, ones, np.zeros(n, dtype=np.int32), h["input_ids"], h["positions"],
+                              h["slots"], h["block_tables"], self.max_blocks, h["context_lens"], h["cu_q"])
+        h["sample_idx"][:n] = np.arange(n, dtype=np.int32)
+        for r, s in enumerate(seqs):
+            p = s.params
+            h["temperature"][r] = p.temperature
+            h["top_k"][r] = p.top_k
+            h["top_p"][r] = p.top_p
+            h["min_p"][r] = p.min_p
+            h["seeds"][r] = s.seed
+            h["offsets"][r] = len(s.output_ids) + 1
+        self._pad_decode(n, g)
+        h["header"][:7] = (self.MODE_RUN, T, n, n, n, 0, g)
+        self._publish()
+        self.d["input_ids"][:n].copy_(prev[3][:n])  # step k's sampled ids, stream-ordered
+        return self._handle(self._run(T, n, n, n, 0, g), n)
 
     def _publish(self) -> None:
         self.dev_buf.copy_(self.host_buf, non_blocking=True)
+        if self.device.type == "cuda":
+            ev = self._h2d_events[self._cur]
+            if ev is None:
+                ev = self._h2d_events[self._cur] = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
         if self.model.st.tp_size > 1:
             from ..parallel import comm
             comm.tp_broadcast_tensor(self.dev_buf)

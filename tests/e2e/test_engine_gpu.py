@@ -99,3 +99,26 @@ def test_fused_decode_chain_matches_unfused(name):
         LlamaForCausalLM.FUSED_DECODE = old
     torch.testing.assert_close(logits[1], logits[0], atol=0.1, rtol=0.05)
     assert toks[0] == toks[1]
+
+
+def test_continuation_steps_match_synchronous_engine():
+    """Pipelined decode continuations (next step launched from the GPU-resident sampled ids
+    before the host reads them) produce exactly the synchronous engine's tokens, for greedy and
+    seeded sampling, with staggered lengths so sequences finish while a step is in flight."""
+    _, gpu = _models("tiny-llama-gqa4")
+    prompts = [[1] + list(range(5, 5 + n)) for n in (3, 17, 40, 9)]
+    params = [SamplingParams(max_tokens=m, temperature=t, seed=7, ignore_eos=True)
+              for m, t in ((20, 0.0), (13, 0.8), (31, 0.0), (5, 1.0))]
+    res = []
+    for overlap in (False, True):
+        e = LLMEngine(EngineConfig(model="tiny-llama-gqa4", max_num_seqs=8, max_num_batched_tokens=256,
+                                   max_model_len=512, hip_graphs=True, device="cuda", overlap=overlap),
+                      ParallelState(device=torch.device("cuda")), model=gpu)
+        seqs = [e.add_request(p, sp) for p, sp in zip(prompts, params)]
+        while e.has_unfinished():
+            e.step()
+        res.append([s.output_ids for s in seqs])
+        if overlap:
+            assert e.continuation_steps > 0
+        assert e.bm.num_free == e.bm.num_blocks
+    assert res[0] == res[1]
