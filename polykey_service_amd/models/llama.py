@@ -260,13 +260,11 @@ class LlamaForCausalLM(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def embed_tokens(self, ids: torch.Tensor) -> torch.Tensor:
-        if self.st.tp_size == 1:
-            return F.embedding(ids, self.embed)
-        local = ids - self.vocab_start
-        mask = (local >= 0) & (local < self.vocab_local)
-        x = F.embedding(torch.where(mask, local, torch.zeros_like(local)), self.embed)
-        x = x * mask.unsqueeze(-1).to(x.dtype)
-        return comm.tp_all_reduce(x)
+        """Vocab-parallel embedding: one gather kernel with the out-of-shard mask fused
+        (``ops.embedding``), then the TP all-reduce assembles the rows."""
+        start = self.vocab_start if self.st.tp_size > 1 else 0
+        x = ops.embedding(ids, self.embed, start, self.embed.shape[0] if self.st.tp_size == 1 else self.vocab_local)
+        return comm.tp_all_reduce(x) if self.st.tp_size > 1 else x
 
     def forward(self, input_ids: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata,
                 kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:

@@ -45,7 +45,6 @@ SIGNATURES = {
     "pk_moe_unpermute": [P, P, P, P, I32, I32, I32, P],
     "pk_moe_gemm": [P, P, P, P, I32, I32, I32, I32, I32, I32, P],
     "pk_moe_unpermute_partial": [P, P, I32, I32, P, P, I32, I32, I32, P],
-    "pk_argmax": [P, P, I32, I32, I32, P],
     "pk_silu_and_mul_il": [P, P, I32, I32, P],
     "pk_skinny_gemm": [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P],
     "pk_splitk_reduce": [P, P, I32, I32, I32, I32, I32, P],

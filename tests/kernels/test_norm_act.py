@@ -45,3 +45,16 @@ def test_native_library_is_loaded():
     assert native.lib().pk_kernels_abi_version() == 1
     with open("/proc/self/maps") as f:
         assert "libpk_kernels.so" in f.read()
+
+
+@pytest.mark.parametrize("start,local", [(0, 1000), (250, 300)])
+def test_embedding_vocab_parallel_mask(start, local):
+    from polykey_service_amd import ops
+    V, H, T = 1000, 4096, 77
+    table = torch.randn(local, H, device="cuda").to(torch.bfloat16)
+    ids = torch.randint(0, V, (T,), device="cuda", dtype=torch.int32)
+    y = ops.embedding(ids, table, start, local)
+    loc = ids.long() - start
+    mask = (loc >= 0) & (loc < local)
+    exp = torch.where(mask[:, None], table[loc.clamp(0, local - 1)], torch.zeros_like(table[:1]))
+    assert torch.equal(y, exp)
