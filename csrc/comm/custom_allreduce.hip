@@ -1,0 +1,233 @@
+// One-shot all-reduce over xGMI peer memory for small TP messages (decode activations).
+//
+// SURVEY.md §2.3 ("C++ IPC one-shot all-reduce ... for small decode messages") and §6: a 70B TP=8
+// decode step issues 160 all-reduces of ~1 MiB; at RCCL's small-message latency these cost
+// as much as the weight streaming.  MI355X GPUs of a node are fully connected by xGMI
+// (7 links per GPU), so every rank can read every peer's buffer directly:
+//
+//   1. each workgroup b copies its chunk of the input into this rank's IPC buffer (slot = call
+//      parity, so a slow peer still reading the previous call is never overwritten);
+//   2. system-scope release, then it stamps flag[b][rank] = epoch in EVERY peer's signal area
+//      (remote stores over xGMI);
+//   3. it polls its own flag[b][j] == epoch for all peers j (relaxed system-scope loads, bounded
+//      spin), acquires, reads chunk b from all W buffers (peer reads over xGMI), sums in fp32 in
+//      a fixed rank order (bit-identical on every rank) and writes bf16 output.
+//
+// No grid-wide barrier: chunk b only depends on the W workgroups b of the W ranks.  The epoch
+// lives in device memory (per workgroup), so the kernel replays correctly inside HIP graphs.
+// IPC buffers are allocated uncached (hipDeviceMallocUncached): peers' stores become visible
+// to polling loads without cache maintenance, and remote data reads are never served stale.
+// A spin that exceeds its bound sets an error word and exits instead of hanging the GPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstring>
+
+#define PK_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 256;
+constexpr int kThreads = 512;
+
+struct Signals {                                 // at the start of every rank's IPC buffer
+  uint32_t flag[kMaxBlocks][kMaxRanks];          // written by peers (remote stores)
+  uint32_t epoch[kMaxBlocks];                    // this rank's per-workgroup call counter
+  uint32_t error;                                // set when a spin times out
+};
+
+constexpr size_t kSigBytes = (sizeof(Signals) + 4095) / 4096 * 4096;
+
+struct PeerPtrs {
+  char* base[kMaxRanks];  // every rank's IPC buffer as mapped in this process (own included)
+};
+
+struct Ctx {
+  int rank = 0, world = 0;
+  size_t data_bytes = 0;  // per parity slot
+  char* local = nullptr;  // own IPC buffer
+  PeerPtrs peers{};
+  PeerPtrs* d_peers = nullptr;
+  bool opened[kMaxRanks] = {};
+};
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
+}
+
+// n16: message size in 16-byte vectors (8 bf16).  Each workgroup owns a contiguous chunk.
+template <int W>
+__global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __restrict__ peers, int rank,
+                                                             size_t data_bytes, const uint4* __restrict__ inp,
+                                                             uint4* __restrict__ out, int64_t n16) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
+  __shared__ uint32_t e_s;
+  if (threadIdx.x == 0) e_s = my_sig->epoch[b] + 1;
+  __syncthreads();
+  const uint32_t e = e_s;
+  const size_t slot = kSigBytes + (e & 1u) * data_bytes;
+  const int64_t per = (n16 + nb - 1) / nb;
+  const int64_t lo = b * per, hi = min(n16, lo + per);
+
+  // 1. stage my chunk into my own buffer
+  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + slot);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) mine[i] = inp[i];
+  // 2. publish: every thread's stores drained, system release, then one lane stamps every peer
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < W) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
+    __hip_atomic_store(&ps->flag[b][rank], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 3. wait for all peers' chunk b, then reduce
+  if (threadIdx.x < W) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(&my_sig->flag[b][threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {
+        __hip_atomic_store(&my_sig->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  const uint4* src[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) src[j] = reinterpret_cast<const uint4*>(peers->base[j] + slot);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    uint4 v[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) v[j] = src[j][i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[2 * q] += bf2f(static_cast<uint16_t>(w4[q] & 0xffffu));
+        acc[2 * q + 1] += bf2f(static_cast<uint16_t>(w4[q] >> 16));
+      }
+    }
+    out[i] = make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
+  }
+  if (threadIdx.x == 0) my_sig->epoch[b] = e;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- host API
+PK_EXPORT int pk_car_abi_version() { return 1; }
+
+PK_EXPORT int pk_car_ipc_handle_size() { return static_cast<int>(sizeof(hipIpcMemHandle_t)); }
+
+// Allocate this rank's IPC buffer (signals + 2 data slots of data_bytes) on the current device.
+PK_EXPORT void* pk_car_create(int rank, int world, long long data_bytes) {
+  if (world < 2 || world > kMaxRanks || rank < 0 || rank >= world || data_bytes <= 0 || data_bytes % 16) return nullptr;
+  Ctx* c = new Ctx();
+  c->rank = rank;
+  c->world = world;
+  c->data_bytes = static_cast<size_t>(data_bytes);
+  const size_t total = kSigBytes + 2 * c->data_bytes;
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, total, hipDeviceMallocUncached) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  if (hipMemset(p, 0, total) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    delete c;
+    return nullptr;
+  }
+  c->local = static_cast<char*>(p);
+  c->peers.base[rank] = c->local;
+  return c;
+}
+
+PK_EXPORT int pk_car_get_handle(void* ctx, void* out) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, c->local) != hipSuccess) return -1;
+  std::memcpy(out, &h, sizeof(h));
+  return 0;
+}
+
+// handles: world * pk_car_ipc_handle_size() bytes, rank-major (own entry ignored).
+PK_EXPORT int pk_car_open(void* ctx, const void* handles) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  const char* hb = static_cast<const char*>(handles);
+  for (int j = 0; j < c->world; ++j) {
+    if (j == c->rank) continue;
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, hb + j * sizeof(h), sizeof(h));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -1 - j;
+    c->peers.base[j] = static_cast<char*>(p);
+    c->opened[j] = true;
+  }
+  if (hipMalloc(&c->d_peers, sizeof(PeerPtrs)) != hipSuccess) return -20;
+  if (hipMemcpy(c->d_peers, &c->peers, sizeof(PeerPtrs), hipMemcpyHostToDevice) != hipSuccess) return -21;
+  return 0;
+}
+
+// bf16 sum over the group: out = sum_j inp_j ; bytes % 16 == 0 and bytes <= data_bytes.
+PK_EXPORT int pk_car_allreduce_bf16(void* ctx, const void* inp, void* out, long long bytes, int blocks,
+                                    hipStream_t stream) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr || c->d_peers == nullptr) return -1;
+  if (bytes <= 0) return 0;
+  if (bytes % 16 || static_cast<size_t>(bytes) > c->data_bytes) return -2;
+  const int64_t n16 = bytes / 16;
+  if (blocks <= 0) blocks = static_cast<int>(std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, n16 / (kThreads * 2))));
+  blocks = std::min(blocks, kMaxBlocks);
+  const uint4* in4 = static_cast<const uint4*>(inp);
+  uint4* out4 = static_cast<uint4*>(out);
+  switch (c->world) {
+#define PK_CAR_CASE(WW)                                                                                          \
+  case WW:                                                                                                     \
+    allreduce_1shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, n16); \
+    break;
+    PK_CAR_CASE(2)
+    PK_CAR_CASE(3)
+    PK_CAR_CASE(4)
+    PK_CAR_CASE(5)
+    PK_CAR_CASE(6)
+    PK_CAR_CASE(7)
+    PK_CAR_CASE(8)
+#undef PK_CAR_CASE
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+// 1 if any spin of this rank timed out since the last call (and clears it).
+PK_EXPORT int pk_car_check_error(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  uint32_t err = 0;
+  Signals* s = reinterpret_cast<Signals*>(c->local);
+  if (hipMemcpy(&err, &s->error, sizeof(err), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (err) {
+    const uint32_t z = 0;
+    (void)hipMemcpy(&s->error, &z, sizeof(z), hipMemcpyHostToDevice);
+  }
+  return static_cast<int>(err);
+}
+
+PK_EXPORT void pk_car_destroy(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr) return;
+  (void)hipDeviceSynchronize();
+  for (int j = 0; j < c->world; ++j)
+    if (c->opened[j]) (void)hipIpcCloseMemHandle(c->peers.base[j]);
+  if (c->d_peers) (void)hipFree(c->d_peers);
+  if (c->local) (void)hipFree(c->local);
+  delete c;
+}

@@ -21,6 +21,9 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     st = get_state()
     if st.tp_size == 1:
         return x
+    car = st.custom_ar
+    if car is not None and car.supports(x):
+        return car.all_reduce(x)  # one-shot xGMI kernel (small decode messages)
     dist.all_reduce(x, group=st.tp_group)
     return x
 

@@ -1,0 +1,115 @@
+"""One-shot all-reduce over xGMI peer memory (csrc/comm/custom_allreduce.hip).
+
+For the small activations of TP decode (a 70B TP=8 step issues 160 all-reduces of ~1 MiB,
+SURVEY.md §6) a single kernel in which every rank reads every peer's buffer over xGMI beats
+RCCL's ring/tree latency.  The group's IPC buffers are exchanged once over the gloo control
+group; messages larger than the buffer, non-bf16 tensors, or a failed start-up self-test fall
+back to RCCL (``dist.all_reduce``).  ``POLYKEY_CUSTOM_AR=0`` disables it.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .._native.loader import load_cdll
+
+log = logging.getLogger(__name__)
+
+_P, _I, _LL = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+
+
+def _lib() -> ctypes.CDLL:
+    lib = load_cdll("libpk_comm")
+    if not getattr(lib, "_pk_typed", False):
+        lib.pk_car_create.argtypes = [_I, _I, _LL]
+        lib.pk_car_create.restype = _P
+        lib.pk_car_get_handle.argtypes = [_P, _P]
+        lib.pk_car_open.argtypes = [_P, _P]
+        lib.pk_car_allreduce_bf16.argtypes = [_P, _P, _P, _LL, _I, _P]
+        lib.pk_car_check_error.argtypes = [_P]
+        lib.pk_car_destroy.argtypes = [_P]
+        lib.pk_car_destroy.restype = None
+        lib._pk_typed = True
+    return lib
+
+
+class CustomAllReduce:
+    def __init__(self, cpu_group, rank: int, world: int, device: torch.device, max_bytes: int = 16 << 20,
+                 blocks: int = 0):
+        self.lib = _lib()
+        self.rank, self.world, self.device = rank, world, device
+        self.max_bytes = max_bytes
+        self.blocks = blocks
+        with torch.cuda.device(device):
+            self.ctx = self.lib.pk_car_create(rank, world, max_bytes)
+        if not self.ctx:
+            raise RuntimeError("pk_car_create failed (uncached IPC buffer allocation)")
+        hsz = self.lib.pk_car_ipc_handle_size()
+        mine = ctypes.create_string_buffer(hsz)
+        if self.lib.pk_car_get_handle(self.ctx, mine) != 0:
+            raise RuntimeError("hipIpcGetMemHandle failed")
+        allh = [None] * world
+        dist.all_gather_object(allh, bytes(mine.raw), group=cpu_group)
+        blob = ctypes.create_string_buffer(b"".join(allh), hsz * world)
+        with torch.cuda.device(device):
+            rc = self.lib.pk_car_open(self.ctx, blob)
+        if rc != 0:
+            raise RuntimeError(f"pk_car_open failed ({rc})")
+
+    def supports(self, x: torch.Tensor) -> bool:
+        n = x.numel() * x.element_size()
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n % 16 == 0
+                and 0 < n <= self.max_bytes)
+
+    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        out = torch.empty_like(x) if out is None else out
+        rc = self.lib.pk_car_allreduce_bf16(self.ctx, x.data_ptr(), out.data_ptr(), x.numel() * x.element_size(),
+                                            self.blocks, torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"custom all-reduce launch failed ({rc})")
+        return out
+
+    def error(self) -> int:
+        return self.lib.pk_car_check_error(self.ctx)
+
+    def self_test(self) -> bool:
+        """Rank-dependent pattern reduced twice (both buffer parities) and checked on the host."""
+        ok = True
+        for it in range(2):
+            n = 4096 * (it + 1) + 8
+            x = torch.full((n,), float(self.rank + 1 + it), dtype=torch.bfloat16, device=self.device)
+            y = self.all_reduce(x)
+            torch.cuda.synchronize(self.device)
+            want = sum(r + 1 + it for r in range(self.world))
+            ok &= bool((y.float() == want).all().item())
+        return ok and self.error() == 0
+
+    def close(self) -> None:
+        if self.ctx:
+            self.lib.pk_car_destroy(self.ctx)
+            self.ctx = None
+
+
+def maybe_create(st) -> Optional[CustomAllReduce]:
+    """Custom all-reduce for this rank's TP group when it is a single-node GPU group."""
+    if os.environ.get("POLYKEY_CUSTOM_AR", "1") == "0" or st.tp_size < 2 or st.device.type != "cuda":
+        return None
+    if st.tp_size > 8 or int(os.environ.get("LOCAL_WORLD_SIZE", str(st.world_size))) < st.tp_size:
+        return None
+    try:
+        car = CustomAllReduce(st.tp_cpu_group, st.tp_rank, st.tp_size, st.device)
+        good = car.self_test()
+        votes = [None] * st.tp_size
+        dist.all_gather_object(votes, good, group=st.tp_cpu_group)
+        if all(votes):
+            return car
+        log.warning("custom all-reduce self-test failed on some rank; using RCCL")
+        car.close()
+    except Exception as e:  # noqa: BLE001 - any failure → RCCL path
+        log.warning("custom all-reduce unavailable (%s); using RCCL", e)
+    return None

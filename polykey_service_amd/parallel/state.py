@@ -31,6 +31,7 @@ class ParallelState:
     ep_rank: int = 0
     tp_group: Optional[object] = None      # device collectives (RCCL / gloo on CPU)
     tp_cpu_group: Optional[object] = None  # gloo: control-plane broadcast of step metadata
+    custom_ar: Optional[object] = None     # one-shot xGMI all-reduce (parallel/custom_ar.py)
     backend: str = "none"
     device: torch.device = dataclasses.field(default_factory=lambda: torch.device("cpu"))
 
@@ -89,11 +90,17 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
             gc = dist.new_group(ranks, backend="gloo") if be != "gloo" else g
             if rank in ranks:
                 st.tp_group, st.tp_cpu_group = g, gc
+        if be == "nccl":
+            from .custom_ar import maybe_create
+            st.custom_ar = maybe_create(st)
     set_state(st)
     return st
 
 
 def destroy_parallel() -> None:
+    car = get_state().custom_ar
+    if car is not None:
+        car.close()
     if dist.is_initialized():
         dist.destroy_process_group()
     set_state(ParallelState())
