@@ -4,7 +4,8 @@ For the small activations of TP decode (a 70B TP=8 step issues 160 all-reduces o
 SURVEY.md §6) a single kernel in which every rank reads every peer's buffer over xGMI beats
 RCCL's ring/tree latency.  The group's IPC buffers are exchanged once over the gloo control
 group; messages larger than the buffer, non-bf16 tensors, or a failed start-up self-test fall
-back to RCCL (``dist.all_reduce``).  ``POLYKEY_CUSTOM_AR=0`` disables it.
+back to RCCL (``dist.all_reduce``).  ``POLYKEY_CUSTOM_AR=0`` disables it; ``force`` also
+enables it on a gloo-backed GPU group (tests run TP ranks that share one GPU that way).
 """
 from __future__ import annotations
 

@@ -90,7 +90,7 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
             gc = dist.new_group(ranks, backend="gloo") if be != "gloo" else g
             if rank in ranks:
                 st.tp_group, st.tp_cpu_group = g, gc
-        if be == "nccl":
+        if be == "nccl" or (os.environ.get("POLYKEY_CUSTOM_AR") == "force" and dev.type == "cuda"):
             from .custom_ar import maybe_create
             st.custom_ar = maybe_create(st)
     set_state(st)
