@@ -57,6 +57,9 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
         S = gemm.choose_split(w.shape[0], x.shape[1], x.shape[0])
         if ws.numel() >= S * x.shape[0] * w.shape[0]:
             return gemm.linear_partial(x, w, ws, S, packed=wp)
+    if x.shape[0] > gemm.SKINNY_MAX_M:
+        # prefill: the all-reduce of one row chunk overlaps the GEMM of the next
+        return comm.tp_row_parallel_overlapped(x, w.shape[0], lambda rows, out: gemm.linear(rows, w, out=out))
     return comm.tp_all_reduce(_proj(x, w, ws, wp))
 
 

@@ -9,6 +9,7 @@ MiB and bandwidth-bound over the 7 xGMI links.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -18,14 +19,55 @@ from .state import get_state
 
 
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    """Sum over the TP group, in place (returns ``x``)."""
     st = get_state()
     if st.tp_size == 1:
         return x
     car = st.custom_ar
     if car is not None and car.supports(x):
-        return car.all_reduce(x)  # one-shot xGMI kernel (small decode messages)
+        return car.all_reduce(x, out=x)  # one-shot xGMI kernel (small decode messages)
     dist.all_reduce(x, group=st.tp_group)
     return x
+
+
+_COMM_STREAMS = {}
+
+
+def _comm_stream(device: torch.device) -> "torch.cuda.Stream":
+    s = _COMM_STREAMS.get(device)
+    if s is None:
+        s = _COMM_STREAMS[device] = torch.cuda.Stream(device)
+    return s
+
+
+OVERLAP_MIN_ROWS = int(os.environ.get("POLYKEY_TP_OVERLAP_MIN_ROWS", "256"))
+
+
+def tp_row_parallel_overlapped(x: torch.Tensor, n_out: int, fn, chunks: int = 2,
+                               min_rows: Optional[int] = None) -> torch.Tensor:
+    """``all_reduce(fn(x))`` for a row-parallel projection with the collective of chunk i on a
+    dedicated HIP stream while the GEMM of chunk i+1 runs on the compute stream (prefill-sized
+    ``x``; SURVEY.md §2.3 TP: RCCL all-reduce overlapped with the GEMMs).  ``fn(rows, out)``
+    writes the local partial product of ``rows`` into ``out``."""
+    st = get_state()
+    T = x.shape[0]
+    out = torch.empty((T, n_out), dtype=x.dtype, device=x.device)
+    min_rows = OVERLAP_MIN_ROWS if min_rows is None else min_rows
+    if st.tp_size == 1 or not x.is_cuda or T < min_rows * chunks:
+        fn(x, out)
+        return tp_all_reduce(out)
+    main = torch.cuda.current_stream(x.device)
+    cs = _comm_stream(x.device)
+    bounds = [T * i // chunks for i in range(chunks + 1)]
+    for i in range(chunks):
+        sl = slice(bounds[i], bounds[i + 1])
+        fn(x[sl], out[sl])
+        cs.wait_stream(main)
+        with torch.cuda.stream(cs):
+            tp_all_reduce(out[sl])
+    main.wait_stream(cs)
+    out.record_stream(cs)
+    return out
 
 
 def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:

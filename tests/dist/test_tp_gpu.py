@@ -1,6 +1,7 @@
 """Tensor parallelism on the GPU code path with 2 ranks sharing one MI355X (gloo carries the
 collectives that RCCL would across GPUs; the one-shot IPC all-reduce kernel carries the TP
-all-reduces): TP=2 must reproduce TP=1 (same random-init weights)."""
+all-reduces; prefill row-parallel projections take the chunked comm-stream overlap path):
+TP=2 must reproduce TP=1 (same random-init weights)."""
 import os
 import socket
 
@@ -41,7 +42,7 @@ def _run(eng):
 
 def _worker(rank, port, model, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
-                      LOCAL_RANK="0", POLYKEY_CUSTOM_AR="force")
+                      LOCAL_RANK="0", POLYKEY_CUSTOM_AR="force", POLYKEY_TP_OVERLAP_MIN_ROWS="8")
     from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
     st = init_parallel(tp=2, device="cuda", backend="gloo")
     assert st.custom_ar is not None, "custom all-reduce did not come up"
