@@ -33,6 +33,7 @@ constexpr int kHD = 128;
 constexpr int kStep = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1e30f;
+constexpr int kDecodeZ = 4;  // partition workgroups per (seq, kv head)
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
 
@@ -159,97 +160,102 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     int max_blocks, int q_stride, int out_stride, int n_parts, float scale2) {
   __shared__ float o_lds[4][16][kHD + 4];
   __shared__ float ml_lds[4][16][2];
-  const int h = blockIdx.x, seq = blockIdx.y, part = blockIdx.z;
+  __shared__ int last;
+  const int h = blockIdx.x, seq = blockIdx.y;
   const int ctx = context_lens[seq];
-  const int begin = part * kPart;
   const int G = n_q / n_kv;
-  if (begin >= ctx) {
-    if (part == 0)  // ctx == 0: a padded (graph) row -> zeros
+  if (ctx <= 0) {
+    if (blockIdx.z == 0)  // a padded (graph) row -> zeros
       for (int idx = threadIdx.x; idx < G * kHD; idx += 256)
         out[static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD] = 0;
     return;
   }
-  const int end = min(ctx, begin + kPart);
+  const int n_used = (ctx + kPart - 1) / kPart;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
-
   bf16x8_t qf[4];
   load_q(qf, q + static_cast<int64_t>(seq) * q_stride + (h * G + r) * kHD, r < G);
-  WaveState st;
-  init_state(st);
-  attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs, blk_stride,
-         block_tables + static_cast<int64_t>(seq) * max_blocks, bs, begin + kStep * w, end, 4 * kStep, ctx, ctx - 1,
-         scale2);
-  const float lsum = col_sum(st.l);
+
+  // the grid's z dimension is small (<= 4); a workgroup walks partitions z, z + gridDim.z, ...
+  for (int part = blockIdx.z; part < n_used; part += gridDim.z) {
+    const int begin = part * kPart;
+    const int end = min(ctx, begin + kPart);
+    WaveState st;
+    init_state(st);
+    attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs, blk_stride,
+           block_tables + static_cast<int64_t>(seq) * max_blocks, bs, begin + kStep * w, end, 4 * kStep, ctx,
+           ctx - 1, scale2);
+    const float lsum = col_sum(st.l);
+    __syncthreads();  // the previous partition's LDS readers are done
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
+    for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o_lds[w][r][16 * dt + 4 * g + i] = st.o[dt][i];
-  if (g == 0) {
-    ml_lds[w][r][0] = st.m;
-    ml_lds[w][r][1] = lsum;
-  }
-  __syncthreads();
-  const int n_used = (ctx + kPart - 1) / kPart;
-  for (int idx = threadIdx.x; idx < G * kHD; idx += 256) {
-    const int c = idx / kHD, d = idx % kHD;
-    float M = kNegBig;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
-    float O = 0.f, L = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-      const float f = exp2f(ml_lds[ww][c][0] - M);
-      O += f * o_lds[ww][c][d];
-      L += f * ml_lds[ww][c][1];
+      for (int i = 0; i < 4; ++i) o_lds[w][r][16 * dt + 4 * g + i] = st.o[dt][i];
+    if (g == 0) {
+      ml_lds[w][r][0] = st.m;
+      ml_lds[w][r][1] = lsum;
     }
-    const int hq = h * G + c;
-    if (n_used == 1) {
-      out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
-    } else {
-      const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + part;
-      part_o[pi * kHD + d] = O;
-      if (d == 0) {
-        part_ml[2 * pi] = M;
-        part_ml[2 * pi + 1] = L;
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < G * kHD; idx += 256) {
+      const int c = idx / kHD, d = idx % kHD;
+      float M = kNegBig;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
+      float O = 0.f, L = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const float f = exp2f(ml_lds[ww][c][0] - M);
+        O += f * o_lds[ww][c][d];
+        L += f * ml_lds[ww][c][1];
+      }
+      const int hq = h * G + c;
+      if (n_used == 1) {
+        out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
+      } else {
+        const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + part;
+        part_o[pi * kHD + d] = O;
+        if (d == 0) {
+          part_ml[2 * pi] = M;
+          part_ml[2 * pi + 1] = L;
+        }
       }
     }
-  }
-  if (n_used == 1 || counters == nullptr) return;
-  // ---- in-launch split-K merge: the last partition to arrive combines all of them
-  // (guide §5 "In-launch split-K reduction": plain slab stores, every wave drains, one agent
-  // release + ticket; the last arriver acquires, merges and re-arms the counter).
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (n_used == 1 || counters == nullptr) continue;
+    // ---- in-launch split-K merge: the last partition to arrive combines all of them
+    // (guide §5 "In-launch split-K reduction": plain slab stores, every wave drains, one agent
+    // release + ticket; the last arriver acquires, merges and re-arms the counter).
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int* ctr = counters + seq * n_kv + h;
-    const int t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == n_used - 1);
-    if (last) {
-      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int* ctr = counters + seq * n_kv + h;
+      const int t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (t == n_used - 1);
+      if (last) {
+        __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
-  }
-  __syncthreads();
-  if (!last) return;
-  for (int idx = threadIdx.x; idx < G * kHD; idx += 256) {
-    const int c = idx / kHD, d = idx % kHD;
-    const int hq = h * G + c;
-    const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
-    float M = kNegBig;
-    for (int p = 0; p < n_used; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
-    float O = 0.f, L = 0.f;
-    for (int p = 0; p < n_used; ++p) {
-      const float f = exp2f(part_ml[2 * (base + p)] - M);
-      O += f * part_o[(base + p) * kHD + d];
-      L += f * part_ml[2 * (base + p) + 1];
+    __syncthreads();
+    if (!last) continue;
+    for (int idx = threadIdx.x; idx < G * kHD; idx += 256) {
+      const int c = idx / kHD, d = idx % kHD;
+      const int hq = h * G + c;
+      const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
+      float M = kNegBig;
+      for (int p = 0; p < n_used; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
+      float O = 0.f, L = 0.f;
+      for (int p = 0; p < n_used; ++p) {
+        const float f = exp2f(part_ml[2 * (base + p)] - M);
+        O += f * part_o[(base + p) * kHD + d];
+        L += f * part_ml[2 * (base + p) + 1];
+      }
+      out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
     }
-    out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
+    return;  // every partition has arrived
   }
 }
 
@@ -342,7 +348,9 @@ PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, con
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
   const int n_parts = (max_blocks * bs + kDecodePart - 1) / kDecodePart;
   if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
-  dim3 grid(n_kv, n_seqs, n_parts);
+  // z is capped: a short context leaves the extra z-workgroups idle, and graph capture fixes
+  // the grid for max_model_len, so a z of n_parts would launch mostly-empty workgroups
+  dim3 grid(n_kv, n_seqs, n_parts < kDecodeZ ? n_parts : kDecodeZ);
   paged_decode_kernel<kDecodePart><<<grid, 256, 0, stream>>>(
       static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
       static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables), static_cast<const int*>(context_lens),

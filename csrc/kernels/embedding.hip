@@ -31,3 +31,27 @@ PK_EXPORT int pk_embedding(void* out, const void* table, const void* ids, int T,
                                           static_cast<const int*>(ids), H, vocab_start, vocab_local);
   return PK_CHECK_LAUNCH();
 }
+
+// ----------------------------------------------------------------------------------------------
+// Host → device copy done by a kernel reading pinned (hipHostMalloc'd, device-mapped) memory.
+// The per-step staging buffer is small; copying it on the compute queue avoids handing the
+// copy to an SDMA engine, whose cross-queue synchronisation cost ~65 us per step in the decode
+// loop (rocprofv3 --memory-copy-trace, tools/trace_timeline.py).
+namespace {
+
+__global__ void __launch_bounds__(256) copy_from_host_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                             int64_t n16) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += static_cast<int64_t>(gridDim.x) * 256)
+    dst[i] = src[i];
+}
+
+}  // namespace
+
+PK_EXPORT int pk_copy_from_host(void* dst, const void* pinned_src, long long bytes, hipStream_t stream) {
+  if (bytes <= 0) return 0;
+  if (bytes % 16) return -1;
+  const int64_t n16 = bytes / 16;
+  const int grid = static_cast<int>(n16 / 256 + 1 < 64 ? n16 / 256 + 1 : 64);
+  copy_from_host_kernel<<<grid, 256, 0, stream>>>(static_cast<uint4*>(dst), static_cast<const uint4*>(pinned_src), n16);
+  return PK_CHECK_LAUNCH();
+}

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -24,6 +25,7 @@ import numpy as np
 import torch
 
 from ..ops import attention as attn_ops
+from ..ops import native
 from ..ops import sampler as sampler_ops
 from .scheduler import ScheduledBatch
 from .sequence import Sequence
@@ -39,6 +41,10 @@ class RunnerConfig:
     gpu_mem_fraction: float = 0.90
     hip_graphs: bool = True
     graph_batch_sizes: Tuple[int, ...] = ()
+
+
+# stage step inputs with a kernel reading pinned memory instead of an SDMA copy
+HOST_COPY_KERNEL = os.environ.get("POLYKEY_HOST_COPY_KERNEL", "1") == "1"
 
 
 class _Layout:
@@ -223,7 +229,7 @@ class ModelRunner:
             if g:
                 self._pad_decode(nd, g)
         h["header"][:7] = (self.MODE_RUN, T, n, nd, ns, max_q, g)
-        self._publish()
+        self._publish(max(n, g))
         toks = self._run(T, n, nd, ns, max_q, g)
         return self._handle(toks, ns)
 
@@ -282,12 +288,23 @@ class ModelRunner:
             h["offsets"][r] = len(s.output_ids) + 1
         self._pad_decode(n, g)
         h["header"][:7] = (self.MODE_RUN, T, n, n, n, 0, g)
-        self._publish()
+        self._publish(max(n, g))
         self.d["input_ids"][:n].copy_(prev[3][:n])  # step k's sampled ids, stream-ordered
         return self._handle(self._run(T, n, n, n, 0, g), n)
 
-    def _publish(self) -> None:
-        self.dev_buf.copy_(self.host_buf, non_blocking=True)
+    def _publish(self, n_bt_rows: Optional[int] = None) -> None:
+        """Stage the step inputs on the device.  On the GPU a kernel reads the pinned staging
+        buffer directly (no SDMA hand-off); only the prefix up to the used block-table rows
+        (the last section) is copied."""
+        if self.device.type == "cuda" and HOST_COPY_KERNEL:
+            off, _ = self.layout.sections["block_tables"]
+            rows = self.cfg.max_num_seqs if n_bt_rows is None else n_bt_rows
+            n = min(self.layout.size, off + rows * self.max_blocks)
+            n = (n + 3) // 4 * 4  # 16-byte multiple
+            native.call("pk_copy_from_host", self.dev_buf.data_ptr(), self.host_buf.data_ptr(), n * 4,
+                        native.stream_ptr(self.device))
+        else:
+            self.dev_buf.copy_(self.host_buf, non_blocking=True)
         if self.device.type == "cuda":
             ev = self._h2d_events[self._cur]
             if ev is None:

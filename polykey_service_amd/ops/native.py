@@ -53,6 +53,7 @@ SIGNATURES = {
     "pk_skinny_gemm_ex": [P, I32, P],
     "pk_gemm_args_size": [],
     "pk_norm_apply": [P, P, P, I32, P, I32, I32, F32, P],
+    "pk_copy_from_host": [P, P, I64, P],
 }
 
 
