@@ -67,4 +67,7 @@ compose-logs: ## follow server logs through the Jest-style beautifier
 kill-local-server: ## kill whatever listens on $(PORT)
 	@pid=$$(lsof -t -i :$(PORT) 2>/dev/null); if [ -n "$$pid" ]; then kill $$pid; fi
 
+test-race: ## native cores under ASan/UBSan + concurrency stress (the reference's go test -race)
+	$(PY) -m pytest tests/unit/test_native_sanitizers.py tests/integration -q -k "sanitizer or concurrent or cancel"
+
 ci-check: build test ## what CI runs on a CPU runner

@@ -149,8 +149,23 @@ class AsyncLLM:
             except RuntimeError:
                 pass  # loop closed
 
+    def _profiler(self):
+        """``POLYKEY_TORCH_PROFILE=<dir>``: torch.profiler over engine steps (skip 20, warm up 5,
+        record 20), exported as a Chrome trace into <dir>."""
+        out = os.environ.get("POLYKEY_TORCH_PROFILE")
+        if not out:
+            return None
+        import torch
+        from torch.profiler import ProfilerActivity, profile, schedule, tensorboard_trace_handler
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if torch.cuda.is_available() else [])
+        prof = profile(activities=acts, schedule=schedule(wait=20, warmup=5, active=20, repeat=1),
+                       on_trace_ready=tensorboard_trace_handler(out))
+        prof.start()
+        return prof
+
     def _run(self) -> None:
         eng = self.engine
+        prof = self._profiler()
         try:
             while not self._stop:
                 self._drain_cmds()
@@ -160,6 +175,8 @@ class AsyncLLM:
                     continue
                 t0 = time.perf_counter()
                 outs = eng.step()
+                if prof is not None:
+                    prof.step()
                 dt = time.perf_counter() - t0
                 self.stats["step_time_s"] += dt
                 if self.metrics is not None:
@@ -180,6 +197,9 @@ class AsyncLLM:
                     self.on_fatal(e)
                 except Exception:
                     pass
+        finally:
+            if prof is not None:
+                prof.stop()
 
 
 def _fanout(batch) -> None:

@@ -78,6 +78,9 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
     if world > 1:
         be = backend or ("nccl" if dev.type == "cuda" else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # a hung or failed RCCL collective aborts the communicator and raises in this process
+        # (timeout_s), which takes the engine down → health NOT_SERVING → supervisor restart
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if not dist.is_initialized():
             kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
             if be == "nccl":

@@ -13,6 +13,7 @@ from polykey_service_amd.adapters.local_llm import LLMTool, attach_local_llm
 from polykey_service_amd.config.server_config import ServerConfig
 from polykey_service_amd.engine import EngineConfig, LLMEngine
 from polykey_service_amd.engine.async_llm import AsyncLLM
+from polykey_service_amd.engine.sequence import SamplingParams
 from polykey_service_amd.parallel.state import ParallelState
 from polykey_service_amd.service import ToolRouter
 from polykey_service_amd.utils import slog
@@ -184,3 +185,17 @@ def test_replica_pool_balances_requests():
     assert len(set(outs)) == 1  # same weights (same seed) on both replicas → same greedy text
     assert all(rep.stats["requests"] > 0 for rep in pool.replicas)
     pool.shutdown()
+
+
+def test_torch_profiler_toggle(tmp_path, monkeypatch):
+    """POLYKEY_TORCH_PROFILE=<dir> records a Chrome trace of engine steps."""
+    monkeypatch.setenv("POLYKEY_TORCH_PROFILE", str(tmp_path))
+    llm = AsyncLLM(make_engine())
+
+    async def run():
+        return await llm.generate_all([1, 5, 6, 7], SamplingParams(max_tokens=60, ignore_eos=True))
+
+    toks, last = asyncio.run(run())
+    llm.shutdown()
+    assert len(toks) == 60 and last.finished
+    assert any(p.name.endswith(".json") or p.name.endswith(".json.gz") for p in tmp_path.iterdir())
