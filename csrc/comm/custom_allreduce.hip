@@ -34,6 +34,7 @@ constexpr int kThreads = 512;
 
 struct Signals {                                 // at the start of every rank's IPC buffer
   uint32_t flag[kMaxBlocks][kMaxRanks];          // written by peers (remote stores)
+  uint32_t flag2[kMaxBlocks][kMaxRanks];         // two-shot: reduce-scatter results published
   uint32_t epoch[kMaxBlocks];                    // this rank's per-workgroup call counter
   uint32_t error;                                // set when a spin times out
 };
@@ -122,6 +123,104 @@ __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __re
   if (threadIdx.x == 0) my_sig->epoch[b] = e;
 }
 
+// Bounded relaxed poll of this rank's flag[b][j] for every peer j, then one system acquire.
+template <int W>
+__device__ __forceinline__ void wait_all(uint32_t (*flags)[kMaxRanks], int b, uint32_t e, uint32_t* err) {
+  if (threadIdx.x < W) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(&flags[b][threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+// Drain this workgroup's stores, then stamp flags[b][rank] = e in every rank's signal area.
+template <int W>
+__device__ __forceinline__ void publish(const PeerPtrs* peers, int rank, int b, uint32_t e, bool second) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < W) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
+    __hip_atomic_store(second ? &ps->flag2[b][rank] : &ps->flag[b][rank], e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__device__ __forceinline__ void acc8(float* acc, const uint4& v) {
+  const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    acc[2 * q] += bf2f(static_cast<uint16_t>(w4[q] & 0xffffu));
+    acc[2 * q + 1] += bf2f(static_cast<uint16_t>(w4[q] >> 16));
+  }
+}
+
+// Two-shot all-reduce for larger messages: reduce-scatter (rank r sums slice r of every peer's
+// staged input) then all-gather (every rank reads every reduced slice), so each rank moves
+// ~2 (W-1)/W of the message over xGMI instead of (W-1) x.  Slice s is split into gridDim.x
+// chunks; workgroup b owns chunk b of every slice and synchronises only with workgroups b.
+template <int W>
+__global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __restrict__ peers, int rank,
+                                                             size_t data_bytes, const uint4* __restrict__ inp,
+                                                             uint4* __restrict__ out, int64_t n16) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
+  __shared__ uint32_t e_s;
+  if (threadIdx.x == 0) e_s = my_sig->epoch[b] + 1;
+  __syncthreads();
+  const uint32_t e = e_s;
+  const size_t in_slot = kSigBytes + (e & 1u) * data_bytes;
+  const size_t res_slot = kSigBytes + (2 + (e & 1u)) * data_bytes;
+  const int64_t slice = (n16 + W - 1) / W;
+  const int64_t per = (slice + nb - 1) / nb;
+  auto range = [&](int s, int64_t& lo, int64_t& hi) {
+    lo = min(n16, s * slice + b * per);
+    hi = min(min(n16, (s + 1) * slice), lo + per);
+  };
+  // 1. stage chunk b of every slice
+  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + in_slot);
+  for (int s = 0; s < W; ++s) {
+    int64_t lo, hi;
+    range(s, lo, hi);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) mine[i] = inp[i];
+  }
+  publish<W>(peers, rank, b, e, false);
+  wait_all<W>(my_sig->flag, b, e, &my_sig->error);
+  // 2. reduce chunk b of my slice across all ranks into my result region
+  {
+    int64_t lo, hi;
+    range(rank, lo, hi);
+    uint4* res = reinterpret_cast<uint4*>(peers->base[rank] + res_slot);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      uint4 v[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) v[j] = reinterpret_cast<const uint4*>(peers->base[j] + in_slot)[i];
+#pragma unroll
+      for (int j = 0; j < W; ++j) acc8(acc, v[j]);
+      res[i] = make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
+    }
+  }
+  publish<W>(peers, rank, b, e, true);
+  wait_all<W>(my_sig->flag2, b, e, &my_sig->error);
+  // 3. gather chunk b of every reduced slice
+#pragma unroll
+  for (int s = 0; s < W; ++s) {
+    int64_t lo, hi;
+    range(s, lo, hi);
+    const uint4* res = reinterpret_cast<const uint4*>(peers->base[s] + res_slot);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) out[i] = res[i];
+  }
+  if (threadIdx.x == 0) my_sig->epoch[b] = e;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------- host API
@@ -136,7 +235,7 @@ PK_EXPORT void* pk_car_create(int rank, int world, long long data_bytes) {
   c->rank = rank;
   c->world = world;
   c->data_bytes = static_cast<size_t>(data_bytes);
-  const size_t total = kSigBytes + 2 * c->data_bytes;
+  const size_t total = kSigBytes + 4 * c->data_bytes;  // input slots x2 parities, result slots x2
   void* p = nullptr;
   if (hipExtMallocWithFlags(&p, total, hipDeviceMallocUncached) != hipSuccess) {
     delete c;
@@ -179,8 +278,19 @@ PK_EXPORT int pk_car_open(void* ctx, const void* handles) {
 }
 
 // bf16 sum over the group: out = sum_j inp_j ; bytes % 16 == 0 and bytes <= data_bytes.
+// algo: 1 = one-shot, 2 = two-shot, 0 = by size (one-shot up to kOneShotMax bytes).
+constexpr long long kOneShotMax = 512 << 10;
+
+PK_EXPORT int pk_car_allreduce_bf16_algo(void* ctx, const void* inp, void* out, long long bytes, int blocks, int algo,
+                                         hipStream_t stream);
+
 PK_EXPORT int pk_car_allreduce_bf16(void* ctx, const void* inp, void* out, long long bytes, int blocks,
                                     hipStream_t stream) {
+  return pk_car_allreduce_bf16_algo(ctx, inp, out, bytes, blocks, 0, stream);
+}
+
+PK_EXPORT int pk_car_allreduce_bf16_algo(void* ctx, const void* inp, void* out, long long bytes, int blocks, int algo,
+                                         hipStream_t stream) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (c == nullptr || c->d_peers == nullptr) return -1;
   if (bytes <= 0) return 0;
@@ -190,10 +300,14 @@ PK_EXPORT int pk_car_allreduce_bf16(void* ctx, const void* inp, void* out, long 
   blocks = std::min(blocks, kMaxBlocks);
   const uint4* in4 = static_cast<const uint4*>(inp);
   uint4* out4 = static_cast<uint4*>(out);
+  if (algo == 0) algo = bytes <= kOneShotMax ? 1 : 2;
   switch (c->world) {
-#define PK_CAR_CASE(WW)                                                                                          \
-  case WW:                                                                                                     \
-    allreduce_1shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, n16); \
+#define PK_CAR_CASE(WW)                                                                                            \
+  case WW:                                                                                                       \
+    if (algo == 1)                                                                                               \
+      allreduce_1shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, n16); \
+    else                                                                                                         \
+      allreduce_2shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, n16); \
     break;
     PK_CAR_CASE(2)
     PK_CAR_CASE(3)

@@ -1,4 +1,4 @@
-"""One-shot all-reduce over xGMI peer memory (csrc/comm/custom_allreduce.hip).
+"""One-shot / two-shot all-reduce over xGMI peer memory (csrc/comm/custom_allreduce.hip).
 
 For the small activations of TP decode (a 70B TP=8 step issues 160 all-reduces of ~1 MiB,
 SURVEY.md §6) a single kernel in which every rank reads every peer's buffer over xGMI beats
@@ -32,6 +32,7 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_get_handle.argtypes = [_P, _P]
         lib.pk_car_open.argtypes = [_P, _P]
         lib.pk_car_allreduce_bf16.argtypes = [_P, _P, _P, _LL, _I, _P]
+        lib.pk_car_allreduce_bf16_algo.argtypes = [_P, _P, _P, _LL, _I, _I, _P]
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_destroy.argtypes = [_P]
         lib.pk_car_destroy.restype = None
@@ -67,10 +68,12 @@ class CustomAllReduce:
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n % 16 == 0
                 and 0 < n <= self.max_bytes)
 
-    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, algo: int = 0) -> torch.Tensor:
+        """algo: 0 = by size (one-shot <= 512 KiB, two-shot above), 1 = one-shot, 2 = two-shot."""
         out = torch.empty_like(x) if out is None else out
-        rc = self.lib.pk_car_allreduce_bf16(self.ctx, x.data_ptr(), out.data_ptr(), x.numel() * x.element_size(),
-                                            self.blocks, torch.cuda.current_stream(self.device).cuda_stream)
+        rc = self.lib.pk_car_allreduce_bf16_algo(self.ctx, x.data_ptr(), out.data_ptr(),
+                                                 x.numel() * x.element_size(), self.blocks, algo,
+                                                 torch.cuda.current_stream(self.device).cuda_stream)
         if rc != 0:
             raise RuntimeError(f"custom all-reduce launch failed ({rc})")
         return out

@@ -37,8 +37,12 @@ def _worker(rank, world, port, q):
             xs = [torch.empty_like(x) for _ in range(world)]
             dist.all_gather(xs, x)
             exp = torch.stack([t.float() for t in xs]).sum(0)
-            y = car.all_reduce(x.to(dev)).cpu().float()
-            torch.testing.assert_close(y, exp.to(torch.bfloat16).float(), atol=1e-2, rtol=1e-2)
+            for algo in (0, 1, 2):  # by size, one-shot, two-shot (reduce-scatter + all-gather)
+                y = car.all_reduce(x.to(dev), algo=algo).cpu().float()
+                torch.testing.assert_close(y, exp.to(torch.bfloat16).float(), atol=1e-2, rtol=1e-2)
+            xi = x.to(dev)
+            car.all_reduce(xi, out=xi, algo=2)  # in place
+            torch.testing.assert_close(xi.cpu().float(), exp.to(torch.bfloat16).float(), atol=1e-2, rtol=1e-2)
         # graph replay: the epoch lives in device memory, so replays stay in step
         xin = torch.zeros(4096, dtype=torch.bfloat16, device=dev)
         s = torch.cuda.Stream()
