@@ -70,4 +70,20 @@ kill-local-server: ## kill whatever listens on $(PORT)
 test-race: ## native cores under ASan/UBSan + concurrency stress (the reference's go test -race)
 	$(PY) -m pytest tests/unit/test_native_sanitizers.py tests/integration -q -k "sanitizer or concurrent or cancel"
 
+security-scan: ## Trivy filesystem + image scan (CRITICAL/HIGH fail), if trivy is installed
+	@if command -v trivy >/dev/null 2>&1; then \
+	  trivy fs --severity CRITICAL,HIGH --exit-code 1 . && \
+	  trivy image --severity CRITICAL,HIGH --exit-code 1 polykey-amd:latest; \
+	else echo "trivy not installed (no network in this image); CI runs the scan"; fi
+
+sbom: ## SPDX SBOM of the server image (trivy), if available
+	@if command -v trivy >/dev/null 2>&1; then trivy image --format spdx-json -o sbom.spdx.json polykey-amd:latest; \
+	else echo "trivy not installed"; fi
+
+docker-build: ## build the server image (ROCm base)
+	docker build --target server -t polykey-amd:latest .
+
+install-deps: ## verify the offline Python dependencies this repo needs are importable
+	$(PY) -c "import grpc, google.protobuf, fastapi, uvicorn, prometheus_client, safetensors, tokenizers, pybind11; print('ok')"
+
 ci-check: build test ## what CI runs on a CPU runner

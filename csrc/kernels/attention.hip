@@ -73,6 +73,7 @@ __device__ __forceinline__ void attend(WaveState& st, const bf16x8_t (&qf)[4], c
       int tok = s + 8 * (r >> 2) + 4 * t + (r & 3);
       tok = min(tok, n_valid - 1);
       const int blk = bt[tok / bs];
+      PK_DEVICE_ASSERT(blk >= 0);
       const bf16_t* p = kc + blk * blk_stride + (tok % bs) * kHD + 32 * g;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) kf[t][kk] = ld8(p + 8 * kk);

@@ -85,3 +85,13 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }  // namespace pk
 
 #define PK_CHECK_LAUNCH() (static_cast<int>(hipGetLastError()))
+
+// Device-side bounds checks, compiled in only for debug builds (POLYKEY_DEBUG_KERNELS=1 →
+// -DPK_DEBUG): a failing check prints the condition and traps the kernel, so an out-of-range
+// block table / slot / token id is reported at its source instead of corrupting the KV cache.
+#ifdef PK_DEBUG
+#include <cassert>
+#define PK_DEVICE_ASSERT(c) assert(c)
+#else
+#define PK_DEVICE_ASSERT(c) ((void)0)
+#endif

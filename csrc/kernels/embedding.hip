@@ -14,6 +14,7 @@ __global__ void __launch_bounds__(256) embedding_kernel(bf16_t* __restrict__ out
                                                         int vocab_local) {
   const int t = blockIdx.x;
   const int local = ids[t] - vocab_start;
+  PK_DEVICE_ASSERT(ids[t] >= 0);
   const bool mine = local >= 0 && local < vocab_local;
   const u32x4* src = reinterpret_cast<const u32x4*>(table + static_cast<int64_t>(mine ? local : 0) * H);
   u32x4* dst = reinterpret_cast<u32x4*>(out + static_cast<int64_t>(t) * H);

@@ -65,6 +65,8 @@ def targets() -> List[Target]:
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
              "-Wno-unused-variable", "-Wno-unused-result", "-ffp-contract=fast", "-munsafe-fp-atomics"]
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-fvisibility=hidden"]
+if os.environ.get("POLYKEY_DEBUG_KERNELS", "0") == "1":  # device bounds asserts (PK_DEVICE_ASSERT)
+    HIP_FLAGS = HIP_FLAGS + ["-DPK_DEBUG", "-g"]
 
 
 def _hash(t: Target, flags: List[str]) -> str:
