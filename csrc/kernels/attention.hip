@@ -57,77 +57,103 @@ struct WaveState {
   f32x4 o[8];     // O^T: o[dt][i] = O[col = lane&15][d = 16*dt + 4*g + i]
 };
 
-// Process keys [k_begin, k_end) in 32-key steps (k_begin multiple of 32), stride `k_stride`
-// between this wave's steps.  Keys >= n_valid or > col_limit are masked.
-__device__ __forceinline__ void attend(WaveState& st, const bf16x8_t (&qf)[4], const bf16_t* __restrict__ kc,
-                                       const bf16_t* __restrict__ vc, int64_t blk_stride, const int* __restrict__ bt,
-                                       int bs, int k_begin, int k_end, int k_stride, int n_valid, int col_limit,
-                                       float scale2) {
+// K/V fragments of one 32-key step (16 B per lane each): K as the A operand of S^T = K Q^T
+// (2 key tiles x 4 head-dim k-steps), V^T as the A operand of O^T += V^T P^T (8 d-tiles).
+struct KVFrag {
+  bf16x8_t k[2][4];
+  bf16x8_t v[8];
+};
+
+// bt[i - bt_base] = physical block of logical block i; `lim` bounds the tokens a load may touch
+// (past it the address is clamped, the data never used), so the block lookups stay inside the
+// caller's block-table window.
+__device__ __forceinline__ void load_kv(KVFrag& f, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                                        int64_t blk_stride, const int* __restrict__ bt, int bt_base, int bs, int s,
+                                        int lim) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
-  for (int s = k_begin; s < k_end; s += k_stride) {
-    // ---- issue K loads (2 tiles x 4 k-steps x 16 B) and V loads (8 d-tiles x 16 B)
-    bf16x8_t kf[2][4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      int tok = s + 8 * (r >> 2) + 4 * t + (r & 3);
-      tok = min(tok, n_valid - 1);
-      const int blk = bt[tok / bs];
-      PK_DEVICE_ASSERT(blk >= 0);
-      const bf16_t* p = kc + blk * blk_stride + (tok % bs) * kHD + 32 * g;
+  for (int t = 0; t < 2; ++t) {
+    int tok = s + 8 * (r >> 2) + 4 * t + (r & 3);
+    tok = min(tok, lim - 1);
+    const int blk = bt[tok / bs - bt_base];
+    PK_DEVICE_ASSERT(blk >= 0);
+    const bf16_t* p = kc + blk * blk_stride + (tok % bs) * kHD + 32 * g;
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) kf[t][kk] = ld8(p + 8 * kk);
+    for (int kk = 0; kk < 4; ++kk) f.k[t][kk] = ld8(p + 8 * kk);
+  }
+  int tok0 = s + 8 * g;
+  tok0 = min(tok0, ((lim - 1) >> 3) << 3);
+  const int blk = bt[tok0 / bs - bt_base];
+  const bf16_t* p = vc + blk * blk_stride + r * bs + (tok0 % bs);
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld8(p + dt * 16 * bs);
+}
+
+__device__ __forceinline__ void attend_step(WaveState& st, const bf16x8_t (&qf)[4], const KVFrag& f, int s,
+                                            int n_valid, int col_limit, float scale2) {
+  const int g = (threadIdx.x & 63) >> 4;
+  // ---- S^T = K . Q^T
+  f32x4 acc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k[t][kk], qf[kk], acc[t], 0, 0, 0);
+  }
+  // ---- online softmax over this step's 32 keys (8 per lane)
+  float sv[8];
+  float mx = kNegBig;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = s + 8 * g + 4 * t + i;
+      const bool ok = key < n_valid && key <= col_limit;
+      const float v = ok ? acc[t][i] * scale2 : -INFINITY;
+      sv[4 * t + i] = v;
+      mx = fmaxf(mx, v);
     }
-    bf16x8_t vf[8];
-    {
-      int tok0 = s + 8 * g;
-      tok0 = min(tok0, ((n_valid - 1) >> 3) << 3);
-      const int blk = bt[tok0 / bs];
-      const bf16_t* p = vc + blk * blk_stride + r * bs + (tok0 % bs);
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float m_new = fmaxf(st.m, mx);
+  const float alpha = exp2f(st.m - m_new);
+  st.m = m_new;
+  float p[8];
+  float psum = 0.f;
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) vf[dt] = ld8(p + dt * 16 * bs);
-    }
-    // ---- S^T = K . Q^T
-    f32x4 acc[2];
+  for (int i = 0; i < 8; ++i) {
+    p[i] = exp2f(sv[i] - m_new);
+    psum += p[i];
+  }
+  st.l = st.l * alpha + psum;
+  const bf16x8_t pb = pack_p(p);
+  // ---- O^T += V^T . P^T
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][kk], qf[kk], acc[t], 0, 0, 0);
-    }
-    // ---- online softmax over this step's 32 keys (8 per lane)
-    float sv[8];
-    float mx = kNegBig;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = s + 8 * g + 4 * t + i;
-        const bool ok = key < n_valid && key <= col_limit;
-        const float v = ok ? acc[t][i] * scale2 : -INFINITY;
-        sv[4 * t + i] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(st.m, mx);
-    const float alpha = exp2f(st.m - m_new);
-    st.m = m_new;
-    float p[8];
-    float psum = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      p[i] = exp2f(sv[i] - m_new);
-      psum += p[i];
-    }
-    st.l = st.l * alpha + psum;
-    const bf16x8_t pb = pack_p(p);
-    // ---- O^T += V^T . P^T
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      st.o[dt] *= alpha;
-      st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pb, st.o[dt], 0, 0, 0);
-    }
+  for (int dt = 0; dt < 8; ++dt) {
+    st.o[dt] *= alpha;
+    st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.v[dt], pb, st.o[dt], 0, 0, 0);
+  }
+}
+
+// Process keys [k_begin, k_end) in 32-key steps (k_begin multiple of 32), stride `k_stride`
+// between this wave's steps.  Keys >= n_valid or > col_limit are masked.  Software-pipelined
+// over two fragment sets: the next step's K/V loads are in flight while this step computes
+// (loads past the end are clamped to valid addresses and never consumed).
+__device__ __forceinline__ void attend(WaveState& st, const bf16x8_t (&qf)[4], const bf16_t* __restrict__ kc,
+                                       const bf16_t* __restrict__ vc, int64_t blk_stride, const int* __restrict__ bt,
+                                       int bt_base, int bs, int k_begin, int k_end, int k_stride, int n_valid,
+                                       int col_limit, float scale2) {
+  if (k_begin >= k_end) return;
+  const int lim = min(n_valid, k_end);
+  KVFrag fa, fb;
+  load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, k_begin, lim);
+  for (int s = k_begin; s < k_end; s += 2 * k_stride) {
+    load_kv(fb, kc, vc, blk_stride, bt, bt_base, bs, s + k_stride, lim);
+    attend_step(st, qf, fa, s, n_valid, col_limit, scale2);
+    if (s + k_stride >= k_end) break;
+    load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, s + 2 * k_stride, lim);
+    attend_step(st, qf, fb, s + k_stride, n_valid, col_limit, scale2);
   }
 }
 
@@ -162,6 +188,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   __shared__ float o_lds[4][16][kHD + 4];
   __shared__ float ml_lds[4][16][2];
   __shared__ int last;
+  __shared__ int bt_s[kPart / 8 + 2];  // this partition's block-table window (LDS: lookups use lgkmcnt)
   const int h = blockIdx.x, seq = blockIdx.y;
   const int ctx = context_lens[seq];
   const int G = n_q / n_kv;
@@ -182,13 +209,15 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   for (int part = blockIdx.z; part < n_used; part += gridDim.z) {
     const int begin = part * kPart;
     const int end = min(ctx, begin + kPart);
+    const int b0 = begin / bs, nblk = (end - 1) / bs - b0 + 1;
+    __syncthreads();  // the previous partition's LDS readers are done
+    for (int i = threadIdx.x; i < nblk; i += 256) bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
+    __syncthreads();
     WaveState st;
     init_state(st);
-    attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs, blk_stride,
-           block_tables + static_cast<int64_t>(seq) * max_blocks, bs, begin + kStep * w, end, 4 * kStep, ctx,
-           ctx - 1, scale2);
+    attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs, blk_stride, bt_s,
+           b0, bs, begin + kStep * w, end, 4 * kStep, ctx, ctx - 1, scale2);
     const float lsum = col_sum(st.l);
-    __syncthreads();  // the previous partition's LDS readers are done
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
@@ -317,8 +346,8 @@ __global__ void __launch_bounds__(512) paged_prefill_kernel(
   WaveState st;
   init_state(st);
   attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs,
-         static_cast<int64_t>(n_kv) * bs * kHD, block_tables + static_cast<int64_t>(seq) * max_blocks, bs, 0, k_end,
-         kStep, ctx, valid ? qpos : -1, scale2);
+         static_cast<int64_t>(n_kv) * bs * kHD, block_tables + static_cast<int64_t>(seq) * max_blocks, 0, bs, 0,
+         k_end, kStep, ctx, valid ? qpos : -1, scale2);
   const float lsum = col_sum(st.l);
   if (!valid) return;
   const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
