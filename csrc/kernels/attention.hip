@@ -33,7 +33,7 @@ constexpr int kHD = 128;
 constexpr int kStep = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1e30f;
-constexpr int kDecodeZ = 4;  // partition workgroups per (seq, kv head)
+int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
 
@@ -380,7 +380,7 @@ PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, con
   if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
   // z is capped: a short context leaves the extra z-workgroups idle, and graph capture fixes
   // the grid for max_model_len, so a z of n_parts would launch mostly-empty workgroups
-  dim3 grid(n_kv, n_seqs, n_parts < kDecodeZ ? n_parts : kDecodeZ);
+  dim3 grid(n_kv, n_seqs, n_parts < g_decode_z ? n_parts : g_decode_z);
   paged_decode_kernel<kDecodePart><<<grid, 256, 0, stream>>>(
       static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
       static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables), static_cast<const int*>(context_lens),
@@ -393,6 +393,12 @@ PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, con
       static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
       static_cast<const int*>(context_lens), n_q, out_stride, n_parts);
   return PK_CHECK_LAUNCH();
+}
+
+PK_EXPORT int pk_set_decode_z(int z) {
+  if (z < 1) return -1;
+  g_decode_z = z;
+  return 0;
 }
 
 PK_EXPORT int pk_paged_prefill(void* out, const void* q, const void* k_cache, const void* v_cache,

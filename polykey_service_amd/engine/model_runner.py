@@ -43,6 +43,11 @@ class RunnerConfig:
     graph_batch_sizes: Tuple[int, ...] = ()
 
 
+# Long-context decode merges its partitions in a second kernel by default: the in-kernel
+# last-arriver merge needs an agent-scope release per partition (an L2 write-back on each XCD)
+# and measured 1.7-1.9x slower at 1-4K contexts (tools/bench_attn.py); contexts that fit one
+# partition need no merge either way.
+DECODE_INKERNEL_MERGE = os.environ.get("POLYKEY_DECODE_INKERNEL_MERGE", "0") == "1"
 # stage step inputs with a kernel reading pinned memory instead of an SDMA copy
 HOST_COPY_KERNEL = os.environ.get("POLYKEY_HOST_COPY_KERNEL", "1") == "1"
 
@@ -184,7 +189,8 @@ class ModelRunner:
             slot_mapping=d["slots"][:T],
             decode_block_tables=d["block_tables"][:nd] if nd else None,
             decode_context_lens=d["context_lens"][:nd] if nd else None,
-            decode_part_o=self.part_o, decode_part_ml=self.part_ml, decode_counters=self.part_ctr)
+            decode_part_o=self.part_o, decode_part_ml=self.part_ml,
+            decode_counters=self.part_ctr if DECODE_INKERNEL_MERGE else None)
         if npf:
             md.prefill_block_tables = d["block_tables"][nd:n]
             md.prefill_context_lens = d["context_lens"][nd:n]
