@@ -33,6 +33,7 @@ constexpr int kHD = 128;
 constexpr int kStep = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1e30f;
+constexpr int kDecodeWaves = 4;  // waves per (seq, kv head, partition); 8 measured ~10 % slower at 384 keys
 int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
@@ -178,15 +179,15 @@ __device__ __forceinline__ float col_sum(float l) {
 }
 
 // ------------------------------------------------------------------------------ decode
-// grid (n_kv, n_seqs, n_parts), block 256 (4 waves).  LDS: 4 waves x 16 cols x 128 d fp32.
-template <int kPart>
-__global__ void __launch_bounds__(256) paged_decode_kernel(
+// grid (n_kv, n_seqs, min(n_parts, z)), block 64*NW (NW waves).  LDS: NW waves x 16 cols x 128 d fp32.
+template <int kPart, int NW>
+__global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
     float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int n_q, int n_kv, int bs,
     int max_blocks, int q_stride, int out_stride, int n_parts, float scale2) {
-  __shared__ float o_lds[4][16][kHD + 4];
-  __shared__ float ml_lds[4][16][2];
+  __shared__ float o_lds[NW][16][kHD + 4];
+  __shared__ float ml_lds[NW][16][2];
   __shared__ int last;
   __shared__ int bt_s[kPart / 8 + 2];  // this partition's block-table window (LDS: lookups use lgkmcnt)
   const int h = blockIdx.x, seq = blockIdx.y;
@@ -194,7 +195,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   const int G = n_q / n_kv;
   if (ctx <= 0) {
     if (blockIdx.z == 0)  // a padded (graph) row -> zeros
-      for (int idx = threadIdx.x; idx < G * kHD; idx += 256)
+      for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW)
         out[static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD] = 0;
     return;
   }
@@ -211,12 +212,12 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     const int end = min(ctx, begin + kPart);
     const int b0 = begin / bs, nblk = (end - 1) / bs - b0 + 1;
     __syncthreads();  // the previous partition's LDS readers are done
-    for (int i = threadIdx.x; i < nblk; i += 256) bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
+    for (int i = threadIdx.x; i < nblk; i += 64 * NW) bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
     __syncthreads();
     WaveState st;
     init_state(st);
     attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs, blk_stride, bt_s,
-           b0, bs, begin + kStep * w, end, 4 * kStep, ctx, ctx - 1, scale2);
+           b0, bs, begin + kStep * w, end, NW * kStep, ctx, ctx - 1, scale2);
     const float lsum = col_sum(st.l);
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
@@ -227,14 +228,14 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       ml_lds[w][r][1] = lsum;
     }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < G * kHD; idx += 256) {
+    for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
       const int c = idx / kHD, d = idx % kHD;
       float M = kNegBig;
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
+      for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
       float O = 0.f, L = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) {
+      for (int ww = 0; ww < NW; ++ww) {
         const float f = exp2f(ml_lds[ww][c][0] - M);
         O += f * o_lds[ww][c][d];
         L += f * ml_lds[ww][c][1];
@@ -271,7 +272,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     }
     __syncthreads();
     if (!last) continue;
-    for (int idx = threadIdx.x; idx < G * kHD; idx += 256) {
+    for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
       const int c = idx / kHD, d = idx % kHD;
       const int hq = h * G + c;
       const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
@@ -381,7 +382,7 @@ PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, con
   // z is capped: a short context leaves the extra z-workgroups idle, and graph capture fixes
   // the grid for max_model_len, so a z of n_parts would launch mostly-empty workgroups
   dim3 grid(n_kv, n_seqs, n_parts < g_decode_z ? n_parts : g_decode_z);
-  paged_decode_kernel<kDecodePart><<<grid, 256, 0, stream>>>(
+  paged_decode_kernel<kDecodePart, kDecodeWaves><<<grid, 64 * kDecodeWaves, 0, stream>>>(
       static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
       static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables), static_cast<const int*>(context_lens),
       static_cast<float*>(part_o), static_cast<float*>(part_ml), static_cast<int*>(counters), n_q, n_kv, bs,
