@@ -144,11 +144,11 @@ __device__ __forceinline__ void attend_step(WaveState& st, const bf16x8_t (&qf)[
 __device__ __forceinline__ void attend(WaveState& st, const bf16x8_t (&qf)[4], const bf16_t* __restrict__ kc,
                                        const bf16_t* __restrict__ vc, int64_t blk_stride, const int* __restrict__ bt,
                                        int bt_base, int bs, int k_begin, int k_end, int k_stride, int n_valid,
-                                       int col_limit, float scale2) {
+                                       int col_limit, float scale2, KVFrag& fa, bool fa_loaded = false) {
   if (k_begin >= k_end) return;
   const int lim = min(n_valid, k_end);
-  KVFrag fa, fb;
-  load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, k_begin, lim);
+  KVFrag fb;
+  if (!fa_loaded) load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, k_begin, lim);
   for (int s = k_begin; s < k_end; s += 2 * k_stride) {
     load_kv(fb, kc, vc, blk_stride, bt, bt_base, bs, s + k_stride, lim);
     attend_step(st, qf, fa, s, n_valid, col_limit, scale2);
@@ -180,12 +180,25 @@ __device__ __forceinline__ float col_sum(float l) {
 
 // ------------------------------------------------------------------------------ decode
 // grid (n_kv, n_seqs, min(n_parts, z)), block 64*NW (NW waves).  LDS: NW waves x 16 cols x 128 d fp32.
-template <int kPart, int NW>
+// Decode attention fed straight from the QKV projection's split-K slabs (FROM_QKV): the
+// workgroup of (seq, kv head h) sums the S fp32 slabs of its G query heads and of k/v head h,
+// rounds to bf16 (the unfused GEMM output), applies RoPE, keeps q in LDS, and — the workgroup
+// that owns the partition holding the new token — writes k / v into the paged cache before
+// attending.  Replaces the separate QKV-reduce + RoPE + cache-write kernel of a decode layer.
+struct QkvIn {
+  const float* partial;    // [S, M, (n_q + 2 n_kv) * 128]
+  const int* positions;    // [M]
+  const float* cos_sin;    // [max_pos, 128] = cos[64] | sin[64]
+  const int* slots;        // [M], < 0: nothing cached
+  int S, M;
+};
+
+template <int kPart, int NW, bool FROM_QKV, int SS = 0>
 __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
-    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
-    const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, bf16_t* __restrict__ kc,
+    bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
     float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int n_q, int n_kv, int bs,
-    int max_blocks, int q_stride, int out_stride, int n_parts, float scale2) {
+    int max_blocks, int q_stride, int out_stride, int n_parts, float scale2, const QkvIn qi) {
   __shared__ float o_lds[NW][16][kHD + 4];
   __shared__ float ml_lds[NW][16][2];
   __shared__ int last;
@@ -200,11 +213,82 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     return;
   }
   const int n_used = (ctx + kPart - 1) / kPart;
+  if (static_cast<int>(blockIdx.z) >= n_used) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
+  const bf16_t* kch = kc + static_cast<int64_t>(h) * bs * kHD;
+  const bf16_t* vch = vc + static_cast<int64_t>(h) * kHD * bs;
+  // (prefetching the first K/V step across the q preparation below was measured: it pushes
+  // the kernel to 256 VGPRs + AGPRs, one wave per SIMD, and is slower overall)
   bf16x8_t qf[4];
-  load_q(qf, q + static_cast<int64_t>(seq) * q_stride + (h * G + r) * kHD, r < G);
+  if constexpr (FROM_QKV) {
+    __shared__ __attribute__((aligned(16))) bf16_t q_s[16][kHD];
+    const int N = (n_q + 2 * n_kv) * kHD;
+    const int64_t slab = static_cast<int64_t>(qi.M) * N;
+    const float* base = qi.partial + static_cast<int64_t>(seq) * N;
+    const float* cs = qi.cos_sin + static_cast<int64_t>(qi.positions[seq]) * kHD;
+    const int slot = qi.slots[seq];
+    const bool writer = slot >= 0 && static_cast<int>(blockIdx.z) == (n_used - 1) % static_cast<int>(gridDim.z);
+    const int n_items = G * 64 + (writer ? 128 : 0);
+    for (int it = threadIdx.x; it < n_items; it += 64 * NW) {
+      int col, j;
+      if (it < G * 64) {
+        j = it & 63;
+        col = (h * G + (it >> 6)) * kHD + j;
+      } else if (it < G * 64 + 64) {
+        j = it - G * 64;
+        col = (n_q + h) * kHD + j;
+      } else {
+        j = it - G * 64 - 64;
+        col = (n_q + n_kv + h) * kHD + j;
+      }
+      float a = 0.f, b = 0.f;
+      if constexpr (SS > 0) {  // all slab loads in flight before the first add
+        float va[SS], vb[SS];
+#pragma unroll
+        for (int sp = 0; sp < SS; ++sp) {
+          va[sp] = base[sp * slab + col];
+          vb[sp] = base[sp * slab + col + 64];
+        }
+#pragma unroll
+        for (int sp = 0; sp < SS; ++sp) {
+          a += va[sp];
+          b += vb[sp];
+        }
+      } else {
+        for (int sp = 0; sp < qi.S; ++sp) {
+          a += base[sp * slab + col];
+          b += base[sp * slab + col + 64];
+        }
+      }
+      if (it < G * 64 + 64) {  // q or k: round (the GEMM output), rotate (neox)
+        a = bf2f(f2bf(a));
+        b = bf2f(f2bf(b));
+        const float co = cs[j], si = cs[64 + j];
+        const bf16_t ra = f2bf(a * co - b * si), rb = f2bf(b * co + a * si);
+        if (it < G * 64) {
+          q_s[it >> 6][j] = ra;
+          q_s[it >> 6][j + 64] = rb;
+        } else {
+          bf16_t* d = kc + ((static_cast<int64_t>(slot / bs) * n_kv + h) * bs + slot % bs) * kHD;
+          d[j] = ra;
+          d[j + 64] = rb;
+        }
+      } else {
+        bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs + slot % bs;
+        d[static_cast<int64_t>(j) * bs] = f2bf(a);
+        d[static_cast<int64_t>(j + 64) * bs] = f2bf(b);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new k/v rows are in L2 before any wave reads them
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      qf[kk] = r < G ? *reinterpret_cast<const bf16x8_t*>(&q_s[r][32 * g + 8 * kk]) : zero8();
+  } else {
+    load_q(qf, q + static_cast<int64_t>(seq) * q_stride + (h * G + r) * kHD, r < G);
+  }
 
   // the grid's z dimension is small (<= 4); a workgroup walks partitions z, z + gridDim.z, ...
   for (int part = blockIdx.z; part < n_used; part += gridDim.z) {
@@ -216,8 +300,8 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     __syncthreads();
     WaveState st;
     init_state(st);
-    attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs, blk_stride, bt_s,
-           b0, bs, begin + kStep * w, end, NW * kStep, ctx, ctx - 1, scale2);
+    KVFrag fa;
+    attend(st, qf, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w, end, NW * kStep, ctx, ctx - 1, scale2, fa);
     const float lsum = col_sum(st.l);
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
@@ -346,9 +430,10 @@ __global__ void __launch_bounds__(512) paged_prefill_kernel(
   load_q(qf, q + static_cast<int64_t>(q0 + (valid ? qi : 0)) * q_stride + hq * kHD, valid);
   WaveState st;
   init_state(st);
+  KVFrag fa;
   attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs,
          static_cast<int64_t>(n_kv) * bs * kHD, block_tables + static_cast<int64_t>(seq) * max_blocks, 0, bs, 0,
-         k_end, kStep, ctx, valid ? qpos : -1, scale2);
+         k_end, kStep, ctx, valid ? qpos : -1, scale2, fa);
   const float lsum = col_sum(st.l);
   if (!valid) return;
   const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
@@ -371,10 +456,10 @@ PK_EXPORT int pk_decode_num_parts(int max_context) { return (max_context + kDeco
 
 // counters: [n_seqs, n_kv] int32, zero-initialised once (the merging workgroup re-arms its
 // counter); with counters == null the partitions are merged by a second kernel instead.
-PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
-                              const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
-                              void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
-                              int out_stride, float scale, hipStream_t stream) {
+static int decode_launch(void* out, const void* q, const QkvIn& qi, const void* k_cache, const void* v_cache,
+                         const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
+                         void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
+                         int out_stride, float scale, hipStream_t stream) {
   if (n_seqs <= 0) return 0;
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
   const int n_parts = (max_blocks * bs + kDecodePart - 1) / kDecodePart;
@@ -382,11 +467,21 @@ PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, con
   // z is capped: a short context leaves the extra z-workgroups idle, and graph capture fixes
   // the grid for max_model_len, so a z of n_parts would launch mostly-empty workgroups
   dim3 grid(n_kv, n_seqs, n_parts < g_decode_z ? n_parts : g_decode_z);
-  paged_decode_kernel<kDecodePart, kDecodeWaves><<<grid, 64 * kDecodeWaves, 0, stream>>>(
-      static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),
-      static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables), static_cast<const int*>(context_lens),
-      static_cast<float*>(part_o), static_cast<float*>(part_ml), static_cast<int*>(counters), n_q, n_kv, bs,
-      max_blocks, q_stride, out_stride, n_parts, scale * kLog2e);
+#define PK_DECODE_ARGS                                                                                            \
+  static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<bf16_t*>(const_cast<void*>(k_cache)),   \
+      static_cast<bf16_t*>(const_cast<void*>(v_cache)), static_cast<const int*>(block_tables),                  \
+      static_cast<const int*>(context_lens), static_cast<float*>(part_o), static_cast<float*>(part_ml),          \
+      static_cast<int*>(counters), n_q, n_kv, bs, max_blocks, q_stride, out_stride, n_parts, scale * kLog2e, qi
+  if (qi.partial != nullptr) {
+    switch (qi.S) {
+      case 2: paged_decode_kernel<kDecodePart, kDecodeWaves, true, 2><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+      case 4: paged_decode_kernel<kDecodePart, kDecodeWaves, true, 4><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+      case 8: paged_decode_kernel<kDecodePart, kDecodeWaves, true, 8><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+      default: paged_decode_kernel<kDecodePart, kDecodeWaves, true, 0><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+    }
+  } else
+    paged_decode_kernel<kDecodePart, kDecodeWaves, false><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS);
+#undef PK_DECODE_ARGS
   int rc = PK_CHECK_LAUNCH();
   if (rc || counters != nullptr || n_parts == 1) return rc;
   dim3 g2(n_q, n_seqs);
@@ -394,6 +489,29 @@ PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, con
       static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
       static_cast<const int*>(context_lens), n_q, out_stride, n_parts);
   return PK_CHECK_LAUNCH();
+}
+
+PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
+                              const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
+                              void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
+                              int out_stride, float scale, hipStream_t stream) {
+  const QkvIn none{};
+  return decode_launch(out, q, none, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, counters, n_seqs,
+                       n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale, stream);
+}
+
+// Decode attention straight from the fused QKV projection's split-K slabs [S, M, (n_q+2n_kv)*128]
+// (RoPE + KV-cache write folded in); rows 0..n_seqs-1 of the slabs are the decode tokens.
+PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, const void* positions,
+                                  const void* cos_sin, const void* slots, void* k_cache, void* v_cache,
+                                  const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
+                                  int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int out_stride, float scale,
+                                  hipStream_t stream) {
+  if (partial == nullptr || S < 1 || M < n_seqs) return -1;
+  QkvIn qi{static_cast<const float*>(partial), static_cast<const int*>(positions), static_cast<const float*>(cos_sin),
+           static_cast<const int*>(slots), S, M};
+  return decode_launch(out, nullptr, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, nullptr,
+                       n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, stream);
 }
 
 PK_EXPORT int pk_set_decode_z(int z) {

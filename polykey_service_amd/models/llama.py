@@ -35,6 +35,11 @@ from .config import ModelConfig
 from .weights import SafetensorsIndex, random_full, shard_cols, shard_rows
 
 
+# decode attention consumes the QKV split-K slabs directly (POLYKEY_FUSED_QKV_ATTN=0: separate
+# reduce + RoPE + cache-write kernel, then attention)
+FUSED_QKV_ATTENTION = os.environ.get("POLYKEY_FUSED_QKV_ATTN", "1") == "1"
+
+
 def _p(t: torch.Tensor) -> nn.Parameter:
     return nn.Parameter(t, requires_grad=False)
 
@@ -91,10 +96,16 @@ class LlamaAttention(nn.Module):
         k_cache, v_cache = kv
         S = gemm.choose_split(self.qkv.shape[0], x.shape[1], T)
         if ws is not None and gemm.skinny_ok(x, self.qkv) and S > 1 and ws.numel() >= S * T * self.qkv.shape[0]:
-            # decode: split-K QKV whose epilogue kernel also applies RoPE and writes the KV cache
-            q = gemm.qkv_reduce_rope_cache(gemm.linear_partial(x, self.qkv, ws, S, packed=self.qkv_p), positions,
-                                           cos_sin, k_cache,
-                                           v_cache, md.slot_mapping, self.nq, self.nkv)
+            p = gemm.linear_partial(x, self.qkv, ws, S, packed=self.qkv_p)
+            if md.num_prefill == 0 and FUSED_QKV_ATTENTION:
+                # pure decode: the attention kernel itself reduces the QKV slabs, applies RoPE
+                # and writes the new k / v into the paged cache
+                a = attn_ops.paged_decode_from_qkv(p, positions, cos_sin, k_cache, v_cache, md, self.scale,
+                                                   self.nq, self.nkv)
+                return _proj_out(a, self.o, ws, self.o_p)
+            # split-K QKV whose epilogue kernel also applies RoPE and writes the KV cache
+            q = gemm.qkv_reduce_rope_cache(p, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq,
+                                           self.nkv)
         else:
             qkv = gemm.linear(x, self.qkv, packed=self.qkv_p)
             attn_ops.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq, self.nkv,

@@ -113,3 +113,21 @@ def _reference(q, k_cache, v_cache, md: AttnMetadata, scale, out):
 
 def default_scale(head_dim: int = 128) -> float:
     return 1.0 / math.sqrt(head_dim)
+
+
+def paged_decode_from_qkv(p, positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor,
+                          v_cache: torch.Tensor, md: AttnMetadata, scale: float, nq: int, nkv: int) -> torch.Tensor:
+    """Pure-decode attention straight from the fused QKV projection's split-K slabs
+    (``gemm.Partial``): the attention kernel reduces the slabs, applies RoPE, writes the new
+    k / v into the paged cache and attends — one kernel instead of reduce+RoPE+cache then
+    attention.  Returns [T, nq*128] bf16."""
+    assert md.num_prefill == 0 and k_cache.shape[-1] == 128
+    T = p.M
+    out = torch.empty((T, nq * 128), dtype=torch.bfloat16, device=p.buf.device)
+    bt = md.decode_block_tables
+    native.call("pk_paged_decode_qkv", out.data_ptr(), p.buf.data_ptr(), p.S, p.M, positions.data_ptr(),
+                cos_sin.data_ptr(), md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                bt.data_ptr(), md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,
+                native.ptr(md.decode_part_ml) or 0, md.num_decode, nq, nkv, k_cache.shape[2], bt.shape[1],
+                out.stride(0), float(scale), native.stream_ptr())
+    return out

@@ -143,3 +143,41 @@ def test_rope_and_cache(nq, nkv, bs):
     torch.testing.assert_close(qkv_d.cpu().float(), qkv_r.float(), atol=1.6e-2, rtol=1e-2)
     torch.testing.assert_close(kc_d.cpu().float(), kc_r.float(), atol=1.6e-2, rtol=1e-2)
     assert torch.equal(vc_d.cpu(), vc_r)
+
+
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 16), (16, 4, 32)])
+@pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [512, 513, 1300, 0]])
+@pytest.mark.parametrize("S", [1, 4])
+def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S):
+    """Attention kernel fed by the QKV split-K slabs (reduce + RoPE + cache write folded in) vs
+    the unfused kernels: same output, same K/V cache contents; ctx 0 = padded row (slot -1)."""
+    from polykey_service_amd.ops import gemm
+    d = "cuda"
+    B = len(ctxs)
+    N = (nq + 2 * nkv) * HD
+    max_blocks = (max(ctxs) + bs - 1) // bs + 3
+    nb = sum((max(c, 1) + bs - 1) // bs for c in ctxs) + 4
+    kc, vc = make_cache(nb, nkv, bs, seed=3)
+    bt = block_tables_for([max(c, 1) for c in ctxs], bs, nb, max_blocks, seed=3)
+    cl = torch.tensor(ctxs, dtype=torch.int32)
+    pos = (cl - 1).clamp(min=0)
+    slots = torch.tensor([int(bt[i, (c - 1) // bs]) * bs + (c - 1) % bs if c > 0 else -1 for i, c in enumerate(ctxs)],
+                         dtype=torch.int32)
+    g = torch.Generator().manual_seed(5)
+    slabs = (torch.randn(S, B, N, generator=g) * (0.5 / S)).to(d)
+    cs = ref.rope_cos_sin_cache(4096, HD, 500000.0).to(d)
+    ws = torch.empty(S * B * N, dtype=torch.float32, device=d)
+    ws[: S * B * N].copy_(slabs.reshape(-1))
+    p = gemm.Partial(ws, S, B, N)
+    po, pml = A.decode_workspace(B, nq, max_blocks, bs, d)
+    mk = lambda: A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0,
+                                slot_mapping=slots.to(d), decode_block_tables=bt.to(d), decode_context_lens=cl.to(d),
+                                decode_part_o=po, decode_part_ml=pml)
+    scale = 1 / math.sqrt(HD)
+    k1, v1 = kc.to(d), vc.to(d)
+    q = gemm.qkv_reduce_rope_cache(p, pos.to(d), cs, k1, v1, slots.to(d), nq, nkv)
+    exp = A.paged_attention(q, k1, v1, mk(), scale)
+    k2, v2 = kc.to(d), vc.to(d)
+    got = A.paged_decode_from_qkv(p, pos.to(d), cs, k2, v2, mk(), scale, nq, nkv)
+    torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
