@@ -45,6 +45,8 @@ struct GemmArgs {
   long long w_stride;        //   out / slabs, W of group e at W + e * w_stride; group = blockIdx.y
   int groups;                // number of groups (grid.y)
   int max_group_rows;        // bound on any group's rows (<= 64): picks the M-tile count
+  const int* a_rows;         // grouped: A row of group row i = a_rows[i] / a_row_div (MoE permute folded
+  int a_row_div;             //   into the A staging: a_rows = expert-sorted slots, a_row_div = top-k)
 };
 
 namespace {
@@ -226,7 +228,7 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     if (M <= 0) return;  // no tokens routed to this expert: its weights are never read
     Wg += static_cast<int64_t>(blockIdx.y) * args.w_stride;
   }
-  const bf16_t* __restrict__ A = args.A + static_cast<int64_t>(row0) * args.lda;
+  const bf16_t* __restrict__ A = args.a_rows != nullptr ? args.A : args.A + static_cast<int64_t>(row0) * args.lda;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
   const int nb = blockIdx.x / S, split = blockIdx.x % S;
@@ -254,13 +256,18 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   constexpr int kPieces = (16 * MT * kKC / 8 + 255) / 256;
   u32x4 stage[kPieces];
   u32x4 stage_w[NORM ? kPieces : 1];
+  const bf16_t* arow[kPieces];  // source row of each staged piece (fixed across k-chunks)
+#pragma unroll
+  for (int p = 0; p < kPieces; ++p) {
+    const int src_row = min((tid + 256 * p) >> 5, M - 1);
+    const int r_a = args.a_rows != nullptr ? args.a_rows[row0 + src_row] / args.a_row_div : src_row;
+    arow[p] = A + static_cast<int64_t>(r_a) * args.lda;
+  }
   auto load_a = [&](int kc) {
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) {
-      const int idx = tid + 256 * p;  // piece index
-      const int row = idx >> 5, col = (idx & 31) * 8;
-      const int src_row = min(row, M - 1);
-      stage[p] = *reinterpret_cast<const u32x4*>(A + static_cast<int64_t>(src_row) * args.lda + kc + col);
+      const int col = ((tid + 256 * p) & 31) * 8;
+      stage[p] = *reinterpret_cast<const u32x4*>(arow[p] + kc + col);
       if constexpr (NORM) stage_w[p] = *reinterpret_cast<const u32x4*>(args.nrm_w + kc + col);
     }
   };
@@ -458,11 +465,21 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
 // One row per workgroup of H/4 (<= 1024) threads, PER float4 column groups per thread; the S
 // slab loads of a group are independent and issued back to back (latency, not bandwidth, is
 // what a 64-row reduction fights).
-template <int PER, int SS>
+// Optional MoE routing of the normalised row (ROUTE): logits = bf16(x . router[e]) for the E
+// experts, softmax, top-k, renormalised weights -> ids[m, k], rw[m, k].  Replaces the router
+// GEMM and the top-k softmax kernel of a Mixtral decode layer.
+struct RouteArgs {
+  const bf16_t* router;  // [E, H]
+  int* ids;              // [M, k]
+  float* w;              // [M, k]
+  int E, k, renorm;
+};
+
+template <int PER, int SS, bool ROUTE = false>
 __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __restrict__ x, bf16_t* __restrict__ residual,
                                                                   const float* __restrict__ partial,
                                                                   const bf16_t* __restrict__ w, int S, int M, int H,
-                                                                  float eps) {
+                                                                  float eps, const RouteArgs ra = RouteArgs{}) {
   __shared__ float red[16];
   const int m = blockIdx.x;
   float v[PER][4];
@@ -512,6 +529,60 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __rest
     o.x = pack2(y[0], y[1]);
     o.y = pack2(y[2], y[3]);
     *reinterpret_cast<uint2*>(xo + c) = o;
+  }
+  if constexpr (ROUTE) {
+    // x row is in registers (normalised, bf16-rounded values y of this thread's columns)
+    __shared__ float part_s[16][64];
+    __shared__ float logit_s[64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int e = 0; e < ra.E; ++e) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = 4 * (threadIdx.x + i * blockDim.x);
+        const uint2 ww = *reinterpret_cast<const uint2*>(w + c);
+        const uint2 rr = *reinterpret_cast<const uint2*>(ra.router + static_cast<int64_t>(e) * H + c);
+        const float y0 = bf2f(f2bf(bf2f(f2bf(v[i][0] * rinv)) * bf2f(static_cast<bf16_t>(ww.x & 0xffff))));
+        const float y1 = bf2f(f2bf(bf2f(f2bf(v[i][1] * rinv)) * bf2f(static_cast<bf16_t>(ww.x >> 16))));
+        const float y2 = bf2f(f2bf(bf2f(f2bf(v[i][2] * rinv)) * bf2f(static_cast<bf16_t>(ww.y & 0xffff))));
+        const float y3 = bf2f(f2bf(bf2f(f2bf(v[i][3] * rinv)) * bf2f(static_cast<bf16_t>(ww.y >> 16))));
+        acc += y0 * bf2f(static_cast<bf16_t>(rr.x & 0xffff)) + y1 * bf2f(static_cast<bf16_t>(rr.x >> 16)) +
+               y2 * bf2f(static_cast<bf16_t>(rr.y & 0xffff)) + y3 * bf2f(static_cast<bf16_t>(rr.y >> 16));
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) part_s[wid][e] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < ra.E) {
+      float t = 0.f;
+      for (int q = 0; q < nw; ++q) t += part_s[q][threadIdx.x];
+      logit_s[threadIdx.x] = bf2f(f2bf(t));  // the router GEMM's bf16 output
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float mx = -INFINITY;
+      for (int e = 0; e < ra.E; ++e) mx = fmaxf(mx, logit_s[e]);
+      float sum = 0.f;
+      for (int e = 0; e < ra.E; ++e) sum += __expf(logit_s[e] - mx);
+      unsigned long long taken = 0ull;
+      float wsum = 0.f;
+      for (int j = 0; j < ra.k; ++j) {
+        int best = 0;
+        float bv = -INFINITY;
+        for (int e = 0; e < ra.E; ++e)
+          if (!((taken >> e) & 1ull) && logit_s[e] > bv) {
+            bv = logit_s[e];
+            best = e;
+          }
+        taken |= 1ull << best;
+        const float pr = __expf(bv - mx) / sum;
+        ra.ids[m * ra.k + j] = best;
+        ra.w[m * ra.k + j] = pr;
+        wsum += pr;
+      }
+      if (ra.renorm)
+        for (int j = 0; j < ra.k; ++j) ra.w[m * ra.k + j] /= wsum;
+    }
   }
 }
 
@@ -669,8 +740,25 @@ PK_EXPORT int pk_splitk_reduce(void* out, const void* partial, int S, int M, int
   return PK_CHECK_LAUNCH();
 }
 
+static int add_rmsnorm_launch(void* x, void* residual, const void* partial, const void* w, int S, int M, int H,
+                              float eps, const RouteArgs* ra, hipStream_t stream);
+
 PK_EXPORT int pk_splitk_add_rmsnorm(void* x, void* residual, const void* partial, const void* w, int S, int M, int H,
                                     float eps, hipStream_t stream) {
+  return add_rmsnorm_launch(x, residual, partial, w, S, M, H, eps, nullptr, stream);
+}
+
+// ... + MoE routing of every normalised row: ids [M, k] int32, weights [M, k] fp32 (E <= 64).
+PK_EXPORT int pk_splitk_add_rmsnorm_route(void* x, void* residual, const void* partial, const void* w, int S, int M,
+                                          int H, float eps, const void* router, int E, int k, int renorm, void* ids,
+                                          void* rw, hipStream_t stream) {
+  if (E > 64 || E < 1 || k > E) return -1;
+  const RouteArgs ra{static_cast<const bf16_t*>(router), static_cast<int*>(ids), static_cast<float*>(rw), E, k, renorm};
+  return add_rmsnorm_launch(x, residual, partial, w, S, M, H, eps, &ra, stream);
+}
+
+static int add_rmsnorm_launch(void* x, void* residual, const void* partial, const void* w, int S, int M, int H,
+                              float eps, const RouteArgs* ra, hipStream_t stream) {
   if (M <= 0) return 0;
   if (H % 1024 || H > 8192) return -1;
   auto xx = static_cast<bf16_t*>(x);
@@ -679,8 +767,12 @@ PK_EXPORT int pk_splitk_add_rmsnorm(void* x, void* residual, const void* partial
   auto ww = static_cast<const bf16_t*>(w);
   const int threads = H / 4 > 1024 ? 1024 : H / 4;
   auto go = [&](auto per, auto ss) {
-    splitk_add_rmsnorm_kernel<decltype(per)::value, decltype(ss)::value><<<M, threads, 0, stream>>>(
-        xx, rr, pp, ww, S, M, H, eps);
+    if (ra != nullptr)
+      splitk_add_rmsnorm_kernel<decltype(per)::value, decltype(ss)::value, true><<<M, threads, 0, stream>>>(
+          xx, rr, pp, ww, S, M, H, eps, *ra);
+    else
+      splitk_add_rmsnorm_kernel<decltype(per)::value, decltype(ss)::value, false><<<M, threads, 0, stream>>>(
+          xx, rr, pp, ww, S, M, H, eps);
   };
   auto go_s = [&](auto per) {
     switch (S) {

@@ -58,10 +58,9 @@ __global__ void topk_softmax_kernel(const bf16_t* __restrict__ logits, int strid
     for (int j = 0; j < k; ++j) w[t * k + j] /= wsum;
 }
 
-// single workgroup of 1024 threads; n = T*k slots; E <= 64.
-__global__ void __launch_bounds__(1024) align_kernel(const int* __restrict__ ids, int n, int E, int e_lo, int e_hi,
-                                                     int* __restrict__ offsets, int* __restrict__ sorted,
-                                                     int* __restrict__ inv) {
+// Stable counting sort by expert; run by ONE workgroup of 1024 threads; n = T*k slots; E <= 64.
+__device__ void align_body(const int* __restrict__ ids, int n, int E, int e_lo, int e_hi, int* __restrict__ offsets,
+                           int* __restrict__ sorted, int* __restrict__ inv) {
   __shared__ int counts[64];
   __shared__ int cursor[64];
   __shared__ int wave_cnt[16][64];
@@ -116,6 +115,70 @@ __global__ void __launch_bounds__(1024) align_kernel(const int* __restrict__ ids
       }
     }
     __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(1024) align_kernel(const int* __restrict__ ids, int n, int E, int e_lo, int e_hi,
+                                                     int* __restrict__ offsets, int* __restrict__ sorted,
+                                                     int* __restrict__ inv) {
+  align_body(ids, n, E, e_lo, e_hi, offsets, sorted, inv);
+}
+
+// MoE combine fused with the residual add and the next RMSNorm (one workgroup per token):
+//   y = bf16(sum_j w[t,j] * moe_out[inv[t*k+j]])   (what unpermute would store)
+//   residual[t] = bf16(residual[t] + y);  x[t] = rmsnorm(residual[t]) * norm_w
+template <int PER>
+__global__ void __launch_bounds__(1024) combine_add_rmsnorm_kernel(bf16_t* __restrict__ xo, bf16_t* __restrict__ residual,
+                                                                   const bf16_t* __restrict__ y,
+                                                                   const int* __restrict__ inv,
+                                                                   const float* __restrict__ w,
+                                                                   const bf16_t* __restrict__ nw, int k, int H,
+                                                                   float eps) {
+  __shared__ float red[16];
+  const int t = blockIdx.x;
+  float v[PER][4];
+  float ss = 0.f;
+  bf16_t* res = residual + static_cast<int64_t>(t) * H;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = 4 * (threadIdx.x + i * blockDim.x);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const int p = inv[t * k + j];
+      if (p < 0) continue;
+      const uint2 yy = *reinterpret_cast<const uint2*>(y + static_cast<int64_t>(p) * H + c);
+      const float ww = w[t * k + j];
+      acc[0] += ww * bf2f(static_cast<bf16_t>(yy.x & 0xffff));
+      acc[1] += ww * bf2f(static_cast<bf16_t>(yy.x >> 16));
+      acc[2] += ww * bf2f(static_cast<bf16_t>(yy.y & 0xffff));
+      acc[3] += ww * bf2f(static_cast<bf16_t>(yy.y >> 16));
+    }
+    const uint2 rr = *reinterpret_cast<const uint2*>(res + c);
+    v[i][0] = bf2f(f2bf(bf2f(f2bf(acc[0])) + bf2f(static_cast<bf16_t>(rr.x & 0xffff))));
+    v[i][1] = bf2f(f2bf(bf2f(f2bf(acc[1])) + bf2f(static_cast<bf16_t>(rr.x >> 16))));
+    v[i][2] = bf2f(f2bf(bf2f(f2bf(acc[2])) + bf2f(static_cast<bf16_t>(rr.y & 0xffff))));
+    v[i][3] = bf2f(f2bf(bf2f(f2bf(acc[3])) + bf2f(static_cast<bf16_t>(rr.y >> 16))));
+    uint2 o;
+    o.x = pack2(v[i][0], v[i][1]);
+    o.y = pack2(v[i][2], v[i][3]);
+    *reinterpret_cast<uint2*>(res + c) = o;
+    ss += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
+  }
+  const float rinv = rsqrtf(block_sum(ss, red) / H + eps);
+  bf16_t* xr = xo + static_cast<int64_t>(t) * H;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = 4 * (threadIdx.x + i * blockDim.x);
+    const uint2 ww = *reinterpret_cast<const uint2*>(nw + c);
+    float o4[4];
+    o4[0] = bf2f(f2bf(v[i][0] * rinv)) * bf2f(static_cast<bf16_t>(ww.x & 0xffff));
+    o4[1] = bf2f(f2bf(v[i][1] * rinv)) * bf2f(static_cast<bf16_t>(ww.x >> 16));
+    o4[2] = bf2f(f2bf(v[i][2] * rinv)) * bf2f(static_cast<bf16_t>(ww.y & 0xffff));
+    o4[3] = bf2f(f2bf(v[i][3] * rinv)) * bf2f(static_cast<bf16_t>(ww.y >> 16));
+    uint2 o;
+    o.x = pack2(o4[0], o4[1]);
+    o.y = pack2(o4[2], o4[3]);
+    *reinterpret_cast<uint2*>(xr + c) = o;
   }
 }
 
@@ -323,6 +386,25 @@ PK_EXPORT int pk_moe_unpermute_partial(void* out, const void* partial, int S, in
   if (H % 4 || S < 1) return -1;
   unpermute_partial_kernel<<<T, 256, 0, stream>>>(static_cast<bf16_t*>(out), static_cast<const float*>(partial), S, R,
                                                   static_cast<const int*>(inv), static_cast<const float*>(w), k, H);
+  return PK_CHECK_LAUNCH();
+}
+
+PK_EXPORT int pk_moe_combine_add_rmsnorm(void* x, void* residual, const void* y, const void* inv, const void* w,
+                                         const void* norm_w, int T, int k, int H, float eps, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 1024 || H > 8192) return -1;
+  const int threads = H / 4 > 1024 ? 1024 : H / 4;
+  auto xx = static_cast<bf16_t*>(x);
+  auto rr = static_cast<bf16_t*>(residual);
+  auto yy = static_cast<const bf16_t*>(y);
+  auto ii = static_cast<const int*>(inv);
+  auto ww = static_cast<const float*>(w);
+  auto nn = static_cast<const bf16_t*>(norm_w);
+  switch (H / (4 * threads)) {
+    case 1: combine_add_rmsnorm_kernel<1><<<T, threads, 0, stream>>>(xx, rr, yy, ii, ww, nn, k, H, eps); break;
+    case 2: combine_add_rmsnorm_kernel<2><<<T, threads, 0, stream>>>(xx, rr, yy, ii, ww, nn, k, H, eps); break;
+    default: return -1;
+  }
   return PK_CHECK_LAUNCH();
 }
 

@@ -28,6 +28,7 @@ from torch import nn
 from .. import ops
 from ..ops import attention as attn_ops
 from ..ops import gemm
+from ..ops import moe as moe_ops
 from ..ops import reference
 from ..parallel import comm
 from ..parallel.state import ParallelState, get_state
@@ -72,6 +73,8 @@ def add_norm(pending, residual: torch.Tensor, w: torch.Tensor, eps: float):
     """residual += pending; x = rms_norm(residual) * w → (x, residual)."""
     if isinstance(pending, gemm.Partial):
         return gemm.partial_add_rms_norm(pending, residual, w, eps)
+    if isinstance(pending, moe_ops.PendingCombine):
+        return moe_ops.combine_add_rms_norm(pending, residual, w, eps)
     return ops.fused_add_rms_norm(pending, residual, w, eps)
 
 
@@ -295,10 +298,14 @@ class LlamaForCausalLM(nn.Module):
             else:
                 x, residual = add_norm(x, residual, layer.ln1, layer.eps)
             x = layer.attn(x, positions, md, self.cos_sin, kv_caches[i], ws)
-            x, residual = add_norm(x, residual, layer.ln2, layer.eps)
-            x = layer.mlp(x, ws)
+            x, residual = self._mlp_block(layer, x, residual, ws)
         x, _ = add_norm(x, residual, self.norm, self.cfg.rms_eps)
         return x
+
+    def _mlp_block(self, layer, x, residual, ws):
+        """post-attention residual add + RMSNorm, then the MLP (its output may be pending)."""
+        x, residual = add_norm(x, residual, layer.ln2, layer.eps)
+        return layer.mlp(x, ws), residual
 
     # ------------------------------------------------------------------ fused decode chain
     # Off by default: measured slower on MI355X (tools/bench_gemm.py "fused decode chain": the

@@ -21,6 +21,7 @@ from torch import nn
 
 from ..ops import gemm, moe
 from ..parallel import comm
+from ..parallel.state import get_state
 from .llama import LlamaForCausalLM, _p
 from .weights import shard_cols, shard_rows
 
@@ -37,12 +38,26 @@ class MixtralMoE(nn.Module):
         self.w13_p = None  # fragment-packed decode copies (MixtralForCausalLM._pack_mlp)
         self.w2_p = None
 
-    def forward(self, x: torch.Tensor, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-        y = moe.fused_moe(x, self.router, self.w13, self.w2, self.k, self.e_lo, self.e_hi, self.w13_p, self.w2_p)
-        return comm.tp_all_reduce(y)
+    def forward(self, x: torch.Tensor, ws: Optional[torch.Tensor] = None, routing=None):
+        """Combined expert output, or (single rank: nothing to all-reduce) a PendingCombine that
+        the next residual add + RMSNorm consumes in one kernel.  ``routing``: (ids, weights)
+        from the norm kernel that produced ``x``."""
+        single = get_state().tp_size == 1
+        y = moe.fused_moe(x, self.router, self.w13, self.w2, self.k, self.e_lo, self.e_hi, self.w13_p, self.w2_p,
+                          defer_combine=single, routing=routing)
+        return y if single else comm.tp_all_reduce(y)
 
 
 class MixtralForCausalLM(LlamaForCausalLM):
+    def _mlp_block(self, layer, x, residual, ws):
+        """Decode (TP = 1, split-K o-projection pending): the residual add + RMSNorm kernel also
+        routes every token, so the MoE starts from ready expert ids and weights."""
+        if isinstance(x, gemm.Partial) and x.M <= 64 and gemm.norm_fusable(x.N):
+            x, residual, ids, w = gemm.partial_add_rms_norm_route(x, residual, layer.ln2, layer.eps, layer.mlp.router,
+                                                                   layer.mlp.k)
+            return layer.mlp(x, ws, routing=(ids, w)), residual
+        return super()._mlp_block(layer, x, residual, ws)
+
     def _make_mlp(self, layer: int) -> nn.Module:
         cfg, st = self.cfg, self.st
         ep = st.ep_size

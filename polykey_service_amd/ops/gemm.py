@@ -45,7 +45,8 @@ class GemmArgs(ctypes.Structure):
                 ("positions", ctypes.c_void_p), ("cos_sin", ctypes.c_void_p), ("k_cache", ctypes.c_void_p),
                 ("v_cache", ctypes.c_void_p), ("slots", ctypes.c_void_p), ("nq", ctypes.c_int),
                 ("nkv", ctypes.c_int), ("bs", ctypes.c_int), ("row_offsets", ctypes.c_void_p),
-                ("w_stride", ctypes.c_longlong), ("groups", ctypes.c_int), ("max_group_rows", ctypes.c_int)]
+                ("w_stride", ctypes.c_longlong), ("groups", ctypes.c_int), ("max_group_rows", ctypes.c_int),
+                ("a_rows", ctypes.c_void_p), ("a_row_div", ctypes.c_int)]
 
 
 _ARGS_CHECKED = False
@@ -68,6 +69,7 @@ def _launch_ex(mode: int, x: torch.Tensor, w: torch.Tensor, packed: Optional[tor
         assert n == ctypes.sizeof(GemmArgs), f"GemmArgs layout mismatch: C {n} vs ctypes {ctypes.sizeof(GemmArgs)}"
         _ARGS_CHECKED = True
     M, K = x.shape
+    M = kw.pop("m_override", None) or M  # grouped + gathered A: rows of the grouped output
     N = kw.pop("n_override", None) or w.shape[0]
     if "groups" in kw:
         N = w.shape[0] // kw["groups"]
@@ -125,19 +127,24 @@ def linear_qkv_rope(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, counters
 
 def grouped_linear(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_rows: int, silu: bool,
                    packed: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-                   S: int = 1) -> torch.Tensor:
+                   S: int = 1, a_rows: Optional[torch.Tensor] = None, a_row_div: int = 1,
+                   n_rows: Optional[int] = None) -> torch.Tensor:
     """Grouped decode GEMM (MoE experts): rows ``a[offsets[e]:offsets[e+1]]`` times ``w[e]^T``,
     ``w`` [G, N, K] (``packed``: :func:`pack_weight` of ``w.view(G*N, K)``), every group <= 64
     rows.  One launch; groups without rows read no weights.  ``silu``: interleaved gate/up →
     [R, N/2] bf16.  Otherwise ``S`` > 1 returns fp32 split-K slabs [S, R, N] in ``ws``."""
     G, N, K = w.shape
-    R = a.shape[0]
+    # a_rows: gather A rows (a_rows[i] // a_row_div) instead of reading group-contiguous rows —
+    # the MoE permute folded into the GEMM's A staging; n_rows = rows of the grouped output
+    R = n_rows if n_rows is not None else a.shape[0]
     out = None
     if silu or S == 1:
         out = torch.empty((R, N // 2 if silu else N), dtype=a.dtype, device=a.device)
     mode = MODE_SILU if silu else (MODE_BF16 if S == 1 else MODE_PARTIAL)
     M2 = a  # A rows are addressed through the offsets
     args = dict(row_offsets=offsets, w_stride=N * K, groups=G, max_group_rows=max_rows)
+    if a_rows is not None:
+        args.update(a_rows=a_rows, a_row_div=a_row_div, m_override=R)
     _launch_ex(mode, M2, w.view(G * N, K), None if packed is None else packed.view(G * N, K), S, out=out,
                ws=ws if S > 1 else None, **args)
     return out if out is not None else ws
@@ -290,6 +297,21 @@ def partial_add_rms_norm(p: Partial, residual: torch.Tensor, weight: torch.Tenso
     native.call("pk_splitk_add_rmsnorm", out.data_ptr(), residual.data_ptr(), p.buf.data_ptr(), weight.data_ptr(),
                 p.S, p.M, p.N, float(eps), native.stream_ptr())
     return out, residual
+
+
+def partial_add_rms_norm_route(p: Partial, residual: torch.Tensor, weight: torch.Tensor, eps: float,
+                               router: torch.Tensor, k: int, renorm: bool = True):
+    """:func:`partial_add_rms_norm` that also routes every normalised row (MoE): router logits
+    (bf16), softmax, top-k → (x, residual, ids [M, k] int32, weights [M, k] fp32)."""
+    M, H = residual.shape
+    E = router.shape[0]
+    out = torch.empty_like(residual)
+    ids = torch.empty((M, k), dtype=torch.int32, device=residual.device)
+    w = torch.empty((M, k), dtype=torch.float32, device=residual.device)
+    native.call("pk_splitk_add_rmsnorm_route", out.data_ptr(), residual.data_ptr(), p.buf.data_ptr(),
+                weight.data_ptr(), p.S, p.M, p.N, float(eps), router.data_ptr(), E, k, int(renorm), ids.data_ptr(),
+                w.data_ptr(), native.stream_ptr())
+    return out, residual, ids, w
 
 
 def silu_and_mul_interleaved(x: torch.Tensor) -> torch.Tensor:

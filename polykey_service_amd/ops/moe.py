@@ -15,6 +15,8 @@ the same all-reduce the dense MLP already does — see parallel/ep.py for the al
 """
 from __future__ import annotations
 
+import dataclasses
+
 from typing import Optional, Tuple
 
 import torch
@@ -117,14 +119,60 @@ def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_ro
     return out
 
 
+@dataclasses.dataclass
+class PendingCombine:
+    """Expert outputs not yet combined: :func:`combine_add_rms_norm` does the weighted top-k
+    combine, the residual add and the next RMSNorm in one kernel."""
+    y: torch.Tensor      # [T*k, H] expert outputs in expert-sorted order
+    inv: torch.Tensor    # [T*k] sorted position of (token, slot); -1 = expert on another EP rank
+    w: torch.Tensor      # [T, k] routing weights
+    T: int
+    k: int
+
+    def combine(self) -> torch.Tensor:
+        return unpermute(self.y, self.inv, self.w, self.T, self.k)
+
+
+def combine_add_rms_norm(p: PendingCombine, residual: torch.Tensor, weight: torch.Tensor, eps: float):
+    """residual += combine(p); x = rms_norm(residual) * weight → (x, residual), one kernel."""
+    H = residual.shape[-1]
+    if not residual.is_cuda or H % 1024 or H > 8192:
+        from .norm import fused_add_rms_norm
+        return fused_add_rms_norm(p.combine(), residual, weight, eps)
+    x = torch.empty_like(residual)
+    native.call("pk_moe_combine_add_rmsnorm", x.data_ptr(), residual.data_ptr(), p.y.data_ptr(), p.inv.data_ptr(),
+                p.w.data_ptr(), weight.data_ptr(), p.T, p.k, H, float(eps), native.stream_ptr())
+    return x, residual
+
+
 def fused_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, k: int,
               e_lo: int = 0, e_hi: Optional[int] = None, w13_p: Optional[torch.Tensor] = None,
-              w2_p: Optional[torch.Tensor] = None) -> torch.Tensor:
+              w2_p: Optional[torch.Tensor] = None, defer_combine: bool = False,
+              routing: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
     """Mixtral sparse MLP for this rank's experts.  x [T, H]; router_w [E, H]; w13 [E_l, 2I, H]
-    (gate/up interleaved by 16); w2 [E_l, H, I].  Returns the (partial, if EP) combined output."""
+    (gate/up interleaved by 16); w2 [E_l, H, I].  Returns the (partial, if EP) combined output,
+    or with ``defer_combine`` a :class:`PendingCombine` for the fused combine+add+norm.
+    ``routing``: (ids, weights) already computed by the preceding norm kernel
+    (:func:`gemm.partial_add_rms_norm_route`).
+
+    Decode (T <= 64): expert sort, the w13 grouped GEMM gathering token rows itself (no
+    permute pass) with the SiLU epilogue, the w2 grouped GEMM, and the combine (fused into the
+    next residual add + RMSNorm when deferred)."""
     T = x.shape[0]
     E = router_w.shape[0]
     e_hi = E if e_hi is None else e_hi
+    N13, K13 = w13.shape[1], w13.shape[2]
+    if (x.is_cuda and T <= 64 and E <= 64 and gemm.SKINNY_ENABLED and N13 % 128 == 0 and K13 % 256 == 0
+            and w2.shape[1] % 128 == 0 and w2.shape[2] % 256 == 0):
+        if routing is not None:
+            ids, wts = routing
+        else:
+            ids, wts = topk_softmax(F.linear(x, router_w), k)
+        offsets, sorted_, inv = align(ids, E, e_lo, e_hi)
+        h = gemm.grouped_linear(x, w13, offsets, T, True, packed=w13_p, a_rows=sorted_, a_row_div=k, n_rows=T * k)
+        y = gemm.grouped_linear(h, w2, offsets, T, False, packed=w2_p)
+        pending = PendingCombine(y, inv, wts, T, k)
+        return pending if defer_combine else pending.combine()
     logits = F.linear(x, router_w)
     ids, wts = topk_softmax(logits, k)
     offsets, sorted_, inv = align(ids, E, e_lo, e_hi)

@@ -47,10 +47,12 @@ SIGNATURES = {
     "pk_moe_unpermute": [P, P, P, P, I32, I32, I32, P],
     "pk_moe_gemm": [P, P, P, P, I32, I32, I32, I32, I32, I32, P],
     "pk_moe_unpermute_partial": [P, P, I32, I32, P, P, I32, I32, I32, P],
+    "pk_moe_combine_add_rmsnorm": [P, P, P, P, P, P, I32, I32, I32, F32, P],
     "pk_silu_and_mul_il": [P, P, I32, I32, P],
     "pk_skinny_gemm": [P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P],
     "pk_splitk_reduce": [P, P, I32, I32, I32, I32, I32, P],
     "pk_splitk_add_rmsnorm": [P, P, P, P, I32, I32, I32, F32, P],
+    "pk_splitk_add_rmsnorm_route": [P, P, P, P, I32, I32, I32, F32, P, I32, I32, I32, P, P, P],
     "pk_qkv_reduce_rope_cache": [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, P],
     "pk_skinny_gemm_ex": [P, I32, P],
     "pk_gemm_args_size": [],

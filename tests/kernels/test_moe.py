@@ -78,3 +78,49 @@ def test_grouped_linear_skips_empty_groups_and_splits():
     p = gemm.grouped_linear(a, w, offsets, 23, silu=False, packed=gemm.pack_weight(w.view(-1, K)).view(w.shape),
                             ws=ws, S=2)
     torch.testing.assert_close(p[: 2 * R * N].view(2, R, N).sum(0), exp, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,E,k", [(1, 8, 2), (64, 8, 2), (17, 64, 4)])
+def test_add_rmsnorm_with_routing(M, E, k):
+    """Split-K residual add + RMSNorm that also routes each row == norm kernel + router GEMM
+    (bf16 logits) + topk_softmax."""
+    from polykey_service_amd.ops import gemm
+    H, S = 4096, 4
+    g = torch.Generator().manual_seed(M + E)
+    slabs = (torch.randn(S, M, H, generator=g) * 0.3).cuda()
+    res = torch.randn(M, H, generator=g).to(torch.bfloat16).cuda()
+    nw = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16).cuda()
+    router = (torch.randn(E, H, generator=g) * 0.05).to(torch.bfloat16).cuda()
+    ws = slabs.reshape(-1).clone()
+    p = gemm.Partial(ws, S, M, H)
+    x1, r1 = gemm.partial_add_rms_norm(p, res.clone(), nw, 1e-5)
+    x2, r2, ids, w = gemm.partial_add_rms_norm_route(p, res.clone(), nw, 1e-5, router, k)
+    assert torch.equal(x1, x2) and torch.equal(r1, r2)
+    ids_ref, w_ref = moe.topk_softmax(torch.nn.functional.linear(x1, router), k)
+    logits = torch.nn.functional.linear(x1, router).float()
+    top = logits.topk(min(k + 1, E), -1).values
+    clear = ((top[:, :-1] - top[:, 1:]).abs() > 1e-2).all(-1)  # rows without a bf16 near-tie
+    assert torch.equal(ids[clear], ids_ref[clear])
+    torch.testing.assert_close(w[clear], w_ref[clear], atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("T,ep", [(5, (0, 8)), (64, (0, 8)), (33, (2, 6))])
+def test_decode_moe_gather_and_fused_combine(T, ep):
+    """Decode MoE (routing kernel, gathered-A w13 GEMM, deferred combine fused with the residual
+    add + RMSNorm) vs the fp32 reference followed by add + RMSNorm."""
+    from polykey_service_amd.ops import reference as ref
+    E, H, I = 8, 1024, 1024
+    router, w13, w2 = weights(E, H, I)
+    lo, hi = ep
+    x = torch.randn(T, H, device="cuda").to(torch.bfloat16)
+    res = torch.randn(T, H, device="cuda").to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    pend = moe.fused_moe(x, router, w13[lo:hi].contiguous(), w2[lo:hi].contiguous(), 2, lo, hi, defer_combine=True)
+    assert isinstance(pend, moe.PendingCombine)
+    y_ref = moe.fused_moe_reference(x, router, w13[lo:hi], w2[lo:hi], 2, lo, hi)
+    torch.testing.assert_close(pend.combine().float(), y_ref, atol=3e-2, rtol=3e-2)
+    r1 = res.clone()
+    xo, r1 = moe.combine_add_rms_norm(pend, r1, nw, 1e-5)
+    r_ref = (pend.combine().float() + res.float()).to(torch.bfloat16)
+    torch.testing.assert_close(r1.float(), r_ref.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(xo.float(), ref.rms_norm(r_ref, nw, 1e-5).float(), atol=5e-2, rtol=3e-2)
