@@ -212,7 +212,9 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
         out[static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD] = 0;
     return;
   }
-  const int n_used = (ctx + kPart - 1) / kPart;
+  // n_parts comes from the launch's context bound; the clamp keeps a violated bound in-bounds
+  const int n_used = min((ctx + kPart - 1) / kPart, n_parts);
+  PK_DEVICE_ASSERT(ctx <= n_parts * kPart);
   if (static_cast<int>(blockIdx.z) >= n_used) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -459,10 +461,13 @@ PK_EXPORT int pk_decode_num_parts(int max_context) { return (max_context + kDeco
 static int decode_launch(void* out, const void* q, const QkvIn& qi, const void* k_cache, const void* v_cache,
                          const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
                          void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
-                         int out_stride, float scale, hipStream_t stream) {
+                         int out_stride, float scale, int max_ctx, hipStream_t stream) {
   if (n_seqs <= 0) return 0;
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
-  const int n_parts = (max_blocks * bs + kDecodePart - 1) / kDecodePart;
+  // max_ctx bounds the contexts of this launch (<= 0: the block-table capacity).  A launch
+  // known to stay within one partition needs no partition grid and no merge kernel.
+  if (max_ctx <= 0 || max_ctx > max_blocks * bs) max_ctx = max_blocks * bs;
+  const int n_parts = (max_ctx + kDecodePart - 1) / kDecodePart;
   if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
   // z is capped: a short context leaves the extra z-workgroups idle, and graph capture fixes
   // the grid for max_model_len, so a z of n_parts would launch mostly-empty workgroups
@@ -491,13 +496,14 @@ static int decode_launch(void* out, const void* q, const QkvIn& qi, const void* 
   return PK_CHECK_LAUNCH();
 }
 
+// max_blocks: block-table row stride; max_ctx: bound on every context of this launch (<= 0: no bound)
 PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
                               const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
                               void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
-                              int out_stride, float scale, hipStream_t stream) {
+                              int out_stride, float scale, int max_ctx, hipStream_t stream) {
   const QkvIn none{};
   return decode_launch(out, q, none, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, counters, n_seqs,
-                       n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale, stream);
+                       n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale, max_ctx, stream);
 }
 
 // Decode attention straight from the fused QKV projection's split-K slabs [S, M, (n_q+2n_kv)*128]
@@ -506,12 +512,12 @@ PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, 
                                   const void* cos_sin, const void* slots, void* k_cache, void* v_cache,
                                   const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
                                   int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int out_stride, float scale,
-                                  hipStream_t stream) {
+                                  int max_ctx, hipStream_t stream) {
   if (partial == nullptr || S < 1 || M < n_seqs) return -1;
   QkvIn qi{static_cast<const float*>(partial), static_cast<const int*>(positions), static_cast<const float*>(cos_sin),
            static_cast<const int*>(slots), S, M};
   return decode_launch(out, nullptr, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, nullptr,
-                       n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, stream);
+                       n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
 }
 
 PK_EXPORT int pk_set_decode_z(int z) {

@@ -50,6 +50,9 @@ class RunnerConfig:
 DECODE_INKERNEL_MERGE = os.environ.get("POLYKEY_DECODE_INKERNEL_MERGE", "0") == "1"
 # stage step inputs with a kernel reading pinned memory instead of an SDMA copy
 HOST_COPY_KERNEL = os.environ.get("POLYKEY_HOST_COPY_KERNEL", "1") == "1"
+# a second decode graph per bucket for steps whose contexts all fit one attention partition:
+# one workgroup per (seq, kv head) and no partition-merge kernel in each layer
+SHORT_DECODE_GRAPHS = os.environ.get("POLYKEY_SHORT_DECODE_GRAPHS", "1") == "1"
 
 
 class _Layout:
@@ -104,11 +107,14 @@ class ModelRunner:
         self.num_blocks = 0
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_out: Dict[int, torch.Tensor] = {}
+        self.short_graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.short_graph_out: Dict[int, torch.Tensor] = {}
+        self.short_ctx = attn_ops._PART if SHORT_DECODE_GRAPHS and cfg.max_model_len > attn_ops._PART else 0
         self.graph_pool = None
         a0 = model.layers[0].attn
         self.part_o, self.part_ml, self.part_ctr = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks,
                                                                              self.bs, device, n_kv=a0.nkv)
-        self.stats = {"steps": 0, "graph_steps": 0, "tokens": 0}
+        self.stats = {"steps": 0, "graph_steps": 0, "short_graph_steps": 0, "tokens": 0}
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None
 
@@ -181,7 +187,8 @@ class ModelRunner:
             h["offsets"][r] = len(s.output_ids)
         return T, n
 
-    def _metadata(self, nd: int, n: int, T: int, max_q: int) -> attn_ops.AttnMetadata:
+    def _metadata(self, nd: int, n: int, T: int, max_q: int, short: bool = False) -> attn_ops.AttnMetadata:
+        """``short``: every decode context is at most ``self.short_ctx`` tokens."""
         d = self.d
         npf = n - nd
         md = attn_ops.AttnMetadata(
@@ -190,7 +197,8 @@ class ModelRunner:
             decode_block_tables=d["block_tables"][:nd] if nd else None,
             decode_context_lens=d["context_lens"][:nd] if nd else None,
             decode_part_o=self.part_o, decode_part_ml=self.part_ml,
-            decode_counters=self.part_ctr if DECODE_INKERNEL_MERGE else None)
+            decode_counters=self.part_ctr if DECODE_INKERNEL_MERGE else None,
+            decode_max_ctx=self.short_ctx if short else 0)
         if npf:
             md.prefill_block_tables = d["block_tables"][nd:n]
             md.prefill_context_lens = d["context_lens"][nd:n]
@@ -199,7 +207,7 @@ class ModelRunner:
         return md
 
     # ----------------------------------------------------------------- execute
-    # header words (section "header"): mode, T, n, nd, ns, max_q, graph bucket
+    # header words (section "header"): mode, T, n, nd, ns, max_q, graph bucket, short-context graph
     MODE_IDLE, MODE_RUN, MODE_STOP = 0, 1, 2
 
     @torch.inference_mode()
@@ -234,10 +242,16 @@ class ModelRunner:
             g = self._graph_bucket(nd) or 0
             if g:
                 self._pad_decode(nd, g)
-        h["header"][:7] = (self.MODE_RUN, T, n, nd, ns, max_q, g)
+        short = self._short(g, nd)
+        h["header"][:8] = (self.MODE_RUN, T, n, nd, ns, max_q, g, short)
         self._publish(max(n, g))
-        toks = self._run(T, n, nd, ns, max_q, g)
+        toks = self._run(T, n, nd, ns, max_q, g, short)
         return self._handle(toks, ns)
+
+    def _short(self, g: int, nd: int) -> int:
+        """1 when the step can replay bucket ``g``'s short-context graph."""
+        return int(bool(g and g in self.short_graphs and nd and
+                        int(self.h["context_lens"][:nd].max()) <= self.short_ctx))
 
     def _handle(self, toks, ns: int):
         self.stats["steps"] += 1
@@ -293,10 +307,11 @@ class ModelRunner:
             h["seeds"][r] = s.seed
             h["offsets"][r] = len(s.output_ids) + 1
         self._pad_decode(n, g)
-        h["header"][:7] = (self.MODE_RUN, T, n, n, n, 0, g)
+        short = self._short(g, n)
+        h["header"][:8] = (self.MODE_RUN, T, n, n, n, 0, g, short)
         self._publish(max(n, g))
         self.d["input_ids"][:n].copy_(prev[3][:n])  # step k's sampled ids, stream-ordered
-        return self._handle(self._run(T, n, n, n, 0, g), n)
+        return self._handle(self._run(T, n, n, n, 0, g, short), n)
 
     def _publish(self, n_bt_rows: Optional[int] = None) -> None:
         """Stage the step inputs on the device.  On the GPU a kernel reads the pinned staging
@@ -325,25 +340,31 @@ class ModelRunner:
         from ..parallel import comm
         while True:
             comm.tp_broadcast_tensor(self.dev_buf)
-            hdr = self.d["header"][:7].tolist()
-            mode, T, n, nd, ns, max_q, g = hdr
+            hdr = self.d["header"][:8].tolist()
+            mode, T, n, nd, ns, max_q, g, short = hdr
             if mode == self.MODE_STOP:
                 return
             if mode == self.MODE_RUN:
                 with torch.inference_mode():
-                    self._run(T, n, nd, ns, max_q, g)
+                    self._run(T, n, nd, ns, max_q, g, short)
 
     def stop_workers(self) -> None:
         if self.model.st.tp_size > 1:
             self.h["header"][0] = self.MODE_STOP
             self._publish()
 
-    def _run(self, T: int, n: int, nd: int, ns: int, max_q: int, g: int):
+    def _run(self, T: int, n: int, nd: int, ns: int, max_q: int, g: int, short: int = 0):
         d = self.d
         if g:
-            self.graphs[g].replay()
+            if short:
+                self.short_graphs[g].replay()
+                self.stats["short_graph_steps"] += 1
+                out = self.short_graph_out[g]
+            else:
+                self.graphs[g].replay()
+                out = self.graph_out[g]
             self.stats["graph_steps"] += 1
-            return self.graph_out[g]
+            return out
         md = self._metadata(nd, n, T, max_q)
         hidden = self.model(d["input_ids"][:T], d["positions"][:T], md, self.kv_caches)
         if ns == 0:
@@ -397,8 +418,9 @@ class ModelRunner:
         self.dev_buf.copy_(self.host_buf)
         torch.cuda.synchronize(self.device)
         stream = torch.cuda.Stream(self.device)
-        for g in sorted(sizes, reverse=True):
-            md = self._metadata(g, g, g, 0)
+        variants = (False, True) if self.short_ctx else (False,)
+        for g, short in [(g, v) for g in sorted(sizes, reverse=True) for v in variants]:
+            md = self._metadata(g, g, g, 0, short)
 
             def run():
                 hidden = self.model(d["input_ids"][:g], d["positions"][:g], md, self.kv_caches)
@@ -416,6 +438,6 @@ class ModelRunner:
                 out = run()
             if self.graph_pool is None:
                 self.graph_pool = graph.pool()
-            self.graphs[g] = graph
-            self.graph_out[g] = out
+            (self.short_graphs if short else self.graphs)[g] = graph
+            (self.short_graph_out if short else self.graph_out)[g] = out
         torch.cuda.synchronize(self.device)

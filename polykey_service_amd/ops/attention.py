@@ -32,6 +32,7 @@ class AttnMetadata:
     decode_part_o: Optional[torch.Tensor] = None         # split-K workspace
     decode_part_ml: Optional[torch.Tensor] = None
     decode_counters: Optional[torch.Tensor] = None       # [n_seqs, n_kv] int32, zero-initialised
+    decode_max_ctx: int = 0  # bound on every decode context of the step (0: block-table capacity)
 
     @property
     def num_tokens(self) -> int:
@@ -87,7 +88,8 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         native.call("pk_paged_decode", out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                     bt.data_ptr(), md.decode_context_lens.data_ptr(),
                     native.ptr(md.decode_part_o) or 0, native.ptr(md.decode_part_ml) or 0,
-                    native.ptr(md.decode_counters) or 0, nd, nq, nkv, bs, bt.shape[1], q.stride(0), out.stride(0), float(scale), stream)
+                    native.ptr(md.decode_counters) or 0, nd, nq, nkv, bs, bt.stride(0), q.stride(0), out.stride(0),
+                    float(scale), int(md.decode_max_ctx), stream)
     if md.num_prefill > 0:
         bt = md.prefill_block_tables
         qp = q[nd:]
@@ -128,6 +130,6 @@ def paged_decode_from_qkv(p, positions: torch.Tensor, cos_sin: torch.Tensor, k_c
     native.call("pk_paged_decode_qkv", out.data_ptr(), p.buf.data_ptr(), p.S, p.M, positions.data_ptr(),
                 cos_sin.data_ptr(), md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                 bt.data_ptr(), md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,
-                native.ptr(md.decode_part_ml) or 0, md.num_decode, nq, nkv, k_cache.shape[2], bt.shape[1],
-                out.stride(0), float(scale), native.stream_ptr())
+                native.ptr(md.decode_part_ml) or 0, md.num_decode, nq, nkv, k_cache.shape[2], bt.stride(0),
+                out.stride(0), float(scale), int(md.decode_max_ctx), native.stream_ptr())
     return out

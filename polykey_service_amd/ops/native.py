@@ -35,9 +35,9 @@ SIGNATURES = {
     "pk_fused_add_rmsnorm": [P, P, P, I32, I32, F32, P],
     "pk_silu_and_mul": [P, P, I32, I32, P],
     "pk_rope_and_cache": [P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P],
-    "pk_paged_decode": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, F32, P],
+    "pk_paged_decode": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, F32, I32, P],
     "pk_set_decode_z": [I32],
-    "pk_paged_decode_qkv": [P, P, I32, I32, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, P],
+    "pk_paged_decode_qkv": [P, P, I32, I32, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, I32, P],
     "pk_paged_prefill": [P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, F32, P],
     "pk_sample": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, P],
     "pk_embedding": [P, P, P, I32, I32, I32, I32, P],

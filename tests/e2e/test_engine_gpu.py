@@ -122,3 +122,21 @@ def test_continuation_steps_match_synchronous_engine():
             assert e.continuation_steps > 0
         assert e.bm.num_free == e.bm.num_blocks
     assert res[0] == res[1]
+
+
+def test_short_and_long_context_graphs_agree_with_eager():
+    """Decode steps whose contexts all fit one attention partition replay the short-context
+    graph (no partition grid, no merge kernel); steps past it replay the long one.  Contexts
+    here cross the 512-token partition mid-generation; tokens match the eager engine."""
+    _, gpu = _models("tiny-llama-gqa4")
+    prompts = [[1] + [(7 * i) % 200 + 2 for i in range(n)] for n in (490, 505, 60)]
+    res = []
+    for graphs in (False, True):
+        e = LLMEngine(EngineConfig(model="tiny-llama-gqa4", max_num_seqs=8, max_num_batched_tokens=1024,
+                                   max_model_len=1024, hip_graphs=graphs, device="cuda"),
+                      ParallelState(device=torch.device("cuda")), model=gpu)
+        res.append(e.generate(prompts, SamplingParams(max_tokens=40, ignore_eos=True)))
+        if graphs:
+            st = e.runner.stats
+            assert 0 < st["short_graph_steps"] < st["graph_steps"], st
+    assert res[0] == res[1]
