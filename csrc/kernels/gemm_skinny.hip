@@ -14,7 +14,11 @@
 //     slabs [S, M, N] reduced by the consumer kernel (reduce / reduce+SiLU / reduce+residual+
 //     RMSNorm), so a split costs no extra launch on the hot path;
 //   * epilogues: bf16 store, fp32 partial store, or fused SiLU(gate)*up when W's gate/up rows
-//     are interleaved in blocks of 16 (then one wave holds gate and up of the same columns).
+//     are interleaved in blocks of 16 (then one wave holds gate and up of the same columns);
+//   * block-packed W (ops/gemm.py pack_weight): per (128-row n-block, 128-deep k-step) the 32 KiB
+//     a workgroup consumes are contiguous, as 32 MFMA A-fragments of 1 KiB in lane order, so
+//     every wave load instruction reads 1 KiB and a workgroup sweeps one linear stream
+//     (tools/gemm_lab.hip: LM head 5.1 -> 5.9 TB/s with non-temporal loads).
 #include <type_traits>
 
 #include "common.h"
@@ -26,7 +30,7 @@ struct GemmArgs {
   bf16_t* out;               // kBF16 / kSiluMul: [M, ldo]; kQkvRope: q [M, nq * 128]
   float* partial;            // fp32 slabs [S, M, N]
   const bf16_t* A;           // [M, lda]; with the norm prologue: the residual stream
-  const bf16_t* W;           // [N, K] row-major or fragment-packed
+  const bf16_t* W;           // [N, K] row-major or block-packed
   int M, N, K, lda, ldo, S;
   int* counters;             // [N / 128] zeroed once; the last arriver re-arms its counter
   const float* nrm_parts;    // norm prologue: per-row sums of squares [nrm_nparts, M]
@@ -66,6 +70,30 @@ enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4
 
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+
+// Experiment knobs for tools/gemm_lab.hip (all 0 in the library build; the NO_* ones give
+// wrong results and exist only to attribute time).
+#ifndef PK_W_DEPTH
+#define PK_W_DEPTH 2         // k-steps of W in flight per wave (register ring; 4 measured slower)
+#endif
+#ifndef PK_LAB_LDS_PAD
+#define PK_LAB_LDS_PAD 0     // extra LDS per workgroup (forces one workgroup per CU)
+#endif
+#ifndef PK_LAB_NO_MFMA
+#define PK_LAB_NO_MFMA 0     // no MFMA / LDS reads: the bare W stream
+#endif
+#ifndef PK_LAB_NO_ASTAGE
+#define PK_LAB_NO_ASTAGE 0   // stage A once, no per-chunk barrier
+#endif
+
+// Weight loads.  NT: non-temporal (no Infinity-Cache allocation) -- measured faster for the
+// large, read-once streams (gate_up 235 MB: -6 %, LM head 1 GB: -10 %) and slower for the
+// small ones, which profit from whatever the Infinity Cache still holds.
+template <bool NT>
+__device__ __forceinline__ bf16x8_t ldw(const bf16_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(p));
+  return *reinterpret_cast<const bf16x8_t*>(p);
+}
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
@@ -207,16 +235,20 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
 // buffered, register-staged: loads for chunk c+1 are issued before chunk c's MFMAs and written
 // after them), while each wave streams its own 32 W rows straight to VGPRs two 128-steps
 // ahead.  Row-major W: lane group g reads bytes [64s + 16g, +16) of a row in instruction s
-// (64 B from each of 16 rows); fragment-packed W (PK): one contiguous KiB per instruction.
+// (64 B from each of 16 rows); block-packed W (PK): one contiguous KiB per instruction.
 // NORM: A is the residual stream and the RMSNorm (x = bf16(bf16(v * rinv[m]) * w[k])) is
 // applied while staging A into LDS, rinv[m] from the producer's sum-of-squares parts.
 constexpr int kKC = 256;           // k per LDS chunk
 constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows shift one 16-B slot)
 
-template <int MT, int MODE, bool PK, bool NORM>
+template <int MT, int MODE, bool PK, bool NORM, bool NT>
 __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kAStride];
   __shared__ float rinv_s[64];
+#if PK_LAB_LDS_PAD
+  __shared__ char lab_pad[PK_LAB_LDS_PAD];  // timing only: force one workgroup per CU
+  if (args.M < 0) lab_pad[threadIdx.x] = 1;
+#endif
   __shared__ int last_s;
   const int N = args.N, K = args.K, S = args.S;
   int M = args.M;  // rows of this workgroup's group (all rows when not grouped)
@@ -249,8 +281,8 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   const bf16_t* wp[kR];
 #pragma unroll
   for (int t = 0; t < kR; ++t)
-    wp[t] = PK ? Wg + (static_cast<int64_t>((n0 >> 4) + t) * (K >> 5)) * 512 + 8 * lane  // fragment-packed
-               : Wg + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                 // row-major [N, K]
+    wp[t] = PK ? Wg + static_cast<int64_t>(nb) * 128 * K + (w * kR + t) * 4 * 512 + 8 * lane  // block-packed
+               : Wg + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                     // row-major [N, K]
 
   // A staging: MT*16 rows x 256 cols = MT*512 16-byte pieces over 256 threads
   constexpr int kPieces = (16 * MT * kKC / 8 + 255) / 256;
@@ -302,9 +334,17 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     for (int t = 0; t < kR; ++t)
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        dst[t][s] = PK ? ld8(wp[t] + static_cast<int64_t>((k >> 5) + s) * 512) : ld8(wp[t] + k + 32 * s);
+        dst[t][s] = PK ? ldw<NT>(wp[t] + static_cast<int64_t>(k >> 7) * (32 * 512) + s * 512)
+                       : ldw<NT>(wp[t] + k + 32 * s);
   };
   auto mma_step = [&](const bf16x8_t (&wf)[kR][4], int buf, int kk) {
+    if constexpr (PK_LAB_NO_MFMA) {  // timing only: consume W with one VALU op per register
+#pragma unroll
+      for (int t = 0; t < kR; ++t)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[t][s & (MT - 1)][0] += __builtin_bit_cast(f32x4, wf[t][s])[0];
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       bf16x8_t af[MT];
@@ -326,6 +366,34 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   const int nchunks = kper / kKC;
   const int rot = (nb * 5) % nchunks;
   auto ck = [&](int c) { return k0 + ((min(c, nchunks - 1) + rot) % nchunks) * kKC; };
+  if constexpr (PK_W_DEPTH > 2) {
+    // W register ring PK_W_DEPTH k-steps deep (step j = half j&1 of chunk j>>1)
+    constexpr int WD = PK_W_DEPTH;
+    bf16x8_t wr[WD][kR][4];
+    const int nsteps = 2 * nchunks;
+    auto ks = [&](int j) { return ck(j >> 1) + (j & 1) * 128; };
+    load_a(ck(0));
+#pragma unroll
+    for (int u = 0; u < WD; ++u) load_w(wr[u], ks(u));
+    store_a(0);
+    int buf = 0;
+    for (int j0 = 0; j0 < nsteps; j0 += WD) {
+#pragma unroll
+      for (int u = 0; u < WD; ++u) {
+        const int j = j0 + u;
+        if ((u & 1) == 0) {
+          load_a(ck((j >> 1) + 1));
+          __syncthreads();
+        }
+        if (j < nsteps) mma_step(wr[u], buf, (u & 1) * 128);
+        load_w(wr[u], ks(j + WD));
+        if (u & 1) {
+          store_a(buf ^ 1);
+          buf ^= 1;
+        }
+      }
+    }
+  } else {
   load_a(ck(0));
   load_w(wa, ck(0));
   load_w(wb, ck(0) + 128);
@@ -333,6 +401,14 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   int buf = 0;
   for (int c = 0; c < nchunks; ++c) {
     const int kn = ck(c + 1);
+    if constexpr (PK_LAB_NO_ASTAGE) {
+      if (c == 0) __syncthreads();
+      mma_step(wa, 0, 0);
+      load_w(wa, kn);
+      mma_step(wb, 0, 128);
+      load_w(wb, kn + 128);
+      continue;
+    }
     load_a(kn);
     __syncthreads();  // chunk c visible in a_lds[buf]; every wave is done with a_lds[buf^1]
     mma_step(wa, buf, 0);
@@ -341,6 +417,7 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     load_w(wb, kn + 128);
     store_a(buf ^ 1);
     buf ^= 1;
+  }
   }
 
   // C^T tile: rows = W rows (n), cols = m:  acc[t][mt][i] = C[m = 16*mt + r][n = n0 + 16*t + 4*g + i]
@@ -646,22 +723,26 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
   }
 }
 
-template <int MODE, bool PK, bool NORM>
+template <int MODE, bool PK, bool NORM, bool NT>
 int launch(const GemmArgs& a, hipStream_t stream) {
   const dim3 grid((a.N / 128) * a.S, a.row_offsets != nullptr ? a.groups : 1);
   switch ((min(a.M, a.max_group_rows > 0 ? a.max_group_rows : a.M) + 15) / 16) {
-    case 1: skinny_gemm_kernel<1, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
-    case 2: skinny_gemm_kernel<2, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
-    case 3: skinny_gemm_kernel<3, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
-    case 4: skinny_gemm_kernel<4, MODE, PK, NORM><<<grid, 256, 0, stream>>>(a); break;
+    case 1: skinny_gemm_kernel<1, MODE, PK, NORM, NT><<<grid, 256, 0, stream>>>(a); break;
+    case 2: skinny_gemm_kernel<2, MODE, PK, NORM, NT><<<grid, 256, 0, stream>>>(a); break;
+    case 3: skinny_gemm_kernel<3, MODE, PK, NORM, NT><<<grid, 256, 0, stream>>>(a); break;
+    case 4: skinny_gemm_kernel<4, MODE, PK, NORM, NT><<<grid, 256, 0, stream>>>(a); break;
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
 }
 
+// non-temporal weight loads are instantiated only for the large single-pass streams
+// (bf16 out: LM head; SiLU: gate_up / MoE w13) on the packed layout
 template <int MODE, bool NORM>
-int launch_pk(const GemmArgs& a, bool packed, hipStream_t stream) {
-  return packed ? launch<MODE, true, NORM>(a, stream) : launch<MODE, false, NORM>(a, stream);
+int launch_pk(const GemmArgs& a, bool packed, bool nt, hipStream_t stream) {
+  if constexpr ((MODE == kBF16 || MODE == kSiluMul) && !NORM)
+    if (packed && nt) return launch<MODE, true, NORM, true>(a, stream);
+  return packed ? launch<MODE, true, NORM, false>(a, stream) : launch<MODE, false, NORM, false>(a, stream);
 }
 
 int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
@@ -671,25 +752,26 @@ int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
                   (mode & 32)))
     return -1;
   if ((!grouped && a.M > 64) || a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;
-  const bool packed = (mode & 16) != 0;  // bit 4: W in fragment-packed layout
+  const bool packed = (mode & 16) != 0;  // bit 4: W in block-packed layout
   const bool norm = (mode & 32) != 0;    // bit 5: RMSNorm prologue on A
+  const bool nt = (mode & 64) != 0;      // bit 6: non-temporal weight loads (hint)
   if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr || a.M > 64)) return -1;
   switch (mode & 7) {
     case kBF16:
       if (a.S != 1 || norm) return -1;
-      return launch_pk<kBF16, false>(a, packed, stream);
+      return launch_pk<kBF16, false>(a, packed, nt, stream);
     case kPartial:
       if (norm) return -1;
-      return launch_pk<kPartial, false>(a, packed, stream);
+      return launch_pk<kPartial, false>(a, packed, nt, stream);
     case kSiluMul:
       if (a.S != 1) return -1;
-      return norm ? launch_pk<kSiluMul, true>(a, packed, stream) : launch_pk<kSiluMul, false>(a, packed, stream);
+      return norm ? launch_pk<kSiluMul, true>(a, packed, nt, stream) : launch_pk<kSiluMul, false>(a, packed, nt, stream);
     case kAddResNorm:
       if (norm || a.counters == nullptr || a.residual == nullptr || a.sumsq_parts == nullptr) return -1;
-      return launch_pk<kAddResNorm, false>(a, packed, stream);
+      return launch_pk<kAddResNorm, false>(a, packed, nt, stream);
     case kQkvRope:
       if (a.counters == nullptr || a.N != (a.nq + 2 * a.nkv) * 128 || a.bs <= 0) return -1;
-      return norm ? launch_pk<kQkvRope, true>(a, packed, stream) : launch_pk<kQkvRope, false>(a, packed, stream);
+      return norm ? launch_pk<kQkvRope, true>(a, packed, nt, stream) : launch_pk<kQkvRope, false>(a, packed, nt, stream);
     default: return -1;
   }
 }
@@ -697,7 +779,7 @@ int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
 }  // namespace
 
 // mode 0: out bf16 [M, ldo] (S must be 1); 1: partial fp32 [S, M, N]; 2: SiLU-mul of interleaved
-// gate/up rows -> out bf16 [M, N/2] (S must be 1); bit 4: fragment-packed W.
+// gate/up rows -> out bf16 [M, N/2] (S must be 1); bit 4: block-packed W; bit 6: non-temporal W.
 // Requires M <= 64, N % 128 == 0, K % (256 S) == 0.
 PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void* W, int M, int N, int K, int lda,
                              int ldo, int S, int mode, hipStream_t stream) {
@@ -711,7 +793,7 @@ PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void
   return dispatch(a, mode, stream);
 }
 
-// Full-featured entry: modes 0-4 (see Mode), bit 4 packed W, bit 5 RMSNorm prologue.
+// Full-featured entry: modes 0-4 (see Mode), bit 4 packed W, bit 5 RMSNorm prologue, bit 6 NT W.
 PK_EXPORT int pk_skinny_gemm_ex(const GemmArgs* args, int mode, hipStream_t stream) {
   return dispatch(*args, mode, stream);
 }

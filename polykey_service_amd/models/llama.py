@@ -48,7 +48,7 @@ def _p(t: torch.Tensor) -> nn.Parameter:
 def _proj(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor],
           wp: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Column-parallel projection → bf16 (skinny split-K + reduce for decode-sized M).
-    ``wp``: the fragment-packed copy of ``w`` streamed by the decode GEMM (None: row-major)."""
+    ``wp``: the block-packed copy of ``w`` streamed by the decode GEMM (None: row-major)."""
     if ws is not None and gemm.skinny_ok(x, w):
         S = gemm.choose_split(w.shape[0], x.shape[1], x.shape[0])
         if S > 1 and ws.numel() >= S * x.shape[0] * w.shape[0]:
@@ -88,7 +88,7 @@ class LlamaAttention(nn.Module):
         self.scale = 1.0 / math.sqrt(self.hd)
         self.qkv = None
         self.o = None
-        self.qkv_p = None  # fragment-packed decode copies (LlamaForCausalLM.pack_decode_weights)
+        self.qkv_p = None  # block-packed decode copies (LlamaForCausalLM.pack_decode_weights)
         self.o_p = None
 
     def forward(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
@@ -159,6 +159,7 @@ class LlamaForCausalLM(nn.Module):
         self.embed = None
         self.norm = None
         self.lm_head = None
+        self.lm_head_p = None  # block-packed decode copy (pack_decode_weights)
         self.register_buffer("cos_sin", reference.rope_cos_sin_cache(cfg.max_position, cfg.head_dim, cfg.rope_theta,
                                                                       cfg.rope_scaling, device=self.device),
                              persistent=False)
@@ -389,23 +390,27 @@ class LlamaForCausalLM(nn.Module):
         return (mlp.gate_up, mlp.down)
 
     def pack_decode_weights(self, mode: Optional[str] = None) -> bool:
-        """Give every dense projection a fragment-packed copy (:func:`gemm.pack_weight`) for the
-        decode GEMM, which streams it ~1.2-1.35x faster than row-major (tools/bench_gemm.py).
-        Prefill keeps using the row-major weight through hipBLASLt, so this doubles projection
-        memory: ``auto`` packs only when both copies fit in 75 % of HBM (8B: +15 GB of 288 GB;
-        Mixtral-8x7B: +90 GB; 70B on one GPU: skipped).  ``POLYKEY_PACKED_WEIGHTS`` = auto | 1 | 0."""
+        """Give every dense projection and the LM head a block-packed copy
+        (:func:`gemm.pack_weight`) for the decode GEMM, which streams it faster than row-major
+        (tools/bench_gemm.py, tools/gemm_lab.hip).  Prefill keeps using the row-major weight
+        through hipBLASLt, so this doubles projection memory: ``auto`` packs only when both
+        copies fit in 75 % of HBM (8B: +16 GB of 288 GB; Mixtral-8x7B: +90 GB; 70B on one GPU:
+        skipped).  ``POLYKEY_PACKED_WEIGHTS`` = auto | 1 | 0."""
         mode = mode or os.environ.get("POLYKEY_PACKED_WEIGHTS", "auto")
         if mode == "0" or self.device.type != "cuda" or not gemm.SKINNY_ENABLED:
             return False
+        head_bytes = self.lm_head.numel() * self.lm_head.element_size()
         if mode == "auto":
             total = torch.cuda.get_device_properties(self.device).total_memory
             proj = sum(w.numel() * w.element_size() for w in self.layers.parameters())
-            if 2 * proj + self.lm_head.numel() * self.lm_head.element_size() > 0.75 * total:
+            if 2 * proj + 2 * head_bytes > 0.75 * total:
                 return False
         for layer in self.layers:
             layer.attn.qkv_p = gemm.pack_weight(layer.attn.qkv)
             layer.attn.o_p = gemm.pack_weight(layer.attn.o)
             self._pack_mlp(layer.mlp)
+        if self.lm_head.shape[0] % 128 == 0 and self.lm_head.shape[1] % 256 == 0:
+            self.lm_head_p = gemm.pack_weight(self.lm_head)
         return True
 
     def _pack_mlp(self, mlp) -> None:
@@ -414,8 +419,13 @@ class LlamaForCausalLM(nn.Module):
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """hidden [B, H] → logits [B, vocab] (bf16; all-gathered across TP)."""
-        # hipBLASLt streams the 1 GB vocab projection faster than the skinny kernel (bench_gemm.py)
-        logits = F.linear(hidden, self.lm_head)
+        # decode: the skinny kernel streams the block-packed vocab projection with non-temporal
+        # loads (1 GB for Llama-3: 179 us vs hipBLASLt's 198-208 us, tools/gemm_lab.hip)
+        wp = getattr(self, "lm_head_p", None)
+        if wp is not None and gemm.skinny_ok(hidden, self.lm_head):
+            logits = gemm.linear(hidden, self.lm_head, packed=wp)
+        else:
+            logits = F.linear(hidden, self.lm_head)
         logits = comm.tp_all_gather_last(logits)
         if logits.shape[-1] != self.cfg.vocab_size:
             logits = logits[..., :self.cfg.vocab_size]

@@ -35,7 +35,7 @@ class MixtralMoE(nn.Module):
         self.router = None
         self.w13 = None  # [E_local, 2*I_local, H], gate/up rows interleaved by 16
         self.w2 = None   # [E_local, H, I_local]
-        self.w13_p = None  # fragment-packed decode copies (MixtralForCausalLM._pack_mlp)
+        self.w13_p = None  # block-packed decode copies (MixtralForCausalLM._pack_mlp)
         self.w2_p = None
 
     def forward(self, x: torch.Tensor, ws: Optional[torch.Tensor] = None, routing=None):

@@ -89,8 +89,7 @@ def _launch_ex(mode: int, x: torch.Tensor, w: torch.Tensor, packed: Optional[tor
         a.eps = float(norm.eps)
     for k, v in kw.items():
         setattr(a, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
-    if packed is not None:
-        mode |= PACKED_BIT
+    mode |= _wmode(packed)
     native.call("pk_skinny_gemm_ex", ctypes.byref(a), mode, native.stream_ptr())
 
 
@@ -208,23 +207,32 @@ def norm_fusable(H: int) -> bool:
 
 
 def pack_weight(w: torch.Tensor) -> torch.Tensor:
-    """Row-major ``[N, K]`` → fragment-packed layout for the decode GEMM (same size).
+    """Row-major ``[N, K]`` → block-packed layout for the decode GEMM (same size).
 
-    Every (16-row tile, 32-k block) fragment is stored as 1 KiB in MFMA A-operand lane order
-    (lane l = 16*g + r holds row r, k = 8g..8g+7), so each wave load instruction reads 1 KiB
-    contiguous instead of 64 B from each of 16 rows."""
+    For every 128-row n-block (one workgroup) and 128-deep k-step, the 32 KiB the workgroup
+    consumes are contiguous: 8 row tiles x 4 k-blocks of 32, each a 1 KiB MFMA A-fragment in
+    lane order (lane l = 16*g + r holds row r, k = 8g..8g+7).  A wave load instruction reads
+    1 KiB and a workgroup sweeps a single linear stream (tools/gemm_lab.hip)."""
     N, K = w.shape
-    assert N % 16 == 0 and K % 32 == 0
-    return w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+    assert N % 128 == 0 and K % 128 == 0
+    # [nb, tile, r, ks, s, g, e] -> [nb, ks, tile, s, g, r, e]
+    return w.view(N // 128, 8, 16, K // 128, 4, 4, 8).permute(0, 3, 1, 4, 5, 2, 6).contiguous().view(N, K)
 
 
 def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
     N, K = wp.shape
-    return wp.view(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().view(N, K)
+    return wp.view(N // 128, K // 128, 8, 4, 4, 16, 8).permute(0, 2, 5, 1, 3, 4, 6).contiguous().view(N, K)
+
+
+# weights at least this large are streamed with non-temporal loads (gate_up, MoE w13, LM head)
+NT_MIN_BYTES = int(os.environ.get("POLYKEY_NT_MIN_BYTES", str(160 << 20)))
+NT_BIT = 64
 
 
 def _wmode(packed: Optional[torch.Tensor]) -> int:
-    return PACKED_BIT if packed is not None else 0
+    if packed is None:
+        return 0
+    return PACKED_BIT | (NT_BIT if packed.numel() * packed.element_size() >= NT_MIN_BYTES else 0)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,

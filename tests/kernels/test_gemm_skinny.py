@@ -186,3 +186,19 @@ def test_norm_apply():
     nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
     y = gemm.norm_apply(res, _sumsq_parts(res), nw, 1e-5)
     torch.testing.assert_close(y.float(), ref.rms_norm(res, nw, 1e-5).float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 64])
+def test_block_packed_nontemporal(M, monkeypatch):
+    """Block-packed weights above the NT threshold stream with non-temporal loads (mode bit 6):
+    the LM-head-sized bf16 projection and the SiLU gate_up projection."""
+    monkeypatch.setattr(gemm, "NT_MIN_BYTES", 1 << 20)
+    x, w = rnd(M, 4096), rnd(2048, 4096, scale=0.02)
+    assert gemm._wmode(gemm.pack_weight(w)) & gemm.NT_BIT
+    exp = x.float() @ w.float().t()
+    torch.testing.assert_close(gemm.linear(x, w, packed=gemm.pack_weight(w)).float(), exp, atol=2e-2, rtol=2e-2)
+    g, u = rnd(1024, 4096, scale=0.05), rnd(1024, 4096, scale=0.05)
+    wgu = gemm.interleave_gate_up(g, u)
+    ref_gu = ref.silu_and_mul(torch.cat([x.float() @ g.float().t(), x.float() @ u.float().t()], -1).to(torch.bfloat16))
+    y = gemm.linear_silu(x, wgu, None, packed=gemm.pack_weight(wgu))
+    torch.testing.assert_close(y.float(), ref_gu.float(), atol=3e-2, rtol=3e-2)
