@@ -90,11 +90,18 @@ async def run_waves(args, engine, st, leaders_group):
     rng = random.Random(args.seed * 1000 + st.rank)
     tool = f"llm.generate:{args.model}"
 
-    async def one():
+    timing = os.environ.get("POLYKEY_BENCH_TIMING") == "1"
+    marks = []
+
+    def build():
         req = proto.ExecuteToolRequest(tool_name=tool)
         req.parameters.update({"prompt_token_ids": [rng.randrange(0, V) for _ in range(args.prompt_len)],
                                "max_tokens": args.max_tokens, "ignore_eos": True, "temperature": 0.0,
                                "return": "struct"})
+        return req
+
+    async def one(req):
+        t_build = time.perf_counter()
         t0 = time.perf_counter()
         if args.mode == "unary":
             resp = await unary(req, timeout=600)
@@ -102,16 +109,38 @@ async def run_waves(args, engine, st, leaders_group):
             resp = None
             async for resp in stream(req, timeout=600):
                 pass
-        dt = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        dt = t1 - t0
         usage = resp.struct_output.fields["usage"].struct_value.fields
+        if timing:
+            m = proto.struct_to_dict(resp.struct_output)["metrics"]
+            marks.append((t_build, t0, t1, m))
         return int(usage["completion_tokens"].number_value), dt
 
-    async def wave():
-        res = await asyncio.gather(*[one() for _ in range(args.concurrency)])
+    async def wave(reqs):
+        marks.clear()
+        tw = time.perf_counter()
+        res = await asyncio.gather(*[one(r) for r in reqs])
+        if timing and marks:
+            # host-side breakdown of the wave (stderr): request build/submit span, the engine's
+            # view (queue, TTFT, e2e) and what the RPC path adds on top of it
+            te = time.perf_counter()
+            sub = max(m[1] for m in marks) - tw
+            rpc = sorted((m[2] - m[1]) - m[3]["server_e2e_s"] for m in marks)
+            ttft = sorted(m[3].get("ttft_s", 0.0) for m in marks)
+            e2e = sorted(m[3].get("e2e_s", 0.0) for m in marks)
+            print(f"[wave] wall {1e3 * (te - tw):.1f} ms | last submit +{1e3 * sub:.1f} ms | engine e2e "
+                  f"min/max {1e3 * e2e[0]:.1f}/{1e3 * e2e[-1]:.1f} ms | ttft min/max {1e3 * ttft[0]:.1f}/"
+                  f"{1e3 * ttft[-1]:.1f} ms | rpc overhead p50/max {1e3 * rpc[len(rpc) // 2]:.2f}/{1e3 * rpc[-1]:.2f} ms | "
+                  f"last response +{1e3 * (max(m[2] for m in marks) - tw):.1f} ms", file=sys.stderr, flush=True)
         return sum(r[0] for r in res), [r[1] for r in res]
 
     for _ in range(args.warmup):
-        await wave()
+        await wave([build() for _ in range(args.concurrency)])
+    # the load generator prepares its synthetic requests up front, as a separate client
+    # process would: building 64 x 256 random ids inside a wave would only steal the event
+    # loop (and the GIL) from the server under test
+    waves = [[build() for _ in range(args.concurrency)] for _ in range(args.steps)]
     dev = engine.device
     if dist.is_initialized():
         dist.barrier(group=leaders_group)
@@ -119,8 +148,8 @@ async def run_waves(args, engine, st, leaders_group):
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     tokens, lats = 0, []
-    for _ in range(args.steps):
-        n, l = await wave()
+    for reqs in waves:
+        n, l = await wave(reqs)
         tokens += n
         lats += l
     if dev.type == "cuda":

@@ -11,8 +11,9 @@ health to NOT_SERVING).
 from __future__ import annotations
 
 import asyncio
-import os
 import collections
+import os
+import sys
 import threading
 import time
 import traceback
@@ -46,6 +47,10 @@ class AsyncLLM:
         self.last_step_time = time.monotonic()
         self.watchdog_s = watchdog_s
         self.stats = {"steps": 0, "requests": 0, "output_tokens": 0, "step_time_s": 0.0}
+        # The engine thread and the asyncio (gRPC) thread share the GIL.  CPython's default 5 ms
+        # switch interval lets a burst of RPC handling hold the engine thread off for whole
+        # decode steps (the GPU idles meanwhile); a short interval hands the GIL over promptly.
+        sys.setswitchinterval(float(os.environ.get("POLYKEY_GIL_SWITCH_S", "0.002")))
         self._thread = threading.Thread(target=self._run, name="polykey-engine", daemon=True)
         self._thread.start()
 
