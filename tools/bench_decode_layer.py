@@ -27,7 +27,8 @@ for ctx in (128, 384, 1024):
     cs = ref.rope_cos_sin_cache(8192, D, 500000.0).cuda()
     po, pml = A.decode_workspace(B, NQ, maxb, BS, "cuda")
     md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0, slot_mapping=slots,
-                        decode_block_tables=bt, decode_context_lens=cl, decode_part_o=po, decode_part_ml=pml)
+                        decode_block_tables=bt, decode_context_lens=cl, decode_part_o=po, decode_part_ml=pml,
+                        decode_max_ctx=512 if ctx + 1 <= 512 else 0)  # short-context graphs
 
     def unfused(i):
         kc, vc = layers[i % 4]
@@ -49,6 +50,7 @@ for ctx in (128, 384, 1024):
             fn(i)
         e1.record()
         torch.cuda.synchronize()
-        row += f" | {name} {e0.elapsed_time(e1) / 40 * 1000:7.1f} us"
+        us = e0.elapsed_time(e1) / 40 * 1000
+        row += f" | {name} {us:7.1f} us {B * ctx * NKV * D * 4 / us / 1e6:5.2f} TB/s"
     print(row, flush=True)
     del layers
