@@ -51,6 +51,8 @@ struct GemmArgs {
   int max_group_rows;        // bound on any group's rows (<= 64): picks the M-tile count
   const int* a_rows;         // grouped: A row of group row i = a_rows[i] / a_row_div (MoE permute folded
   int a_row_div;             //   into the A staging: a_rows = expert-sorted slots, a_row_div = top-k)
+  int row_scale;             // output row m scaled by rinv[m] from nrm_parts (RMSNorm folded: A is the
+                             //   residual stream, the norm weight is pre-multiplied into W's columns)
 };
 
 namespace {
@@ -241,7 +243,7 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
 constexpr int kKC = 256;           // k per LDS chunk
 constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows shift one 16-B slot)
 
-template <int MT, int MODE, bool PK, bool NORM, bool NT>
+template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false>
 __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args) {
   __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kAStride];
   __shared__ float rinv_s[64];
@@ -276,6 +278,15 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
       rinv_s[tid] = rsqrtf(ss / K + args.eps);
     }
     __syncthreads();
+  }
+  // RS (row scale): the sum-of-squares parts of row `tid` are requested before the weight
+  // stream starts and consumed only after the main loop, so they never delay it (unconditional
+  // loads from clamped addresses: a load behind a branch would make hipcc drain vmcnt)
+  float rs_p[RS ? 8 : 1];
+  if constexpr (RS) {
+    const int np = min(args.nrm_nparts, 8), rr = min(tid, M - 1);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rs_p[q] = args.nrm_parts[min(q, np - 1) * M + rr];
   }
 
   const bf16_t* wp[kR];
@@ -420,12 +431,28 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   }
   }
 
+  if constexpr (RS) {
+    if (tid < M) {
+      const int np = min(args.nrm_nparts, 8);
+      float ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss += q < np ? rs_p[q] : 0.f;
+      rinv_s[tid] = rsqrtf(ss / K + args.eps);
+    }
+    __syncthreads();
+  }
+
   // C^T tile: rows = W rows (n), cols = m:  acc[t][mt][i] = C[m = 16*mt + r][n = n0 + 16*t + 4*g + i]
   constexpr bool kSlab = MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = 16 * mt + r;
     if (m >= M) continue;
+    if constexpr (RS) {  // folded RMSNorm: x W^T = rinv[m] * (residual (W diag(w))^T)
+      const float sc = rinv_s[m];
+#pragma unroll
+      for (int t = 0; t < kR; ++t) acc[t][mt] *= sc;
+    }
     if constexpr (kSlab) {
       float* p = args.partial + (static_cast<int64_t>(split) * args.M + row0 + m) * N + n0 + 4 * g;
 #pragma unroll
@@ -536,6 +563,39 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
     o.y = pack2(y[2], y[3]);
     *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * ldo + b * 16 + j) = o;
   }
+}
+
+// Residual update of the folded-RMSNorm decode chain: residual[m] += bf16(sum_s partial[s, m])
+// (partial == null: residual unchanged) and parts[blk, m] = sum of squares of the new residual
+// over columns [1024 blk, 1024 blk + 1024).  The consumer GEMM turns the parts into rinv[m]
+// (GemmArgs::row_scale) and streams the RMSNorm weight pre-multiplied into its W, so no
+// normalised copy of the residual is ever written.  grid (H / 1024, M): 4 x the workgroups of
+// the per-row norm kernel, each with one round trip of slab loads in flight.
+template <int SS>
+__global__ void __launch_bounds__(256) residual_parts_kernel(bf16_t* __restrict__ residual,
+                                                             const float* __restrict__ partial, int S, int M, int H,
+                                                             float* __restrict__ parts) {
+  __shared__ float red[16];
+  const int blk = blockIdx.x, m = blockIdx.y;
+  const int c = blk * 1024 + threadIdx.x * 4;
+  bf16_t* res = residual + static_cast<int64_t>(m) * H + c;
+  const uint2 rr = *reinterpret_cast<const uint2*>(res);
+  float v[4] = {bf2f(static_cast<bf16_t>(rr.x & 0xffff)), bf2f(static_cast<bf16_t>(rr.x >> 16)),
+                bf2f(static_cast<bf16_t>(rr.y & 0xffff)), bf2f(static_cast<bf16_t>(rr.y >> 16))};
+  if (partial != nullptr) {
+    // the projection output is rounded to bf16 first (as the unfused GEMM would store it)
+    const float4 a = slab_sum<SS>(partial + static_cast<int64_t>(m) * H + c, static_cast<int64_t>(M) * H, S);
+    v[0] = rbf(rbf(a.x) + v[0]);
+    v[1] = rbf(rbf(a.y) + v[1]);
+    v[2] = rbf(rbf(a.z) + v[2]);
+    v[3] = rbf(rbf(a.w) + v[3]);
+    uint2 o;
+    o.x = pack2(v[0], v[1]);
+    o.y = pack2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(res) = o;
+  }
+  const float ss = block_sum(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3], red);
+  if (threadIdx.x == 0) parts[static_cast<int64_t>(blk) * M + m] = ss;
 }
 
 // residual = bf16(residual + bf16(sum_s partial[s])); x = rmsnorm(residual) * w.
@@ -723,14 +783,14 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
   }
 }
 
-template <int MODE, bool PK, bool NORM, bool NT>
+template <int MODE, bool PK, bool NORM, bool NT, bool RS = false>
 int launch(const GemmArgs& a, hipStream_t stream) {
   const dim3 grid((a.N / 128) * a.S, a.row_offsets != nullptr ? a.groups : 1);
   switch ((min(a.M, a.max_group_rows > 0 ? a.max_group_rows : a.M) + 15) / 16) {
-    case 1: skinny_gemm_kernel<1, MODE, PK, NORM, NT><<<grid, 256, 0, stream>>>(a); break;
-    case 2: skinny_gemm_kernel<2, MODE, PK, NORM, NT><<<grid, 256, 0, stream>>>(a); break;
-    case 3: skinny_gemm_kernel<3, MODE, PK, NORM, NT><<<grid, 256, 0, stream>>>(a); break;
-    case 4: skinny_gemm_kernel<4, MODE, PK, NORM, NT><<<grid, 256, 0, stream>>>(a); break;
+    case 1: skinny_gemm_kernel<1, MODE, PK, NORM, NT, RS><<<grid, 256, 0, stream>>>(a); break;
+    case 2: skinny_gemm_kernel<2, MODE, PK, NORM, NT, RS><<<grid, 256, 0, stream>>>(a); break;
+    case 3: skinny_gemm_kernel<3, MODE, PK, NORM, NT, RS><<<grid, 256, 0, stream>>>(a); break;
+    case 4: skinny_gemm_kernel<4, MODE, PK, NORM, NT, RS><<<grid, 256, 0, stream>>>(a); break;
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
@@ -740,6 +800,16 @@ int launch(const GemmArgs& a, hipStream_t stream) {
 // (bf16 out: LM head; SiLU: gate_up / MoE w13) on the packed layout
 template <int MODE, bool NORM>
 int launch_pk(const GemmArgs& a, bool packed, bool nt, hipStream_t stream) {
+  // the folded-norm row scale is instantiated for the packed decode projections that take it
+  // (QKV split-K slabs, gate_up SiLU)
+  if constexpr ((MODE == kPartial || MODE == kSiluMul) && !NORM)
+    if (a.row_scale) {
+      if (!packed) return -1;
+      if constexpr (MODE == kSiluMul)
+        if (nt) return launch<MODE, true, NORM, true, true>(a, stream);
+      return launch<MODE, true, NORM, false, true>(a, stream);
+    }
+  if (a.row_scale) return -1;
   if constexpr ((MODE == kBF16 || MODE == kSiluMul) && !NORM)
     if (packed && nt) return launch<MODE, true, NORM, true>(a, stream);
   return packed ? launch<MODE, true, NORM, false>(a, stream) : launch<MODE, false, NORM, false>(a, stream);
@@ -756,6 +826,7 @@ int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
   const bool norm = (mode & 32) != 0;    // bit 5: RMSNorm prologue on A
   const bool nt = (mode & 64) != 0;      // bit 6: non-temporal weight loads (hint)
   if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr || a.M > 64)) return -1;
+  if (a.row_scale && (grouped || norm || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.M > 64)) return -1;
   switch (mode & 7) {
     case kBF16:
       if (a.S != 1 || norm) return -1;
@@ -867,6 +938,23 @@ static int add_rmsnorm_launch(void* x, void* residual, const void* partial, cons
     case 1: go_s(std::integral_constant<int, 1>{}); break;
     case 2: go_s(std::integral_constant<int, 2>{}); break;
     default: return -1;
+  }
+  return PK_CHECK_LAUNCH();
+}
+
+// residual [M, H] += sum of the S fp32 slabs [S, M, H] (partial may be null), parts [H/1024, M].
+PK_EXPORT int pk_residual_parts(void* residual, const void* partial, int S, int M, int H, void* parts,
+                                hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (H % 1024 || (partial != nullptr && S < 1)) return -1;
+  const dim3 grid(H / 1024, M);
+  auto rs = static_cast<bf16_t*>(residual);
+  auto ps = static_cast<const float*>(partial);
+  auto qs = static_cast<float*>(parts);
+  switch (partial == nullptr ? 0 : S) {
+    case 4: residual_parts_kernel<4><<<grid, 256, 0, stream>>>(rs, ps, S, M, H, qs); break;
+    case 8: residual_parts_kernel<8><<<grid, 256, 0, stream>>>(rs, ps, S, M, H, qs); break;
+    default: residual_parts_kernel<0><<<grid, 256, 0, stream>>>(rs, ps, S, M, H, qs); break;
   }
   return PK_CHECK_LAUNCH();
 }

@@ -39,6 +39,11 @@ from .weights import SafetensorsIndex, random_full, shard_cols, shard_rows
 # decode attention consumes the QKV split-K slabs directly (POLYKEY_FUSED_QKV_ATTN=0: separate
 # reduce + RoPE + cache-write kernel, then attention)
 FUSED_QKV_ATTENTION = os.environ.get("POLYKEY_FUSED_QKV_ATTN", "1") == "1"
+# Decode (TP = 1, dense, block-packed weights): every RMSNorm weight is folded into the columns of
+# the projection that consumes it and that projection scales its output rows by rinv, so the
+# per-layer norm kernels shrink to residual updates (4x wider grid, no normalised copy written).
+# POLYKEY_FOLD_NORM=0: normalised activations as in prefill.
+FOLD_NORM = os.environ.get("POLYKEY_FOLD_NORM", "1") == "1"
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:
@@ -90,6 +95,7 @@ class LlamaAttention(nn.Module):
         self.o = None
         self.qkv_p = None  # block-packed decode copies (LlamaForCausalLM.pack_decode_weights)
         self.o_p = None
+        self.qkv_pf = None  # block-packed with ln1 folded in (FOLD_NORM)
 
     def forward(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
                 kv: Tuple[torch.Tensor, torch.Tensor], ws: Optional[torch.Tensor] = None):
@@ -125,6 +131,7 @@ class LlamaMLP(nn.Module):
         self.down = None
         self.gate_up_p = None
         self.down_p = None
+        self.gate_up_pf = None  # block-packed with ln2 folded in (FOLD_NORM)
 
     def forward(self, x: torch.Tensor, ws: Optional[torch.Tensor] = None):
         h = gemm.linear_silu(x, self.gate_up, ws, packed=self.gate_up_p)  # gate/up rows interleaved by 16
@@ -291,6 +298,8 @@ class LlamaForCausalLM(nn.Module):
         ws = self.workspace(x.shape[0])
         if ws is not None and self._fused_decode_ok(x):
             return self._forward_fused(x, positions, md, kv_caches, ws)
+        if ws is not None and self._rowscale_ok(x):
+            return self._forward_rowscale(x, positions, md, kv_caches, ws)
         residual = None
         for i, layer in enumerate(self.layers):
             if residual is None:
@@ -369,6 +378,49 @@ class LlamaForCausalLM(nn.Module):
             gemm.linear_add_residual(h, mlp.down, ws, ctr, residual, parts_mlp, packed=mlp.down_p)
         return gemm.norm_apply(residual, parts_mlp, self.norm, self.cfg.rms_eps)
 
+    # ------------------------------------------------------------------ folded-norm decode chain
+    def _rowscale_ok(self, x: torch.Tensor) -> bool:
+        l0 = self.layers[0]
+        return (self.st.tp_size == 1 and l0.attn.qkv_pf is not None and getattr(l0.mlp, "gate_up_pf", None) is not None
+                and self.cfg.hidden_size % 1024 == 0 and gemm.norm_fusable(self.cfg.hidden_size)
+                and gemm.skinny_ok(x, l0.attn.qkv))
+
+    def _forward_rowscale(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata,
+                          kv_caches: List[Tuple[torch.Tensor, torch.Tensor]], ws: torch.Tensor) -> torch.Tensor:
+        """Decode step with the RMSNorms folded into the projections (FOLD_NORM):
+
+            qkv  = rinv1 * (residual @ (Wqkv diag ln1)^T)   split-K slabs -> attention (RoPE, cache)
+            residual += o-proj(attn)                        + per-row sums of squares (parts)
+            h    = silu / mul of rinv2 * (residual @ (Wgu diag ln2)^T)
+            residual += down(h)                             + parts for the next layer's rinv1
+
+        rinv = rsqrt(mean(residual^2) + eps) is formed by each consumer from the parts."""
+        T, H = x.shape
+        if getattr(self, "_parts_buf", None) is None:
+            self._parts_buf = torch.zeros((H // 1024) * gemm.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
+        buf = self._parts_buf
+        residual = x
+        parts = gemm.residual_parts(None, residual, buf)
+        last = len(self.layers) - 1
+        for i, layer in enumerate(self.layers):
+            at, mlp = layer.attn, layer.mlp
+            kc, vc = kv_caches[i]
+            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf)
+            if md.num_prefill == 0 and FUSED_QKV_ATTENTION:
+                a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
+            else:
+                q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
+                a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
+            parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p), residual, buf)
+            h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf,
+                                 rowscale=gemm.RowScale(parts, layer.eps))
+            d = gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p)
+            if i < last:
+                parts = gemm.residual_parts(d, residual, buf)
+            else:
+                x, _ = gemm.partial_add_rms_norm(d, residual, self.norm, self.cfg.rms_eps)
+        return x
+
     def workspace(self, M: int) -> Optional[torch.Tensor]:
         """fp32 split-K slab buffer for decode-sized batches (fixed address: graph-safe)."""
         if self.device.type != "cuda" or M > gemm.SKINNY_MAX_M:
@@ -405,10 +457,16 @@ class LlamaForCausalLM(nn.Module):
             proj = sum(w.numel() * w.element_size() for w in self.layers.parameters())
             if 2 * proj + 2 * head_bytes > 0.75 * total:
                 return False
+        fold = FOLD_NORM and self.st.tp_size == 1 and isinstance(self.layers[0].mlp, LlamaMLP)
         for layer in self.layers:
-            layer.attn.qkv_p = gemm.pack_weight(layer.attn.qkv)
+            if fold:
+                layer.attn.qkv_pf = gemm.pack_weight(gemm.fold_norm(layer.attn.qkv, layer.ln1))
+                layer.mlp.gate_up_pf = gemm.pack_weight(gemm.fold_norm(layer.mlp.gate_up, layer.ln2))
+                layer.mlp.down_p = gemm.pack_weight(layer.mlp.down)
+            else:
+                layer.attn.qkv_p = gemm.pack_weight(layer.attn.qkv)
+                self._pack_mlp(layer.mlp)
             layer.attn.o_p = gemm.pack_weight(layer.attn.o)
-            self._pack_mlp(layer.mlp)
         if self.lm_head.shape[0] % 128 == 0 and self.lm_head.shape[1] % 256 == 0:
             self.lm_head_p = gemm.pack_weight(self.lm_head)
         return True

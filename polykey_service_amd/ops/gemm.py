@@ -46,10 +46,18 @@ class GemmArgs(ctypes.Structure):
                 ("v_cache", ctypes.c_void_p), ("slots", ctypes.c_void_p), ("nq", ctypes.c_int),
                 ("nkv", ctypes.c_int), ("bs", ctypes.c_int), ("row_offsets", ctypes.c_void_p),
                 ("w_stride", ctypes.c_longlong), ("groups", ctypes.c_int), ("max_group_rows", ctypes.c_int),
-                ("a_rows", ctypes.c_void_p), ("a_row_div", ctypes.c_int)]
+                ("a_rows", ctypes.c_void_p), ("a_row_div", ctypes.c_int), ("row_scale", ctypes.c_int)]
 
 
 _ARGS_CHECKED = False
+
+
+class RowScale(NamedTuple):
+    """Folded RMSNorm: A is the residual stream, W's columns carry the norm weight
+    (:func:`fold_norm`), and output row m is scaled by rinv[m] = rsqrt(sum(parts[:, m]) / K + eps)
+    with ``parts`` [nparts, M] from :func:`residual_parts`."""
+    parts: torch.Tensor
+    eps: float
 
 
 class NormIn(NamedTuple):
@@ -62,7 +70,8 @@ class NormIn(NamedTuple):
 
 def _launch_ex(mode: int, x: torch.Tensor, w: torch.Tensor, packed: Optional[torch.Tensor], S: int,
                out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
-               counters: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None, **kw) -> None:
+               counters: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None,
+               rowscale: Optional[RowScale] = None, **kw) -> None:
     global _ARGS_CHECKED
     if not _ARGS_CHECKED:
         n = native.lib().pk_gemm_args_size()
@@ -87,6 +96,11 @@ def _launch_ex(mode: int, x: torch.Tensor, w: torch.Tensor, packed: Optional[tor
         a.nrm_nparts = norm.parts.shape[0]
         a.nrm_w = norm.weight.data_ptr()
         a.eps = float(norm.eps)
+    if rowscale is not None:
+        a.row_scale = 1
+        a.nrm_parts = rowscale.parts.data_ptr()
+        a.nrm_nparts = rowscale.parts.shape[0]
+        a.eps = float(rowscale.eps)
     for k, v in kw.items():
         setattr(a, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
     mode |= _wmode(packed)
@@ -264,14 +278,16 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
 
 
 def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[torch.Tensor] = None,
-                packed: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None) -> torch.Tensor:
+                packed: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None,
+                rowscale: Optional[RowScale] = None) -> torch.Tensor:
     """silu(x @ Wg^T) * (x @ Wu^T) with interleaved gate/up rows → [M, I].  With ``norm``,
-    ``x`` is the residual stream and the RMSNorm is applied in the kernel's prologue (S = 1)."""
-    if norm is not None:
+    ``x`` is the residual stream and the RMSNorm is applied in the kernel's prologue (S = 1);
+    with ``rowscale`` the norm is folded (W pre-multiplied, rows scaled in the epilogue)."""
+    if norm is not None or rowscale is not None:
         M, K = x.shape
         N = w_gu_interleaved.shape[0]
         out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
-        _launch_ex(MODE_SILU, x, w_gu_interleaved, packed, 1, out=out, norm=norm)
+        _launch_ex(MODE_SILU, x, w_gu_interleaved, packed, 1, out=out, norm=norm, rowscale=rowscale)
         return out
     if not skinny_ok(x, w_gu_interleaved):
         return silu_and_mul_interleaved(linear(x, w_gu_interleaved))
@@ -287,6 +303,38 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         p = linear_partial(x, w_gu_interleaved, ws, S, packed=packed)
         native.call("pk_splitk_reduce", out.data_ptr(), ws.data_ptr(), S, M, N, out.stride(0), 1, native.stream_ptr())
     return out
+
+
+def linear_partial_rowscale(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, rowscale: RowScale,
+                            S: Optional[int] = None, packed: Optional[torch.Tensor] = None) -> Partial:
+    """:func:`linear_partial` of a folded-norm projection: slabs of rinv[m] * (x @ W'^T)."""
+    M, K = x.shape
+    N = w.shape[0]
+    S = S or choose_split(N, K, M)
+    assert ws.numel() >= S * M * N, "split-K workspace too small"
+    _launch_ex(MODE_PARTIAL, x, w, packed, S, ws=ws, rowscale=rowscale)
+    return Partial(ws, S, M, N)
+
+
+def fold_norm(w: torch.Tensor, norm_weight: torch.Tensor) -> torch.Tensor:
+    """W' = W diag(norm_weight): the RMSNorm weight of the projection's input folded into its
+    columns (bf16), for the row-scaled decode GEMM (:class:`RowScale`)."""
+    return (w.float() * norm_weight.float()[None, :]).to(w.dtype)
+
+
+def residual_parts(p: Optional[Partial], residual: torch.Tensor, parts: torch.Tensor) -> torch.Tensor:
+    """residual += sum of ``p``'s slabs (bf16, in place; ``p`` None: unchanged) and
+    parts [H/1024, M] = per-1024-column sums of squares of the new residual rows."""
+    M, H = residual.shape
+    assert parts.numel() >= (H // 1024) * M and residual.is_contiguous()
+    if not residual.is_cuda:
+        if p is not None:
+            residual.copy_((residual.float() + p.view().sum(0).to(torch.bfloat16).float()).to(residual.dtype))
+        parts.view(-1)[: (H // 1024) * M].copy_(residual.float().view(M, H // 1024, 1024).pow(2).sum(-1).t().reshape(-1))
+        return parts.view(-1)[: (H // 1024) * M].view(H // 1024, M)
+    native.call("pk_residual_parts", residual.data_ptr(), 0 if p is None else p.buf.data_ptr(), 0 if p is None else p.S,
+                M, H, parts.data_ptr(), native.stream_ptr())
+    return parts.view(-1)[: (H // 1024) * M].view(H // 1024, M)
 
 
 def reduce_partial(p: Partial, out: Optional[torch.Tensor] = None) -> torch.Tensor:
