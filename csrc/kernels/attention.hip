@@ -449,6 +449,113 @@ __global__ void __launch_bounds__(512) paged_prefill_kernel(
   }
 }
 
+// ------------------------------------------------------- prefill with LDS-shared K/V tiles
+// grid (ceil(max_q_len / (16 QT)), n_seqs, n_kv), block 64 * NW with NW = QT * G (G = n_q / n_kv
+// <= 8): one workgroup per (16 QT-query block, sequence, kv head); wave w computes query head
+// h*G + w % G for the 16 queries of column tile w / G.  Every 32-key K / V tile of the kv head is staged in
+// LDS once per workgroup (register staged, double buffered, one barrier per tile) and consumed
+// by all QT*G waves — K/V bytes per MFMA drop QT*G-fold against paged_prefill_kernel, whose waves
+// each stream K/V from global — while each wave keeps the per-wave register footprint of one
+// 16-query tile, so two waves share every SIMD and hide each other's latencies.
+// LDS images are laid out for the fragment reads: K rows in the order the S^T = K.Q^T
+// A-fragments of key tile t read them (rows t*16 .. t*16+15 contiguous) with a 16-byte pad,
+// V^T rows (channel d, 32 keys) with a 16-byte pad.  The math is attend_step's.
+constexpr int kKRow = kHD + 8;     // K_s row, bf16 elements (272 B)
+constexpr int kVRow = kStep + 8;   // V_s row, bf16 elements (80 B)
+
+__device__ __forceinline__ int k_lds_row(int k) { return ((k >> 2) & 1) * 16 + (k >> 3) * 4 + (k & 3); }
+
+template <int NW, int QT>
+__global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
+    const int* __restrict__ cu_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride, float scale2) {
+  __shared__ __attribute__((aligned(16))) bf16_t K_s[2][kStep][kKRow];
+  __shared__ __attribute__((aligned(16))) bf16_t V_s[2][kHD][kVRow];
+  constexpr int G = NW / QT;             // query heads of the GQA group (QT 16-query tiles each)
+  constexpr int kPQ = 16 * QT;          // queries per workgroup
+  constexpr int NP = 1024 / (64 * NW);  // 16-byte pieces (512 of K, 512 of V^T) per thread per tile
+  const int qb = blockIdx.x, seq = blockIdx.y, h = blockIdx.z;
+  const int q0 = cu_q[seq], L = cu_q[seq + 1] - q0;
+  if (qb * kPQ >= L) return;
+  const int ctx = context_lens[seq];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int hq = h * G + w % G;
+  const int qi = qb * kPQ + (w / G) * 16 + r;
+  const bool valid = qi < L;
+  const int qpos = valid ? ctx - L + qi : -1;
+  const int last_q = min(L - 1, qb * kPQ + kPQ - 1);
+  const int k_end = min(ctx, ctx - L + last_q + 1);  // keys any query of the block can see
+  const int nsteps = (k_end + kStep - 1) / kStep;
+  const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
+  const bf16_t* kch = kc + static_cast<int64_t>(h) * bs * kHD;
+  const bf16_t* vch = vc + static_cast<int64_t>(h) * kHD * bs;
+  const int* bt = block_tables + static_cast<int64_t>(seq) * max_blocks;
+
+  // piece p < 512: K (key p >> 4, 16-byte chunk p & 15); p >= 512: V^T (channel (p-512) >> 2,
+  // keys 8 ((p-512) & 3) .. +8, contiguous in the transposed cache).  Keys past k_end are
+  // clamped to the last visible one (masked in the softmax); no load sits behind a branch.
+  u32x4 stage[NP];
+  auto load_tile = [&](int step) {
+    const int s0 = min(step, nsteps - 1) * kStep;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int p = threadIdx.x + i * 64 * NW;
+      const bool isk = p < 512;
+      const int pv = p & 511;
+      const int tok = isk ? min(s0 + (pv >> 4), k_end - 1) : min(s0 + 8 * (pv & 3), ((k_end - 1) >> 3) << 3);
+      const int64_t base = static_cast<int64_t>(bt[tok / bs]) * blk_stride;
+      const bf16_t* src = isk ? kch + base + (tok % bs) * kHD + (pv & 15) * 8 : vch + base + (pv >> 2) * bs + tok % bs;
+      stage[i] = *reinterpret_cast<const u32x4*>(src);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int p = threadIdx.x + i * 64 * NW;
+      const int pv = p & 511;
+      bf16_t* dst = p < 512 ? &K_s[buf][k_lds_row(pv >> 4)][(pv & 15) * 8] : &V_s[buf][pv >> 2][(pv & 3) * 8];
+      *reinterpret_cast<u32x4*>(dst) = stage[i];
+    }
+  };
+
+  bf16x8_t qf[4];
+  load_q(qf, q + static_cast<int64_t>(q0 + (valid ? qi : 0)) * q_stride + hq * kHD, valid);
+  WaveState st;
+  init_state(st);
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int buf = step & 1;
+    load_tile(step + 1);  // the next tile's global loads fly during this tile's math
+    KVFrag f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) f.k[t][kk] = *reinterpret_cast<const bf16x8_t*>(&K_s[buf][t * 16 + r][32 * g + 8 * kk]);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) f.v[dt] = *reinterpret_cast<const bf16x8_t*>(&V_s[buf][16 * dt + r][8 * g]);
+    attend_step(st, qf, f, step * kStep, ctx, qpos, scale2);
+    store_tile(buf ^ 1);  // every wave finished reading buf ^ 1 before the previous barrier
+    __syncthreads();
+  }
+  const float lsum = col_sum(st.l);
+  if (!valid) return;
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  bf16_t* o = out + static_cast<int64_t>(q0 + qi) * out_stride + hq * kHD;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    uint2 v;
+    v.x = pack2(st.o[dt][0] * inv, st.o[dt][1] * inv);
+    v.y = pack2(st.o[dt][2] * inv, st.o[dt][3] * inv);
+    *reinterpret_cast<uint2*>(o + 16 * dt + 4 * g) = v;
+  }
+}
+
+int g_prefill_lds = 1;  // pk_set_prefill_impl: 1 = LDS-tiled kernel where it applies, 0 = per-wave kernel
+
 constexpr int kDecodePart = 512;
 
 }  // namespace
@@ -520,6 +627,11 @@ PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, 
                        n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
 }
 
+PK_EXPORT int pk_set_prefill_impl(int lds) {
+  g_prefill_lds = lds != 0;
+  return 0;
+}
+
 PK_EXPORT int pk_set_decode_z(int z) {
   if (z < 1) return -1;
   g_decode_z = z;
@@ -533,6 +645,30 @@ PK_EXPORT int pk_paged_prefill(void* out, const void* q, const void* k_cache, co
   if (n_seqs <= 0 || max_q_len <= 0) return 0;
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
   const int G = n_q / n_kv;
+  if (g_prefill_lds && (G == 1 || G == 2 || G == 4 || G == 8)) {
+    // 16-query column tiles per workgroup: 4 (64 queries: more waves share each K/V tile) for
+    // G <= 4 and prompts < 2K; 2 otherwise (the 1024-thread cap; long causal prompts balance
+    // better over more, smaller workgroups — tools/bench_prefill_attn.py)
+    const int qt = G <= 4 && max_q_len < 2048 ? 4 : 2;
+    const dim3 grid((max_q_len + 16 * qt - 1) / (16 * qt), n_seqs, n_kv);
+#define PK_PREFILL_LDS(NW, QT)                                                                                 \
+  paged_prefill_lds_kernel<NW, QT><<<grid, 64 * NW, 0, stream>>>(                                              \
+      static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),          \
+      static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables),                              \
+      static_cast<const int*>(context_lens), static_cast<const int*>(cu_q), n_kv, bs, max_blocks, q_stride,    \
+      out_stride, scale * kLog2e)
+    switch (G * 8 + qt) {
+      case 1 * 8 + 4: PK_PREFILL_LDS(4, 4); break;
+      case 1 * 8 + 2: PK_PREFILL_LDS(2, 2); break;
+      case 2 * 8 + 4: PK_PREFILL_LDS(8, 4); break;
+      case 2 * 8 + 2: PK_PREFILL_LDS(4, 2); break;
+      case 4 * 8 + 4: PK_PREFILL_LDS(16, 4); break;
+      case 4 * 8 + 2: PK_PREFILL_LDS(8, 2); break;
+      default: PK_PREFILL_LDS(16, 2); break;
+    }
+#undef PK_PREFILL_LDS
+    return PK_CHECK_LAUNCH();
+  }
   const int W = G > 8 ? 8 : G;
   if (G % W) return -1;
   dim3 grid((max_q_len + 15) / 16, n_seqs, n_kv * (G / W));
