@@ -78,6 +78,9 @@ __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_c
 #ifndef PK_W_DEPTH
 #define PK_W_DEPTH 2         // k-steps of W in flight per wave (register ring; 4 measured slower)
 #endif
+#ifndef PK_SLAB_NT
+#define PK_SLAB_NT 0         // non-temporal stores for the fp32 split-K slabs
+#endif
 #ifndef PK_LAB_LDS_PAD
 #define PK_LAB_LDS_PAD 0     // extra LDS per workgroup (forces one workgroup per CU)
 #endif
@@ -456,8 +459,13 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     if constexpr (kSlab) {
       float* p = args.partial + (static_cast<int64_t>(split) * args.M + row0 + m) * N + n0 + 4 * g;
 #pragma unroll
-      for (int t = 0; t < kR; ++t) *reinterpret_cast<float4*>(p + 16 * t) =
-          make_float4(acc[t][mt][0], acc[t][mt][1], acc[t][mt][2], acc[t][mt][3]);
+      for (int t = 0; t < kR; ++t) {
+        const f32x4 v = acc[t][mt];
+        if constexpr (PK_SLAB_NT)  // streaming store: no dirty L2 lines left for the launch-end write-back
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p + 16 * t));
+        else
+          *reinterpret_cast<f32x4*>(p + 16 * t) = v;
+      }
     } else if constexpr (MODE == kBF16) {
       bf16_t* o = args.out + static_cast<int64_t>(row0 + m) * args.ldo + n0 + 4 * g;
 #pragma unroll
