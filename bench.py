@@ -47,6 +47,8 @@ def parse_args(argv=None):
     ap.add_argument("--mode", choices=["unary", "stream"], default="unary")
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--num-kv-blocks", type=int, default=0, help="KV blocks per replica (0: size from free HBM)")
+    ap.add_argument("--gpu-mem-fraction", type=float, default=0.90)
     ap.add_argument("--port-base", type=int, default=int(os.environ.get("POLYKEY_BENCH_PORT", "52100")))
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args(argv)
@@ -179,7 +181,8 @@ def main(argv=None) -> int:
     max_len = (max_len + 511) // 512 * 512
     ecfg = EngineConfig(model=args.model, seed=args.seed, max_num_seqs=max(args.concurrency, 1),
                         max_num_batched_tokens=args.max_batched_tokens, max_model_len=max_len,
-                        hip_graphs=not args.no_graphs)
+                        hip_graphs=not args.no_graphs, num_kv_blocks=args.num_kv_blocks,
+                        gpu_mem_fraction=args.gpu_mem_fraction)
     t_init = time.perf_counter()
     engine = LLMEngine(ecfg, st)
     init_s = time.perf_counter() - t_init

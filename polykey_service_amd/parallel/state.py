@@ -65,7 +65,9 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
-    dev = torch.device(f"cuda:{local}") if device == "cuda" else torch.device(device)
+    # more local ranks than GPUs (rehearsing a multi-rank launch on a one-GPU box) share devices
+    n_dev = torch.cuda.device_count() if device == "cuda" else 0
+    dev = torch.device(f"cuda:{local % max(n_dev, 1)}") if device == "cuda" else torch.device(device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     if world % tp:
@@ -76,7 +78,8 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
                        dp_size=world // tp, dp_rank=rank // tp, ep_size=ep, ep_rank=(rank % tp) if ep > 1 else 0,
                        device=dev)
     if world > 1:
-        be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+        # POLYKEY_DIST_BACKEND overrides (gloo: several ranks on one GPU, which RCCL refuses)
+        be = backend or os.environ.get("POLYKEY_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # a hung or failed RCCL collective aborts the communicator and raises in this process
         # (timeout_s), which takes the engine down → health NOT_SERVING → supervisor restart
