@@ -150,3 +150,44 @@ def test_short_and_long_context_graphs_agree_with_eager():
             st = e.runner.stats
             assert 0 < st["short_graph_steps"] < st["graph_steps"], st
     assert res[0] == res[1]
+
+
+def test_folded_norm_decode_matches_normalised(monkeypatch):
+    """Decode with the RMSNorm weights folded into the QKV / gate_up projections (rows scaled by
+    rinv, residual-update kernels instead of norms) gives the hidden states of the normalised
+    chain on the same step inputs and KV cache.  tiny-llama-gqa4 has H = 1024, so the folded path
+    applies; its norm weights are made non-uniform so the fold is not a no-op.  (Whole-engine
+    greedy runs are not compared: a near-tie in the prefill logits can pick a different first
+    token on either path.)"""
+    from polykey_service_amd.models import llama
+    monkeypatch.setattr(llama, "FOLD_NORM", True)
+    _, gpu = _models("tiny-llama-gqa4")
+    with torch.no_grad():
+        for layer in gpu.layers:
+            layer.ln1.mul_(torch.linspace(0.5, 1.5, layer.ln1.numel(), device="cuda").to(layer.ln1.dtype))
+            layer.ln2.mul_(torch.linspace(1.5, 0.5, layer.ln2.numel(), device="cuda").to(layer.ln2.dtype))
+    e = LLMEngine(EngineConfig(model="tiny-llama-gqa4", max_num_seqs=8, max_num_batched_tokens=256,
+                               max_model_len=512, hip_graphs=False, device="cuda"),
+                  ParallelState(device=torch.device("cuda")), model=gpu)
+    assert gpu.layers[0].attn.qkv_pf is not None
+    for p in ([1] + list(range(5, 5 + n)) for n in (3, 17, 40)):
+        e.add_request(p, SamplingParams(max_tokens=3))
+    e.step()  # prefill
+    orig = gpu.forward
+    seen = {}
+
+    def spy(input_ids, positions, md, kv):
+        seen["args"] = (input_ids.clone(), positions.clone(), md, [(k.clone(), v.clone()) for k, v in kv])
+        return orig(input_ids, positions, md, kv)
+
+    gpu.forward = spy
+    e.step()  # first decode step, through the folded chain
+    gpu.forward = orig
+    ids, pos, md, kv0 = seen["args"]
+    outs = []
+    for folded in (True, False):
+        if not folded:
+            monkeypatch.setattr(gpu, "_rowscale_ok", lambda x: False)
+        with torch.inference_mode():
+            outs.append(gpu.forward(ids, pos, md, [(k.clone(), v.clone()) for k, v in kv0]).float())
+    torch.testing.assert_close(outs[0], outs[1], atol=0.1, rtol=0.05)
