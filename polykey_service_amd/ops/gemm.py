@@ -370,12 +370,17 @@ def partial_add_rms_norm_route(p: Partial, residual: torch.Tensor, weight: torch
     return out, residual, ids, w
 
 
-def silu_and_mul_interleaved(x: torch.Tensor) -> torch.Tensor:
+def silu_and_mul_interleaved(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(gate) * up of gate/up columns interleaved by 16 → [..., I]; ``out``: a contiguous
+    destination (e.g. a row slice of a larger buffer) written in place."""
     if not x.is_cuda:
-        return reference.silu_and_mul_interleaved(x)
+        y = reference.silu_and_mul_interleaved(x)
+        return y if out is None else out.copy_(y)
     I2 = x.shape[-1]
     T = x.numel() // I2
-    out = torch.empty(x.shape[:-1] + (I2 // 2,), dtype=x.dtype, device=x.device)
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (I2 // 2,), dtype=x.dtype, device=x.device)
+    assert out.is_contiguous() and out.numel() == T * (I2 // 2)
     native.call("pk_silu_and_mul_il", out.data_ptr(), x.data_ptr(), T, I2 // 2, native.stream_ptr())
     return out
 

@@ -113,9 +113,11 @@ def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_ro
     offs = offsets.tolist()  # prefill: one read-back per layer, then a library GEMM per expert
     for e in range(E_local):
         lo, hi = offs[e], offs[e + 1]
-        if hi > lo:
-            y = F.linear(a[lo:hi], w[e])
-            out[lo:hi] = silu_and_mul_interleaved(y) if silu else y
+        if hi > lo:  # results land in their rows of `out` directly (no slice-assignment copy)
+            if silu:
+                silu_and_mul_interleaved(F.linear(a[lo:hi], w[e]), out=out[lo:hi])
+            else:
+                torch.matmul(a[lo:hi], w[e].t(), out=out[lo:hi])
     return out
 
 
