@@ -556,7 +556,10 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
 
 int g_prefill_lds = 1;  // pk_set_prefill_impl: 1 = LDS-tiled kernel where it applies, 0 = per-wave kernel
 
-constexpr int kDecodePart = 512;
+#ifndef PK_DECODE_PART
+#define PK_DECODE_PART 512  // keys per decode partition (ops/attention.py _PART must match)
+#endif
+constexpr int kDecodePart = PK_DECODE_PART;
 
 }  // namespace
 
