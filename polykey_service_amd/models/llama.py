@@ -44,6 +44,14 @@ FUSED_QKV_ATTENTION = os.environ.get("POLYKEY_FUSED_QKV_ATTN", "1") == "1"
 # per-layer norm kernels shrink to residual updates (4x wider grid, no normalised copy written).
 # POLYKEY_FOLD_NORM=0: normalised activations as in prefill.
 FOLD_NORM = os.environ.get("POLYKEY_FOLD_NORM", "1") == "1"
+# TP > 1 steps with at least SP_MIN_TOKENS tokens (prefill) run with a token-sharded residual
+# stream: reduce-scatter / all-gather around the norms instead of all-reduces (_forward_sp).
+SEQUENCE_PARALLEL = os.environ.get("POLYKEY_SEQUENCE_PARALLEL", "1") == "1"
+SP_MIN_TOKENS = int(os.environ.get("POLYKEY_SP_MIN_TOKENS", "256"))
+# TP > 1 steps with at least SP_MIN_TOKENS tokens (prefill) run with a token-sharded residual
+# stream: reduce-scatter / all-gather around the norms instead of all-reduces (_forward_sp).
+SEQUENCE_PARALLEL = os.environ.get("POLYKEY_SEQUENCE_PARALLEL", "1") == "1"
+SP_MIN_TOKENS = int(os.environ.get("POLYKEY_SP_MIN_TOKENS", "256"))
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:
@@ -116,12 +124,19 @@ class LlamaAttention(nn.Module):
             q = gemm.qkv_reduce_rope_cache(p, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq,
                                            self.nkv)
         else:
-            qkv = gemm.linear(x, self.qkv, packed=self.qkv_p)
-            attn_ops.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq, self.nkv,
-                                    self.hd)
-            q = qkv.view(T, self.nq + 2 * self.nkv, self.hd)[:, :self.nq]
+            return _proj_out(self.attend(gemm.linear(x, self.qkv, packed=self.qkv_p), positions, md, cos_sin, kv),
+                             self.o, ws, self.o_p)
         a = attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
         return _proj_out(a, self.o, ws, self.o_p)
+
+    def attend(self, qkv: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
+               kv: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
+        """RoPE + KV-cache write + paged attention from a projected [T, (nq + 2 nkv) hd] qkv."""
+        k_cache, v_cache = kv
+        attn_ops.rope_and_cache(qkv, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq, self.nkv,
+                                self.hd)
+        q = qkv.view(qkv.shape[0], self.nq + 2 * self.nkv, self.hd)[:, :self.nq]
+        return attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
 
 
 class LlamaMLP(nn.Module):
@@ -294,6 +309,8 @@ class LlamaForCausalLM(nn.Module):
     def forward(self, input_ids: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata,
                 kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
         """Returns the final-normed hidden states [T, H]."""
+        if self._sp_ok(input_ids):
+            return self._forward_sp(input_ids, positions, md, kv_caches)
         x = self.embed_tokens(input_ids)
         ws = self.workspace(x.shape[0])
         if ws is not None and self._fused_decode_ok(x):
@@ -316,6 +333,52 @@ class LlamaForCausalLM(nn.Module):
         """post-attention residual add + RMSNorm, then the MLP (its output may be pending)."""
         x, residual = add_norm(x, residual, layer.ln2, layer.eps)
         return layer.mlp(x, ws), residual
+
+    # ------------------------------------------------------------------ sequence parallel (TP prefill)
+    def _sp_ok(self, ids: torch.Tensor) -> bool:
+        return SEQUENCE_PARALLEL and self.st.tp_size > 1 and ids.shape[0] >= SP_MIN_TOKENS
+
+    def _forward_sp(self, input_ids: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata,
+                    kv_caches: List[Tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+        """TP prefill with a token-sharded residual stream (:mod:`..parallel.comm` SP layout).
+        The vocab-parallel embedding partial is reduce-scattered straight into the shard; then
+        per layer:
+
+            all-gather(h) -> QKV GEMM (chunk-overlapped) -> attention -> o GEMM -> reduce-scatter
+            residual add + RMSNorm on the shard
+            all-gather(h) -> gate_up + SiLU -> down GEMM -> reduce-scatter
+            residual add + RMSNorm on the shard
+
+        and the final-normed shard is all-gathered for the LM head."""
+        T = input_ids.shape[0]
+        chunks = 2 if input_ids.is_cuda and T >= 2 * comm.OVERLAP_MIN_ROWS else 1
+        lay = comm.SPLayout(T, chunks)
+        emb = ops.embedding(input_ids, self.embed, self.vocab_start, self.vocab_local)
+        residual = comm.sp_reduce_scatter(emb, lay)
+        del emb
+        h = ops.rms_norm(residual, self.layers[0].ln1, self.layers[0].eps)
+        for i, layer in enumerate(self.layers):
+            at = layer.attn
+            qkv = comm.sp_all_gather(h, lay, comm.RowsFn(lambda r, o, w=at.qkv: gemm.linear(r, w, out=o),
+                                                         at.qkv.shape[0]))
+            a = at.attend(qkv, positions, md, self.cos_sin, kv_caches[i])
+            del qkv
+            o = comm.sp_reduce_scatter(a, lay, comm.RowsFn(lambda r, out, w=at.o: gemm.linear(r, w, out=out),
+                                                           at.o.shape[0]))
+            h, residual = ops.fused_add_rms_norm(o, residual, layer.ln2, layer.eps)
+            m = self._sp_mlp(layer, h, lay)
+            nxt = self.layers[i + 1].ln1 if i + 1 < len(self.layers) else self.norm
+            h, residual = ops.fused_add_rms_norm(m, residual, nxt, layer.eps)
+        return comm.sp_all_gather(h, lay)
+
+    def _sp_mlp(self, layer, h: torch.Tensor, lay) -> torch.Tensor:
+        """Dense MLP on the SP shard: all-gather → gate_up + SiLU → down → reduce-scatter."""
+        mlp = layer.mlp
+        g = comm.sp_all_gather(h, lay, comm.RowsFn(
+            lambda r, o, w=mlp.gate_up: gemm.silu_and_mul_interleaved(gemm.linear(r, w), out=o),
+            mlp.gate_up.shape[0] // 2))
+        return comm.sp_reduce_scatter(g, lay, comm.RowsFn(lambda r, o, w=mlp.down: gemm.linear(r, w, out=o),
+                                                          mlp.down.shape[0]))
 
     # ------------------------------------------------------------------ fused decode chain
     # Off by default: measured slower on MI355X (tools/bench_gemm.py "fused decode chain": the

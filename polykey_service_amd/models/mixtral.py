@@ -47,6 +47,10 @@ class MixtralMoE(nn.Module):
                           defer_combine=single, routing=routing)
         return y if single else comm.tp_all_reduce(y)
 
+    def local(self, x: torch.Tensor) -> torch.Tensor:
+        """This rank's unreduced expert output (its experts / its intermediate shard)."""
+        return moe.fused_moe(x, self.router, self.w13, self.w2, self.k, self.e_lo, self.e_hi, self.w13_p, self.w2_p)
+
 
 class MixtralForCausalLM(LlamaForCausalLM):
     def _mlp_block(self, layer, x, residual, ws):
@@ -57,6 +61,11 @@ class MixtralForCausalLM(LlamaForCausalLM):
                                                                    layer.mlp.k)
             return layer.mlp(x, ws, routing=(ids, w)), residual
         return super()._mlp_block(layer, x, residual, ws)
+
+    def _sp_mlp(self, layer, h, lay):
+        """Sequence-parallel prefill: every rank routes all tokens of the gathered rows through
+        its experts, and the reduce-scatter that returns to the token shard is the combine."""
+        return comm.sp_reduce_scatter(layer.mlp.local(comm.sp_all_gather(h, lay)), lay)
 
     def _make_mlp(self, layer: int) -> nn.Module:
         cfg, st = self.cfg, self.st

@@ -70,6 +70,133 @@ def tp_row_parallel_overlapped(x: torch.Tensor, n_out: int, fn, chunks: int = 2,
     return out
 
 
+# ---------------------------------------------------------------- sequence parallelism
+# Megatron-style SP for TP prefill (SURVEY.md §2.3 "SP"): the residual stream is sharded by
+# token between the row-parallel projections (reduce-scatter) and the column-parallel ones
+# (all-gather), so RMSNorm and the residual adds run on 1/tp of the rows and each rank holds
+# 1/tp of the residual.  Same bytes on xGMI as the all-reduce it replaces (RS + AG), but the
+# two halves overlap with different GEMMs: the reduce-scatter of row chunk c runs on the comm
+# stream while the row-parallel GEMM of chunk c+1 runs, and the all-gather of chunk c+1 runs
+# while the column-parallel GEMM of chunk c does.
+#
+# Layout: ``Tp`` = T padded to a multiple of tp*chunks, chunk c = rows [c*Tc, (c+1)*Tc) with
+# Tc = Tp/chunks; rank r's shard is [chunks, Tc/tp] rows, chunk c's piece being rows
+# c*Tc + r*Tc/tp + [0, Tc/tp).  Row-wise ops (norm, residual add) do not care about the order.
+
+
+class SPLayout:
+    __slots__ = ("T", "Tp", "chunks", "tp", "rank")
+
+    def __init__(self, T: int, chunks: int = 1):
+        st = get_state()
+        self.T, self.chunks, self.tp, self.rank = T, chunks, st.tp_size, st.tp_rank
+        q = self.tp * chunks
+        self.Tp = (T + q - 1) // q * q
+
+    @property
+    def rows(self) -> int:
+        """Rows of one rank's shard."""
+        return self.Tp // self.tp
+
+    def chunk(self, c: int):
+        Tc = self.Tp // self.chunks
+        return c * Tc, (c + 1) * Tc, c * Tc // self.tp, (c + 1) * Tc // self.tp
+
+
+def _reduce_scatter(out: torch.Tensor, x: torch.Tensor) -> None:
+    st = get_state()
+    if dist.get_backend(st.tp_group) != "gloo":
+        dist.reduce_scatter_tensor(out, x, group=st.tp_group)
+        return
+    t = x.clone()  # gloo has no reduce-scatter: all-reduce and keep this rank's slice
+    dist.all_reduce(t, group=st.tp_group)
+    out.copy_(t.view((st.tp_size, -1) + tuple(x.shape[1:]))[st.tp_rank])
+
+
+def sp_reduce_scatter(y: torch.Tensor, lay: SPLayout, fn=None) -> torch.Tensor:
+    """Row-parallel partials → this rank's summed shard [lay.rows, n].  ``fn(rows, out)``:
+    compute the partial of x-rows ``rows`` into ``out`` chunk by chunk (``y`` = the input x)
+    so the collective of chunk c overlaps the GEMM of chunk c+1; ``fn=None``: ``y`` is the
+    finished [T, n] partial."""
+    T, tp = lay.T, lay.tp
+    n = y.shape[1] if fn is None else fn.n_out
+    full = torch.empty((lay.Tp, n), dtype=y.dtype, device=y.device)
+    if lay.Tp > T:
+        full[T:].zero_()
+    shard = torch.empty((lay.rows, n), dtype=y.dtype, device=y.device)
+    overlap = y.is_cuda and lay.chunks > 1
+    main = torch.cuda.current_stream(y.device) if overlap else None
+    cs = _comm_stream(y.device) if overlap else None
+    for c in range(lay.chunks):
+        lo, hi, slo, shi = lay.chunk(c)
+        rhi = min(hi, T)
+        if rhi > lo:
+            if fn is None:
+                full[lo:rhi].copy_(y[lo:rhi])
+            else:
+                fn(y[lo:rhi], full[lo:rhi])
+        if overlap:
+            cs.wait_stream(main)
+            with torch.cuda.stream(cs):
+                _reduce_scatter(shard[slo:shi], full[lo:hi])
+        else:
+            _reduce_scatter(shard[slo:shi], full[lo:hi])
+    if overlap:
+        main.wait_stream(cs)
+        full.record_stream(cs)
+    return shard
+
+
+def sp_all_gather(shard: torch.Tensor, lay: SPLayout, fn=None) -> torch.Tensor:
+    """Shards → the full [T, n] rows on every rank.  ``fn(rows, out)``: a column-parallel
+    projection applied chunk by chunk as soon as that chunk has arrived (the gather of chunk
+    c+1 overlaps it); returns its [T, fn.n_out] output instead."""
+    st = get_state()
+    T = lay.T
+    full = torch.empty((lay.Tp, shard.shape[1]), dtype=shard.dtype, device=shard.device)
+    overlap = shard.is_cuda and lay.chunks > 1 and fn is not None
+    main = torch.cuda.current_stream(shard.device) if overlap else None
+    cs = _comm_stream(shard.device) if overlap else None
+    events = []
+    if overlap:
+        cs.wait_stream(main)
+    for c in range(lay.chunks):
+        lo, hi, slo, shi = lay.chunk(c)
+        if overlap:
+            with torch.cuda.stream(cs):
+                dist.all_gather_into_tensor(full[lo:hi], shard[slo:shi], group=st.tp_group)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            events.append(ev)
+        else:
+            dist.all_gather_into_tensor(full[lo:hi], shard[slo:shi], group=st.tp_group)
+    if overlap:
+        full.record_stream(cs)
+        shard.record_stream(cs)
+    if fn is None:
+        return full[:T]
+    out = torch.empty((T, fn.n_out), dtype=shard.dtype, device=shard.device)
+    for c in range(lay.chunks):
+        lo, hi, _, _ = lay.chunk(c)
+        hi = min(hi, T)
+        if overlap:
+            main.wait_event(events[c])
+        if hi > lo:
+            fn(full[lo:hi], out[lo:hi])
+    return out
+
+
+class RowsFn:
+    """``fn(rows, out)`` with its output width, for :func:`sp_reduce_scatter` / :func:`sp_all_gather`."""
+    __slots__ = ("f", "n_out")
+
+    def __init__(self, f, n_out: int):
+        self.f, self.n_out = f, n_out
+
+    def __call__(self, rows, out):
+        self.f(rows, out)
+
+
 def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:
     """[.., n] per rank → [.., n * tp] (rank-major along the last dim)."""
     st = get_state()

@@ -35,10 +35,12 @@ def _first_step_logits_and_tokens(eng):
     return logits, [s.output_ids for s in seqs]
 
 
-def _worker(rank, world, port, model, ep, out_path):
+def _worker(rank, world, port, model, ep, out_path, sp=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(2)
+    from polykey_service_amd.models import llama
+    llama.SP_MIN_TOKENS = 1 if sp else 1 << 30  # sp: every step (49-token prefill: padded rows) runs SP
     from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
     st = init_parallel(tp=world, ep=ep, device="cpu", backend="gloo")
     eng = _engine(model, st)
@@ -51,12 +53,16 @@ def _worker(rank, world, port, model, ep, out_path):
     destroy_parallel()
 
 
-@pytest.mark.parametrize("model,ep", [("tiny-llama-gqa4", 1), ("tiny-mixtral", 1), ("tiny-mixtral", 2)])
-def test_tp2_matches_tp1(tmp_path, model, ep):
+@pytest.mark.parametrize("model,ep,sp", [("tiny-llama-gqa4", 1, False), ("tiny-mixtral", 1, False),
+                                         ("tiny-mixtral", 2, False), ("tiny-llama-gqa4", 1, True),
+                                         ("tiny-mixtral", 2, True)])
+def test_tp2_matches_tp1(tmp_path, model, ep, sp):
+    """``sp``: sequence-parallel steps (token-sharded residual, reduce-scatter / all-gather)."""
     from polykey_service_amd.parallel.state import ParallelState
     ref_logits, ref_toks = _first_step_logits_and_tokens(_engine(model, ParallelState()))
     out = str(tmp_path / "tp.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), model, ep, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(2, _free_port(), model, ep, out, sp), nprocs=2, join=True,
+                       start_method="spawn")
     got = torch.load(out, weights_only=True)
     # bf16 row-parallel partials are rounded per rank before the all-reduce: ~1 bf16 ulp noise
     torch.testing.assert_close(got["logits"], ref_logits, atol=1e-1, rtol=5e-2)
@@ -76,7 +82,14 @@ def _comm_worker(rank, world, port, out_path):
     cnt = comm.tp_all_to_all_counts(torch.full((world,), rank + 1, dtype=torch.int64))
     recv = comm.tp_all_to_all(send, cnt.tolist(), [rank + 1] * world)
     obj = comm.tp_broadcast_object({"step": 7} if rank == 0 else None)
-    torch.save({"ar": ar, "ag": ag, "recv": recv, "obj": obj}, f"{out_path}.{rank}")
+    # sequence-parallel layout: 7 rows padded to 8 (2 chunks x 2 ranks x 2 rows)
+    lay = comm.SPLayout(7, chunks=2)
+    full = torch.arange(7 * 2, dtype=torch.float32).view(7, 2) * (rank + 1)
+    shard = comm.sp_reduce_scatter(full, lay)
+    back = comm.sp_all_gather(shard, lay)
+    twice = comm.sp_all_gather(shard, lay, comm.RowsFn(lambda r, o: torch.mul(r, 2, out=o), 2))
+    torch.save({"ar": ar, "ag": ag, "recv": recv, "obj": obj, "shard": shard, "back": back, "twice": twice},
+               f"{out_path}.{rank}")
     destroy_parallel()
 
 
@@ -89,6 +102,11 @@ def test_collectives_gloo(tmp_path):
         assert d["ag"].tolist() == [[0.0, 1.0, 2.0, 10.0, 11.0, 12.0]]
         assert d["recv"][:, 0].tolist() == [0.0] * 1 + [1.0] * 2
         assert d["obj"] == {"step": 7}
+        summed = torch.arange(14, dtype=torch.float32).view(7, 2) * 3
+        padded = torch.cat([summed, torch.zeros(1, 2)])
+        # rank r holds rows {c*4 + 2r, c*4 + 2r + 1} of chunk c
+        assert torch.equal(d["shard"], torch.cat([padded[2 * r:2 * r + 2], padded[4 + 2 * r:6 + 2 * r]]))
+        assert torch.equal(d["back"], summed) and torch.equal(d["twice"], 2 * summed)
 
 
 def _a2a_worker(rank, world, port, out_path):
