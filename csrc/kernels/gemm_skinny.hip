@@ -81,6 +81,9 @@ __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_c
 #ifndef PK_SLAB_NT
 #define PK_SLAB_NT 0         // non-temporal stores for the fp32 split-K slabs
 #endif
+#ifndef PK_SLAB_SC1
+#define PK_SLAB_SC1 0        // write-through (sc1) buffer stores for the fp32 split-K slabs
+#endif
 #ifndef PK_LAB_LDS_PAD
 #define PK_LAB_LDS_PAD 0     // extra LDS per workgroup (forces one workgroup per CU)
 #endif
@@ -458,13 +461,23 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     }
     if constexpr (kSlab) {
       float* p = args.partial + (static_cast<int64_t>(split) * args.M + row0 + m) * N + n0 + 4 * g;
+#if PK_SLAB_SC1
+      // write-through (sc1) stores: the slab lines leave L2 clean, so the launch-end release
+      // has nothing to write back (slabs are < 2 GiB: 32-bit buffer offsets)
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(args.partial, static_cast<short>(0), 0x7ffffff0, 0x00020000);
+      const int boff = static_cast<int>((p - args.partial) * 4);
+#endif
 #pragma unroll
       for (int t = 0; t < kR; ++t) {
         const f32x4 v = acc[t][mt];
+#if PK_SLAB_SC1
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, boff + 64 * t, 0, 16);
+#else
         if constexpr (PK_SLAB_NT)  // streaming store: no dirty L2 lines left for the launch-end write-back
           __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p + 16 * t));
         else
           *reinterpret_cast<f32x4*>(p + 16 * t) = v;
+#endif
       }
     } else if constexpr (MODE == kBF16) {
       bf16_t* o = args.out + static_cast<int64_t>(row0 + m) * args.ldo + n0 + 4 * g;

@@ -21,7 +21,8 @@ from . import native, reference
 import os
 
 SKINNY_MAX_M = 64
-_TARGET_WGS = 192   # measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
+# measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
+_TARGET_WGS = int(os.environ.get("POLYKEY_SKINNY_TARGET_WGS", "192"))
 _ROWS_PER_WG = 128
 _KCHUNK = 256
 # The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see

@@ -40,9 +40,11 @@ def _run(eng):
     return logits, [s.output_ids for s in seqs]
 
 
-def _worker(rank, port, model, out_path):
+def _worker(rank, port, model, out_path, sp=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
-                      LOCAL_RANK="0", POLYKEY_CUSTOM_AR="force", POLYKEY_TP_OVERLAP_MIN_ROWS="8")
+                      LOCAL_RANK="0", POLYKEY_CUSTOM_AR="force", POLYKEY_TP_OVERLAP_MIN_ROWS="8",
+                      # sp: the 49-token prefill runs sequence-parallel with 2 comm-stream chunks
+                      POLYKEY_SP_MIN_TOKENS="16" if sp else "100000")
     from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
     st = init_parallel(tp=2, device="cuda", backend="gloo")
     assert st.custom_ar is not None, "custom all-reduce did not come up"
@@ -56,12 +58,17 @@ def _worker(rank, port, model, out_path):
     destroy_parallel()
 
 
-@pytest.mark.parametrize("model", ["tiny-llama-gqa4", "tiny-mixtral"])
-def test_tp2_on_gpu_matches_tp1(tmp_path, model):
+@pytest.mark.parametrize("model,sp", [("tiny-llama-gqa4", False), ("tiny-mixtral", False),
+                                      ("tiny-llama-gqa4", True), ("tiny-mixtral", True)])
+def test_tp2_on_gpu_matches_tp1(tmp_path, model, sp, monkeypatch):
+    from polykey_service_amd.models import llama
     from polykey_service_amd.parallel.state import ParallelState
+    # like for like: TP > 1 keeps normalised activations, so the TP=1 reference does not fold
+    # the RMSNorm weights into its decode projections (that path has its own e2e test)
+    monkeypatch.setattr(llama, "FOLD_NORM", False)
     ref_logits, ref_toks = _run(_engine(model, ParallelState(device=torch.device("cuda:0"))))
     out = str(tmp_path / "tp.pt")
-    mp.start_processes(_worker, args=(_port(), model, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(_port(), model, out, sp), nprocs=2, join=True, start_method="spawn")
     got = torch.load(out, weights_only=True)
     assert got["car_err"] == 0
     # decode-step logits agree to bf16 noise (row-parallel partials are rounded per rank);
