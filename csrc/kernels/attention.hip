@@ -179,6 +179,9 @@ __device__ __forceinline__ float col_sum(float l) {
 }
 
 // ------------------------------------------------------------------------------ decode
+#ifndef PK_DECODE_BT_PREFETCH
+#define PK_DECODE_BT_PREFETCH 1  // request the block-table window first (see paged_decode_kernel)
+#endif
 // grid (n_kv, n_seqs, min(n_parts, z)), block 64*NW (NW waves).  LDS: NW waves x 16 cols x 128 d fp32.
 // Decode attention fed straight from the QKV projection's split-K slabs (FROM_QKV): the
 // workgroup of (seq, kv head h) sums the S fp32 slabs of its G query heads and of k/v head h,
@@ -204,6 +207,15 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
   __shared__ int last;
   __shared__ int bt_s[kPart / 8 + 2];  // this partition's block-table window (LDS: lookups use lgkmcnt)
   const int h = blockIdx.x, seq = blockIdx.y;
+#if PK_DECODE_BT_PREFETCH
+  // the first partition's block-table window, requested before anything else so its round
+  // trip overlaps the context / q preparation instead of following it (entries past the
+  // sequence's blocks are in-bounds of the row and never used)
+  const int pre_b0 = static_cast<int>(blockIdx.z) * (kPart / bs);
+  int bt_pre = 0;
+  if (static_cast<int>(threadIdx.x) <= kPart / bs && pre_b0 + static_cast<int>(threadIdx.x) < max_blocks)
+    bt_pre = block_tables[static_cast<int64_t>(seq) * max_blocks + pre_b0 + threadIdx.x];
+#endif
   const int ctx = context_lens[seq];
   const int G = n_q / n_kv;
   if (ctx <= 0) {
@@ -298,7 +310,13 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     const int end = min(ctx, begin + kPart);
     const int b0 = begin / bs, nblk = (end - 1) / bs - b0 + 1;
     __syncthreads();  // the previous partition's LDS readers are done
-    for (int i = threadIdx.x; i < nblk; i += 64 * NW) bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
+#if PK_DECODE_BT_PREFETCH
+    if (part == static_cast<int>(blockIdx.z) && kPart % bs == 0) {  // nblk <= kPart / bs <= 64 * NW
+      if (static_cast<int>(threadIdx.x) < nblk) bt_s[threadIdx.x] = bt_pre;
+    } else
+#endif
+      for (int i = threadIdx.x; i < nblk; i += 64 * NW)
+        bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
     __syncthreads();
     WaveState st;
     init_state(st);
