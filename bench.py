@@ -49,7 +49,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--num-kv-blocks", type=int, default=0, help="KV blocks per replica (0: size from free HBM)")
     ap.add_argument("--gpu-mem-fraction", type=float, default=0.90)
-    ap.add_argument("--port-base", type=int, default=int(os.environ.get("POLYKEY_BENCH_PORT", "52100")))
+    ap.add_argument("--port-base", type=int, default=int(os.environ.get("POLYKEY_BENCH_PORT", "0")),
+                    help="gRPC port of rank 0 (rank r: base + r); 0: an ephemeral port per rank")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args(argv)
 
@@ -78,9 +79,9 @@ async def run_waves(args, engine, st, leaders_group):
     router = ToolRouter()
     cfg = ServerConfig(model=args.model, backend="local")
     attach_local_llm(router, cfg, logger, engine=engine)
-    port = args.port_base + st.rank
+    port = args.port_base + st.rank if args.port_base > 0 else 0
     srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
-    await srv.start()
+    port = await srv.start()
     channel = grpc.aio.insecure_channel(f"127.0.0.1:{port}", options=[
         ("grpc.max_receive_message_length", 64 << 20), ("grpc.max_send_message_length", 64 << 20)])
     unary = channel.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,

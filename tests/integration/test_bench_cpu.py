@@ -1,0 +1,31 @@
+"""bench.py driver contract on the CPU (tiny random-init model, gloo for 2 ranks): one JSON line
+from rank 0 with the BASELINE metric, whole-job value, and the DP parallelism / global batch
+of the launch; 2 ranks go through the torchrun child launch the driver itself uses."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ARGS = ["--model", "tiny-llama-gqa4", "--steps", "1", "--warmup", "1", "--concurrency", "4", "--prompt-len", "8",
+        "--max-tokens", "4", "--no-graphs"]
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_json_line(tmp_path, gpus):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus)] + ARGS, cwd=tmp_path,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["metric"].startswith("output tokens/sec via gRPC")
+    assert out["n_gpus"] == gpus and out["steps"] == 1 and out["warmup"] == 1
+    assert out["value"] > 0 and out["ms_per_step"] > 0 and out["higher_is_better"] is True
+    assert out["scaling"] == "weak" and out["dtype"] == "bf16"
+    assert out["config"]["parallelism"] == f"dp{gpus}" and out["config"]["global_batch"] == 4 * gpus
+    # every request completed its 4 tokens: tokens / elapsed over ranks = value
+    assert out["value"] == pytest.approx(4 * 4 * gpus / (out["ms_per_step"] / 1000.0), rel=0.02)
