@@ -198,8 +198,15 @@ def deinterleave_gate_up(w: torch.Tensor, block: int = 16):
     return v[:, 0].reshape(I2 // 2, K), v[:, 1].reshape(I2 // 2, K)
 
 
+# per-shape overrides for A/B runs: POLYKEY_SKINNY_SPLIT="6144x4096:8,4096x4096:4" (N x K : S)
+_SPLIT_OVERRIDE = {tuple(int(v) for v in k.split("x")): int(s) for k, s in
+                   (e.split(":") for e in os.environ.get("POLYKEY_SKINNY_SPLIT", "").split(",") if e)}
+
+
 def choose_split(N: int, K: int, M: int, target: int = _TARGET_WGS) -> int:
     """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows each)."""
+    if (N, K) in _SPLIT_OVERRIDE:
+        return _SPLIT_OVERRIDE[(N, K)]
     blocks = N // _ROWS_PER_WG
     s = 1
     while blocks * s < target and s < 16 and K % (_KCHUNK * s * 2) == 0:
