@@ -13,6 +13,7 @@ Differences: the process exits 1 when the run failed (the reference always exits
 """
 from __future__ import annotations
 
+import os
 import signal
 import sys
 import threading
@@ -146,9 +147,17 @@ def _state_name(st) -> str:
     return st.name if hasattr(st, "name") else str(st)
 
 
-def create_connection(address: str, timeout: float, logger: slog.Logger) -> grpc.Channel:
+def create_connection(address: str, timeout: float, logger: slog.Logger, tls_ca: str = "") -> grpc.Channel:
+    """Insecure channel as in the reference; ``tls_ca`` (or env ``POLYKEY_TLS_CA``): a PEM root
+    certificate to verify a TLS server with instead."""
     logger.info("Creating gRPC connection", server=address)
-    ch = grpc.insecure_channel(address, options=CHANNEL_OPTIONS)
+    tls_ca = tls_ca or os.environ.get("POLYKEY_TLS_CA", "")
+    if tls_ca:
+        with open(tls_ca, "rb") as f:
+            creds = grpc.ssl_channel_credentials(root_certificates=f.read())
+        ch = grpc.secure_channel(address, creds, options=CHANNEL_OPTIONS)
+    else:
+        ch = grpc.insecure_channel(address, options=CHANNEL_OPTIONS)
     try:
         wait_for_connection(ch, timeout, logger)
     except Exception as e:

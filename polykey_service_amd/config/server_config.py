@@ -40,6 +40,8 @@ class ServerConfig:
     device: str = "cuda"
     seed: int = 0
     shutdown_grace: float = 10.0
+    tls_cert: str = ""             # PEM certificate chain; with tls_key: TLS instead of insecure
+    tls_key: str = ""              # PEM private key
 
     @property
     def random_init(self) -> bool:
@@ -70,6 +72,8 @@ _ENV = {
     "device": "POLYKEY_DEVICE",
     "seed": "POLYKEY_SEED",
     "shutdown_grace": "POLYKEY_SHUTDOWN_GRACE",
+    "tls_cert": "POLYKEY_TLS_CERT",
+    "tls_key": "POLYKEY_TLS_KEY",
 }
 
 

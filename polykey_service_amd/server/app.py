@@ -11,6 +11,8 @@ Transport parameters (``main.go:68-72``): MaxConnectionIdle 5 min, Time 2 h, Tim
 streams): the reference's clients ping every 10 s with PermitWithoutStream while its server
 keeps grpc-go's 5 min default, which ends long-lived connections with GOAWAY
 ``too_many_pings``.
+[NEW] optional TLS: with a PEM certificate chain and key the port is bound
+with ``grpc.ssl_server_credentials`` instead of the reference's insecure transport.
 """
 from __future__ import annotations
 
@@ -50,8 +52,10 @@ def grpc_bind_address(addr: str) -> str:
 
 class PolykeyServer:
     def __init__(self, service, logger: Optional[slog.Logger] = None, listen_addr: str = ":50051",
-                 metrics=None, extra_handlers: Optional[List] = None, own_service: bool = True):
+                 metrics=None, extra_handlers: Optional[List] = None, own_service: bool = True,
+                 tls_cert: str = "", tls_key: str = ""):
         self.logger = logger or slog.Logger()
+        self.tls = (tls_cert, tls_key) if tls_cert and tls_key else None
         self.listen_addr = listen_addr
         self.service = service
         self.health = HealthServicer()
@@ -67,7 +71,14 @@ class PolykeyServer:
     async def start(self) -> int:
         bind = grpc_bind_address(self.listen_addr)
         try:
-            self.port = self.server.add_insecure_port(bind)
+            if self.tls is not None:
+                with open(self.tls[0], "rb") as f:
+                    chain = f.read()
+                with open(self.tls[1], "rb") as f:
+                    key = f.read()
+                self.port = self.server.add_secure_port(bind, grpc.ssl_server_credentials([(key, chain)]))
+            else:
+                self.port = self.server.add_insecure_port(bind)
         except RuntimeError as e:
             self.logger.error("failed to listen", error=str(e))
             raise
@@ -84,7 +95,8 @@ class PolykeyServer:
             for m in methods:
                 self.logger.info("Method available", service=name, method=m)
 
-        self.logger.info("server starting", address=self.listen_addr)
+        extra = {"tls": True} if self.tls is not None else {}  # the reference's schema otherwise
+        self.logger.info("server starting", address=self.listen_addr, **extra)
         await self.server.start()
         return self.port
 
@@ -164,7 +176,8 @@ async def amain(argv=None) -> int:
         from ..utils.metrics import Metrics
         metrics = Metrics.start(cfg.metrics_addr)
     service = build_service(cfg, logger)
-    srv = PolykeyServer(service, logger, cfg.listen_addr, metrics=metrics)
+    srv = PolykeyServer(service, logger, cfg.listen_addr, metrics=metrics, tls_cert=cfg.tls_cert,
+                        tls_key=cfg.tls_key)
     await srv.start()
     if getattr(service, "llm", None) is not None:
         service.llm.watchdog_s = 60.0

@@ -12,7 +12,8 @@ from polykey_service_amd.utils import slog
 class ServerThread:
     """Runs a PolykeyServer on its own event loop thread."""
 
-    def __init__(self, service=None):
+    def __init__(self, service=None, **server_kw):
+        self.server_kw = server_kw
         self.log = io.StringIO()
         self.service = service or ToolRouter()
         self.loop = asyncio.new_event_loop()
@@ -21,7 +22,8 @@ class ServerThread:
 
     def _run(self):
         asyncio.set_event_loop(self.loop)
-        self.srv = PolykeyServer(self.service, slog.Logger(self.log), "127.0.0.1:0", own_service=False)
+        self.srv = PolykeyServer(self.service, slog.Logger(self.log), "127.0.0.1:0", own_service=False,
+                                 **self.server_kw)
         self.port = self.loop.run_until_complete(self.srv.start())
         self.ready.set()
         self.loop.run_forever()
