@@ -239,7 +239,13 @@ def test_rowscale_folded_norm(M):
     wgu = gemm.interleave_gate_up(g, u)
     y = gemm.linear_silu(res, wgu, packed=gemm.pack_weight(gemm.fold_norm(wgu, nw)), rowscale=rs)
     exp = ref.silu_and_mul(torch.cat([xin @ g.float().t(), xin @ u.float().t()], -1).to(torch.bfloat16)).float()
-    # the rounding points differ (bf16 W diag(w) vs bf16 normalised x): |silu(g) u| reaches ~30
-    # here, so compare against the output scale rather than per element
+    # exact-op reference: rinv[m] * (residual @ (W diag(w))^T) in fp32, same bf16 folded weights
+    rinv = torch.rsqrt(res.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    h = (res.float() @ gemm.fold_norm(wgu, nw).float().t()) * rinv
+    exp_folded = ref.silu_and_mul_interleaved(h.to(torch.bfloat16)).float()
+    err = (y.float() - exp_folded).abs().max().item()
+    assert err <= 0.01 * exp_folded.abs().max().item(), err
+    # vs the unfolded op the rounding points differ (bf16 W diag(w) vs bf16 normalised x) and
+    # |silu(g) u| reaches ~90, so compare against the output scale rather than per element
     err = (y.float() - exp).abs().max().item()
-    assert err <= 0.01 * exp.abs().max().item(), err
+    assert err <= 0.025 * exp.abs().max().item(), err
