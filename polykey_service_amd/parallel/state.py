@@ -79,7 +79,10 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
                        device=dev)
     if world > 1:
         # POLYKEY_DIST_BACKEND overrides (gloo: several ranks on one GPU, which RCCL refuses)
-        be = backend or os.environ.get("POLYKEY_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
+        # and by default when this node has more local ranks than GPUs
+        shared = dev.type == "cuda" and int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > max(n_dev, 1)
+        be = backend or os.environ.get("POLYKEY_DIST_BACKEND") or ("nccl" if dev.type == "cuda" and not shared
+                                                                   else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # a hung or failed RCCL collective aborts the communicator and raises in this process
         # (timeout_s), which takes the engine down → health NOT_SERVING → supervisor restart
