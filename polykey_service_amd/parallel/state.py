@@ -56,6 +56,14 @@ def set_state(st: ParallelState) -> None:
     _STATE = st
 
 
+def pick_backend(dev_type: str, n_dev: int, local_world: int, override: Optional[str] = None) -> str:
+    """RCCL ("nccl") for one rank per GPU; gloo on CPU and when a node runs more local ranks
+    than it has GPUs (RCCL refuses two ranks on one device); ``override`` wins."""
+    if override:
+        return override
+    return "nccl" if dev_type == "cuda" and local_world <= max(n_dev, 1) else "gloo"
+
+
 def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backend: Optional[str] = None,
                   timeout_s: float = 600.0) -> ParallelState:
     """Initialise from torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).
@@ -79,10 +87,8 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
                        device=dev)
     if world > 1:
         # POLYKEY_DIST_BACKEND overrides (gloo: several ranks on one GPU, which RCCL refuses)
-        # and by default when this node has more local ranks than GPUs
-        shared = dev.type == "cuda" and int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > max(n_dev, 1)
-        be = backend or os.environ.get("POLYKEY_DIST_BACKEND") or ("nccl" if dev.type == "cuda" and not shared
-                                                                   else "gloo")
+        be = pick_backend(dev.type, n_dev, int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
+                          backend or os.environ.get("POLYKEY_DIST_BACKEND"))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # a hung or failed RCCL collective aborts the communicator and raises in this process
         # (timeout_s), which takes the engine down → health NOT_SERVING → supervisor restart
