@@ -199,10 +199,13 @@ def main(argv=None) -> int:
     if dist.is_initialized():
         # TP workers contribute (0 tokens, 0 s, no latencies); elapsed = max over ranks
         allr = [None] * st.world_size
-        dist.all_gather_object(allr, (tokens, elapsed, lats))
+        dist.all_gather_object(allr, (tokens, elapsed, lats, engine.scheduler.num_cached_tokens))
         tokens = sum(x[0] for x in allr)
         elapsed = max(x[1] for x in allr)
         lats = [l for x in allr for l in x[2]]
+        cached = sum(x[3] for x in allr)
+    else:
+        cached = engine.scheduler.num_cached_tokens
     if st.rank == 0:
         p50 = statistics.median(lats) if lats else None
         value = tokens / elapsed if elapsed > 0 else 0.0
@@ -230,6 +233,9 @@ def main(argv=None) -> int:
                 "concurrency_per_replica": args.concurrency,
                 "rpc": f"ExecuteTool ({args.mode})",
                 "hip_graphs": not args.no_graphs,
+                # every prompt is unique, so the prefix cache must serve nothing (no skipped work)
+                "prefix_caching": ecfg.prefix_caching,
+                "prefix_cache_hit_tokens": cached,
                 "init_s": round(init_s, 1),
             },
         }

@@ -16,10 +16,24 @@
 namespace py = pybind11;
 using I32 = py::array_t<int32_t, py::array::c_style>;
 using I64 = py::array_t<int64_t, py::array::c_style>;
+using U64 = py::array_t<uint64_t, py::array::c_style>;
 
 class BlockManager : public pk::BlockManagerCore {
  public:
   using pk::BlockManagerCore::BlockManagerCore;
+
+  U64 prefix_hashes_py(I32 tokens, int64_t max_blocks) const {
+    const int64_t n = tokens.shape(0);
+    U64 out(std::max<int64_t>(0, std::min<int64_t>(n / block_size(), max_blocks)));
+    prefix_hashes(tokens.data(), n, out.mutable_data(), out.shape(0));
+    return out;
+  }
+  int64_t match_prefix_py(int64_t seq, U64 hashes, int64_t n) {
+    return match_prefix(seq, hashes.data(), std::min<int64_t>(n, hashes.shape(0)));
+  }
+  void commit_prefix_py(int64_t seq, U64 hashes, int64_t n) {
+    commit_prefix(seq, hashes.data(), std::min<int64_t>(n, hashes.shape(0)));
+  }
 
   int64_t pack_step(I64 seq_ids, I32 num_computed, I32 num_new, I32 tokens, I32 input_ids, I32 positions,
                     I32 slot_mapping, I32 block_tables, int max_blocks, I32 context_lens, I32 cu_q) {
@@ -41,8 +55,17 @@ class BlockManager : public pk::BlockManagerCore {
 PYBIND11_MODULE(_pk_runtime, m) {
   m.doc() = "polykey native runtime: paged KV block manager and step packer";
   py::class_<BlockManager>(m, "BlockManager")
-      .def(py::init<int64_t, int, int64_t>(), py::arg("num_blocks"), py::arg("block_size"),
-           py::arg("watermark_blocks") = 0)
+      .def(py::init<int64_t, int, int64_t, bool>(), py::arg("num_blocks"), py::arg("block_size"),
+           py::arg("watermark_blocks") = 0, py::arg("prefix_caching") = false)
+      .def_property_readonly("prefix_caching", &BlockManager::prefix_caching)
+      .def_property_readonly("num_cached", &BlockManager::num_cached)
+      .def_property_readonly("prefix_queries", &BlockManager::prefix_queries)
+      .def_property_readonly("prefix_hits", &BlockManager::prefix_hits)
+      .def("prefix_hashes", &BlockManager::prefix_hashes_py, py::arg("tokens"), py::arg("max_blocks") = INT64_MAX)
+      .def("match_prefix", &BlockManager::match_prefix_py, py::arg("seq"), py::arg("hashes"), py::arg("n"))
+      .def("commit_prefix", &BlockManager::commit_prefix_py, py::arg("seq"), py::arg("hashes"), py::arg("n"))
+      .def("reset_prefix_cache", &BlockManager::reset_prefix_cache)
+      .def("ref_count", &BlockManager::ref_count)
       .def_property_readonly("num_free", &BlockManager::num_free)
       .def_property_readonly("num_blocks", &BlockManager::num_blocks)
       .def_property_readonly("block_size", &BlockManager::block_size)

@@ -1,8 +1,16 @@
 // Paged KV-cache block manager core (no Python dependency): used by the pybind11 module
 // (block_manager.cpp) and by the sanitizer test binary (csrc/tests/test_native.cpp).
+//
+// Automatic prefix caching (optional): a full block of prompt tokens whose KV has been computed
+// is registered under a chained hash of all tokens up to and including it (prefix_hashes).  A
+// newly admitted sequence takes the longest run of registered blocks matching its own hashes
+// (match_prefix, reference-counted, shared read-only) and computes only the rest.  Released
+// blocks that carry a hash stay cached in an LRU list and count as free; allocation evicts
+// the least recently released one only when the plain free list is empty.
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <list>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -12,14 +20,23 @@ namespace pk {
 
 class BlockManagerCore {
  public:
-  BlockManagerCore(int64_t num_blocks, int block_size, int64_t watermark_blocks)
-      : num_blocks_(num_blocks), block_size_(block_size), watermark_(watermark_blocks) {
+  BlockManagerCore(int64_t num_blocks, int block_size, int64_t watermark_blocks, bool prefix_caching = false)
+      : num_blocks_(num_blocks), block_size_(block_size), watermark_(watermark_blocks), prefix_caching_(prefix_caching) {
     if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("num_blocks and block_size must be > 0");
     free_.reserve(num_blocks);
     for (int64_t b = num_blocks - 1; b >= 0; --b) free_.push_back(static_cast<int32_t>(b));
+    ref_.assign(num_blocks, 0);
+    hash_.assign(num_blocks, 0);
+    lru_pos_.resize(num_blocks);
+    in_lru_.assign(num_blocks, 0);
   }
 
-  int64_t num_free() const { return static_cast<int64_t>(free_.size()); }
+  // free = never-used / unhashed blocks + cached blocks nobody references (evictable)
+  int64_t num_free() const { return static_cast<int64_t>(free_.size() + lru_.size()); }
+  int64_t num_cached() const { return static_cast<int64_t>(cached_.size()); }
+  bool prefix_caching() const { return prefix_caching_; }
+  int64_t prefix_queries() const { return queries_; }
+  int64_t prefix_hits() const { return hits_; }
   int64_t num_blocks() const { return num_blocks_; }
   int block_size() const { return block_size_; }
   int64_t blocks_for(int64_t tokens) const { return (tokens + block_size_ - 1) / block_size_; }
@@ -38,18 +55,74 @@ class BlockManagerCore {
     const int64_t need = needed(seq, total_tokens);
     if (need > num_free()) return false;
     auto& t = tables_[seq];
-    for (int64_t i = 0; i < need; ++i) {
-      t.push_back(free_.back());
-      free_.pop_back();
-    }
+    for (int64_t i = 0; i < need; ++i) t.push_back(take_block());
     return true;
   }
 
   void free_seq(int64_t seq) {
     auto it = tables_.find(seq);
     if (it == tables_.end()) return;
-    for (auto r = it->second.rbegin(); r != it->second.rend(); ++r) free_.push_back(*r);
+    for (auto r = it->second.rbegin(); r != it->second.rend(); ++r) release(*r);
     tables_.erase(it);
+  }
+
+  // Chained hashes of the full blocks of tokens[0:n] (at most max_out): h_i covers every token
+  // of blocks 0..i, so equal hashes mean equal prefixes (up to 64-bit collisions).  Never 0.
+  int64_t prefix_hashes(const int32_t* tokens, int64_t n, uint64_t* out, int64_t max_out) const {
+    const int64_t nb = std::min<int64_t>(n / block_size_, max_out);
+    uint64_t h = 0x6a09e667f3bcc908ULL;
+    for (int64_t b = 0; b < nb; ++b) {
+      for (int j = 0; j < block_size_; ++j) {
+        h ^= static_cast<uint32_t>(tokens[b * block_size_ + j]);
+        h *= 0x100000001b3ULL;  // FNV-1a step over each token
+      }
+      h = mix(h + static_cast<uint64_t>(b));
+      out[b] = h ? h : 1;
+    }
+    return nb;
+  }
+
+  // A sequence without blocks takes the longest run of cached blocks matching hashes[0:n];
+  // returns the number of blocks taken (its first matched * block_size tokens are computed).
+  int64_t match_prefix(int64_t seq, const uint64_t* hashes, int64_t n) {
+    if (!prefix_caching_ || n <= 0 || tables_.count(seq)) return 0;
+    queries_ += n;
+    std::vector<int32_t> t;
+    for (int64_t i = 0; i < n; ++i) {
+      auto it = cached_.find(hashes[i]);
+      if (it == cached_.end()) break;
+      const int32_t b = it->second;
+      if (in_lru_[b]) {
+        lru_.erase(lru_pos_[b]);
+        in_lru_[b] = 0;
+      }
+      ++ref_[b];
+      t.push_back(b);
+    }
+    hits_ += static_cast<int64_t>(t.size());
+    const int64_t got = static_cast<int64_t>(t.size());
+    if (got) tables_[seq] = std::move(t);
+    return got;
+  }
+
+  // Registers the sequence's first n blocks (their KV computed) under hashes[0:n].  A block
+  // already registered, or a hash another block already holds, is left as it is.
+  void commit_prefix(int64_t seq, const uint64_t* hashes, int64_t n) {
+    if (!prefix_caching_) return;
+    auto it = tables_.find(seq);
+    if (it == tables_.end()) return;
+    const int64_t m = std::min<int64_t>(n, static_cast<int64_t>(it->second.size()));
+    for (int64_t i = 0; i < m; ++i) {
+      const int32_t b = it->second[i];
+      if (hash_[b] != 0 || hashes[i] == 0 || cached_.count(hashes[i])) continue;
+      hash_[b] = hashes[i];
+      cached_.emplace(hashes[i], b);
+    }
+  }
+
+  // Drops every cached block nobody references (back to the plain free list).
+  void reset_prefix_cache() {
+    while (!lru_.empty()) evict_front(true);
   }
 
   bool has(int64_t seq) const { return tables_.count(seq) != 0; }
@@ -62,6 +135,7 @@ class BlockManagerCore {
     return p ? *p : std::vector<int32_t>{};
   }
   int64_t num_seqs() const { return static_cast<int64_t>(tables_.size()); }
+  int32_t ref_count(int32_t b) const { return ref_.at(b); }
 
   // Raw-pointer step packer (see block_manager.cpp for the layout).  Returns T.
   int64_t pack(int64_t n, const int64_t* sid, const int32_t* nc, const int32_t* nn, const int32_t* tok, int32_t* ids,
@@ -93,10 +167,57 @@ class BlockManagerCore {
   }
 
  private:
+  static uint64_t mix(uint64_t z) {  // splitmix64 finaliser
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+  }
+
+  void evict_front(bool to_free_list) {
+    const int32_t b = lru_.front();
+    lru_.pop_front();
+    in_lru_[b] = 0;
+    cached_.erase(hash_[b]);
+    hash_[b] = 0;
+    if (to_free_list) free_.push_back(b);
+  }
+
+  int32_t take_block() {
+    int32_t b;
+    if (!free_.empty()) {
+      b = free_.back();
+      free_.pop_back();
+    } else {  // the least recently released cached block
+      b = lru_.front();
+      evict_front(false);
+    }
+    ref_[b] = 1;
+    return b;
+  }
+
+  void release(int32_t b) {
+    if (--ref_[b] > 0) return;
+    if (hash_[b] != 0) {
+      lru_.push_back(b);
+      lru_pos_[b] = std::prev(lru_.end());
+      in_lru_[b] = 1;
+    } else {
+      free_.push_back(b);
+    }
+  }
+
   int64_t num_blocks_;
   int block_size_;
   int64_t watermark_;
+  bool prefix_caching_;
+  int64_t queries_ = 0, hits_ = 0;
   std::vector<int32_t> free_;
+  std::vector<int32_t> ref_;
+  std::vector<uint64_t> hash_;
+  std::list<int32_t> lru_;
+  std::vector<std::list<int32_t>::iterator> lru_pos_;
+  std::vector<char> in_lru_;
+  std::unordered_map<uint64_t, int32_t> cached_;
   std::unordered_map<int64_t, std::vector<int32_t>> tables_;
 };
 

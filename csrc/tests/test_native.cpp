@@ -73,6 +73,57 @@ static void test_block_manager_churn() {
   CHECK(bm.can_allocate(999, (NB - 4) * BS, true));
 }
 
+// Prefix caching under ASan/UBSan: sequences over 4 shared token prefixes are admitted through
+// match_prefix / commit_prefix, grown, and freed at random; refcounts must equal table
+// membership, free + referenced must equal the pool, and the LRU eviction path is exercised
+// because the pool is far smaller than the working set.
+static void test_prefix_cache_churn() {
+  const int64_t NB = 64;
+  const int BS = 8;
+  pk::BlockManagerCore bm(NB, BS, 0, true);
+  std::mt19937_64 rng(99);
+  std::vector<std::vector<uint64_t>> pref(4, std::vector<uint64_t>(4));
+  for (int p = 0; p < 4; ++p) {
+    std::vector<int32_t> toks(4 * BS);
+    for (int i = 0; i < 4 * BS; ++i) toks[i] = p * 1000 + (i % 7);
+    CHECK(bm.prefix_hashes(toks.data(), 4 * BS, pref[p].data(), 4) == 4);
+  }
+  std::unordered_map<int64_t, int64_t> len;
+  for (int it = 0; it < 20000; ++it) {
+    const int op = static_cast<int>(rng() % 3);
+    const int64_t seq = static_cast<int64_t>(rng() % 24);
+    if (op == 0 && !len.count(seq)) {
+      const auto& h = pref[rng() % 4];
+      const int64_t got = bm.match_prefix(seq, h.data(), 3);
+      if (bm.allocate(seq, 4 * BS)) {
+        bm.commit_prefix(seq, h.data(), 4);
+        len[seq] = 4 * BS;
+      } else {
+        bm.free_seq(seq);
+        CHECK(got >= 0);
+      }
+    } else if (op == 1 && len.count(seq)) {
+      const int64_t total = len[seq] + 1 + static_cast<int64_t>(rng() % 40);
+      if (bm.allocate(seq, total)) len[seq] = total;
+    } else if (op == 2) {
+      bm.free_seq(seq);
+      len.erase(seq);
+    }
+    if (it % 499 == 0) {
+      std::unordered_map<int32_t, int> refs;
+      for (auto& kv : len)
+        for (int32_t b : bm.table(kv.first)) ++refs[b];
+      for (auto& kv : refs) CHECK(bm.ref_count(kv.first) == kv.second);
+      CHECK(static_cast<int64_t>(refs.size()) + bm.num_free() == NB);
+    }
+  }
+  for (auto& kv : len) bm.free_seq(kv.first);
+  CHECK(bm.num_free() == NB);
+  CHECK(bm.prefix_hits() > 0);
+  bm.reset_prefix_cache();
+  CHECK(bm.num_cached() == 0 && bm.num_free() == NB);
+}
+
 static void test_pack() {
   pk::BlockManagerCore bm(32, 4, 0);
   CHECK(bm.allocate(7, 6));   // 2 blocks
@@ -131,6 +182,7 @@ static void test_aes() {
 
 int main() {
   test_block_manager_churn();
+  test_prefix_cache_churn();
   test_pack();
   test_aes();
   if (g_fail) {

@@ -7,6 +7,7 @@ The async/gRPC face is :mod:`polykey_service_amd.engine.async_llm`.
 from __future__ import annotations
 
 import dataclasses
+import os
 import time
 import uuid
 from typing import Dict, Iterable, List, Optional
@@ -41,6 +42,9 @@ class EngineConfig:
     watermark: float = 0.01
     device: str = ""
     overlap: bool = False  # pipelined steps (see LLMEngine.step); AsyncLLM turns it on
+    # automatic prefix caching (csrc/runtime/block_manager.h); POLYKEY_PREFIX_CACHING=0 disables
+    prefix_caching: bool = dataclasses.field(
+        default_factory=lambda: os.environ.get("POLYKEY_PREFIX_CACHING", "1") != "0")
 
     @classmethod
     def from_server_config(cls, sc) -> "EngineConfig":
@@ -79,7 +83,7 @@ class LLMEngine:
         self.runner = ModelRunner(model, rcfg, dev)
         nblocks = self.runner.allocate_kv_cache()
         rt = load_extension("_pk_runtime")
-        self.bm = rt.BlockManager(nblocks, cfg.block_size, int(nblocks * cfg.watermark))
+        self.bm = rt.BlockManager(nblocks, cfg.block_size, int(nblocks * cfg.watermark), cfg.prefix_caching)
         self.runner.bm = self.bm
         self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
         if cfg.hip_graphs and dev.type == "cuda":
@@ -153,6 +157,7 @@ class LLMEngine:
         now = time.monotonic()
         for s, n in batch.prefills:
             s.num_computed += n
+            self.scheduler.commit_prefix(s)  # the step that wrote these blocks' KV has completed
         for s in batch.decodes:
             s.num_computed += 1
         done = []

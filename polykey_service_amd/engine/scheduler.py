@@ -12,6 +12,12 @@ sequence cap (``max_num_seqs``):
    blocks the queue (no overtaking → no starvation).
 
 KV bookkeeping lives in the native :class:`_pk_runtime.BlockManager` (``csrc/runtime``).
+
+Automatic prefix caching (block manager built with ``prefix_caching=True``): a sequence
+admitted with nothing computed first takes the cached blocks matching the longest prefix of
+its tokens (chained block hashes) and starts its prefill after them — leaving at least two
+tokens to compute, so it still runs a prefill that samples.  The engine registers a prefill's
+full blocks (:meth:`Scheduler.commit_prefix`) once the step that wrote their KV completed.
 """
 from __future__ import annotations
 
@@ -19,6 +25,8 @@ import collections
 import dataclasses
 import time
 from typing import Deque, Dict, List, Optional, Tuple
+
+import numpy as np
 
 from .sequence import FinishReason, Sequence, SeqStatus
 
@@ -56,6 +64,9 @@ class Scheduler:
         self.running: List[Sequence] = []
         self.by_request: Dict[str, Sequence] = {}
         self.num_preemptions = 0
+        self.prefix_caching = bool(getattr(block_manager, "prefix_caching", False))
+        self._hashes: Dict[int, np.ndarray] = {}  # seq_id -> chained block hashes at admission
+        self.num_cached_tokens = 0  # prompt tokens served from the prefix cache
 
     # --------------------------------------------------------------- queue ops
     def add(self, seq: Sequence) -> None:
@@ -86,6 +97,7 @@ class Scheduler:
             except ValueError:
                 pass
         self.bm.free_seq(seq.seq_id)
+        self._hashes.pop(seq.seq_id, None)
         seq.status = SeqStatus.FINISHED
         seq.finish_reason = FinishReason.ABORT
         seq.finish_time = time.monotonic()
@@ -96,6 +108,7 @@ class Scheduler:
         seq.finish_reason = reason
         seq.finish_time = time.monotonic()
         self.bm.free_seq(seq.seq_id)
+        self._hashes.pop(seq.seq_id, None)
         self.by_request.pop(seq.request_id, None)
 
     def remove_finished(self) -> None:
@@ -106,6 +119,31 @@ class Scheduler:
 
     def num_unfinished(self) -> int:
         return len(self.waiting) + len(self.running)
+
+    # ------------------------------------------------------------ prefix cache
+    def _match_prefix(self, seq: Sequence) -> None:
+        """Admission of a sequence with nothing computed: reuse cached blocks of its prefix."""
+        if not self.prefix_caching or seq.num_computed != 0 or self.bm.has(seq.seq_id):
+            return
+        bs = self.bm.block_size
+        toks = np.asarray(seq.token_slice(0, seq.num_tokens), dtype=np.int32)
+        h = self.bm.prefix_hashes(toks)
+        self._hashes[seq.seq_id] = h
+        usable = max(0, (seq.num_tokens - 2) // bs)  # >= 2 tokens left: the step still samples
+        got = self.bm.match_prefix(seq.seq_id, h, min(usable, len(h)))
+        seq.num_computed = got * bs
+
+    def _unmatch(self, seq: Sequence) -> None:
+        """Admission failed after a match: hand the blocks back (they stay cached)."""
+        if self.prefix_caching and seq.num_computed and self.bm.has(seq.seq_id):
+            self.bm.free_seq(seq.seq_id)
+            seq.num_computed = 0
+
+    def commit_prefix(self, seq: Sequence) -> None:
+        """Register the sequence's full blocks whose KV is now in the cache."""
+        h = self._hashes.get(seq.seq_id)
+        if h is not None and not seq.is_finished():
+            self.bm.commit_prefix(seq.seq_id, h, seq.num_computed // self.bm.block_size)
 
     # ------------------------------------------------------------------ policy
     def _preempt_youngest(self, protect: Sequence) -> Optional[Sequence]:
@@ -168,10 +206,14 @@ class Scheduler:
             seq = self.waiting[0]
             if seq.seq_id in {s.seq_id for s in preempted}:
                 break  # do not thrash: re-admit preempted sequences next step
+            self._match_prefix(seq)
             n = min(seq.num_pending, budget, self.max_prefill_chunk)
             if not self.bm.can_allocate(seq.seq_id, seq.num_computed + n, True):
+                self._unmatch(seq)
                 break
             self.bm.allocate(seq.seq_id, seq.num_computed + n)
+            self.num_cached_tokens += seq.num_computed
+            seq.num_cached_tokens += seq.num_computed
             self.waiting.popleft()
             seq.status = SeqStatus.RUNNING
             if seq.first_scheduled is None:

@@ -73,7 +73,7 @@ _ids = itertools.count(1)
 class Sequence:
     __slots__ = ("seq_id", "request_id", "prompt_ids", "output_ids", "params", "status", "num_computed",
                  "arrival", "first_scheduled", "first_token_time", "finish_time", "finish_reason",
-                 "num_preemptions", "eos_token_id", "token_times", "user")
+                 "num_preemptions", "eos_token_id", "token_times", "user", "num_cached_tokens")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams, eos_token_id: int = -1,
                  user=None):
@@ -90,6 +90,7 @@ class Sequence:
         self.finish_time: Optional[float] = None
         self.finish_reason: Optional[FinishReason] = None
         self.num_preemptions = 0
+        self.num_cached_tokens = 0  # tokens whose KV came from the prefix cache
         self.eos_token_id = eos_token_id
         self.token_times: List[float] = []
         self.user = user
@@ -152,4 +153,5 @@ def seq_metrics(s: Sequence) -> dict:
     return {
         "queue_s": (s.first_scheduled - t0) if s.first_scheduled else None,
         "ttft_s": ttft, "e2e_s": e2e, "mean_itl_s": itl, "preemptions": s.num_preemptions,
+        "cached_prompt_tokens": s.num_cached_tokens,
     }
