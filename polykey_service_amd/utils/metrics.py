@@ -37,6 +37,10 @@ class Metrics:
         self.step_seconds = Histogram("polykey_engine_step_seconds", "engine step wall time", buckets=_TOK_BUCKETS,
                                       registry=r)
         self.preemptions = Gauge("polykey_engine_preemptions", "preemptions so far", registry=r)
+        self.cached_tokens = Gauge("polykey_engine_prefix_cache_hit_tokens", "prompt tokens served from the "
+                                   "prefix cache so far", registry=r)
+        self.cached_blocks = Gauge("polykey_engine_prefix_cache_blocks", "KV blocks registered in the prefix cache",
+                                   registry=r)
 
     @classmethod
     def start(cls, addr: str) -> "Metrics":
@@ -57,6 +61,8 @@ class Metrics:
         bm = engine.bm
         self.kv_util.set(1.0 - bm.num_free / max(bm.num_blocks, 1))
         self.preemptions.set(sch.num_preemptions)
+        self.cached_tokens.set(getattr(sch, "num_cached_tokens", 0))
+        self.cached_blocks.set(getattr(bm, "num_cached", 0))
         n = 0
         for o in outputs:
             n += len(o.new_token_ids)

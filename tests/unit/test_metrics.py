@@ -6,11 +6,11 @@ from polykey_service_amd.utils.metrics import Metrics
 
 
 class _BM:
-    num_free, num_blocks = 30, 40
+    num_free, num_blocks, num_cached = 30, 40, 5
 
 
 class _Sch:
-    running, waiting, num_preemptions = [1, 2], [3], 2
+    running, waiting, num_preemptions, num_cached_tokens = [1, 2], [3], 2, 160
 
 
 class _Eng:
@@ -29,3 +29,4 @@ def test_metrics_export():
     assert 'polykey_llm_requests_total{finish_reason="length"} 1.0' in text
     assert "polykey_engine_kv_utilization 0.25" in text
     assert "polykey_engine_running_seqs 2.0" in text and "polykey_llm_ttft_seconds_count 1.0" in text
+    assert "polykey_engine_prefix_cache_hit_tokens 160.0" in text and "polykey_engine_prefix_cache_blocks 5.0" in text
