@@ -21,6 +21,13 @@ _SAMPLING_KEYS = ("max_tokens", "temperature", "top_p", "top_k", "min_p", "seed"
                   "stop_token_ids")
 
 
+
+def _usage(n_prompt: int, n_out: int, metrics) -> dict:
+    """OpenAI usage block; ``prompt_tokens_details.cached_tokens`` = prompt tokens whose KV came
+    from the prefix cache (engine/scheduler.py)."""
+    return {"prompt_tokens": n_prompt, "completion_tokens": n_out, "total_tokens": n_prompt + n_out,
+            "prompt_tokens_details": {"cached_tokens": int((metrics or {}).get("cached_prompt_tokens") or 0)}}
+
 def _llm(router, model: Optional[str]):
     """The AsyncLLM serving ``model`` (the ``llm.chat`` tool registered for it)."""
     models = router.models("llm.chat")
@@ -96,6 +103,7 @@ def create_app(router):
                 toks: List[int] = []
                 detok = IncrementalDetokenizer(tok)
                 finish = None
+                final_metrics = None
                 if chat:
                     first = {"id": rid, "object": "chat.completion.chunk", "created": created, "model": model,
                              "choices": [{"index": 0, "delta": {"role": "assistant"}, "finish_reason": None}]}
@@ -105,6 +113,7 @@ def create_app(router):
                     async for out in agen:
                         toks.extend(out.new_token_ids)
                         finish = out.finish_reason
+                        final_metrics = out.metrics or final_metrics
                         delta = detok.push(out.new_token_ids)
                         if delta:
                             choice = ({"index": 0, "delta": {"content": delta}, "finish_reason": None} if chat
@@ -118,8 +127,7 @@ def create_app(router):
                                else {"index": 0, "text": "", "finish_reason": finish})
                 last = {"id": rid, "object": obj + (".chunk" if chat else ""), "created": created, "model": model,
                         "choices": [last_choice],
-                        "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": len(toks),
-                                  "total_tokens": len(prompt_ids) + len(toks)}}
+                        "usage": _usage(len(prompt_ids), len(toks), final_metrics)}
                 yield f"data: {json.dumps(last)}\n\n"
                 yield "data: [DONE]\n\n"
 
@@ -135,8 +143,7 @@ def create_app(router):
                    "finish_reason": last.finish_reason if last else None} if chat
                   else {"index": 0, "text": text, "finish_reason": last.finish_reason if last else None})
         return {"id": rid, "object": obj, "created": created, "model": model, "choices": [choice],
-                "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": len(toks),
-                          "total_tokens": len(prompt_ids) + len(toks)}}
+                "usage": _usage(len(prompt_ids), len(toks), last.metrics if last else None)}
 
     @app.post("/v1/chat/completions")
     async def chat_completions(request: Request):

@@ -151,7 +151,14 @@ def test_openai_routes(router):
     assert body["usage"]["completion_tokens"] == 5 and body["choices"][0]["message"]["role"] == "assistant"
     r = c.post("/v1/completions", json={"model": "tiny-llama", "prompt": [1, 4, 5], "max_tokens": 3,
                                         "ignore_eos": True})
-    assert r.json()["usage"] == {"prompt_tokens": 3, "completion_tokens": 3, "total_tokens": 6}
+    assert r.json()["usage"] == {"prompt_tokens": 3, "completion_tokens": 3, "total_tokens": 6,
+                                 "prompt_tokens_details": {"cached_tokens": 0}}
+    # the same 70-token prompt again: its first two 32-token KV blocks come from the prefix cache
+    long_prompt = [1] + list(range(500, 569))
+    for cached in (0, 64):
+        r = c.post("/v1/completions", json={"model": "tiny-llama", "prompt": long_prompt, "max_tokens": 2,
+                                            "ignore_eos": True})
+        assert r.json()["usage"]["prompt_tokens_details"]["cached_tokens"] == cached
     with c.stream("POST", "/v1/chat/completions", json={"model": "tiny-llama", "stream": True, "max_tokens": 6,
                                                         "ignore_eos": True,
                                                         "messages": [{"role": "user", "content": "s"}]}) as resp:
