@@ -27,5 +27,7 @@ def test_bench_json_line(tmp_path, gpus):
     assert out["value"] > 0 and out["ms_per_step"] > 0 and out["higher_is_better"] is True
     assert out["scaling"] == "weak" and out["dtype"] == "bf16"
     assert out["config"]["parallelism"] == f"dp{gpus}" and out["config"]["global_batch"] == 4 * gpus
+    # unique random prompts: the prefix cache serves nothing, so no prefill work is skipped
+    assert out["config"]["prefix_caching"] is True and out["config"]["prefix_cache_hit_tokens"] == 0
     # every request completed its 4 tokens: tokens / elapsed over ranks = value
     assert out["value"] == pytest.approx(4 * 4 * gpus / (out["ms_per_step"] / 1000.0), rel=0.02)
