@@ -104,8 +104,7 @@ async def run_waves(args, engine, st, leaders_group):
         return req
 
     async def one(req):
-        t_build = time.perf_counter()
-        t0 = time.perf_counter()
+        t0 = time.perf_counter()  # submit time (requests are prebuilt: see `waves` below)
         if args.mode == "unary":
             resp = await unary(req, timeout=600)
         else:
@@ -117,7 +116,7 @@ async def run_waves(args, engine, st, leaders_group):
         usage = resp.struct_output.fields["usage"].struct_value.fields
         if timing:
             m = proto.struct_to_dict(resp.struct_output)["metrics"]
-            marks.append((t_build, t0, t1, m))
+            marks.append((t0, t1, m))
         return int(usage["completion_tokens"].number_value), dt
 
     async def wave(reqs):
@@ -128,14 +127,14 @@ async def run_waves(args, engine, st, leaders_group):
             # host-side breakdown of the wave (stderr): request build/submit span, the engine's
             # view (queue, TTFT, e2e) and what the RPC path adds on top of it
             te = time.perf_counter()
-            sub = max(m[1] for m in marks) - tw
-            rpc = sorted((m[2] - m[1]) - m[3]["server_e2e_s"] for m in marks)
-            ttft = sorted(m[3].get("ttft_s", 0.0) for m in marks)
-            e2e = sorted(m[3].get("e2e_s", 0.0) for m in marks)
+            sub = max(m[0] for m in marks) - tw
+            rpc = sorted((m[1] - m[0]) - m[2]["server_e2e_s"] for m in marks)
+            ttft = sorted(m[2].get("ttft_s", 0.0) for m in marks)
+            e2e = sorted(m[2].get("e2e_s", 0.0) for m in marks)
             print(f"[wave] wall {1e3 * (te - tw):.1f} ms | last submit +{1e3 * sub:.1f} ms | engine e2e "
                   f"min/max {1e3 * e2e[0]:.1f}/{1e3 * e2e[-1]:.1f} ms | ttft min/max {1e3 * ttft[0]:.1f}/"
                   f"{1e3 * ttft[-1]:.1f} ms | rpc overhead p50/max {1e3 * rpc[len(rpc) // 2]:.2f}/{1e3 * rpc[-1]:.2f} ms | "
-                  f"last response +{1e3 * (max(m[2] for m in marks) - tw):.1f} ms", file=sys.stderr, flush=True)
+                  f"last response +{1e3 * (max(m[1] for m in marks) - tw):.1f} ms", file=sys.stderr, flush=True)
         return sum(r[0] for r in res), [r[1] for r in res]
 
     for _ in range(args.warmup):

@@ -17,7 +17,11 @@
 // lives in device memory (per workgroup), so the kernel replays correctly inside HIP graphs.
 // IPC buffers are allocated uncached (hipDeviceMallocUncached): peers' stores become visible
 // to polling loads without cache maintenance, and remote data reads are never served stale.
-// A spin that exceeds its bound sets an error word and exits instead of hanging the GPU.
+// Failure: a peer that does not arrive within the wall-clock timeout sets the
+// error word -- in host-mapped pinned memory, so the engine reads it every step without a GPU
+// sync -- and from then on every call of this context (and of every peer, which in turn times
+// out waiting for it) skips its waits and its output: the engine sees the word, fails loudly
+// (health NOT_SERVING, non-zero exit) instead of serving tokens summed from stale peer slots.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -36,7 +40,13 @@ struct Signals {                                 // at the start of every rank's
   uint32_t flag[kMaxBlocks][kMaxRanks];          // written by peers (remote stores)
   uint32_t flag2[kMaxBlocks][kMaxRanks];         // two-shot: reduce-scatter results published
   uint32_t epoch[kMaxBlocks];                    // this rank's per-workgroup call counter
-  uint32_t error;                                // set when a spin times out
+  uint32_t error;                                // device-side copy of the sticky error word
+};
+
+// per-call failure state handed to the kernels
+struct Fail {
+  uint32_t* host_err;      // host-mapped pinned word: polled by the engine, sticky
+  long long timeout;       // wall-clock ticks a wait may take
 };
 
 constexpr size_t kSigBytes = (sizeof(Signals) + 4095) / 4096 * 4096;
@@ -52,7 +62,25 @@ struct Ctx {
   PeerPtrs peers{};
   PeerPtrs* d_peers = nullptr;
   bool opened[kMaxRanks] = {};
+  uint32_t* h_err = nullptr;   // host-mapped error word (hipHostMalloc mapped | coherent)
+  uint32_t* d_err = nullptr;   // its device alias
+  long long timeout_ticks = 0;
 };
+
+// Bounded wait for flags[b][j] == e of every peer j (one lane per peer).  On timeout the lane
+// records the failure in the device copy and the host-mapped word and stops waiting.
+__device__ __forceinline__ void spin_wait(uint32_t* flag, uint32_t e, Signals* my_sig, const Fail& f) {
+  const long long t0 = wall_clock64();
+  uint32_t it = 0;
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((++it & 255u) == 0 && wall_clock64() - t0 > f.timeout) {
+      __hip_atomic_store(&my_sig->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(f.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+}
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
@@ -66,12 +94,16 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 template <int W>
 __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __restrict__ peers, int rank,
                                                              size_t data_bytes, const uint4* __restrict__ inp,
-                                                             uint4* __restrict__ out, int64_t n16) {
+                                                             uint4* __restrict__ out, int64_t n16, const Fail fail) {
   const int b = blockIdx.x, nb = gridDim.x;
   Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
-  __shared__ uint32_t e_s;
-  if (threadIdx.x == 0) e_s = my_sig->epoch[b] + 1;
+  __shared__ uint32_t e_s, err_s;
+  if (threadIdx.x == 0) {
+    e_s = my_sig->epoch[b] + 1;
+    err_s = my_sig->error;  // same round trip as the epoch (uncached signal area)
+  }
   __syncthreads();
+  if (err_s) return;  // this group already failed: fail fast, never wait again
   const uint32_t e = e_s;
   const size_t slot = kSigBytes + (e & 1u) * data_bytes;
   const int64_t per = (n16 + nb - 1) / nb;
@@ -90,17 +122,12 @@ __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __re
   }
   // 3. wait for all peers' chunk b, then reduce
   if (threadIdx.x < W) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load(&my_sig->flag[b][threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {
-        __hip_atomic_store(&my_sig->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
+    spin_wait(&my_sig->flag[b][threadIdx.x], e, my_sig, fail);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (__hip_atomic_load(&my_sig->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) err_s = 1u;
   }
   __syncthreads();
+  if (err_s) return;  // a peer never arrived: leave the output alone (the engine fails the step)
   const uint4* src[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) src[j] = reinterpret_cast<const uint4*>(peers->base[j] + slot);
@@ -124,20 +151,20 @@ __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __re
 }
 
 // Bounded relaxed poll of this rank's flag[b][j] for every peer j, then one system acquire.
+// Returns false when some peer timed out (every thread of the workgroup sees the same answer).
 template <int W>
-__device__ __forceinline__ void wait_all(uint32_t (*flags)[kMaxRanks], int b, uint32_t e, uint32_t* err) {
+__device__ __forceinline__ bool wait_all(uint32_t (*flags)[kMaxRanks], int b, uint32_t e, Signals* my_sig,
+                                         const Fail& fail) {
+  __shared__ uint32_t bad_s;
+  if (threadIdx.x == 0) bad_s = 0u;
+  __syncthreads();
   if (threadIdx.x < W) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load(&flags[b][threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
+    spin_wait(&flags[b][threadIdx.x], e, my_sig, fail);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (__hip_atomic_load(&my_sig->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) bad_s = 1u;
   }
   __syncthreads();
+  return bad_s == 0u;
 }
 
 // Drain this workgroup's stores, then stamp flags[b][rank] = e in every rank's signal area.
@@ -169,12 +196,16 @@ __device__ __forceinline__ void acc8(float* acc, const uint4& v) {
 template <int W>
 __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __restrict__ peers, int rank,
                                                              size_t data_bytes, const uint4* __restrict__ inp,
-                                                             uint4* __restrict__ out, int64_t n16) {
+                                                             uint4* __restrict__ out, int64_t n16, const Fail fail) {
   const int b = blockIdx.x, nb = gridDim.x;
   Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
-  __shared__ uint32_t e_s;
-  if (threadIdx.x == 0) e_s = my_sig->epoch[b] + 1;
+  __shared__ uint32_t e_s, err_s;
+  if (threadIdx.x == 0) {
+    e_s = my_sig->epoch[b] + 1;
+    err_s = my_sig->error;
+  }
   __syncthreads();
+  if (err_s) return;
   const uint32_t e = e_s;
   const size_t in_slot = kSigBytes + (e & 1u) * data_bytes;
   const size_t res_slot = kSigBytes + (2 + (e & 1u)) * data_bytes;
@@ -192,7 +223,7 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
     for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) mine[i] = inp[i];
   }
   publish<W>(peers, rank, b, e, false);
-  wait_all<W>(my_sig->flag, b, e, &my_sig->error);
+  if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
   // 2. reduce chunk b of my slice across all ranks into my result region
   {
     int64_t lo, hi;
@@ -209,7 +240,7 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
     }
   }
   publish<W>(peers, rank, b, e, true);
-  wait_all<W>(my_sig->flag2, b, e, &my_sig->error);
+  if (!wait_all<W>(my_sig->flag2, b, e, my_sig, fail)) return;
   // 3. gather chunk b of every reduced slice
 #pragma unroll
   for (int s = 0; s < W; ++s) {
@@ -248,7 +279,38 @@ PK_EXPORT void* pk_car_create(int rank, int world, long long data_bytes) {
   }
   c->local = static_cast<char*>(p);
   c->peers.base[rank] = c->local;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    (void)hipFree(p);
+    delete c;
+    return nullptr;
+  }
+  c->h_err = static_cast<uint32_t*>(h);
+  *c->h_err = 0u;
+  void* dh = nullptr;
+  if (hipHostGetDevicePointer(&dh, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    (void)hipFree(p);
+    delete c;
+    return nullptr;
+  }
+  c->d_err = static_cast<uint32_t*>(dh);
+  int dev = 0, khz = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  c->timeout_ticks = 30LL * 1000 * khz;  // 30 s default (pk_car_set_timeout_ms)
   return c;
+}
+
+// Wall-clock bound of every wait of this context (a peer that is this late is treated as dead).
+PK_EXPORT int pk_car_set_timeout_ms(void* ctx, long long ms) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr || ms <= 0) return -1;
+  int dev = 0, khz = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  c->timeout_ticks = ms * khz;
+  return 0;
 }
 
 PK_EXPORT int pk_car_get_handle(void* ctx, void* out) {
@@ -301,13 +363,14 @@ PK_EXPORT int pk_car_allreduce_bf16_algo(void* ctx, const void* inp, void* out, 
   const uint4* in4 = static_cast<const uint4*>(inp);
   uint4* out4 = static_cast<uint4*>(out);
   if (algo == 0) algo = bytes <= kOneShotMax ? 1 : 2;
+  const Fail fail{c->d_err, c->timeout_ticks};
   switch (c->world) {
 #define PK_CAR_CASE(WW)                                                                                            \
   case WW:                                                                                                       \
     if (algo == 1)                                                                                               \
-      allreduce_1shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, n16); \
+      allreduce_1shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, n16, fail); \
     else                                                                                                         \
-      allreduce_2shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, n16); \
+      allreduce_2shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, n16, fail); \
     break;
     PK_CAR_CASE(2)
     PK_CAR_CASE(3)
@@ -322,17 +385,25 @@ PK_EXPORT int pk_car_allreduce_bf16_algo(void* ctx, const void* inp, void* out, 
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
-// 1 if any spin of this rank timed out since the last call (and clears it).
+// 1 once any wait of this rank has timed out (sticky).  A plain read of host-mapped memory:
+// no GPU synchronisation, cheap enough to poll every engine step.
 PK_EXPORT int pk_car_check_error(void* ctx) {
   Ctx* c = static_cast<Ctx*>(ctx);
-  uint32_t err = 0;
+  if (c == nullptr || c->h_err == nullptr) return -1;
+  return static_cast<int>(__atomic_load_n(c->h_err, __ATOMIC_ACQUIRE));
+}
+
+// Tests only: re-arm a failed context (device copy and host word).  The caller must have
+// re-synchronised the group (every rank's epochs advance only on completed calls).
+PK_EXPORT int pk_car_clear_error(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  const uint32_t z = 0;
   Signals* s = reinterpret_cast<Signals*>(c->local);
-  if (hipMemcpy(&err, &s->error, sizeof(err), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (err) {
-    const uint32_t z = 0;
-    (void)hipMemcpy(&s->error, &z, sizeof(z), hipMemcpyHostToDevice);
-  }
-  return static_cast<int>(err);
+  if (hipMemcpy(&s->error, &z, sizeof(z), hipMemcpyHostToDevice) != hipSuccess) return -3;
+  __atomic_store_n(c->h_err, 0u, __ATOMIC_RELEASE);
+  return 0;
 }
 
 PK_EXPORT void pk_car_destroy(void* ctx) {
@@ -343,5 +414,6 @@ PK_EXPORT void pk_car_destroy(void* ctx) {
     if (c->opened[j]) (void)hipIpcCloseMemHandle(c->peers.base[j]);
   if (c->d_peers) (void)hipFree(c->d_peers);
   if (c->local) (void)hipFree(c->local);
+  if (c->h_err) (void)hipHostFree(c->h_err);
   delete c;
 }

@@ -270,11 +270,19 @@ class ModelRunner:
 
     def fetch(self, handle) -> List[int]:
         toks, ns, ev, _ = handle
-        if ns == 0:
-            return []
         if ev is not None:
             ev.synchronize()
+        self._check_comm()
+        if ns == 0:
+            return []
         return toks[:ns].tolist()
+
+    def _check_comm(self) -> None:
+        """Fail loudly once a custom all-reduce of this step (or an earlier one) timed out: the
+        step's tokens were computed from incomplete sums (parallel/custom_ar.py)."""
+        car = self.model.st.custom_ar
+        if car is not None:
+            car.check()
 
     def launch_continuation(self, batch: ScheduledBatch, prev) -> Optional[tuple]:
         """Decode step k+1 of ``batch.decodes`` enqueued while step k (``prev``) may still run:
@@ -342,6 +350,7 @@ class ModelRunner:
             comm.tp_broadcast_tensor(self.dev_buf)
             hdr = self.d["header"][:8].tolist()
             mode, T, n, nd, ns, max_q, g, short = hdr
+            self._check_comm()  # the header read synchronised with the previous step
             if mode == self.MODE_STOP:
                 return
             if mode == self.MODE_RUN:

@@ -48,10 +48,6 @@ FOLD_NORM = os.environ.get("POLYKEY_FOLD_NORM", "1") == "1"
 # stream: reduce-scatter / all-gather around the norms instead of all-reduces (_forward_sp).
 SEQUENCE_PARALLEL = os.environ.get("POLYKEY_SEQUENCE_PARALLEL", "1") == "1"
 SP_MIN_TOKENS = int(os.environ.get("POLYKEY_SP_MIN_TOKENS", "256"))
-# TP > 1 steps with at least SP_MIN_TOKENS tokens (prefill) run with a token-sharded residual
-# stream: reduce-scatter / all-gather around the norms instead of all-reduces (_forward_sp).
-SEQUENCE_PARALLEL = os.environ.get("POLYKEY_SEQUENCE_PARALLEL", "1") == "1"
-SP_MIN_TOKENS = int(os.environ.get("POLYKEY_SP_MIN_TOKENS", "256"))
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:

@@ -84,6 +84,8 @@ def unpermute(y: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, T: int, k: in
     H = y.shape[-1]
     if not y.is_cuda:
         out = torch.zeros((T, H), dtype=torch.float32)
+        if y.shape[0] == 0:  # no slot routed to this rank's experts (EP): zero contribution
+            return out.to(y.dtype)
         invl = inv.view(T, k).long()
         for j in range(k):
             valid = invl[:, j] >= 0

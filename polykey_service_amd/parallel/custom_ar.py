@@ -6,6 +6,12 @@ RCCL's ring/tree latency.  The group's IPC buffers are exchanged once over the g
 group; messages larger than the buffer, non-bf16 tensors, or a failed start-up self-test fall
 back to RCCL (``dist.all_reduce``).  ``POLYKEY_CUSTOM_AR=0`` disables it; ``force`` also
 enables it on a gloo-backed GPU group (tests run TP ranks that share one GPU that way).
+
+Failure detection: every wait in the kernel is bounded by a wall-clock timeout
+(``POLYKEY_CUSTOM_AR_TIMEOUT_S``, default 30 s).  A peer that misses it sets a sticky error word
+in host-mapped memory; :meth:`CustomAllReduce.error` reads it without a GPU sync and the model
+runner checks it after every step, raising :class:`CustomAllReduceError` — the engine loop dies,
+health goes NOT_SERVING and the server exits non-zero for its supervisor to restart.
 """
 from __future__ import annotations
 
@@ -34,15 +40,21 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_allreduce_bf16.argtypes = [_P, _P, _P, _LL, _I, _P]
         lib.pk_car_allreduce_bf16_algo.argtypes = [_P, _P, _P, _LL, _I, _I, _P]
         lib.pk_car_check_error.argtypes = [_P]
+        lib.pk_car_clear_error.argtypes = [_P]
+        lib.pk_car_set_timeout_ms.argtypes = [_P, _LL]
         lib.pk_car_destroy.argtypes = [_P]
         lib.pk_car_destroy.restype = None
         lib._pk_typed = True
     return lib
 
 
+class CustomAllReduceError(RuntimeError):
+    """A TP peer did not arrive at a custom all-reduce within the timeout."""
+
+
 class CustomAllReduce:
     def __init__(self, cpu_group, rank: int, world: int, device: torch.device, max_bytes: int = 16 << 20,
-                 blocks: int = 0):
+                 blocks: int = 0, timeout_s: Optional[float] = None):
         self.lib = _lib()
         self.rank, self.world, self.device = rank, world, device
         self.max_bytes = max_bytes
@@ -51,6 +63,9 @@ class CustomAllReduce:
             self.ctx = self.lib.pk_car_create(rank, world, max_bytes)
         if not self.ctx:
             raise RuntimeError("pk_car_create failed (uncached IPC buffer allocation)")
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("POLYKEY_CUSTOM_AR_TIMEOUT_S", "30"))
+        self.set_timeout(timeout_s)
         hsz = self.lib.pk_car_ipc_handle_size()
         mine = ctypes.create_string_buffer(hsz)
         if self.lib.pk_car_get_handle(self.ctx, mine) != 0:
@@ -78,8 +93,22 @@ class CustomAllReduce:
             raise RuntimeError(f"custom all-reduce launch failed ({rc})")
         return out
 
+    def set_timeout(self, seconds: float) -> None:
+        self.lib.pk_car_set_timeout_ms(self.ctx, max(1, int(seconds * 1000)))
+
     def error(self) -> int:
+        """1 once a wait timed out (sticky; host-mapped word, no GPU sync)."""
         return self.lib.pk_car_check_error(self.ctx)
+
+    def check(self) -> None:
+        """Raise :class:`CustomAllReduceError` if a peer has timed out (called every engine step)."""
+        if self.ctx and self.lib.pk_car_check_error(self.ctx):
+            raise CustomAllReduceError(f"custom all-reduce: a TP peer of rank {self.rank} did not arrive within "
+                                       "the timeout (group failed; restart the job)")
+
+    def clear_error(self) -> None:
+        """Tests only: re-arm after a deliberately provoked timeout."""
+        self.lib.pk_car_clear_error(self.ctx)
 
     def self_test(self) -> bool:
         """Rank-dependent pattern reduced twice (both buffer parities) and checked on the host."""

@@ -67,6 +67,13 @@ class PolykeyServer:
         self._extra = extra_handlers or []
         self.own_service = own_service  # stop() also closes the service (engine thread)
         self._stopped = asyncio.Event()
+        self._quit: Optional[asyncio.Event] = None
+        # the engine loop died (HIP error, TP peer timeout, ...): health goes NOT_SERVING at once
+        # and, with exit_on_fatal, the process stops with a non-zero status for its supervisor
+        # (compose ``restart: unless-stopped``, Kubernetes) to restart it
+        self.fatal_error: Optional[BaseException] = None
+        self.exit_on_fatal = True
+        self.fatal_grace_s = 2.0
 
     async def start(self) -> int:
         bind = grpc_bind_address(self.listen_addr)
@@ -121,8 +128,12 @@ class PolykeyServer:
 
         def fatal(exc):
             self.logger.error("engine loop died", error=repr(exc))
+            self.fatal_error = exc
             loop.call_soon_threadsafe(self.health.set_serving_status, proto.POLYKEY_SERVICE, NOT_SERVING)
             loop.call_soon_threadsafe(self.health.set_serving_status, "", NOT_SERVING)
+            if self.exit_on_fatal:
+                # give probes a moment to observe NOT_SERVING, then leave serve_until_signal
+                loop.call_soon_threadsafe(loop.call_later, self.fatal_grace_s, self._request_quit)
 
         llm.on_fatal = fatal
 
@@ -139,9 +150,16 @@ class PolykeyServer:
         self._watch = asyncio.create_task(poll())
         return self._watch
 
-    async def serve_until_signal(self, grace: float = 10.0) -> None:
+    def _request_quit(self) -> None:
+        if self._quit is not None:
+            self._quit.set()
+
+    async def serve_until_signal(self, grace: float = 10.0) -> int:
+        """Serve until SIGINT/SIGTERM (exit status 0) or a fatal engine failure (status 1)."""
         loop = asyncio.get_running_loop()
-        quit_ev = asyncio.Event()
+        self._quit = quit_ev = asyncio.Event()
+        if self.fatal_error is not None and self.exit_on_fatal:
+            quit_ev.set()
         for sig in (signal.SIGINT, signal.SIGTERM):
             try:
                 loop.add_signal_handler(sig, quit_ev.set)
@@ -149,6 +167,7 @@ class PolykeyServer:
                 pass
         await quit_ev.wait()
         await self.stop(grace)
+        return 1 if self.fatal_error is not None else 0
 
 
 def build_service(cfg, logger: slog.Logger):
@@ -186,10 +205,12 @@ async def amain(argv=None) -> int:
     if cfg.http_addr:
         from ..api.openai import serve_openai
         http = await serve_openai(service, cfg.http_addr, logger)
-    await srv.serve_until_signal(cfg.shutdown_grace)
+    rc = await srv.serve_until_signal(cfg.shutdown_grace)
     if http is not None:
         await http.shutdown()
-    return 0
+    if rc:
+        logger.error("exiting after engine failure", error=repr(srv.fatal_error))
+    return rc
 
 
 def main(argv=None) -> int:

@@ -48,3 +48,55 @@ def test_engine_death_fails_streams_and_health():
             time.sleep(0.05)
         assert hc(proto.HealthCheckRequest(service="polykey.v2.PolykeyService"), timeout=5).status == NOT_SERVING
     router.llm.shutdown()
+
+
+class _TimedOutAllReduce:
+    """Stands in for parallel/custom_ar.CustomAllReduce whose kernel saw a TP peer miss the
+    timeout on the 3rd step: ``check`` raises exactly like the host-mapped error word does."""
+
+    def __init__(self, after: int):
+        self.after, self.calls = after, 0
+
+    def check(self):
+        from polykey_service_amd.parallel.custom_ar import CustomAllReduceError
+        self.calls += 1
+        if self.calls >= self.after:
+            raise CustomAllReduceError("custom all-reduce: a TP peer of rank 0 did not arrive within the timeout")
+
+
+def test_allreduce_timeout_goes_not_serving_and_exits_nonzero():
+    """a TP collective that times out must not produce tokens: the step fails,
+    health flips to NOT_SERVING and the server process ends with a non-zero status."""
+    import asyncio
+
+    from polykey_service_amd.server import PolykeyServer
+
+    st = ParallelState()
+    eng = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=4, max_num_batched_tokens=64, max_model_len=256,
+                                 hip_graphs=False, device="cpu"), st)
+    st.custom_ar = _TimedOutAllReduce(after=3)
+    router = ToolRouter()
+    attach_local_llm(router, ServerConfig(model="tiny-llama", backend="local"), slog.Logger(open("/dev/null", "w")),
+                     engine=eng)
+
+    async def run():
+        srv = PolykeyServer(router, slog.Logger(open("/dev/null", "w")), "127.0.0.1:0", own_service=True)
+        srv.fatal_grace_s = 0.3
+        port = await srv.start()
+        srv.watch_backend(router.llm, 0.05)
+        serving = asyncio.create_task(srv.serve_until_signal(grace=1.0))
+        async with grpc.aio.insecure_channel(f"127.0.0.1:{port}") as ch:
+            call = ch.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                                  response_deserializer=proto.ExecuteToolResponse.FromString)
+            r = proto.ExecuteToolRequest(tool_name="llm.generate")
+            r.parameters.update({"prompt": "x", "max_tokens": 20, "ignore_eos": True})
+            with pytest.raises(grpc.aio.AioRpcError) as ei:
+                await call(r, timeout=30)
+            assert "did not arrive" in ei.value.details()
+        statuses = [srv.health.get(proto.POLYKEY_SERVICE)]
+        rc = await asyncio.wait_for(serving, timeout=20)
+        return rc, statuses
+
+    rc, statuses = asyncio.run(run())
+    assert rc == 1
+    assert statuses[0] == NOT_SERVING

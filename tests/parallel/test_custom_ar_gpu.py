@@ -1,8 +1,10 @@
-"""One-shot xGMI all-reduce (csrc/comm/custom_allreduce.hip) with 2 ranks.
+"""One-shot / two-shot xGMI all-reduce (csrc/comm/custom_allreduce.hip) with 2 and 8 ranks.
 
-On a one-GPU box both ranks share cuda:0: IPC handles, peer flags, parity slots and graph
-replay are exercised exactly as across GPUs (the loads just do not cross xGMI).  Small grids
-keep both ranks' kernels co-resident; a spin that times out sets the error word (no hang)."""
+On a one-GPU box all ranks share cuda:0: IPC handles, peer flags, parity slots and graph
+replay are exercised exactly as across GPUs (the loads just do not cross xGMI); 8 ranks run
+the W=8 instantiation that 70B TP=8 uses.  Small grids keep every rank's kernels co-resident;
+every wait is bounded by a wall-clock timeout that sets the sticky error word (no hang).
+The last phase provokes that timeout on purpose: one rank skips a call."""
 import os
 import socket
 
@@ -29,7 +31,7 @@ def _worker(rank, world, port, q):
         torch.cuda.set_device(0)
         from polykey_service_amd.parallel.custom_ar import CustomAllReduce
         dev = torch.device("cuda:0")
-        car = CustomAllReduce(dist.group.WORLD, rank, world, dev, max_bytes=1 << 22, blocks=4)
+        car = CustomAllReduce(dist.group.WORLD, rank, world, dev, max_bytes=1 << 22, blocks=4, timeout_s=20.0)
         assert car.self_test(), "self test"
         g = torch.Generator().manual_seed(100 + rank)
         for n in (8, 1000 * 8, 64 * 4096, 64 * 8192):
@@ -61,6 +63,27 @@ def _worker(rank, world, port, q):
             want = float(sum(r + it for r in range(world)))
             assert bool((yg.float() == want).all()), (it, yg[:4])
         assert car.error() == 0
+        # a rank that skips a call: every rank that waits for it times out and fails loudly
+        # (sticky error word, read without a GPU sync), and later calls return at once
+        car.set_timeout(1.0)
+        dist.barrier()
+        if rank != world - 1:
+            import time
+            xs = torch.ones(4096, dtype=torch.bfloat16, device=dev)
+            car.all_reduce(xs)
+            torch.cuda.synchronize()
+            assert car.error() == 1, "timeout not reported"
+            t0 = time.monotonic()
+            car.all_reduce(xs)
+            torch.cuda.synchronize()
+            assert time.monotonic() - t0 < 0.5, "a failed group must not wait again"
+            from polykey_service_amd.parallel.custom_ar import CustomAllReduceError
+            try:
+                car.check()
+                raise AssertionError("check() did not raise")
+            except CustomAllReduceError:
+                pass
+        dist.barrier()
         car.close()
         dist.barrier()
         dist.destroy_process_group()
@@ -69,14 +92,15 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-def test_custom_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 8])
+def test_custom_allreduce_ranks_share_one_gpu(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: "ok", 1: "ok"}, res
+    assert res == {r: "ok" for r in range(world)}, res

@@ -1,5 +1,8 @@
-"""Tensor / expert parallel correctness on CPU with gloo (world size 2): the sharded model must
-reproduce the single-rank model (same random-init weights, shards sliced from the full tensors)."""
+"""Tensor / expert / sequence parallel correctness on CPU with gloo at 2, 4 and 8 ranks: the
+sharded model must reproduce the single-rank model (same random-init weights, shards sliced from
+the full tensors).  ``tiny-llama-g8`` has the per-rank shape of Llama-3-70B at TP=8 (one KV head
+per rank, GQA group 8, padded vocab shards) and ``tiny-mixtral-e8`` Mixtral's 8 experts (one per
+rank at EP=8), so the north-star configs' rank counts run here (BASELINE.json:10-11)."""
 import os
 import socket
 
@@ -35,10 +38,10 @@ def _first_step_logits_and_tokens(eng):
     return logits, [s.output_ids for s in seqs]
 
 
-def _worker(rank, world, port, model, ep, out_path, sp=False):
+def _worker(rank, world, port, model, ep, out_path, sp=False):  # noqa: PLR0913
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
-    torch.set_num_threads(2)
+    torch.set_num_threads(max(1, 8 // world))
     from polykey_service_amd.models import llama
     llama.SP_MIN_TOKENS = 1 if sp else 1 << 30  # sp: every step (49-token prefill: padded rows) runs SP
     from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
@@ -53,15 +56,19 @@ def _worker(rank, world, port, model, ep, out_path, sp=False):
     destroy_parallel()
 
 
-@pytest.mark.parametrize("model,ep,sp", [("tiny-llama-gqa4", 1, False), ("tiny-mixtral", 1, False),
-                                         ("tiny-mixtral", 2, False), ("tiny-llama-gqa4", 1, True),
-                                         ("tiny-mixtral", 2, True)])
-def test_tp2_matches_tp1(tmp_path, model, ep, sp):
+@pytest.mark.parametrize("model,world,ep,sp", [
+    ("tiny-llama-gqa4", 2, 1, False), ("tiny-mixtral", 2, 1, False), ("tiny-mixtral", 2, 2, False),
+    ("tiny-llama-gqa4", 2, 1, True), ("tiny-mixtral", 2, 2, True),
+    # 70B TP=8 shape: 8-way all-reduces, one KV head per rank, 126-row vocab shards
+    ("tiny-llama-g8", 4, 1, False), ("tiny-llama-g8", 8, 1, False), ("tiny-llama-g8", 8, 1, True),
+    # Mixtral at 8 ranks: tensor-parallel experts (EP=1) and one expert per rank (EP=8)
+    ("tiny-mixtral-e8", 8, 1, False), ("tiny-mixtral-e8", 8, 8, False), ("tiny-mixtral-e8", 8, 8, True)])
+def test_tp_matches_tp1(tmp_path, model, world, ep, sp):
     """``sp``: sequence-parallel steps (token-sharded residual, reduce-scatter / all-gather)."""
     from polykey_service_amd.parallel.state import ParallelState
     ref_logits, ref_toks = _first_step_logits_and_tokens(_engine(model, ParallelState()))
     out = str(tmp_path / "tp.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), model, ep, out, sp), nprocs=2, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), model, ep, out, sp), nprocs=world, join=True,
                        start_method="spawn")
     got = torch.load(out, weights_only=True)
     # bf16 row-parallel partials are rounded per rank before the all-reduce: ~1 bf16 ulp noise
@@ -93,19 +100,24 @@ def _comm_worker(rank, world, port, out_path):
     destroy_parallel()
 
 
-def test_collectives_gloo(tmp_path):
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_collectives_gloo(tmp_path, world):
     out = str(tmp_path / "c")
-    mp.start_processes(_comm_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
-    for r in range(2):
-        d = torch.load(f"{out}.{r}", weights_only=False)
-        assert torch.equal(d["ar"], torch.full((2, 3), 3.0))
-        assert d["ag"].tolist() == [[0.0, 1.0, 2.0, 10.0, 11.0, 12.0]]
-        assert d["recv"][:, 0].tolist() == [0.0] * 1 + [1.0] * 2
+    mp.start_processes(_comm_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    summed = torch.arange(14, dtype=torch.float32).view(7, 2) * (world * (world + 1) // 2)
+    Tp = (7 + 2 * world - 1) // (2 * world) * (2 * world)
+    padded = torch.cat([summed, torch.zeros(Tp - 7, 2)])
+    Tc = Tp // 2
+    for r in range(world):
+        d = torch.load(f"{out}.{r}", weights_only=True)
+        assert torch.equal(d["ar"], torch.full((2, 3), float(world * (world + 1) // 2)))
+        assert d["ag"].tolist() == [[float(10 * q + j) for q in range(world) for j in range(3)]]
+        assert d["recv"][:, 0].tolist() == [float(q) for q in range(world) for _ in range(q + 1)]
         assert d["obj"] == {"step": 7}
-        summed = torch.arange(14, dtype=torch.float32).view(7, 2) * 3
-        padded = torch.cat([summed, torch.zeros(1, 2)])
-        # rank r holds rows {c*4 + 2r, c*4 + 2r + 1} of chunk c
-        assert torch.equal(d["shard"], torch.cat([padded[2 * r:2 * r + 2], padded[4 + 2 * r:6 + 2 * r]]))
+        # rank r holds rows [c*Tc + r*Tc/world, +Tc/world) of chunk c
+        per = Tc // world
+        want = torch.cat([padded[c * Tc + r * per:c * Tc + (r + 1) * per] for c in range(2)])
+        assert torch.equal(d["shard"], want)
         assert torch.equal(d["back"], summed) and torch.equal(d["twice"], 2 * summed)
 
 
