@@ -252,6 +252,45 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
   if (threadIdx.x == 0) my_sig->epoch[b] = e;
 }
 
+// All-gather along the last dim: every rank contributes rows x row16 16-byte units and receives
+// out[row][j * row16 + col] = rank j's inp[row][col] (the vocab-parallel LM head's logits, so
+// every rank samples the same tokens from the full row without a collective library call
+// inside the decode graph).  Same slot parity / per-workgroup flag protocol as the one-shot
+// all-reduce; workgroup b owns a contiguous chunk of the flattened input.
+template <int W>
+__global__ void __launch_bounds__(kThreads) allgather_1shot(const PeerPtrs* __restrict__ peers, int rank,
+                                                             size_t data_bytes, const uint4* __restrict__ inp,
+                                                             uint4* __restrict__ out, int64_t rows, int64_t row16,
+                                                             const Fail fail) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
+  __shared__ uint32_t e_s, err_s;
+  if (threadIdx.x == 0) {
+    e_s = my_sig->epoch[b] + 1;
+    err_s = my_sig->error;
+  }
+  __syncthreads();
+  if (err_s) return;
+  const uint32_t e = e_s;
+  const size_t slot = kSigBytes + (e & 1u) * data_bytes;
+  const int64_t n16 = rows * row16;
+  const int64_t per = (n16 + nb - 1) / nb;
+  const int64_t lo = b * per, hi = min(n16, lo + per);
+  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + slot);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) mine[i] = inp[i];
+  publish<W>(peers, rank, b, e, false);
+  if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
+    const int64_t row = i / row16, col = i - row * row16;
+    uint4 v[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) v[j] = reinterpret_cast<const uint4*>(peers->base[j] + slot)[i];
+#pragma unroll
+    for (int j = 0; j < W; ++j) out[(row * W + j) * row16 + col] = v[j];
+  }
+  if (threadIdx.x == 0) my_sig->epoch[b] = e;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------- host API
@@ -416,4 +455,37 @@ PK_EXPORT void pk_car_destroy(void* ctx) {
   if (c->local) (void)hipFree(c->local);
   if (c->h_err) (void)hipHostFree(c->h_err);
   delete c;
+}
+
+// All-gather of a [rows, row_bytes] row block per rank into out [rows, world * row_bytes]
+// (rank-major within each row).  row_bytes % 16 == 0, rows * row_bytes <= data_bytes.
+PK_EXPORT int pk_car_allgather(void* ctx, const void* inp, void* out, long long rows, long long row_bytes, int blocks,
+                               hipStream_t stream) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr || c->d_peers == nullptr) return -1;
+  if (rows <= 0 || row_bytes <= 0) return 0;
+  if (row_bytes % 16 || static_cast<size_t>(rows * row_bytes) > c->data_bytes) return -2;
+  const int64_t row16 = row_bytes / 16, n16 = rows * row16;
+  if (blocks <= 0) blocks = static_cast<int>(std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, n16 / (kThreads * 2))));
+  blocks = std::min(blocks, kMaxBlocks);
+  const Fail fail{c->d_err, c->timeout_ticks};
+  const uint4* in4 = static_cast<const uint4*>(inp);
+  uint4* out4 = static_cast<uint4*>(out);
+  switch (c->world) {
+#define PK_CAG_CASE(WW)                                                                                         \
+  case WW:                                                                                                    \
+    allgather_1shot<WW><<<blocks, kThreads, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, in4, out4, rows, \
+                                                         row16, fail);                                        \
+    break;
+    PK_CAG_CASE(2)
+    PK_CAG_CASE(3)
+    PK_CAG_CASE(4)
+    PK_CAG_CASE(5)
+    PK_CAG_CASE(6)
+    PK_CAG_CASE(7)
+    PK_CAG_CASE(8)
+#undef PK_CAG_CASE
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
 }

@@ -52,8 +52,11 @@ class BlockManager : public pk::BlockManagerCore {
   }
 };
 
+void bind_step_channel(py::module_& m);  // step_channel.cpp
+
 PYBIND11_MODULE(_pk_runtime, m) {
-  m.doc() = "polykey native runtime: paged KV block manager and step packer";
+  m.doc() = "polykey native runtime: paged KV block manager, step packer, TP step channel";
+  bind_step_channel(m);
   py::class_<BlockManager>(m, "BlockManager")
       .def(py::init<int64_t, int, int64_t, bool>(), py::arg("num_blocks"), py::arg("block_size"),
            py::arg("watermark_blocks") = 0, py::arg("prefix_caching") = false)

@@ -9,6 +9,14 @@ with ``hipGraphLaunch`` (torch.cuda.CUDAGraph on ROCm) — the launch-bound deco
 32–80 layers × ~10 kernels collapses into one graph launch (guide: "capture launch-bound
 inner loops in hipGraphs").
 
+Tensor parallelism: the TP leader schedules; every other rank of its group runs
+:meth:`ModelRunner.worker_loop`.  The leader publishes each step's packed staging bytes (header
+included) through a shared-memory ring (``_pk_runtime.StepChannel``, csrc/runtime/step_channel.h);
+a worker copies them into its own pinned staging buffer, reads the header on the host and
+launches the same graph / kernels at once — no collective and no GPU sync per step on the
+control plane.  Decode continuations replicate on workers too: every rank samples the same ids
+from the all-gathered logits, so a worker feeds its own previous sampled ids forward.
+
 KV cache: one allocation per layer pair, K ``[blocks, n_kv, bs, 128]`` and transposed V
 ``[blocks, n_kv, 128, bs]`` (see ops/attention.py), sized from free HBM after weights and
 a measured activation peak — at 288 GB per MI355X an 8B model gets ~1.9 M cached tokens.
@@ -95,6 +103,7 @@ class ModelRunner:
         # step's H2D copy is still queued behind the GPU (continuation launches, LLMEngine.step)
         self._host_bufs = [torch.zeros(self.layout.size, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
         self._hs = [{k: self.layout.view(b, k).numpy() for k in self.layout.sections} for b in self._host_bufs]
+        self._hnp = [b.numpy() for b in self._host_bufs]  # whole-buffer views (step channel I/O)
         self._h2d_events = [None, None]
         self._cur = 0
         self.host_buf, self.h = self._host_bufs[0], self._hs[0]
@@ -117,6 +126,30 @@ class ModelRunner:
         self.stats = {"steps": 0, "graph_steps": 0, "short_graph_steps": 0, "tokens": 0}
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None
+        self.channel = None
+        self._prev_toks = None  # worker: last step's sampled ids (device), for continuations
+        if model.st.tp_size > 1:
+            self._open_channel()
+
+    # ------------------------------------------------------------- TP control plane
+    def _open_channel(self) -> None:
+        """Leader creates the step ring in /dev/shm and tells its group the name (one gloo
+        broadcast at start-up); workers attach as consumers tp_rank - 1."""
+        import uuid
+
+        from .._native.loader import load_extension
+        from ..parallel import comm
+        st = self.model.st
+        rt = load_extension("_pk_runtime")
+        slot_bytes = self.layout.size * 4
+        if st.tp_rank == 0:
+            name = f"/pk_step_{os.getpid()}_{st.dp_rank}_{uuid.uuid4().hex[:8]}"
+            self.channel = rt.StepChannel(name, True, 4, st.tp_size - 1, slot_bytes)
+            comm.tp_broadcast_object(name)
+        else:
+            name = comm.tp_broadcast_object(None)
+            self.channel = rt.StepChannel(name, False, consumer_index=st.tp_rank - 1)
+        comm.barrier(st.tp_cpu_group)  # every consumer attached before the first publish
 
     # ---------------------------------------------------------------- KV cache
     def kv_bytes_per_block(self) -> int:
@@ -207,7 +240,8 @@ class ModelRunner:
         return md
 
     # ----------------------------------------------------------------- execute
-    # header words (section "header"): mode, T, n, nd, ns, max_q, graph bucket, short-context graph
+    # header words (section "header"): mode, T, n, nd, ns, max_q, graph bucket, short-context graph,
+    # continuation (input ids = the previous step's sampled ids, already on the device)
     MODE_IDLE, MODE_RUN, MODE_STOP = 0, 1, 2
 
     @torch.inference_mode()
@@ -243,7 +277,7 @@ class ModelRunner:
             if g:
                 self._pad_decode(nd, g)
         short = self._short(g, nd)
-        h["header"][:8] = (self.MODE_RUN, T, n, nd, ns, max_q, g, short)
+        h["header"][:9] = (self.MODE_RUN, T, n, nd, ns, max_q, g, short, 0)
         self._publish(max(n, g))
         toks = self._run(T, n, nd, ns, max_q, g, short)
         return self._handle(toks, ns)
@@ -293,7 +327,7 @@ class ModelRunner:
         seqs = batch.decodes
         n = len(seqs)
         g = self._graph_bucket(n) if self.graphs else None
-        if not g or prev[3] is None or batch.prefills or self.model.st.tp_size > 1:
+        if not g or prev[3] is None or batch.prefills:
             return None
         for s in seqs:
             if s.num_computed + 2 > self.cfg.max_model_len or not self.bm.allocate(s.seq_id, s.num_computed + 2):
@@ -316,51 +350,75 @@ class ModelRunner:
             h["offsets"][r] = len(s.output_ids) + 1
         self._pad_decode(n, g)
         short = self._short(g, n)
-        h["header"][:8] = (self.MODE_RUN, T, n, n, n, 0, g, short)
+        h["header"][:9] = (self.MODE_RUN, T, n, n, n, 0, g, short, 1)
         self._publish(max(n, g))
         self.d["input_ids"][:n].copy_(prev[3][:n])  # step k's sampled ids, stream-ordered
         return self._handle(self._run(T, n, n, n, 0, g, short), n)
 
+    def _staged_words(self, n_bt_rows: Optional[int]) -> int:
+        """int32 words of the staging buffer a step uses: everything up to the used block-table
+        rows (the last section), rounded to 16 bytes."""
+        off, _ = self.layout.sections["block_tables"]
+        rows = self.cfg.max_num_seqs if n_bt_rows is None else n_bt_rows
+        n = min(self.layout.size, off + rows * self.max_blocks)
+        return (n + 3) // 4 * 4
+
     def _publish(self, n_bt_rows: Optional[int] = None) -> None:
-        """Stage the step inputs on the device.  On the GPU a kernel reads the pinned staging
-        buffer directly (no SDMA hand-off); only the prefix up to the used block-table rows
-        (the last section) is copied."""
+        """Hand the step inputs to the TP workers (shared-memory ring, host to host) and stage
+        them on this rank's device."""
+        n = self._staged_words(n_bt_rows)
+        if self.channel is not None and self.model.st.tp_rank == 0:
+            if not self.channel.publish(self._hnp[self._cur], n * 4, 600000):
+                raise RuntimeError("TP step channel: a worker stopped consuming steps")
+        self._stage_local(n)
+
+    def _stage_local(self, n: int) -> None:
+        """Copy the first ``n`` words of the current pinned staging buffer to the device.  On
+        the GPU a kernel reads the pinned buffer directly (no SDMA hand-off)."""
         if self.device.type == "cuda" and HOST_COPY_KERNEL:
-            off, _ = self.layout.sections["block_tables"]
-            rows = self.cfg.max_num_seqs if n_bt_rows is None else n_bt_rows
-            n = min(self.layout.size, off + rows * self.max_blocks)
-            n = (n + 3) // 4 * 4  # 16-byte multiple
             native.call("pk_copy_from_host", self.dev_buf.data_ptr(), self.host_buf.data_ptr(), n * 4,
                         native.stream_ptr(self.device))
         else:
-            self.dev_buf.copy_(self.host_buf, non_blocking=True)
+            self.dev_buf[:n].copy_(self.host_buf[:n], non_blocking=True)
         if self.device.type == "cuda":
             ev = self._h2d_events[self._cur]
             if ev is None:
                 ev = self._h2d_events[self._cur] = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.device))
-        if self.model.st.tp_size > 1:
-            from ..parallel import comm
-            comm.tp_broadcast_tensor(self.dev_buf)
 
     def worker_loop(self) -> None:
-        """Non-leader TP ranks: receive each step's inputs and run the same forward."""
-        from ..parallel import comm
+        """Non-leader TP ranks: take each step from the leader's ring into the next pinned
+        staging buffer, read its header on the host and launch the same work — the worker never
+        waits for its own GPU (only, through the double-buffered staging, for a step two back)."""
+        chan = self.channel
         while True:
-            comm.tp_broadcast_tensor(self.dev_buf)
-            hdr = self.d["header"][:8].tolist()
-            mode, T, n, nd, ns, max_q, g, short = hdr
-            self._check_comm()  # the header read synchronised with the previous step
+            self._next_staging()
+            nbytes = chan.consume(self._hnp[self._cur], 1000)
+            self._check_comm()
+            if nbytes == -1:
+                continue  # idle leader: poll again (and re-check the comm error word)
+            if nbytes == -2:
+                return
+            mode, T, n, nd, ns, max_q, g, short, cont = (int(v) for v in self.h["header"][:9])
             if mode == self.MODE_STOP:
                 return
-            if mode == self.MODE_RUN:
-                with torch.inference_mode():
-                    self._run(T, n, nd, ns, max_q, g, short)
+            if mode != self.MODE_RUN:
+                continue
+            self._stage_local(nbytes // 4)
+            with torch.inference_mode():
+                if cont:
+                    self.d["input_ids"][:n].copy_(self._prev_toks[:n])
+                toks = self._run(T, n, nd, ns, max_q, g, short)
+            if toks is not None:
+                self._prev_toks = toks
+            self.stats["steps"] += 1
 
     def stop_workers(self) -> None:
-        if self.model.st.tp_size > 1:
-            self.h["header"][0] = self.MODE_STOP
-            self._publish()
+        if self.channel is not None and self.model.st.tp_rank == 0:
+            self._next_staging()
+            self.h["header"][:9] = (self.MODE_STOP, 0, 0, 0, 0, 0, 0, 0, 0)
+            self.channel.publish(self._hnp[self._cur], 64, 60000)
+            self.channel.close()
 
     def _run(self, T: int, n: int, nd: int, ns: int, max_q: int, g: int, short: int = 0):
         d = self.d

@@ -198,11 +198,16 @@ class RowsFn:
 
 
 def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:
-    """[.., n] per rank → [.., n * tp] (rank-major along the last dim)."""
+    """[.., n] per rank → [.., n * tp] (rank-major along the last dim).  Decode-sized 2-D
+    inputs (the LM head's logits) go through the IPC all-gather kernel, so a TP decode step's
+    graph holds no collective-library call (parallel/custom_ar.py)."""
     st = get_state()
     if st.tp_size == 1:
         return x
     x = x.contiguous()
+    car = st.custom_ar
+    if car is not None and car.supports_gather(x):
+        return car.all_gather_last(x)
     out = torch.empty((st.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x, group=st.tp_group)
     out = out.view((st.tp_size,) + tuple(x.shape))

@@ -39,6 +39,7 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_open.argtypes = [_P, _P]
         lib.pk_car_allreduce_bf16.argtypes = [_P, _P, _P, _LL, _I, _P]
         lib.pk_car_allreduce_bf16_algo.argtypes = [_P, _P, _P, _LL, _I, _I, _P]
+        lib.pk_car_allgather.argtypes = [_P, _P, _P, _LL, _LL, _I, _P]
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_clear_error.argtypes = [_P]
         lib.pk_car_set_timeout_ms.argtypes = [_P, _LL]
@@ -91,6 +92,23 @@ class CustomAllReduce:
                                                  torch.cuda.current_stream(self.device).cuda_stream)
         if rc != 0:
             raise RuntimeError(f"custom all-reduce launch failed ({rc})")
+        return out
+
+    def supports_gather(self, x: torch.Tensor) -> bool:
+        """[rows, cols] with 16-byte rows that fit one slot (LM-head logits of a decode step)."""
+        if not (x.is_cuda and x.dim() == 2 and x.is_contiguous()):
+            return False
+        row = x.shape[1] * x.element_size()
+        return row % 16 == 0 and 0 < x.shape[0] * row <= self.max_bytes
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        """[rows, cols] per rank -> [rows, world * cols], rank-major along the last dim."""
+        out = torch.empty((x.shape[0], self.world * x.shape[1]), dtype=x.dtype, device=x.device)
+        rc = self.lib.pk_car_allgather(self.ctx, x.data_ptr(), out.data_ptr(), x.shape[0],
+                                       x.shape[1] * x.element_size(), self.blocks,
+                                       torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"custom all-gather launch failed ({rc})")
         return out
 
     def set_timeout(self, seconds: float) -> None:

@@ -75,3 +75,60 @@ def test_tp2_on_gpu_matches_tp1(tmp_path, model, sp, monkeypatch):
     # random weights give near-ties, so only the prefill tokens must match exactly
     torch.testing.assert_close(got["logits"], ref_logits, atol=1e-1, rtol=5e-2)
     assert [t[0] for t in got["tokens"]] == [t[0] for t in ref_toks]
+
+
+def _engine2(model, st, graphs):
+    from polykey_service_amd.engine import EngineConfig, LLMEngine
+    return LLMEngine(EngineConfig(model=model, max_num_seqs=8, max_num_batched_tokens=128, max_model_len=256,
+                                  hip_graphs=graphs, device="cuda:0", overlap=graphs), st)
+
+
+def _run_greedy(eng, max_tokens=8):
+    from polykey_service_amd.engine import SamplingParams
+    seqs = [eng.add_request(p, SamplingParams(max_tokens=max_tokens, ignore_eos=True)) for p in PROMPTS]
+    while eng.has_unfinished():
+        eng.step()
+    return [s.output_ids for s in seqs], dict(eng.runner.stats), eng.continuation_steps
+
+
+def _graph_worker(rank, port, model, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK="0", POLYKEY_CUSTOM_AR="force")
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    st = init_parallel(tp=2, device="cuda", backend="gloo")
+    assert st.custom_ar is not None, "custom all-reduce did not come up"
+    eager = _engine2(model, st, graphs=False)   # same TP group, same weights, no graphs
+    graphed = _engine2(model, st, graphs=True)  # decode graphs + pipelined continuations
+    assert graphed.runner.graphs, "no decode graphs captured"
+    if st.tp_rank == 0:
+        want, _, _ = _run_greedy(eager)
+        eager.runner.stop_workers()
+        toks, stats, cont = _run_greedy(graphed)
+        graphed.runner.stop_workers()
+        torch.save({"tokens": toks, "eager": want, "graph_steps": stats["graph_steps"], "cont": cont,
+                    "car_err": st.custom_ar.error()}, out_path)
+    else:
+        eager.runner.worker_loop()
+        graphed.runner.worker_loop()
+        torch.save({"worker_steps": graphed.runner.stats["steps"]}, out_path + ".w")
+    destroy_parallel()
+
+
+@pytest.mark.parametrize("model", ["tiny-llama-gqa4", "tiny-mixtral"])
+def test_tp2_hip_graphs_with_continuations(tmp_path, model):
+    """TP decode inside HIP graphs: every collective of the captured step is an IPC kernel (one-shot
+    all-reduce, LM-head all-gather), the worker takes steps from the shared-memory ring without a
+    GPU sync, and pipelined decode continuations run on both ranks.  The graphed, pipelined TP=2
+    engine must generate exactly the tokens of the eager TP=2 engine (same kernels, same sums);
+    the prefill token must also match TP=1."""
+    from polykey_service_amd.parallel.state import ParallelState
+    ref, _, _ = _run_greedy(_engine2(model, ParallelState(device=torch.device("cuda:0")), graphs=False))
+    out = str(tmp_path / "tpg.pt")
+    mp.start_processes(_graph_worker, args=(_port(), model, out), nprocs=2, join=True, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    wk = torch.load(out + ".w", weights_only=True)
+    assert got["car_err"] == 0
+    assert got["graph_steps"] > 0 and got["cont"] > 0, got
+    assert wk["worker_steps"] >= got["graph_steps"]
+    assert got["tokens"] == got["eager"]
+    assert [t[0] for t in got["tokens"]] == [t[0] for t in ref]
