@@ -59,7 +59,10 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 
-constexpr int kR = 2;        // 16-row W tiles per wave
+// 16-row W tiles per wave: KR = 2 (n-block of 128 rows per 4-wave workgroup; required by the
+// SiLU and QKV-RoPE epilogues, whose 32 / 128 columns must sit in one wave / workgroup) or
+// KR = 1 (64-row n-blocks: twice the n-blocks, so half the split-K for the same grid -- half
+// the fp32 slab bytes, and a 4x smaller last-arriver reduction in kAddResNorm).
 
 // Epilogues.  kAddResNorm / kQkvRope are split-K with an in-launch reduction: every split
 // stores its fp32 slab, the last workgroup of an n-block to arrive (agent-scope release /
@@ -92,6 +95,9 @@ __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_c
 #endif
 #ifndef PK_LAB_NO_ASTAGE
 #define PK_LAB_NO_ASTAGE 0   // stage A once, no per-chunk barrier
+#endif
+#ifndef PK_LAB_NO_SLAB
+#define PK_LAB_NO_SLAB 0     // skip the fp32 split-K slab stores (timing only)
 #endif
 
 // Weight loads.  NT: non-temporal (no Infinity-Cache allocation) -- measured faster for the
@@ -129,25 +135,27 @@ __device__ __forceinline__ float4 slab_sum(const float* src, int64_t slab, int S
   }
 }
 
-template <int MODE, int SS>
+template <int MODE, int SS, int KR>
 __device__ void epilogue(const GemmArgs& args, int nb) {
   const int M = args.M, N = args.N, S = args.S, tid = threadIdx.x;
   const int64_t slab = static_cast<int64_t>(M) * N;
-  const int nbase = nb * 128;
+  constexpr int NCOL = 64 * KR;  // columns of an n-block
+  const int nbase = nb * NCOL;
   constexpr int RB = (SS == 0 || SS >= 16) ? 1 : (SS == 8 ? 2 : 4);  // rows per thread per batch
   if constexpr (MODE == kAddResNorm) {
-    // 32 threads (half a wave) per row, 4 columns each; 8 rows per pass of the workgroup
-    const int c = nbase + (tid & 31) * 4;
-    for (int m0 = tid >> 5; m0 < M; m0 += 8 * RB) {
+    // TPR threads per row (4 columns each), RPP rows per pass of the workgroup
+    constexpr int TPR = NCOL / 4, RPP = 256 / TPR;
+    const int c = nbase + (tid % TPR) * 4;
+    for (int m0 = tid / TPR; m0 < M; m0 += RPP * RB) {
       float4 a[RB];
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
-        const int m = min(m0 + 8 * i, M - 1);
+        const int m = min(m0 + RPP * i, M - 1);
         a[i] = slab_sum<SS>(args.partial + static_cast<int64_t>(m) * N + c, slab, S);
       }
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
-        const int m = m0 + 8 * i;
+        const int m = m0 + RPP * i;
         if (m >= M) break;  // uniform per half-wave
         bf16_t* res = args.residual + static_cast<int64_t>(m) * N + c;
         const uint2 rr = *reinterpret_cast<const uint2*>(res);
@@ -161,8 +169,8 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
         *reinterpret_cast<uint2*>(res) = o;
         float sq = v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
 #pragma unroll
-        for (int off = 16; off > 0; off >>= 1) sq += __shfl_xor(sq, off, 32);
-        if ((tid & 31) == 0) args.sumsq_parts[static_cast<int64_t>(nb) * M + m] = sq;
+        for (int off = TPR / 2; off > 0; off >>= 1) sq += __shfl_xor(sq, off, TPR);
+        if (tid % TPR == 0) args.sumsq_parts[static_cast<int64_t>(nb) * M + m] = sq;
       }
     }
   } else {  // kQkvRope: n-block nb is head nb of q | k | v
@@ -249,8 +257,9 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
 constexpr int kKC = 256;           // k per LDS chunk
 constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows shift one 16-B slot)
 
-template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false>
+template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2>
 __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args) {
+  constexpr int kR = KR;
   __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kAStride];
   __shared__ float rinv_s[64];
 #if PK_LAB_LDS_PAD
@@ -275,7 +284,7 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   const int kper = K / S;
   const int k0 = split * kper;
   const int r = lane & 15, g = lane >> 4;
-  const int n0 = nb * 128 + w * 16 * kR;
+  const int n0 = nb * 64 * kR + w * 16 * kR;
 
   if constexpr (NORM) {
     if (tid < M) {
@@ -288,17 +297,19 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   // RS (row scale): the sum-of-squares parts of row `tid` are requested before the weight
   // stream starts and consumed only after the main loop, so they never delay it (unconditional
   // loads from clamped addresses: a load behind a branch would make hipcc drain vmcnt)
-  float rs_p[RS ? 8 : 1];
+  // (up to 64 parts per row: 4 threads per row, 16 loads each)
+  constexpr int kRsLoads = 16;
+  float rs_p[RS ? kRsLoads : 1];
   if constexpr (RS) {
-    const int np = min(args.nrm_nparts, 8), rr = min(tid, M - 1);
+    const int np = min(args.nrm_nparts, 4 * kRsLoads), rr = min(tid >> 2, M - 1), sub = tid & 3;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) rs_p[q] = args.nrm_parts[min(q, np - 1) * M + rr];
+    for (int q = 0; q < kRsLoads; ++q) rs_p[q] = args.nrm_parts[min(sub + 4 * q, np - 1) * M + rr];
   }
 
   const bf16_t* wp[kR];
 #pragma unroll
   for (int t = 0; t < kR; ++t)
-    wp[t] = PK ? Wg + static_cast<int64_t>(nb) * 128 * K + (w * kR + t) * 4 * 512 + 8 * lane  // block-packed
+    wp[t] = PK ? Wg + static_cast<int64_t>(n0 >> 7) * 128 * K + (((n0 & 127) >> 4) + t) * 4 * 512 + 8 * lane  // block-packed
                : Wg + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                     // row-major [N, K]
 
   // A staging: MT*16 rows x 256 cols = MT*512 16-byte pieces over 256 threads
@@ -438,18 +449,22 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   }
 
   if constexpr (RS) {
-    if (tid < M) {
-      const int np = min(args.nrm_nparts, 8);
-      float ss = 0.f;
+    const int np = min(args.nrm_nparts, 4 * kRsLoads), sub = tid & 3;
+    float ss = 0.f;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) ss += q < np ? rs_p[q] : 0.f;
-      rinv_s[tid] = rsqrtf(ss / K + args.eps);
-    }
+    for (int q = 0; q < kRsLoads; ++q) ss += sub + 4 * q < np ? rs_p[q] : 0.f;
+    ss += __shfl_xor(ss, 1, 4);
+    ss += __shfl_xor(ss, 2, 4);
+    if (sub == 0 && (tid >> 2) < M) rinv_s[tid >> 2] = rsqrtf(ss / K + args.eps);
     __syncthreads();
   }
 
   // C^T tile: rows = W rows (n), cols = m:  acc[t][mt][i] = C[m = 16*mt + r][n = n0 + 16*t + 4*g + i]
   constexpr bool kSlab = MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope;
+  // the in-launch residual update hands its slabs over write-through (measured faster than plain
+  // stores + release: tools/gemm_lab.hip o_res / down_res); the plain split-K slabs are read by
+  // the next kernel and stay plain (write-through made those slower)
+  constexpr bool kSlabSc1 = MODE == kAddResNorm || PK_SLAB_SC1;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = 16 * mt + r;
@@ -460,24 +475,30 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
       for (int t = 0; t < kR; ++t) acc[t][mt] *= sc;
     }
     if constexpr (kSlab) {
-      float* p = args.partial + (static_cast<int64_t>(split) * args.M + row0 + m) * N + n0 + 4 * g;
-#if PK_SLAB_SC1
-      // write-through (sc1) stores: the slab lines leave L2 clean, so the launch-end release
-      // has nothing to write back (slabs are < 2 GiB: 32-bit buffer offsets)
-      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(args.partial, static_cast<short>(0), 0x7ffffff0, 0x00020000);
-      const int boff = static_cast<int>((p - args.partial) * 4);
-#endif
+      if (PK_LAB_NO_SLAB && args.M > 0) {  // timing only: keep acc live, store nothing
 #pragma unroll
-      for (int t = 0; t < kR; ++t) {
-        const f32x4 v = acc[t][mt];
-#if PK_SLAB_SC1
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, boff + 64 * t, 0, 16);
-#else
-        if constexpr (PK_SLAB_NT)  // streaming store: no dirty L2 lines left for the launch-end write-back
-          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p + 16 * t));
-        else
-          *reinterpret_cast<f32x4*>(p + 16 * t) = v;
-#endif
+        for (int t = 0; t < kR; ++t) asm volatile("" ::"v"(acc[t][mt]));
+        continue;
+      }
+      float* p = args.partial + (static_cast<int64_t>(split) * args.M + row0 + m) * N + n0 + 4 * g;
+      if constexpr (kSlabSc1) {
+        // write-through (sc1) stores: the slab lines leave the XCD L2 clean, so the split-K
+        // hand-off needs no release fence (an L2 write-back per workgroup, guide §5 "In-launch
+        // split-K reduction"); slabs are < 2 GiB: 32-bit buffer offsets
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(args.partial, static_cast<short>(0), 0x7ffffff0, 0x00020000);
+        const int boff = static_cast<int>((p - args.partial) * 4);
+#pragma unroll
+        for (int t = 0; t < kR; ++t)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t][mt]), rsrc, boff + 64 * t, 0, 16);
+      } else {
+#pragma unroll
+        for (int t = 0; t < kR; ++t) {
+          const f32x4 v = acc[t][mt];
+          if constexpr (PK_SLAB_NT)  // streaming store: no dirty L2 lines left for the launch-end write-back
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p + 16 * t));
+          else
+            *reinterpret_cast<f32x4*>(p + 16 * t) = v;
+        }
       }
     } else if constexpr (MODE == kBF16) {
       bf16_t* o = args.out + static_cast<int64_t>(row0 + m) * args.ldo + n0 + 4 * g;
@@ -506,7 +527,8 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     if (tid == 0) {
       int last = 1;
       if (S > 1) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // write-through (sc1) slabs are already past the XCD L2: no release (L2 write-back) needed
+        if constexpr (!kSlabSc1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int t = __hip_atomic_fetch_add(args.counters + nb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = t == S - 1;
@@ -521,12 +543,12 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     __syncthreads();
     if (!last_s) return;
     switch (S) {
-      case 1: epilogue<MODE, 1>(args, nb); break;
-      case 2: epilogue<MODE, 2>(args, nb); break;
-      case 4: epilogue<MODE, 4>(args, nb); break;
-      case 8: epilogue<MODE, 8>(args, nb); break;
-      case 16: epilogue<MODE, 16>(args, nb); break;
-      default: epilogue<MODE, 0>(args, nb); break;
+      case 1: epilogue<MODE, 1, KR>(args, nb); break;
+      case 2: epilogue<MODE, 2, KR>(args, nb); break;
+      case 4: epilogue<MODE, 4, KR>(args, nb); break;
+      case 8: epilogue<MODE, 8, KR>(args, nb); break;
+      case 16: epilogue<MODE, 16, KR>(args, nb); break;
+      default: epilogue<MODE, 0, KR>(args, nb); break;
     }
   }
 }
@@ -804,14 +826,14 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
   }
 }
 
-template <int MODE, bool PK, bool NORM, bool NT, bool RS = false>
+template <int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2>
 int launch(const GemmArgs& a, hipStream_t stream) {
-  const dim3 grid((a.N / 128) * a.S, a.row_offsets != nullptr ? a.groups : 1);
+  const dim3 grid((a.N / (64 * KR)) * a.S, a.row_offsets != nullptr ? a.groups : 1);
   switch ((min(a.M, a.max_group_rows > 0 ? a.max_group_rows : a.M) + 15) / 16) {
-    case 1: skinny_gemm_kernel<1, MODE, PK, NORM, NT, RS><<<grid, 256, 0, stream>>>(a); break;
-    case 2: skinny_gemm_kernel<2, MODE, PK, NORM, NT, RS><<<grid, 256, 0, stream>>>(a); break;
-    case 3: skinny_gemm_kernel<3, MODE, PK, NORM, NT, RS><<<grid, 256, 0, stream>>>(a); break;
-    case 4: skinny_gemm_kernel<4, MODE, PK, NORM, NT, RS><<<grid, 256, 0, stream>>>(a); break;
+    case 1: skinny_gemm_kernel<1, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a); break;
+    case 2: skinny_gemm_kernel<2, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a); break;
+    case 3: skinny_gemm_kernel<3, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a); break;
+    case 4: skinny_gemm_kernel<4, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a); break;
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
@@ -846,8 +868,22 @@ int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
   const bool packed = (mode & 16) != 0;  // bit 4: W in block-packed layout
   const bool norm = (mode & 32) != 0;    // bit 5: RMSNorm prologue on A
   const bool nt = (mode & 64) != 0;      // bit 6: non-temporal weight loads (hint)
+  const bool half = (mode & 128) != 0;   // bit 7: 64-row n-blocks (KR = 1)
   if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr || a.M > 64)) return -1;
-  if (a.row_scale && (grouped || norm || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.M > 64)) return -1;
+  if (half) {  // split-K projections only: fp32 slabs or the in-launch residual update
+    if (grouped || norm || a.row_scale || nt) return -1;
+    if ((mode & 7) == kPartial)
+      return packed ? launch<kPartial, true, false, false, false, 1>(a, stream)
+                    : launch<kPartial, false, false, false, false, 1>(a, stream);
+    if ((mode & 7) == kAddResNorm) {
+      if (a.counters == nullptr || a.residual == nullptr || a.sumsq_parts == nullptr) return -1;
+      return packed ? launch<kAddResNorm, true, false, false, false, 1>(a, stream)
+                    : launch<kAddResNorm, false, false, false, false, 1>(a, stream);
+    }
+    return -1;
+  }
+  if (a.row_scale && (grouped || norm || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64 || a.M > 64))
+    return -1;
   switch (mode & 7) {
     case kBF16:
       if (a.S != 1 || norm) return -1;

@@ -48,6 +48,14 @@ FOLD_NORM = os.environ.get("POLYKEY_FOLD_NORM", "1") == "1"
 # stream: reduce-scatter / all-gather around the norms instead of all-reduces (_forward_sp).
 SEQUENCE_PARALLEL = os.environ.get("POLYKEY_SEQUENCE_PARALLEL", "1") == "1"
 SP_MIN_TOKENS = int(os.environ.get("POLYKEY_SP_MIN_TOKENS", "256"))
+# Folded-norm decode: the o / down projections (64-row n-blocks, split-K INLAUNCH_SPLIT) reduce
+# their own split-K slabs in-launch -- the last split of each n-block to arrive adds the sum into
+# the residual and writes the row sums of squares the next projection's RowScale needs -- instead
+# of a separate residual-update kernel after each (tools/gemm_lab.hip o_res / down_res: -2 us per
+# projection in isolation; neutral on the graph-captured 8B step, profiles/r2_decode_ab.txt, so off
+# by default).
+INLAUNCH_RESIDUAL = os.environ.get("POLYKEY_INLAUNCH_RESIDUAL", "0") == "1"
+INLAUNCH_SPLIT = int(os.environ.get("POLYKEY_INLAUNCH_SPLIT", "4"))
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:
@@ -456,11 +464,14 @@ class LlamaForCausalLM(nn.Module):
         rinv = rsqrt(mean(residual^2) + eps) is formed by each consumer from the parts."""
         T, H = x.shape
         if getattr(self, "_parts_buf", None) is None:
-            self._parts_buf = torch.zeros((H // 1024) * gemm.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
-        buf = self._parts_buf
+            self._parts_buf = torch.zeros((H // 64) * gemm.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
+            self._parts_buf2 = torch.zeros_like(self._parts_buf)
+        buf, buf2 = self._parts_buf, self._parts_buf2
         residual = x
         parts = gemm.residual_parts(None, residual, buf)
         last = len(self.layers) - 1
+        inlaunch = INLAUNCH_RESIDUAL and H % 64 == 0
+        ctr = self._fused_buffers()[0] if inlaunch else None
         for i, layer in enumerate(self.layers):
             at, mlp = layer.attn, layer.mlp
             kc, vc = kv_caches[i]
@@ -470,9 +481,19 @@ class LlamaForCausalLM(nn.Module):
             else:
                 q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
                 a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
-            parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p), residual, buf)
+            if inlaunch:  # the o-projection's last splits add into the residual themselves
+                parts = gemm.linear_add_residual(a, at.o, ws, ctr, residual, buf2, S=INLAUNCH_SPLIT, packed=at.o_p,
+                                                 half=True)
+            else:
+                parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p), residual, buf2)
             h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf,
                                  rowscale=gemm.RowScale(parts, layer.eps))
+            if inlaunch:
+                parts = gemm.linear_add_residual(h, mlp.down, ws, ctr, residual, buf, S=INLAUNCH_SPLIT,
+                                                 packed=mlp.down_p, half=True)
+                if i == last:
+                    x = gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
+                continue
             d = gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p)
             if i < last:
                 parts = gemm.residual_parts(d, residual, buf)

@@ -108,17 +108,24 @@ def _launch_ex(mode: int, x: torch.Tensor, w: torch.Tensor, packed: Optional[tor
     native.call("pk_skinny_gemm_ex", ctypes.byref(a), mode, native.stream_ptr())
 
 
+HALF_BIT = 128  # 64-row n-blocks (KR = 1): twice the n-blocks, half the split-K
+
+
 def linear_add_residual(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, counters: torch.Tensor,
                         residual: torch.Tensor, sumsq_parts: torch.Tensor, S: Optional[int] = None,
-                        packed: Optional[torch.Tensor] = None) -> None:
-    """residual += x @ w^T (split-K reduced in-kernel) and sumsq_parts[N/128, M] = per-row
-    sums of squares of the new residual over each 128-column block (for the next NormIn)."""
+                        packed: Optional[torch.Tensor] = None, half: bool = False) -> torch.Tensor:
+    """residual += x @ w^T (split-K reduced in-kernel by the last split of each n-block to
+    arrive) and sumsq_parts[N/nblk, M] = per-row sums of squares of the new residual over each
+    n-block of columns (128, or 64 with ``half``), for the next projection's RowScale / NormIn.
+    Returns the parts view."""
     M, K = x.shape
     N = w.shape[0]
+    nblk = 64 if half else 128
     S = S or choose_split(N, K, M)
-    assert ws.numel() >= S * M * N and sumsq_parts.numel() >= (N // 128) * M and counters.numel() >= N // 128
-    _launch_ex(MODE_ADD_RES_NORM, x, w, packed, S, ws=ws, counters=counters, residual=residual,
-               sumsq_parts=sumsq_parts)
+    assert ws.numel() >= S * M * N and sumsq_parts.numel() >= (N // nblk) * M and counters.numel() >= N // nblk
+    _launch_ex(MODE_ADD_RES_NORM | (HALF_BIT if half else 0), x, w, packed, S, ws=ws, counters=counters,
+               residual=residual, sumsq_parts=sumsq_parts)
+    return sumsq_parts.view(-1)[: (N // nblk) * M].view(N // nblk, M)
 
 
 def linear_qkv_rope(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, counters: torch.Tensor,

@@ -113,9 +113,9 @@ def test_fragment_packed_silu():
     torch.testing.assert_close(y.float(), exp.float(), atol=3e-2, rtol=3e-2)
 
 
-def _sumsq_parts(res: torch.Tensor) -> torch.Tensor:
+def _sumsq_parts(res: torch.Tensor, blk: int = 128) -> torch.Tensor:
     M, H = res.shape
-    return res.float().view(M, H // 128, 128).pow(2).sum(-1).t().contiguous()
+    return res.float().view(M, H // blk, blk).pow(2).sum(-1).t().contiguous()
 
 
 @pytest.mark.parametrize("packed", [False, True])
@@ -134,6 +134,42 @@ def test_add_residual_epilogue(M, H, K, S, packed):
         torch.testing.assert_close(r.float(), exp.float(), atol=3e-2, rtol=2e-2)
         torch.testing.assert_close(parts, _sumsq_parts(r), atol=1e-2, rtol=1e-3)
     assert int(ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M,H,K,S", [(64, 4096, 4096, 4), (5, 4096, 14336, 4), (33, 1024, 512, 2), (64, 8192, 3584, 2)])
+def test_add_residual_epilogue_half_blocks(M, H, K, S):
+    """64-row n-blocks (KR = 1) with write-through slabs: the decode o / down projections of the
+    folded-norm chain.  Parts are per 64-column block."""
+    x, w = rnd(M, K), rnd(H, K, scale=0.05)
+    res = rnd(M, H)
+    ws = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
+    ctr = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    buf = torch.full((H // 64 * M,), -1.0, device="cuda")
+    exp = ((x.float() @ w.float().t()).to(torch.bfloat16).float() + res.float()).to(torch.bfloat16)
+    for _ in range(3):  # later rounds check the tickets re-armed
+        r = res.clone()
+        parts = gemm.linear_add_residual(x, w, ws, ctr, r, buf, S, packed=gemm.pack_weight(w), half=True)
+        torch.testing.assert_close(r.float(), exp.float(), atol=3e-2, rtol=2e-2)
+        assert parts.shape == (H // 64, M)
+        torch.testing.assert_close(parts, _sumsq_parts(r, 64), atol=1e-2, rtol=1e-3)
+    assert int(ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M", [3, 64])
+def test_rowscale_from_64_parts(M):
+    """RowScale with 64 sum-of-squares parts per row (what the half-block residual update
+    writes for H = 4096) gives the same rinv as 4 parts."""
+    H, N = 4096, 1024
+    res = rnd(M, H)
+    w = rnd(N, H, scale=0.02)
+    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wp = gemm.pack_weight(gemm.fold_norm(w, nw))
+    ws = torch.empty(2 * 4 * M * N, dtype=torch.float32, device="cuda")
+    p4 = gemm.residual_parts(None, res.clone(), torch.empty(4 * 64, device="cuda"))
+    p64 = _sumsq_parts(res, 64)
+    a = gemm.linear_partial_rowscale(res, w, ws[: 4 * M * N], gemm.RowScale(p4, 1e-5), S=4, packed=wp).view().sum(0)
+    b = gemm.linear_partial_rowscale(res, w, ws[4 * M * N:], gemm.RowScale(p64, 1e-5), S=4, packed=wp).view().sum(0)
+    torch.testing.assert_close(a, b, atol=1e-3, rtol=1e-3)
 
 
 @pytest.mark.parametrize("use_norm", [False, True])

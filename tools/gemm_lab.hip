@@ -29,14 +29,30 @@ struct Shape {
 int main(int argc, char** argv) {
   const int M = argc > 1 ? std::atoi(argv[1]) : 64;
   const char* tag = argc > 2 ? argv[2] : "";
-  const Shape shapes[] = {{"qkv", 6144, 4096, 4, 1 | 16},   {"o", 4096, 4096, 8, 1 | 16},
-                          {"gate_up", 28672, 4096, 1, 2 | 16 | 64}, {"down", 4096, 14336, 8, 1 | 16},
-                          {"lm_head", 128256, 4096, 1, 0 | 16 | 64}};
+  // mode: bits 0-2 epilogue (0 bf16, 1 fp32 slabs, 2 SiLU, 3 in-launch residual add + row sums of
+  // squares), bit 4 block-packed, bit 6 non-temporal, bit 7 64-row n-blocks (KR = 1)
+  const Shape all_shapes[] = {{"qkv", 6144, 4096, 4, 1 | 16},   {"o", 4096, 4096, 8, 1 | 16},
+                              {"gate_up", 28672, 4096, 1, 2 | 16 | 64}, {"down", 4096, 14336, 8, 1 | 16},
+                              {"lm_head", 128256, 4096, 1, 0 | 16 | 64},
+                              {"o_kr1_s4", 4096, 4096, 4, 1 | 16 | 128}, {"down_kr1_s4", 4096, 14336, 4, 1 | 16 | 128},
+                              {"qkv_kr1_s4", 6144, 4096, 4, 1 | 16 | 128}, {"qkv_kr1_s2", 6144, 4096, 2, 1 | 16 | 128},
+                              {"o_res_s8", 4096, 4096, 8, 3 | 16}, {"o_res_kr1_s4", 4096, 4096, 4, 3 | 16 | 128},
+                              {"down_res_s8", 4096, 14336, 8, 3 | 16}, {"down_res_kr1_s4", 4096, 14336, 4, 3 | 16 | 128}};
+  const char* only = argc > 4 ? argv[4] : "";
+  std::vector<Shape> shapes;
+  for (const Shape& s : all_shapes)
+    if (!*only || std::string(only).find(std::string(",") + s.name + ",") != std::string::npos) shapes.push_back(s);
   void *A, *out, *part;
   CHECK(hipMalloc(&A, 64ull * 16384 * 2));
   CHECK(hipMalloc(&out, 64ull * 131072 * 2));
   CHECK(hipMalloc(&part, 16ull * 64 * 131072 * 4));
   CHECK(hipMemset(A, 0x3c, 64ull * 16384 * 2));
+  void *res, *parts, *ctr;
+  CHECK(hipMalloc(&res, 64ull * 16384 * 2));
+  CHECK(hipMalloc(&parts, 64ull * 1024 * 4));
+  CHECK(hipMalloc(&ctr, 4096 * 4));
+  CHECK(hipMemset(res, 0, 64ull * 16384 * 2));
+  CHECK(hipMemset(ctr, 0, 4096 * 4));
   for (const Shape& s : shapes) {
     const size_t wbytes = static_cast<size_t>(s.N) * s.K * 2;
     // "hot": one copy re-read every call (served from the Infinity Cache when it fits)
@@ -48,8 +64,16 @@ int main(int argc, char** argv) {
       CHECK(hipMemset(w, 0x11, wbytes));
     }
     auto call = [&](int i) {
-      const int rc = pk_skinny_gemm(out, part, A, W[i % copies], M, s.N, s.K, s.K, (s.mode & 7) == 2 ? s.N / 2 : s.N,
-                                    s.S, s.mode, nullptr);
+      GemmArgs g{};
+      g.out = static_cast<bf16_t*>(out);
+      g.partial = static_cast<float*>(part);
+      g.A = static_cast<const bf16_t*>(A);
+      g.W = static_cast<const bf16_t*>(W[i % copies]);
+      g.M = M; g.N = s.N; g.K = s.K; g.lda = s.K; g.ldo = (s.mode & 7) == 2 ? s.N / 2 : s.N; g.S = s.S;
+      g.counters = static_cast<int*>(ctr);
+      g.residual = static_cast<bf16_t*>(res);
+      g.sumsq_parts = static_cast<float*>(parts);
+      const int rc = pk_skinny_gemm_ex(&g, s.mode, nullptr);
       if (rc) {
         std::fprintf(stderr, "launch rc %d\n", rc);
         std::exit(1);
@@ -68,7 +92,7 @@ int main(int argc, char** argv) {
     float ms = 0.f;
     CHECK(hipEventElapsedTime(&ms, a, b));
     const double us = ms * 1e3 / iters;
-    std::printf("%-10s %-8s N=%6d K=%5d S=%2d  %7.2f us  %5.2f TB/s\n", tag, s.name, s.N, s.K, s.S, us,
+    std::printf("%-10s %-16s N=%6d K=%5d S=%2d  %7.2f us  %5.2f TB/s\n", tag, s.name, s.N, s.K, s.S, us,
                 wbytes / us / 1e6);
     for (auto& w : W) CHECK(hipFree(w));
   }
