@@ -22,17 +22,17 @@ class BlockManager : public pk::BlockManagerCore {
  public:
   using pk::BlockManagerCore::BlockManagerCore;
 
-  U64 prefix_hashes_py(I32 tokens, int64_t max_blocks) const {
+  U64 prefix_hashes_py(I32 tokens, int64_t max_blocks, uint64_t salt) const {
     const int64_t n = tokens.shape(0);
     U64 out(std::max<int64_t>(0, std::min<int64_t>(n / block_size(), max_blocks)));
-    prefix_hashes(tokens.data(), n, out.mutable_data(), out.shape(0));
+    prefix_hashes(tokens.data(), n, out.mutable_data(), out.shape(0), salt);
     return out;
   }
-  int64_t match_prefix_py(int64_t seq, U64 hashes, int64_t n) {
-    return match_prefix(seq, hashes.data(), std::min<int64_t>(n, hashes.shape(0)));
+  int64_t match_prefix_py(int64_t seq, U64 hashes, I32 tokens, int64_t n) {
+    return match_prefix(seq, hashes.data(), tokens.data(), tokens.shape(0), std::min<int64_t>(n, hashes.shape(0)));
   }
-  void commit_prefix_py(int64_t seq, U64 hashes, int64_t n) {
-    commit_prefix(seq, hashes.data(), std::min<int64_t>(n, hashes.shape(0)));
+  void commit_prefix_py(int64_t seq, U64 hashes, I32 tokens, int64_t n) {
+    commit_prefix(seq, hashes.data(), tokens.data(), tokens.shape(0), std::min<int64_t>(n, hashes.shape(0)));
   }
 
   int64_t pack_step(I64 seq_ids, I32 num_computed, I32 num_new, I32 tokens, I32 input_ids, I32 positions,
@@ -58,15 +58,19 @@ PYBIND11_MODULE(_pk_runtime, m) {
   m.doc() = "polykey native runtime: paged KV block manager, step packer, TP step channel";
   bind_step_channel(m);
   py::class_<BlockManager>(m, "BlockManager")
-      .def(py::init<int64_t, int, int64_t, bool>(), py::arg("num_blocks"), py::arg("block_size"),
-           py::arg("watermark_blocks") = 0, py::arg("prefix_caching") = false)
+      .def(py::init<int64_t, int, int64_t, bool, uint64_t>(), py::arg("num_blocks"), py::arg("block_size"),
+           py::arg("watermark_blocks") = 0, py::arg("prefix_caching") = false, py::arg("hash_key") = 0)
       .def_property_readonly("prefix_caching", &BlockManager::prefix_caching)
       .def_property_readonly("num_cached", &BlockManager::num_cached)
       .def_property_readonly("prefix_queries", &BlockManager::prefix_queries)
       .def_property_readonly("prefix_hits", &BlockManager::prefix_hits)
-      .def("prefix_hashes", &BlockManager::prefix_hashes_py, py::arg("tokens"), py::arg("max_blocks") = INT64_MAX)
-      .def("match_prefix", &BlockManager::match_prefix_py, py::arg("seq"), py::arg("hashes"), py::arg("n"))
-      .def("commit_prefix", &BlockManager::commit_prefix_py, py::arg("seq"), py::arg("hashes"), py::arg("n"))
+      .def_property_readonly("prefix_collisions", &BlockManager::prefix_collisions)
+      .def("prefix_hashes", &BlockManager::prefix_hashes_py, py::arg("tokens"), py::arg("max_blocks") = INT64_MAX,
+           py::arg("salt") = 0)
+      .def("match_prefix", &BlockManager::match_prefix_py, py::arg("seq"), py::arg("hashes"), py::arg("tokens"),
+           py::arg("n"))
+      .def("commit_prefix", &BlockManager::commit_prefix_py, py::arg("seq"), py::arg("hashes"), py::arg("tokens"),
+           py::arg("n"))
       .def("reset_prefix_cache", &BlockManager::reset_prefix_cache)
       .def("ref_count", &BlockManager::ref_count)
       .def_property_readonly("num_free", &BlockManager::num_free)

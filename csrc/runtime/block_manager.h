@@ -7,10 +7,18 @@
 // (match_prefix, reference-counted, shared read-only) and computes only the rest.  Released
 // blocks that carry a hash stay cached in an LRU list and count as free; allocation evicts
 // the least recently released one only when the plain free list is empty.
+//
+// Cache-poisoning hardening (cf. vLLM CVE-2025-25183): the chained hash is keyed with a
+// per-process random secret (optionally mixed with a per-request salt, e.g. a tenant id), and a
+// hash hit alone never shares a block -- match_prefix also requires the cached block's stored
+// tokens to equal the request's and its registered parent hash to equal the request's previous
+// block hash, so a forged 64-bit collision cannot serve one prompt another prompt's KV.
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <list>
+#include <random>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -20,9 +28,20 @@ namespace pk {
 
 class BlockManagerCore {
  public:
-  BlockManagerCore(int64_t num_blocks, int block_size, int64_t watermark_blocks, bool prefix_caching = false)
+  // hash_key 0: a random per-process key (tests pass a fixed one for reproducible hashes)
+  BlockManagerCore(int64_t num_blocks, int block_size, int64_t watermark_blocks, bool prefix_caching = false,
+                   uint64_t hash_key = 0)
       : num_blocks_(num_blocks), block_size_(block_size), watermark_(watermark_blocks), prefix_caching_(prefix_caching) {
     if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("num_blocks and block_size must be > 0");
+    if (hash_key == 0) {
+      std::random_device rd;
+      hash_key = (static_cast<uint64_t>(rd()) << 32) ^ rd();
+    }
+    key_ = mix(hash_key ^ 0x6a09e667f3bcc908ULL);
+    if (prefix_caching_) {
+      tokens_.assign(static_cast<size_t>(num_blocks) * block_size, 0);
+      parent_.assign(num_blocks, 0);
+    }
     free_.reserve(num_blocks);
     for (int64_t b = num_blocks - 1; b >= 0; --b) free_.push_back(static_cast<int32_t>(b));
     ref_.assign(num_blocks, 0);
@@ -37,6 +56,7 @@ class BlockManagerCore {
   bool prefix_caching() const { return prefix_caching_; }
   int64_t prefix_queries() const { return queries_; }
   int64_t prefix_hits() const { return hits_; }
+  int64_t prefix_collisions() const { return collisions_; }
   int64_t num_blocks() const { return num_blocks_; }
   int block_size() const { return block_size_; }
   int64_t blocks_for(int64_t tokens) const { return (tokens + block_size_ - 1) / block_size_; }
@@ -66,11 +86,12 @@ class BlockManagerCore {
     tables_.erase(it);
   }
 
-  // Chained hashes of the full blocks of tokens[0:n] (at most max_out): h_i covers every token
-  // of blocks 0..i, so equal hashes mean equal prefixes (up to 64-bit collisions).  Never 0.
-  int64_t prefix_hashes(const int32_t* tokens, int64_t n, uint64_t* out, int64_t max_out) const {
+  // Keyed chained hashes of the full blocks of tokens[0:n] (at most max_out): h_i covers every
+  // token of blocks 0..i and the salt.  Never 0.  Lookups verify tokens (match_prefix), so the
+  // hash only has to spread, not to be collision-free.
+  int64_t prefix_hashes(const int32_t* tokens, int64_t n, uint64_t* out, int64_t max_out, uint64_t salt = 0) const {
     const int64_t nb = std::min<int64_t>(n / block_size_, max_out);
-    uint64_t h = 0x6a09e667f3bcc908ULL;
+    uint64_t h = salt ? mix(key_ ^ mix(salt)) : key_;
     for (int64_t b = 0; b < nb; ++b) {
       for (int j = 0; j < block_size_; ++j) {
         h ^= static_cast<uint32_t>(tokens[b * block_size_ + j]);
@@ -82,9 +103,11 @@ class BlockManagerCore {
     return nb;
   }
 
-  // A sequence without blocks takes the longest run of cached blocks matching hashes[0:n];
-  // returns the number of blocks taken (its first matched * block_size tokens are computed).
-  int64_t match_prefix(int64_t seq, const uint64_t* hashes, int64_t n) {
+  // A sequence without blocks takes the longest run of cached blocks matching hashes[0:n] whose
+  // stored tokens equal tokens[i*bs:(i+1)*bs] and whose parent hash is hashes[i-1]; returns the
+  // number of blocks taken (its first matched * block_size tokens are computed).
+  int64_t match_prefix(int64_t seq, const uint64_t* hashes, const int32_t* tokens, int64_t n_tokens, int64_t n) {
+    n = std::min<int64_t>(n, n_tokens / block_size_);
     if (!prefix_caching_ || n <= 0 || tables_.count(seq)) return 0;
     queries_ += n;
     std::vector<int32_t> t;
@@ -92,6 +115,12 @@ class BlockManagerCore {
       auto it = cached_.find(hashes[i]);
       if (it == cached_.end()) break;
       const int32_t b = it->second;
+      if (parent_[b] != (i ? hashes[i - 1] : 0) ||
+          std::memcmp(&tokens_[static_cast<size_t>(b) * block_size_], tokens + i * block_size_,
+                      sizeof(int32_t) * block_size_) != 0) {
+        ++collisions_;
+        break;
+      }
       if (in_lru_[b]) {
         lru_.erase(lru_pos_[b]);
         in_lru_[b] = 0;
@@ -105,17 +134,21 @@ class BlockManagerCore {
     return got;
   }
 
-  // Registers the sequence's first n blocks (their KV computed) under hashes[0:n].  A block
-  // already registered, or a hash another block already holds, is left as it is.
-  void commit_prefix(int64_t seq, const uint64_t* hashes, int64_t n) {
+  // Registers the sequence's first n blocks (their KV computed) under hashes[0:n], keeping each
+  // block's tokens and parent hash for match_prefix.  A block already registered, or a hash
+  // another block already holds, is left as it is.
+  void commit_prefix(int64_t seq, const uint64_t* hashes, const int32_t* tokens, int64_t n_tokens, int64_t n) {
     if (!prefix_caching_) return;
     auto it = tables_.find(seq);
     if (it == tables_.end()) return;
-    const int64_t m = std::min<int64_t>(n, static_cast<int64_t>(it->second.size()));
+    const int64_t m = std::min<int64_t>({n, static_cast<int64_t>(it->second.size()), n_tokens / block_size_});
     for (int64_t i = 0; i < m; ++i) {
       const int32_t b = it->second[i];
       if (hash_[b] != 0 || hashes[i] == 0 || cached_.count(hashes[i])) continue;
       hash_[b] = hashes[i];
+      parent_[b] = i ? hashes[i - 1] : 0;
+      std::memcpy(&tokens_[static_cast<size_t>(b) * block_size_], tokens + i * block_size_,
+                  sizeof(int32_t) * block_size_);
       cached_.emplace(hashes[i], b);
     }
   }
@@ -210,7 +243,10 @@ class BlockManagerCore {
   int block_size_;
   int64_t watermark_;
   bool prefix_caching_;
-  int64_t queries_ = 0, hits_ = 0;
+  uint64_t key_ = 0;
+  int64_t queries_ = 0, hits_ = 0, collisions_ = 0;
+  std::vector<int32_t> tokens_;   // [num_blocks, block_size] tokens of each registered block
+  std::vector<uint64_t> parent_;  // hash of the block before it in its sequence (0: first block)
   std::vector<int32_t> free_;
   std::vector<int32_t> ref_;
   std::vector<uint64_t> hash_;

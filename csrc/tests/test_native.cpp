@@ -83,20 +83,21 @@ static void test_prefix_cache_churn() {
   pk::BlockManagerCore bm(NB, BS, 0, true);
   std::mt19937_64 rng(99);
   std::vector<std::vector<uint64_t>> pref(4, std::vector<uint64_t>(4));
+  std::vector<std::vector<int32_t>> ptoks(4, std::vector<int32_t>(4 * BS));
   for (int p = 0; p < 4; ++p) {
-    std::vector<int32_t> toks(4 * BS);
-    for (int i = 0; i < 4 * BS; ++i) toks[i] = p * 1000 + (i % 7);
-    CHECK(bm.prefix_hashes(toks.data(), 4 * BS, pref[p].data(), 4) == 4);
+    for (int i = 0; i < 4 * BS; ++i) ptoks[p][i] = p * 1000 + (i % 7);
+    CHECK(bm.prefix_hashes(ptoks[p].data(), 4 * BS, pref[p].data(), 4) == 4);
   }
   std::unordered_map<int64_t, int64_t> len;
   for (int it = 0; it < 20000; ++it) {
     const int op = static_cast<int>(rng() % 3);
     const int64_t seq = static_cast<int64_t>(rng() % 24);
     if (op == 0 && !len.count(seq)) {
-      const auto& h = pref[rng() % 4];
-      const int64_t got = bm.match_prefix(seq, h.data(), 3);
+      const int p = static_cast<int>(rng() % 4);
+      const auto& h = pref[p];
+      const int64_t got = bm.match_prefix(seq, h.data(), ptoks[p].data(), 4 * BS, 3);
       if (bm.allocate(seq, 4 * BS)) {
-        bm.commit_prefix(seq, h.data(), 4);
+        bm.commit_prefix(seq, h.data(), ptoks[p].data(), 4 * BS, 4);
         len[seq] = 4 * BS;
       } else {
         bm.free_seq(seq);

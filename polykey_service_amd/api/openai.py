@@ -18,7 +18,7 @@ from ..engine.sequence import SamplingParams
 from ..service.base import ToolError
 
 _SAMPLING_KEYS = ("max_tokens", "temperature", "top_p", "top_k", "min_p", "seed", "stop", "ignore_eos",
-                  "stop_token_ids")
+                  "stop_token_ids", "cache_salt")
 
 
 

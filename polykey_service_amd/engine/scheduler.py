@@ -52,6 +52,15 @@ class ScheduledBatch:
         return out
 
 
+def _salt(s: Optional[str]) -> int:
+    """Per-request prefix-cache salt (a tenant id): requests only share cached blocks with
+    requests of the same salt.  0 = the shared namespace."""
+    if not s:
+        return 0
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(s.encode(), digest_size=8).digest(), "little") or 1
+
+
 class Scheduler:
     def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
                  max_model_len: int = 8192, max_prefill_chunk: Optional[int] = None):
@@ -65,7 +74,8 @@ class Scheduler:
         self.by_request: Dict[str, Sequence] = {}
         self.num_preemptions = 0
         self.prefix_caching = bool(getattr(block_manager, "prefix_caching", False))
-        self._hashes: Dict[int, np.ndarray] = {}  # seq_id -> chained block hashes at admission
+        # seq_id -> (chained block hashes, prompt tokens) at admission
+        self._hashes: Dict[int, Tuple[np.ndarray, np.ndarray]] = {}
         self.num_cached_tokens = 0  # prompt tokens served from the prefix cache
 
     # --------------------------------------------------------------- queue ops
@@ -127,10 +137,10 @@ class Scheduler:
             return
         bs = self.bm.block_size
         toks = np.asarray(seq.token_slice(0, seq.num_tokens), dtype=np.int32)
-        h = self.bm.prefix_hashes(toks)
-        self._hashes[seq.seq_id] = h
+        h = self.bm.prefix_hashes(toks, salt=_salt(seq.cache_salt))
+        self._hashes[seq.seq_id] = (h, toks)
         usable = max(0, (seq.num_tokens - 2) // bs)  # >= 2 tokens left: the step still samples
-        got = self.bm.match_prefix(seq.seq_id, h, min(usable, len(h)))
+        got = self.bm.match_prefix(seq.seq_id, h, toks, min(usable, len(h)))
         seq.num_computed = got * bs
 
     def _unmatch(self, seq: Sequence) -> None:
@@ -141,9 +151,9 @@ class Scheduler:
 
     def commit_prefix(self, seq: Sequence) -> None:
         """Register the sequence's full blocks whose KV is now in the cache."""
-        h = self._hashes.get(seq.seq_id)
-        if h is not None and not seq.is_finished():
-            self.bm.commit_prefix(seq.seq_id, h, seq.num_computed // self.bm.block_size)
+        ht = self._hashes.get(seq.seq_id)
+        if ht is not None and not seq.is_finished():
+            self.bm.commit_prefix(seq.seq_id, ht[0], ht[1], seq.num_computed // self.bm.block_size)
 
     # ------------------------------------------------------------------ policy
     def _preempt_youngest(self, protect: Sequence) -> Optional[Sequence]:
@@ -212,12 +222,14 @@ class Scheduler:
                 self._unmatch(seq)
                 break
             self.bm.allocate(seq.seq_id, seq.num_computed + n)
-            self.num_cached_tokens += seq.num_computed
-            seq.num_cached_tokens += seq.num_computed
             self.waiting.popleft()
             seq.status = SeqStatus.RUNNING
             if seq.first_scheduled is None:
+                # cache hits count once per request: a preempted sequence re-admitted later
+                # re-matches its own committed blocks (prompt + output), which is no hit
                 seq.first_scheduled = time.monotonic()
+                seq.num_cached_tokens = min(seq.num_computed, len(seq.prompt_ids))
+                self.num_cached_tokens += seq.num_cached_tokens
             self.running.append(seq)
             if seq.num_pending == 1 and n == 1:
                 decodes.append(seq)

@@ -19,6 +19,7 @@ class SamplingParams:
     stop_token_ids: Seq[int] = ()
     ignore_eos: bool = False
     stop: Seq[str] = ()           # stop strings (checked on detokenized text)
+    cache_salt: Optional[str] = None  # prefix-cache namespace (e.g. a tenant id); None = shared
 
     def validate(self, max_model_len: int) -> None:
         if self.max_tokens < 1:
@@ -50,6 +51,8 @@ class SamplingParams:
                     v = (v,) if isinstance(v, str) else tuple(v)
                 elif f.name == "ignore_eos":
                     v = bool(v)
+                elif f.name == "cache_salt":
+                    v = str(v)
                 kw[f.name] = v
         return cls(**kw)
 
@@ -73,10 +76,11 @@ _ids = itertools.count(1)
 class Sequence:
     __slots__ = ("seq_id", "request_id", "prompt_ids", "output_ids", "params", "status", "num_computed",
                  "arrival", "first_scheduled", "first_token_time", "finish_time", "finish_reason",
-                 "num_preemptions", "eos_token_id", "token_times", "user", "num_cached_tokens")
+                 "num_preemptions", "eos_token_id", "token_times", "user", "num_cached_tokens",
+                 "cache_salt")
 
     def __init__(self, request_id: str, prompt_ids: List[int], params: SamplingParams, eos_token_id: int = -1,
-                 user=None):
+                 user=None, cache_salt: Optional[str] = None):
         self.seq_id = next(_ids)
         self.request_id = request_id
         self.prompt_ids = list(prompt_ids)
@@ -94,6 +98,8 @@ class Sequence:
         self.eos_token_id = eos_token_id
         self.token_times: List[float] = []
         self.user = user
+        # prefix-cache namespace (Scheduler._salt); None = the request's params.cache_salt
+        self.cache_salt = cache_salt if cache_salt is not None else getattr(params, "cache_salt", None)
 
     @property
     def num_tokens(self) -> int:

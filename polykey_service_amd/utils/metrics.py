@@ -37,10 +37,27 @@ class Metrics:
         self.step_seconds = Histogram("polykey_engine_step_seconds", "engine step wall time", buckets=_TOK_BUCKETS,
                                       registry=r)
         self.preemptions = Gauge("polykey_engine_preemptions", "preemptions so far", registry=r)
-        self.cached_tokens = Gauge("polykey_engine_prefix_cache_hit_tokens", "prompt tokens served from the "
-                                   "prefix cache so far", registry=r)
+        # cumulative engine counts exported as Counters (advanced by the delta since the last step)
+        self.cached_tokens = Counter("polykey_engine_prefix_cache_hit_tokens", "prompt tokens served from the "
+                                     "prefix cache", registry=r)
+        self.prefix_queries = Counter("polykey_engine_prefix_cache_queries", "full prompt blocks looked up in the "
+                                      "prefix cache", registry=r)
+        self.prefix_hits = Counter("polykey_engine_prefix_cache_hits", "prompt blocks served from the prefix cache",
+                                   registry=r)
+        self.prefix_collisions = Counter("polykey_engine_prefix_cache_rejected", "hash matches rejected by the "
+                                         "token / parent check", registry=r)
+        self._last: dict = {}
         self.cached_blocks = Gauge("polykey_engine_prefix_cache_blocks", "KV blocks registered in the prefix cache",
                                    registry=r)
+
+    def _advance(self, counter, key: str, total: int) -> None:
+        """Counter += growth of an engine-side cumulative count (a restarted engine's count
+        starting over from 0 is taken as growth from 0)."""
+        prev = self._last.get(key, 0)
+        delta = total - prev if total >= prev else total
+        if delta > 0:
+            counter.inc(delta)
+        self._last[key] = total
 
     @classmethod
     def start(cls, addr: str) -> "Metrics":
@@ -61,7 +78,10 @@ class Metrics:
         bm = engine.bm
         self.kv_util.set(1.0 - bm.num_free / max(bm.num_blocks, 1))
         self.preemptions.set(sch.num_preemptions)
-        self.cached_tokens.set(getattr(sch, "num_cached_tokens", 0))
+        self._advance(self.cached_tokens, "tokens", getattr(sch, "num_cached_tokens", 0))
+        self._advance(self.prefix_queries, "queries", getattr(bm, "prefix_queries", 0))
+        self._advance(self.prefix_hits, "hits", getattr(bm, "prefix_hits", 0))
+        self._advance(self.prefix_collisions, "collisions", getattr(bm, "prefix_collisions", 0))
         self.cached_blocks.set(getattr(bm, "num_cached", 0))
         n = 0
         for o in outputs:
