@@ -41,6 +41,9 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--ep", type=int, default=1,
+                    help="expert parallel degree (MoE): = --tp for EP inside the TP group, or = --gpus with "
+                         "--tp 1 for DP attention + expert all-to-all")
     ap.add_argument("--concurrency", type=int, default=64, help="concurrent gRPC clients per replica")
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--max-tokens", type=int, default=256)
@@ -92,6 +95,7 @@ async def run_waves(args, engine, st, leaders_group):
     V = engine.mcfg.vocab_size
     rng = random.Random(args.seed * 1000 + st.rank)
     tool = f"llm.generate:{args.model}"
+    llm = router.llm
 
     timing = os.environ.get("POLYKEY_BENCH_TIMING") == "1"
     marks = []
@@ -161,6 +165,8 @@ async def run_waves(args, engine, st, leaders_group):
     elapsed = time.perf_counter() - t0
     await channel.close()
     await srv.server.stop(0)
+    if engine.lockstep:  # DP attention + EP: leave the lockstep loop together with the other ranks
+        await asyncio.get_running_loop().run_in_executor(None, llm.shutdown)
     return tokens, elapsed, lats
 
 
@@ -176,7 +182,7 @@ def main(argv=None) -> int:
     from polykey_service_amd.engine.llm_engine import EngineConfig, LLMEngine
     from polykey_service_amd.parallel.state import init_parallel
 
-    st = init_parallel(tp=args.tp)
+    st = init_parallel(tp=args.tp, ep=args.ep)
     max_len = args.prompt_len + args.max_tokens + 32
     max_len = (max_len + 511) // 512 * 512
     ecfg = EngineConfig(model=args.model, seed=args.seed, max_num_seqs=max(args.concurrency, 1),
@@ -227,8 +233,9 @@ def main(argv=None) -> int:
                 "global_batch": args.concurrency * (st.world_size // st.tp_size),
                 "seq_len": args.prompt_len,
                 "output_len": args.max_tokens,
-                "parallelism": (f"tp{st.tp_size}" + (f"_dp{st.dp_size}" if st.dp_size > 1 else "")) if st.tp_size > 1
-                else f"dp{st.world_size}",
+                "parallelism": (f"tp{st.tp_size}" + (f"_dp{st.dp_size}" if st.dp_size > 1 else "")
+                                + (f"_ep{st.ep_size}" if st.ep_size > 1 else "")) if st.tp_size > 1
+                else f"dp{st.world_size}" + (f"_ep{st.ep_size}_a2a" if st.ep_size > 1 else ""),
                 "concurrency_per_replica": args.concurrency,
                 "rpc": f"ExecuteTool ({args.mode})",
                 "hip_graphs": not args.no_graphs,

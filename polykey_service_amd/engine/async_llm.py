@@ -106,7 +106,11 @@ class AsyncLLM:
             last = out
         return toks, last
 
-    def shutdown(self, timeout: float = 10.0) -> None:
+    def shutdown(self, timeout: Optional[float] = None) -> None:
+        """Stop the engine thread (DP attention + EP: waits until every rank has asked to stop,
+        up to ``timeout``; default 10 s, 600 s in lockstep)."""
+        if timeout is None:
+            timeout = 600.0 if self.engine.lockstep else 10.0
         self._stop = True
         self._wake.set()
         self._thread.join(timeout)
@@ -172,9 +176,20 @@ class AsyncLLM:
         eng = self.engine
         prof = self._profiler()
         try:
-            while not self._stop:
+            while True:
                 self._drain_cmds()
-                if not eng.has_unfinished():
+                if eng.lockstep:
+                    # DP attention + EP: one vote per iteration on every rank; the loop ends only
+                    # when every rank is stopping and none has work left (a rank leaving alone
+                    # would strand the others in their next all-to-all)
+                    busy, all_stop = eng.lockstep_vote(self._stop)
+                    if all_stop and not busy:
+                        break
+                else:
+                    if self._stop:
+                        break
+                    busy = eng.has_unfinished()
+                if not busy:
                     self._wake.wait(0.05)
                     self._wake.clear()
                     continue

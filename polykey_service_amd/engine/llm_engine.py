@@ -62,6 +62,16 @@ class LLMEngine:
         if cfg.max_model_len > mcfg.max_position:
             cfg = dataclasses.replace(cfg, max_model_len=mcfg.max_position)
             self.cfg = cfg
+        # DP attention + EP (ParallelState.dp_attention): every rank schedules its own requests
+        # and the ranks step in lockstep because each MoE layer is an all-to-all over all of
+        # them.  Steps are synchronous (no overlap / continuations) and eager: the dispatch
+        # sizes are read back per layer, which a captured graph cannot do.
+        self.lockstep = self.st.dp_attention
+        if self.lockstep:
+            if not mcfg.is_moe:
+                raise ValueError("DP attention + EP (tp=1, ep>1) needs an MoE model")
+            cfg = dataclasses.replace(cfg, hip_graphs=False, overlap=False)
+            self.cfg = cfg
         self.mcfg = mcfg
         dev = torch.device(cfg.device) if cfg.device else self.st.device
         self.device = dev
@@ -123,6 +133,8 @@ class LLMEngine:
         completed batch's :class:`RequestOutput` objects built and returned — so output
         construction and the caller's delivery of them run while the GPU executes the next
         step.  Without ``overlap`` each call launches and completes its own batch."""
+        if self.lockstep:
+            return self._step_lockstep()
         done = None
         if self._inflight is not None:
             batch, sampling, handle = self._inflight
@@ -141,6 +153,34 @@ class LLMEngine:
                 done = self._complete(*self._inflight)
                 self._inflight = None
         return self._outputs(done) if done else []
+
+    def _step_lockstep(self) -> List[RequestOutput]:
+        """DP attention + EP step: one host vote (gloo) per step decides whether the EP group
+        runs a forward; a rank with nothing scheduled joins it through the model's idle pass."""
+        from ..parallel import comm
+        batch = self.scheduler.schedule()
+        if not comm.ep_any(not batch.empty):
+            return []
+        if batch.empty:
+            self.model.idle_forward()
+            self.runner.stats["idle_steps"] = self.runner.stats.get("idle_steps", 0) + 1
+            return []
+        done = self._complete(batch, batch.sampling_seqs(), self.runner.launch(batch))
+        return self._outputs(done)
+
+    def lockstep_vote(self, stopping: bool):
+        """DP attention + EP loop vote → (any rank has work, every rank is stopping)."""
+        from ..parallel import comm
+        return comm.ep_vote(self.has_unfinished(), stopping)
+
+    def any_unfinished(self) -> bool:
+        """Whether the engine loop must keep stepping: its own work, or (DP attention + EP) any
+        rank's -- a collective vote every rank makes once per loop iteration."""
+        local = self.has_unfinished()
+        if not self.lockstep:
+            return local
+        from ..parallel import comm
+        return comm.ep_any(local)
 
     def _continuation(self, batch, handle):
         """Launch the next decode step of ``batch`` before its current step has been read back
@@ -181,7 +221,7 @@ class LLMEngine:
 
     def generate(self, prompts: List[List[int]], params: SamplingParams) -> List[List[int]]:
         seqs = [self.add_request(p, dataclasses.replace(params)) for p in prompts]
-        while self.has_unfinished():
+        while self.any_unfinished():
             self.step()
         return [s.output_ids for s in seqs]
 

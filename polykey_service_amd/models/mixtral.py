@@ -7,8 +7,11 @@ Expert placement on a TP group of size ``tp``:
 * ``ep == tp`` — expert parallel: rank r holds experts ``[r*E/ep, (r+1)*E/ep)`` unsharded.
   Tokens are already replicated on every rank by the TP attention, so each rank routes all
   tokens, computes only its local experts (a rank whose experts received no token reads no
-  expert weights at all) and the combine is one all-reduce; :mod:`..parallel.ep` has the
-  all-to-all dispatch/combine used when tokens are *not* replicated.
+  expert weights at all) and the combine is one all-reduce;
+* ``tp == 1, ep == world`` — DP attention + EP: each rank serves its own requests with a full
+  copy of the attention weights and routes its tokens to the experts' owners with the
+  all-to-all dispatch / combine of :mod:`..parallel.ep` (ranks step in lockstep; a rank with
+  nothing scheduled runs :meth:`MixtralForCausalLM.idle_forward`).
 
 Mixtral bf16 (~93 GB) also fits a single 288 GB MI355X (``tp = ep = 1``).
 """
@@ -20,7 +23,7 @@ import torch
 from torch import nn
 
 from ..ops import gemm, moe
-from ..parallel import comm
+from ..parallel import comm, ep as ep_comm
 from ..parallel.state import get_state
 from .llama import LlamaForCausalLM, _p
 from .weights import shard_cols, shard_rows
@@ -42,7 +45,11 @@ class MixtralMoE(nn.Module):
         """Combined expert output, or (single rank: nothing to all-reduce) a PendingCombine that
         the next residual add + RMSNorm consumes in one kernel.  ``routing``: (ids, weights)
         from the norm kernel that produced ``x``."""
-        single = get_state().tp_size == 1
+        st = get_state()
+        if st.dp_attention:  # this rank's tokens → their experts' owners and back
+            return ep_comm.ep_moe(x, self.router, self.w13, self.w2, self.k, routing=routing, w13_p=self.w13_p,
+                                  w2_p=self.w2_p, defer_combine=True)
+        single = st.tp_size == 1
         y = moe.fused_moe(x, self.router, self.w13, self.w2, self.k, self.e_lo, self.e_hi, self.w13_p, self.w2_p,
                           defer_combine=single, routing=routing)
         return y if single else comm.tp_all_reduce(y)
@@ -53,6 +60,14 @@ class MixtralMoE(nn.Module):
 
 
 class MixtralForCausalLM(LlamaForCausalLM):
+    def idle_forward(self) -> None:
+        """DP attention + EP: a rank with no tokens this step still serves the other ranks' rows
+        at every MoE layer (the all-to-alls are collective over the EP group)."""
+        x = torch.zeros((0, self.cfg.hidden_size), dtype=self.dtype, device=self.device)
+        for layer in self.layers:
+            m = layer.mlp
+            ep_comm.ep_moe(x, m.router, m.w13, m.w2, m.k, w13_p=m.w13_p, w2_p=m.w2_p)
+
     def _mlp_block(self, layer, x, residual, ws):
         """Decode (TP = 1, split-K o-projection pending): the residual add + RMSNorm kernel also
         routes every token, so the MoE starts from ready expert ids and weights."""

@@ -234,6 +234,51 @@ def tp_all_to_all_counts(counts: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def ep_all_to_all(x: torch.Tensor, out_splits: List[int], in_splits: List[int]) -> torch.Tensor:
+    """Variable-size all-to-all along dim 0 over the expert-parallel group."""
+    st = get_state()
+    if st.ep_size == 1:
+        return x
+    if x.is_cuda and dist.get_backend(st.ep_group) == "gloo":
+        # ranks sharing one GPU (rehearsal / tests): gloo moves host copies
+        return ep_all_to_all(x.cpu(), out_splits, in_splits).to(x.device)
+    out = torch.empty((sum(out_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_to_all_single(out, x.contiguous(), out_splits, in_splits, group=st.ep_group)
+    return out
+
+
+def ep_all_to_all_counts(counts: torch.Tensor) -> torch.Tensor:
+    """Per-destination row counts (int64 [ep]) → counts received from each EP rank."""
+    st = get_state()
+    if st.ep_size == 1:
+        return counts
+    if counts.is_cuda and dist.get_backend(st.ep_group) == "gloo":
+        return ep_all_to_all_counts(counts.cpu()).to(counts.device)
+    out = torch.empty_like(counts)
+    dist.all_to_all_single(out, counts.contiguous(), group=st.ep_group)
+    return out
+
+
+def ep_any(flag: bool) -> bool:
+    """Lockstep vote of the DP-attention ranks (gloo, host): True if any rank's flag is set."""
+    st = get_state()
+    if st.ep_size == 1 or st.ep_cpu_group is None:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=st.ep_cpu_group)
+    return bool(t.item())
+
+
+def ep_vote(busy: bool, stopping: bool):
+    """One host all-reduce over the EP ranks → (any rank busy, every rank stopping)."""
+    st = get_state()
+    if st.ep_size == 1 or st.ep_cpu_group is None:
+        return bool(busy), bool(stopping)
+    t = torch.tensor([1 if busy else 0, 0 if stopping else 1], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=st.ep_cpu_group)
+    return bool(t[0].item()), not bool(t[1].item())
+
+
 def tp_broadcast_object(obj=None):
     """Control plane: TP leader → other ranks of its group (gloo, CPU)."""
     st = get_state()

@@ -1,19 +1,32 @@
-"""Expert parallelism with all-to-all dispatch / combine (tokens sharded across ranks).
+"""Expert parallelism with all-to-all dispatch / combine (DP attention + EP).
 
-Used when each EP rank holds a *different* slice of tokens (data-parallel attention in front
-of the MoE).  Per MoE layer (SURVEY.md §2.3 "Mixtral EP all-to-all"):
+Each EP rank runs attention for its *own* requests (``ParallelState.dp_attention``: tp = 1,
+ep = world) and owns experts ``[r*E/ep, (r+1)*E/ep)``.  Per MoE layer (SURVEY.md §2.3
+"Mixtral EP all-to-all"; BASELINE.json config 5):
 
-1. route local tokens (router GEMM + top-k softmax kernel);
-2. order the T_local*k (token, expert) slots by owning rank; exchange per-rank counts
-   (all-to-all of ``[ep]`` int64), then the token rows and their expert ids;
-3. run the received rows through this rank's experts (align / grouped GEMM kernels with k=1);
-4. all-to-all the results back and combine them with the routing weights.
+1. route the local tokens (router GEMM + the top-k softmax kernel, or the routing the fused
+   residual-add + RMSNorm kernel already produced);
+2. order the ``T_local * k`` (token, slot) pairs by owning rank with the expert-align
+   counting sort keyed by destination rank, gather the rows into that order (the MoE permute
+   kernel) -- the send buffer is contiguous per destination;
+3. exchange per-destination counts (one int64 all-to-all; the only host read-back), then the
+   token rows and their expert ids (two variable-size all-to-alls over RCCL / xGMI);
+4. the received rows run through this rank's experts (align / grouped GEMM with the SiLU
+   epilogue / grouped GEMM, k = 1) and are put back into arrival order;
+5. the results travel back with the inverse all-to-all, landing in the same per-destination
+   order the rows left in, so the combine is the ordinary weighted un-permute of the MoE
+   kernels -- deferred into the next residual add + RMSNorm kernel when the caller allows.
 
-With TP attention the tokens are already replicated on every rank, and
-:class:`~polykey_service_amd.models.mixtral.MixtralMoE` instead computes local experts for all
-tokens and all-reduces (one collective instead of two all-to-alls + an all-gather).
+A rank with no tokens this step still takes part (it sends nothing and serves the others'
+rows): :meth:`~polykey_service_amd.models.mixtral.MixtralForCausalLM.idle_forward`.
+
+With attention TP (``ep == tp``) the tokens are already replicated on every rank and
+:class:`~polykey_service_amd.models.mixtral.MixtralMoE` computes local experts for all of them
+and all-reduces instead (one collective instead of two all-to-alls).
 """
 from __future__ import annotations
+
+from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -23,38 +36,60 @@ from . import comm
 from .state import get_state
 
 
-def moe_all_to_all(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, k: int) -> torch.Tensor:
-    """x: this rank's tokens [T_local, H]; w13/w2: this rank's experts.  Returns [T_local, H]."""
+def _local_experts(recv_x: torch.Tensor, recv_e: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
+                   w13_p: Optional[torch.Tensor], w2_p: Optional[torch.Tensor]) -> torch.Tensor:
+    """Rows received from every rank × their local expert → outputs in arrival order."""
+    n = recv_x.shape[0]
+    if n == 0:
+        return recv_x
+    per = w13.shape[0]
+    offsets, sorted_, inv = moe_ops.align(recv_e, per, 0, per)
+    xs = moe_ops.permute(recv_x, sorted_, offsets, 1)
+    h = moe_ops.grouped_gemm(xs, w13, offsets, n, silu=True, packed=w13_p)
+    y = moe_ops.grouped_gemm(h, w2, offsets, n, silu=False, packed=w2_p)
+    ones = torch.ones((n, 1), dtype=torch.float32, device=recv_x.device)
+    return moe_ops.unpermute(y, inv, ones, n, 1)
+
+
+def ep_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, k: int,
+           routing: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, w13_p: Optional[torch.Tensor] = None,
+           w2_p: Optional[torch.Tensor] = None, defer_combine: bool = False):
+    """x: this rank's tokens [T_local, H] (T_local may be 0); w13 / w2: this rank's experts.
+    Returns [T_local, H], or a :class:`~polykey_service_amd.ops.moe.PendingCombine`."""
     st = get_state()
-    ep, r = st.tp_size, st.tp_rank
+    ep = st.ep_size
     E = router_w.shape[0]
     per = E // ep
-    T = x.shape[0]
-    logits = F.linear(x, router_w)
-    ids, wts = moe_ops.topk_softmax(logits, k)
-    flat = ids.reshape(-1).long()
-    dest = flat // per
-    order = torch.sort(dest, stable=True).indices
-    send_counts = torch.bincount(dest, minlength=ep).to(torch.int64)
-    recv_counts = comm.tp_all_to_all_counts(send_counts.to(x.device)).cpu()
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
-    send_x = x.index_select(0, order // k)
-    send_e = (flat[order] - dest[order] * per).to(torch.int32).view(-1, 1)
-    recv_x = comm.tp_all_to_all(send_x, rc, sc)
-    recv_e = comm.tp_all_to_all(send_e.to(x.device), rc, sc).view(-1, 1)
-    n = recv_x.shape[0]
-    if n > 0:
-        ones = torch.ones((n, 1), dtype=torch.float32, device=x.device)
-        offsets, sorted_, inv = moe_ops.align(recv_e, per, 0, per)
-        xs = moe_ops.permute(recv_x, sorted_, offsets, 1)
-        h = moe_ops.grouped_gemm(xs, w13, offsets, n, silu=True)
-        y = moe_ops.grouped_gemm(h, w2, offsets, n, silu=False)
-        y = moe_ops.unpermute(y, inv, ones, n, 1)
+    T, H = x.shape
+    dev = x.device
+    if T > 0:
+        ids, wts = routing if routing is not None else moe_ops.topk_softmax(F.linear(x, router_w), k)
+        dest = torch.div(ids, per, rounding_mode="floor").to(torch.int32)
+        offsets, sorted_, inv = moe_ops.align(dest, ep, 0, ep)  # every slot is "local" in rank space
+        send_x = moe_ops.permute(x, sorted_, offsets, k)
+        sl = sorted_.long()
+        send_e = (ids.reshape(-1).long()[sl] - dest.reshape(-1).long()[sl] * per).to(torch.int32).view(-1, 1)
+        send_counts = (offsets[1:] - offsets[:-1]).to(torch.int64)
     else:
-        y = recv_x
-    back = comm.tp_all_to_all(y, sc, rc)
-    # combine: slot order[i] received back[i]
-    contrib = torch.zeros((T * k, x.shape[1]), dtype=torch.float32, device=x.device)
-    contrib[order] = back.float()
-    contrib = contrib.view(T, k, -1) * wts.view(T, k, 1).float()
-    return contrib.sum(1).to(x.dtype)
+        ids = torch.zeros((0, k), dtype=torch.int32, device=dev)
+        wts = torch.zeros((0, k), dtype=torch.float32, device=dev)
+        inv = torch.zeros((0,), dtype=torch.int32, device=dev)
+        send_x = x
+        send_e = torch.zeros((0, 1), dtype=torch.int32, device=dev)
+        send_counts = torch.zeros(ep, dtype=torch.int64, device=dev)
+    recv_counts = comm.ep_all_to_all_counts(send_counts.to(dev))
+    counts = torch.stack([send_counts.to(dev), recv_counts]).cpu()  # one read-back for both
+    sc, rc = counts[0].tolist(), counts[1].tolist()
+    recv_x = comm.ep_all_to_all(send_x, rc, sc)
+    recv_e = comm.ep_all_to_all(send_e, rc, sc).view(-1, 1)
+    y = _local_experts(recv_x, recv_e, w13, w2, w13_p, w2_p)
+    back = comm.ep_all_to_all(y, sc, rc)  # [T*k, H] in the send (destination-sorted) order
+    pending = moe_ops.PendingCombine(back, inv, wts, T, k)
+    if defer_combine and T > 0:
+        return pending
+    return pending.combine() if T > 0 else x.new_zeros((0, H))
+
+
+def moe_all_to_all(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, k: int) -> torch.Tensor:
+    """Combined expert output for this rank's tokens (see :func:`ep_moe`)."""
+    return ep_moe(x, router_w, w13, w2, k)

@@ -4,8 +4,14 @@ on ROCm) between GPUs of one node, gloo for CPU tests and for the CPU-side contr
 Layout of a job with ``world`` ranks and tensor-parallel degree ``tp``:
 ``dp = world // tp`` independent replicas (request-level data parallel, SURVEY.md §2.3 "DP"),
 each a TP group of consecutive ranks (``[r*tp, (r+1)*tp)``) so a TP group stays inside one
-xGMI-connected node.  Expert parallelism reuses the TP group (Mixtral EP=8 with attention
-TP=8, SURVEY.md §2.3 "EP").
+xGMI-connected node.  Expert parallelism (SURVEY.md §2.3 "EP") comes in two layouts:
+
+* ``ep == tp``: EP inside the TP group (Mixtral EP=8 with attention TP=8): tokens are
+  replicated by the TP attention, each rank computes its experts for all of them and the
+  combine is the TP all-reduce;
+* ``tp == 1, ep == world`` (*DP attention + EP*): every rank is its own attention / scheduling
+  replica with its own requests, and the MoE layers exchange token rows with an expert
+  all-to-all over the EP group (``parallel/ep.py``).  Ranks step in lockstep (LLMEngine).
 """
 from __future__ import annotations
 
@@ -29,6 +35,8 @@ class ParallelState:
     dp_rank: int = 0
     ep_size: int = 1
     ep_rank: int = 0
+    ep_group: Optional[object] = None      # expert all-to-all (the TP group, or WORLD with DP attention)
+    ep_cpu_group: Optional[object] = None  # gloo: DP-attention lockstep votes
     tp_group: Optional[object] = None      # device collectives (RCCL / gloo on CPU)
     tp_cpu_group: Optional[object] = None  # gloo: control-plane broadcast of step metadata
     custom_ar: Optional[object] = None     # one-shot xGMI all-reduce (parallel/custom_ar.py)
@@ -42,6 +50,11 @@ class ParallelState:
     @property
     def distributed(self) -> bool:
         return self.world_size > 1
+
+    @property
+    def dp_attention(self) -> bool:
+        """Attention replicated per rank (tp = 1) with experts spread over ep > 1 ranks."""
+        return self.ep_size > 1 and self.tp_size == 1
 
 
 _STATE = ParallelState()
@@ -80,11 +93,15 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
         torch.cuda.set_device(dev)
     if world % tp:
         raise ValueError(f"world size {world} not divisible by tp={tp}")
-    if ep not in (1, tp):
-        raise ValueError("expert parallelism must be 1 or equal to tp (EP reuses the TP group)")
+    dp_attn = tp == 1 and ep > 1
+    if dp_attn and ep != world:
+        raise ValueError(f"DP attention + EP needs ep == world size ({world}), got ep={ep}")
+    if not dp_attn and ep not in (1, tp):
+        raise ValueError("expert parallelism must be 1, equal to tp (EP inside the TP group), or the world size "
+                         "with tp=1 (DP attention + expert all-to-all)")
     st = ParallelState(world_size=world, rank=rank, local_rank=local, tp_size=tp, tp_rank=rank % tp,
-                       dp_size=world // tp, dp_rank=rank // tp, ep_size=ep, ep_rank=(rank % tp) if ep > 1 else 0,
-                       device=dev)
+                       dp_size=world // tp, dp_rank=rank // tp, ep_size=ep,
+                       ep_rank=rank if dp_attn else ((rank % tp) if ep > 1 else 0), device=dev)
     if world > 1:
         # POLYKEY_DIST_BACKEND overrides (gloo: several ranks on one GPU, which RCCL refuses)
         be = pick_backend(dev.type, n_dev, int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
@@ -105,6 +122,13 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
             gc = dist.new_group(ranks, backend="gloo") if be != "gloo" else g
             if rank in ranks:
                 st.tp_group, st.tp_cpu_group = g, gc
+        if dp_attn:
+            st.ep_group = dist.group.WORLD
+            # a dedicated gloo group: the engine thread's lockstep votes must never interleave
+            # with another thread's collectives on WORLD
+            st.ep_cpu_group = dist.new_group(list(range(world)), backend="gloo")
+        elif ep > 1:
+            st.ep_group, st.ep_cpu_group = st.tp_group, st.tp_cpu_group
         if be == "nccl" or (os.environ.get("POLYKEY_CUSTOM_AR") == "force" and dev.type == "cuda"):
             from .custom_ar import maybe_create
             st.custom_ar = maybe_create(st)

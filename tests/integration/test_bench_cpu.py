@@ -31,3 +31,17 @@ def test_bench_json_line(tmp_path, gpus):
     assert out["config"]["prefix_caching"] is True and out["config"]["prefix_cache_hit_tokens"] == 0
     # every request completed its 4 tokens: tokens / elapsed over ranks = value
     assert out["value"] == pytest.approx(4 * 4 * gpus / (out["ms_per_step"] / 1000.0), rel=0.02)
+
+
+def test_bench_dp_attention_expert_all_to_all():
+    """Mixtral-shaped MoE with DP attention + EP=2 (expert all-to-all between the two ranks'
+    engines, lockstep steps, coordinated shutdown) through the same torchrun child launch."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    args = ["--model", "tiny-mixtral", "--ep", "2", "--steps", "1", "--warmup", "1", "--concurrency", "3",
+            "--prompt-len", "8", "--max-tokens", "4", "--no-graphs"]
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"] + args, cwd=REPO,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["config"]["parallelism"] == "dp2_ep2_a2a" and out["config"]["global_batch"] == 6
+    assert out["value"] == pytest.approx(3 * 4 * 2 / (out["ms_per_step"] / 1000.0), rel=0.02)

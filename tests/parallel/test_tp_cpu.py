@@ -126,7 +126,7 @@ def _a2a_worker(rank, world, port, out_path):
     from polykey_service_amd.ops import gemm
     from polykey_service_amd.parallel.ep import moe_all_to_all
     from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
-    init_parallel(tp=world, ep=world, device="cpu", backend="gloo")
+    init_parallel(tp=1, ep=world, device="cpu", backend="gloo")
     g = torch.Generator().manual_seed(1)
     E, H, I, k = 4, 256, 256, 2
     router = (torch.randn(E, H, generator=g) * 0.2).to(torch.bfloat16)
@@ -150,3 +150,61 @@ def test_moe_all_to_all_matches_dense(tmp_path):
     y = torch.cat([d0["y"], d1["y"]]).float()
     ref = fused_moe_reference(d0["x"], d0["router"], d0["w13"], d0["w2"], 2)
     torch.testing.assert_close(y, ref, atol=3e-2, rtol=3e-2)
+
+
+# DP attention + EP: each rank serves its own prompts; ranks 2.. of the 8-rank case get none
+# (they only serve the others' expert rows), and rank 0 generates longer, so every other rank
+# keeps joining its MoE all-to-alls after finishing its own requests.
+DPEP_PROMPTS = {0: [[1, 5, 6, 7, 8, 9], [1, 2]], 1: [[1] + list(range(20, 60))], 3: [[1, 3, 3, 7]]}
+
+
+def _dpep_max_tokens(rank):
+    return 6 if rank == 0 else 3
+
+
+def _dpep_worker(rank, world, port, model, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(max(1, 8 // world))
+    from polykey_service_amd.engine import SamplingParams
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    st = init_parallel(tp=1, ep=world, device="cpu", backend="gloo")
+    assert st.dp_attention and st.ep_rank == rank
+    eng = _engine(model, st)
+    eng.runner.keep_logits = True
+    prompts = DPEP_PROMPTS.get(rank, [])
+    seqs = [eng.add_request(p, SamplingParams(max_tokens=_dpep_max_tokens(rank))) for p in prompts]
+    eng.step()
+    logits = eng.runner.last_logits.float().clone() if prompts else None
+    while eng.any_unfinished():
+        eng.step()
+    torch.save({"logits": logits, "tokens": [s.output_ids for s in seqs],
+                "idle": eng.runner.stats.get("idle_steps", 0)}, f"{out_path}.{rank}")
+    destroy_parallel()
+
+
+@pytest.mark.parametrize("model,world", [("tiny-mixtral", 2), ("tiny-mixtral-e8", 8)])
+def test_dp_attention_expert_all_to_all_matches_tp1(tmp_path, model, world):
+    """Mixtral with DP attention + EP (one expert per rank at 8): every rank's first-step logits
+    and first tokens equal a single-rank engine's on the same prompts."""
+    from polykey_service_amd.engine import SamplingParams
+    from polykey_service_amd.parallel.state import ParallelState
+    out = str(tmp_path / "dpep")
+    mp.start_processes(_dpep_worker, args=(world, _free_port(), model, out), nprocs=world, join=True,
+                       start_method="spawn")
+    ref_eng = _engine(model, ParallelState())
+    for r in range(world):
+        d = torch.load(f"{out}.{r}", weights_only=True)
+        prompts = DPEP_PROMPTS.get(r, [])
+        if not prompts:
+            assert d["tokens"] == [] and d["idle"] > 0  # served the other ranks' rows only
+            continue
+        ref_eng.runner.keep_logits = True
+        seqs = [ref_eng.add_request(p, SamplingParams(max_tokens=_dpep_max_tokens(r))) for p in prompts]
+        ref_eng.step()
+        ref_logits = ref_eng.runner.last_logits.float().clone()
+        while ref_eng.has_unfinished():
+            ref_eng.step()
+        torch.testing.assert_close(d["logits"], ref_logits, atol=1e-1, rtol=5e-2)
+        assert [t[0] for t in d["tokens"]] == [s.output_ids[0] for s in seqs]
+        assert [len(t) for t in d["tokens"]] == [_dpep_max_tokens(r)] * len(prompts)
