@@ -17,7 +17,5 @@ USER appuser
 ENV LISTEN_ADDR=:50051 POLYKEY_BACKEND=mock HSA_ENABLE_IPC_MODE_LEGACY=0
 EXPOSE 50051 8000 9100
 HEALTHCHECK --interval=10s --timeout=5s --start-period=20s --retries=3 \
-  CMD python3 -c "import grpc,sys; from polykey_service_amd import proto; ch=grpc.insecure_channel('127.0.0.1:50051'); \
-r=ch.unary_unary(proto.HEALTH_CHECK, request_serializer=proto.HealthCheckRequest.SerializeToString, \
-response_deserializer=proto.HealthCheckResponse.FromString)(proto.HealthCheckRequest(), timeout=4); sys.exit(r.status!=1)"
+  CMD ["python3", "-m", "polykey_service_amd.client.health_probe", "-addr=:50051"]
 ENTRYPOINT ["python3", "-m", "polykey_service_amd.server"]

@@ -6,7 +6,7 @@ PY        ?= python3
 SERVER_ADDR ?= localhost:50051
 PORT      ?= 50051
 
-.PHONY: help build clean run-server run-llm-server run-test-client test test-gpu test-dist test-integration \
+.PHONY: help build clean run-server run-llm-server run-test-client test test-gpu test-dist test-integration test-integration-local health \
         bench bench-gpu8 prof compose-up compose-down compose-logs lint ci-check kill-local-server
 
 help: ## show targets
@@ -39,11 +39,22 @@ test: build ## CPU test suite (unit + integration + gloo multi-process) with a J
 test-gpu: build ## kernel numerics + GPU engine tests (needs an MI355X)
 	$(PY) -m pytest tests -q -m gpu
 
-test-dist: ## multi-process TP/EP tests on gloo (CPU)
-	$(PY) -m pytest tests/dist -q
+test-dist: ## multi-process TP/EP/SP/DP-EP tests on gloo (CPU, 2/4/8 ranks)
+	$(PY) -m pytest tests/parallel -q
 
-test-integration: build ## in-process server + dev client, health, reflection, LLM tools
+test-integration-local: build ## in-process server + dev client, health, reflection, LLM tools
 	$(PY) -m pytest tests/integration -q
+
+test-integration: compose-up ## container flow: compose up -> wait healthy -> remote tests + dev client -> down
+	@echo "waiting for polykey-server to become healthy"
+	@until [ "$$(docker inspect -f {{.State.Health.Status}} $$(docker compose -f compose.yml ps -q polykey-server))" = "healthy" ]; do \
+		sleep 1; \
+	done
+	POLYKEY_SERVER_ADDR=$(SERVER_ADDR) $(PY) -m pytest tests/integration/test_remote_server.py -q; \
+	  rc=$$?; $(MAKE) run-test-client || rc=1; $(MAKE) compose-down; exit $$rc
+
+health: ## gRPC health probe of $(SERVER_ADDR) (grpc_health_probe contract)
+	$(PY) -m polykey_service_amd.client.health_probe -addr=$(SERVER_ADDR)
 
 bench: build ## headline benchmark on 1 GPU (output tokens/s via gRPC, Llama-3-8B)
 	$(PY) bench.py --gpus 1

@@ -5,7 +5,10 @@ Registers model tools on the :class:`ToolRouter`:
 
 * ``llm.generate:<model>`` — ``parameters = {prompt | prompt_token_ids, max_tokens, temperature,
   top_p, top_k, min_p, seed, ignore_eos, stop, stop_token_ids, return: "text"|"struct"}``
-* ``llm.chat:<model>``     — same with ``messages = [{role, content}, ...]``
+* ``llm.chat:<model>``     — same with ``messages = [{role, content}, ...]``, and optionally
+  OpenAI ``tools`` / ``tool_choice`` plus ``execute_tools`` / ``tool_secret_id`` /
+  ``max_tool_rounds`` (service/tool_calls.py): the struct output then also carries
+  ``tool_calls`` and ``tool_results``
 
 Unary ``ExecuteTool`` returns the completion as ``string_output`` (what the reference's dev
 client logs), or a ``struct_output`` ``{text, finish_reason, usage, metrics}`` when
@@ -21,6 +24,7 @@ from .. import proto
 from ..engine.sequence import SamplingParams
 from ..engine.tokenizer import IncrementalDetokenizer
 from ..service.base import RequestContext, ToolError, ok_status
+from ..service.tool_calls import run_chat, validate_tools
 
 
 def _status():
@@ -36,6 +40,7 @@ class LLMTool:
         self.llm = llm
         self.chat = chat
         self.tok = llm.tokenizer
+        self.router = None  # set by attach_local_llm: executes model-emitted tool calls
 
     # ------------------------------------------------------------- params
     def _prompt(self, params: dict) -> List[int]:
@@ -79,8 +84,43 @@ class LLMTool:
                 return i
         return None
 
+    def _tools(self, params: dict):
+        """(tools, tool_choice) when this chat request uses function tools, else None."""
+        if not self.chat or not (params.get("tools") or params.get("tool_choice")):
+            return None
+        try:
+            tools, choice = validate_tools(params.get("tools"), params.get("tool_choice"))
+        except ValueError as e:
+            raise ToolError("INVALID_ARGUMENT", str(e))
+        return (tools, choice) if tools and choice != "none" else None
+
+    async def _run_tools(self, ctx: RequestContext, params: dict, tc) -> "proto.ExecuteToolResponse":
+        t0 = time.monotonic()
+        msgs = params.get("messages")
+        if not isinstance(msgs, list) or not msgs:
+            raise ToolError("INVALID_ARGUMENT", "llm.chat requires a non-empty 'messages' list")
+        sp = self._sampling(params)
+        oc = await run_chat(self.llm, self.tok.chat_template, msgs, sp, tc[0], tc[1], router=self.router,
+                            execute=bool(params.get("execute_tools")), secret_id=params.get("tool_secret_id"),
+                            max_rounds=int(params.get("max_tool_rounds", 3)), request_id=ctx.request_id)
+        resp = proto.ExecuteToolResponse(status=_status())
+        if params.get("return") == "struct" or oc.tool_calls or oc.executed:
+            m = oc.metrics or {}
+            resp.struct_output.update({
+                "model": self.model_name, "text": oc.content, "tool_calls": oc.tool_calls,
+                "tool_results": oc.executed, "finish_reason": oc.finish_reason,
+                "usage": {"prompt_tokens": oc.prompt_tokens, "completion_tokens": oc.completion_tokens,
+                          "total_tokens": oc.prompt_tokens + oc.completion_tokens},
+                "metrics": {k: v for k, v in {**m, "server_e2e_s": time.monotonic() - t0}.items() if v is not None}})
+        else:
+            resp.string_output = oc.content
+        return resp
+
     # ------------------------------------------------------------- tool API
     async def run(self, ctx: RequestContext, params: dict, secret, metadata: Dict[str, str]):
+        tc = self._tools(params)
+        if tc is not None:
+            return await self._run_tools(ctx, params, tc)
         t0 = time.monotonic()
         prompt = self._prompt(params)
         sp = self._sampling(params)
@@ -106,6 +146,10 @@ class LLMTool:
         return resp
 
     async def stream(self, ctx: RequestContext, params: dict, secret, metadata: Dict[str, str]):
+        tc = self._tools(params)
+        if tc is not None:  # a tool-enabled chat is decided whole: one final message
+            yield await self._run_tools(ctx, params, tc)
+            return
         t0 = time.monotonic()
         prompt = self._prompt(params)
         sp = self._sampling(params)
@@ -208,7 +252,9 @@ def attach_local_llm(router, cfg, logger, engine=None):
         llm = AsyncLLM(engine)
     name = cfg.model if isinstance(cfg.model, str) else "model"
     router.register_model_tool("llm.generate", name, LLMTool("llm.generate", name, llm, chat=False))
-    router.register_model_tool("llm.chat", name, LLMTool("llm.chat", name, llm, chat=True))
+    chat_tool = LLMTool("llm.chat", name, llm, chat=True)
+    chat_tool.router = router
+    router.register_model_tool("llm.chat", name, chat_tool)
     router.llm = llm
     logger.info("local LLM backend ready", model=name, kv_blocks=engine.runner.num_blocks,
                 block_size=engine.cfg.block_size, tp=engine.st.tp_size,

@@ -3,6 +3,11 @@ route").  No reference counterpart (no HTTP/OpenAI route in polyk
 
 Endpoints: ``POST /v1/chat/completions`` and ``POST /v1/completions`` (``stream: true`` →
 server-sent events ending with ``data: [DONE]``), ``GET /v1/models``, ``GET /health``.
+Chat requests accept OpenAI ``tools`` / ``tool_choice`` (calls returned as ``tool_calls`` with
+``finish_reason: "tool_calls"``) plus the polykey extensions ``execute_tools`` (route the calls
+to the gateway's own tools and continue the chat), ``tool_secret_id`` and ``max_tool_rounds``
+(service/tool_calls.py).  A tool-enabled chat is decided whole before it is streamed, so its
+SSE stream carries the content or the calls in one delta.
 Requests are served by the same :class:`ToolRouter` model tools as gRPC, so both fronts share
 one continuous-batching engine; ``model`` selects the backend like ``llm.chat:<model>``.
 """
@@ -16,6 +21,7 @@ from typing import Any, Dict, List, Optional
 
 from ..engine.sequence import SamplingParams
 from ..service.base import ToolError
+from ..service.tool_calls import run_chat, validate_tools
 
 _SAMPLING_KEYS = ("max_tokens", "temperature", "top_p", "top_k", "min_p", "seed", "stop", "ignore_eos",
                   "stop_token_ids", "cache_salt")
@@ -84,6 +90,12 @@ def create_app(router):
             msgs = body.get("messages")
             if not isinstance(msgs, list) or not msgs:
                 return err(400, "'messages' must be a non-empty list")
+            try:
+                tools, choice = validate_tools(body.get("tools"), body.get("tool_choice"))
+            except ValueError as e:
+                return err(400, str(e))
+            if tools and choice != "none":
+                return await _run_tools(body, llm, model, msgs, sp, tools, choice)
             prompt_ids = tok.encode(tok.apply_chat_template(msgs))
         else:
             p = body.get("prompt")
@@ -144,6 +156,40 @@ def create_app(router):
                   else {"index": 0, "text": text, "finish_reason": last.finish_reason if last else None})
         return {"id": rid, "object": obj, "created": created, "model": model, "choices": [choice],
                 "usage": _usage(len(prompt_ids), len(toks), last.metrics if last else None)}
+
+    async def _run_tools(body, llm, model, msgs, sp, tools, choice):
+        rid = "chatcmpl-" + uuid.uuid4().hex[:24]
+        created = int(time.time())
+        try:
+            oc = await run_chat(llm, llm.tokenizer.chat_template, msgs, sp, tools, choice, router=router,
+                                execute=bool(body.get("execute_tools")), secret_id=body.get("tool_secret_id"),
+                                max_rounds=int(body.get("max_tool_rounds", 3)), request_id=rid)
+        except (ValueError, TypeError) as e:
+            return err(400, str(e))
+        usage = _usage(oc.prompt_tokens, oc.completion_tokens, oc.metrics)
+        extra = {"polykey_tool_results": oc.executed} if oc.executed else {}
+        if not body.get("stream"):
+            msg = {"role": "assistant", "content": oc.content if oc.content or not oc.tool_calls else None}
+            if oc.tool_calls:
+                msg["tool_calls"] = oc.tool_calls
+            return {"id": rid, "object": "chat.completion", "created": created, "model": model,
+                    "choices": [{"index": 0, "message": msg, "finish_reason": oc.finish_reason}], "usage": usage,
+                    **extra}
+
+        async def sse():
+            def chunk(delta, finish=None, **kw):
+                return "data: " + json.dumps({"id": rid, "object": "chat.completion.chunk", "created": created,
+                                              "model": model, "choices": [{"index": 0, "delta": delta,
+                                                                           "finish_reason": finish}], **kw}) + "\n\n"
+            yield chunk({"role": "assistant"})
+            if oc.tool_calls:
+                yield chunk({"tool_calls": [{"index": i, **c} for i, c in enumerate(oc.tool_calls)]})
+            elif oc.content:
+                yield chunk({"content": oc.content})
+            yield chunk({}, oc.finish_reason, usage=usage, **extra)
+            yield "data: [DONE]\n\n"
+
+        return StreamingResponse(sse(), media_type="text/event-stream")
 
     @app.post("/v1/chat/completions")
     async def chat_completions(request: Request):

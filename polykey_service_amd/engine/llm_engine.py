@@ -85,7 +85,9 @@ class LLMEngine:
         self.model = model
         if hasattr(model, "pack_decode_weights"):
             model.pack_decode_weights()
-        self.tokenizer = get_tokenizer(cfg.tokenizer, mcfg.vocab_size, mcfg.bos_token_id, mcfg.eos_token_id)
+        from .chat_template import family_for
+        self.tokenizer = get_tokenizer(cfg.tokenizer, mcfg.vocab_size, mcfg.bos_token_id, mcfg.eos_token_id,
+                                       family_for(mcfg.name, mcfg.is_moe))
         rcfg = RunnerConfig(block_size=cfg.block_size, max_num_seqs=cfg.max_num_seqs,
                             max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=cfg.max_model_len,
                             num_kv_blocks=cfg.num_kv_blocks, gpu_mem_fraction=cfg.gpu_mem_fraction,

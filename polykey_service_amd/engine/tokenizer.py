@@ -3,16 +3,21 @@
 No network: a real Llama-3 / Mixtral ``tokenizer.json`` is used when a local path is given
 (HF ``tokenizers`` is installed); otherwise :class:`ByteTokenizer` maps UTF-8 bytes to ids
 ``[offset, offset+256)`` so prompts round-trip and random-weight outputs decode to text.
+Chats are rendered by the model family's :class:`~.chat_template.ChatTemplate` (Llama-3 or
+Mistral markup, or the tokenizer directory's own Jinja template).
 """
 from __future__ import annotations
 
-import json
 import os
 from typing import Dict, List, Optional
 
+from .chat_template import LLAMA3, ChatTemplate, load_chat_template
+
 
 class ByteTokenizer:
-    def __init__(self, vocab_size: int, bos_token_id: int = 1, eos_token_id: int = 2, offset: int = 3):
+    def __init__(self, vocab_size: int, bos_token_id: int = 1, eos_token_id: int = 2, offset: int = 3,
+                 chat_template: Optional[ChatTemplate] = None):
+        self.chat_template = chat_template or ChatTemplate(LLAMA3)
         self.vocab_size = vocab_size
         self.bos_token_id = bos_token_id
         self.eos_token_id = eos_token_id
@@ -22,7 +27,7 @@ class ByteTokenizer:
         ids = [b + self.offset for b in text.encode("utf-8")]
         return ([self.bos_token_id] if add_bos else []) + ids
 
-    def decode(self, ids: List[int]) -> str:
+    def decode(self, ids: List[int], keep_special: bool = False) -> str:
         out = bytearray()
         for i in ids:
             b = i - self.offset
@@ -33,13 +38,14 @@ class ByteTokenizer:
                 out.extend(b"\xc2\xb7")  # '·'
         return out.decode("utf-8", errors="replace")
 
-    def apply_chat_template(self, messages: List[Dict[str, str]]) -> str:
-        return format_chat(messages)
+    def apply_chat_template(self, messages: List[Dict[str, str]], tools=None) -> str:
+        return self.chat_template.render(messages, tools)
 
 
 class HFTokenizer:
-    def __init__(self, path: str, bos_token_id: int, eos_token_id: int):
+    def __init__(self, path: str, bos_token_id: int, eos_token_id: int, chat_template: Optional[ChatTemplate] = None):
         from tokenizers import Tokenizer
+        self.chat_template = chat_template or ChatTemplate(LLAMA3)
         self.tok = Tokenizer.from_file(path)
         self.bos_token_id = bos_token_id
         self.eos_token_id = eos_token_id
@@ -49,11 +55,13 @@ class HFTokenizer:
         ids = self.tok.encode(text, add_special_tokens=False).ids
         return ([self.bos_token_id] if add_bos else []) + ids
 
-    def decode(self, ids: List[int]) -> str:
-        return self.tok.decode(ids, skip_special_tokens=True)
+    def decode(self, ids: List[int], keep_special: bool = False) -> str:
+        """``keep_special``: keep special tokens (tool-call markers such as <|python_tag|> or
+        [TOOL_CALLS] are parsed from the text; the chat parsers strip end-of-turn ones)."""
+        return self.tok.decode(ids, skip_special_tokens=not keep_special)
 
-    def apply_chat_template(self, messages: List[Dict[str, str]]) -> str:
-        return format_chat(messages)
+    def apply_chat_template(self, messages: List[Dict[str, str]], tools=None) -> str:
+        return self.chat_template.render(messages, tools)
 
 
 class IncrementalDetokenizer:
@@ -87,17 +95,18 @@ class IncrementalDetokenizer:
 
 
 def format_chat(messages: List[Dict[str, str]]) -> str:
-    """Llama-3 style chat markup (header/eot markers as plain text for the byte tokenizer)."""
-    parts = []
-    for m in messages:
-        parts.append(f"<|start_header_id|>{m.get('role', 'user')}<|end_header_id|>\n\n{m.get('content', '')}<|eot_id|>")
-    parts.append("<|start_header_id|>assistant<|end_header_id|>\n\n")
-    return "".join(parts)
+    """Llama-3 chat markup (header/eot markers as plain text for the byte tokenizer)."""
+    return ChatTemplate(LLAMA3).render(messages)
 
 
-def get_tokenizer(path: str, vocab_size: int, bos_token_id: int, eos_token_id: int):
+def get_tokenizer(path: str, vocab_size: int, bos_token_id: int, eos_token_id: int, family: str = LLAMA3):
+    """``path``: a tokenizer.json or a directory holding one (and optionally its
+    tokenizer_config.json chat template); empty: the byte tokenizer.  ``family`` picks the
+    built-in chat template (chat_template.family_for)."""
     if path:
+        d = path if os.path.isdir(path) else os.path.dirname(path)
         if os.path.isdir(path):
             path = os.path.join(path, "tokenizer.json")
-        return HFTokenizer(path, bos_token_id, eos_token_id)
-    return ByteTokenizer(vocab_size, bos_token_id, eos_token_id, offset=3 if bos_token_id < 3 else 0)
+        return HFTokenizer(path, bos_token_id, eos_token_id, load_chat_template(d, family))
+    return ByteTokenizer(vocab_size, bos_token_id, eos_token_id, offset=3 if bos_token_id < 3 else 0,
+                         chat_template=ChatTemplate(family))
