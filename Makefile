@@ -98,3 +98,8 @@ install-deps: ## verify the offline Python dependencies this repo needs are impo
 	$(PY) -c "import grpc, google.protobuf, fastapi, uvicorn, prometheus_client, safetensors, tokenizers, pybind11; print('ok')"
 
 ci-check: build test ## what CI runs on a CPU runner
+
+lint: ## ruff (as in CI) when installed, else a byte-compile pass over every Python file
+	@if command -v ruff >/dev/null 2>&1; then \
+	  ruff check --select E9,F,I --line-length 120 polykey_service_amd tests bench.py __graft_entry__.py tools; \
+	else $(PY) -m compileall -q polykey_service_amd tests tools bench.py __graft_entry__.py && echo "compile ok"; fi
