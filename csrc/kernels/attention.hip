@@ -37,6 +37,17 @@ constexpr int kDecodeWaves = 4;  // waves per (seq, kv head, partition); 8 measu
 int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
+#ifndef PK_DECODE_KV_NT
+#define PK_DECODE_KV_NT 0  // in-situ decode step 4.43 (plain) vs 4.45 ms (NT): tools/ab_decode.py
+#endif
+// K/V stream loads (read once per step: non-temporal when PK_DECODE_KV_NT)
+__device__ __forceinline__ bf16x8_t ldkv(const bf16_t* p) {
+#if PK_DECODE_KV_NT
+  return __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(p));
+#else
+  return ld8(p);
+#endif
+}
 
 __device__ __forceinline__ bf16x8_t zero8() {
   u32x4 z = {0u, 0u, 0u, 0u};
@@ -67,28 +78,27 @@ struct KVFrag {
 
 // bt[i - bt_base] = physical block of logical block i; `lim` bounds the tokens a load may touch
 // (past it the address is clamped, the data never used), so the block lookups stay inside the
-// caller's block-table window.
+// caller's block-table window.  K comes from the fragment-native cache tile of step s (common.h
+// kcache_off: one contiguous KiB per load instruction); V^T rows are 64 B of 32 keys, lane group
+// g reading keys 8g..8g+7 (ldkv: plain loads; PK_DECODE_KV_NT=1 makes them non-temporal).
 __device__ __forceinline__ void load_kv(KVFrag& f, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                                         int64_t blk_stride, const int* __restrict__ bt, int bt_base, int bs, int s,
                                         int lim) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
+  const int ks = min(s, lim - 1) & ~31;  // the step's 32-key tile (clamped past the end)
+  const bf16_t* kt = kc + bt[ks / bs - bt_base] * blk_stride + (ks % bs) * kHD + 8 * lane;
+  PK_DEVICE_ASSERT(bt[ks / bs - bt_base] >= 0);
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    int tok = s + 8 * (r >> 2) + 4 * t + (r & 3);
-    tok = min(tok, lim - 1);
-    const int blk = bt[tok / bs - bt_base];
-    PK_DEVICE_ASSERT(blk >= 0);
-    const bf16_t* p = kc + blk * blk_stride + (tok % bs) * kHD + 32 * g;
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) f.k[t][kk] = ld8(p + 8 * kk);
-  }
+    for (int kk = 0; kk < 4; ++kk) f.k[t][kk] = ldkv(kt + (t * 4 + kk) * 512);
   int tok0 = s + 8 * g;
   tok0 = min(tok0, ((lim - 1) >> 3) << 3);
   const int blk = bt[tok0 / bs - bt_base];
   const bf16_t* p = vc + blk * blk_stride + r * bs + (tok0 % bs);
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt) f.v[dt] = ld8(p + dt * 16 * bs);
+  for (int dt = 0; dt < 8; ++dt) f.v[dt] = ldkv(p + dt * 16 * bs);
 }
 
 __device__ __forceinline__ void attend_step(WaveState& st, const bf16x8_t (&qf)[4], const KVFrag& f, int s,
@@ -285,9 +295,9 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
           q_s[it >> 6][j] = ra;
           q_s[it >> 6][j + 64] = rb;
         } else {
-          bf16_t* d = kc + ((static_cast<int64_t>(slot / bs) * n_kv + h) * bs + slot % bs) * kHD;
-          d[j] = ra;
-          d[j + 64] = rb;
+          bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * n_kv + h) * bs * kHD;
+          d[kcache_off(slot % bs, j)] = ra;
+          d[kcache_off(slot % bs, j + 64)] = rb;
         }
       } else {
         bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs + slot % bs;
@@ -481,8 +491,6 @@ __global__ void __launch_bounds__(512) paged_prefill_kernel(
 constexpr int kKRow = kHD + 8;     // K_s row, bf16 elements (272 B)
 constexpr int kVRow = kStep + 8;   // V_s row, bf16 elements (80 B)
 
-__device__ __forceinline__ int k_lds_row(int k) { return ((k >> 2) & 1) * 16 + (k >> 3) * 4 + (k & 3); }
-
 template <int NW, int QT>
 __global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
@@ -522,9 +530,10 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
       const int p = threadIdx.x + i * 64 * NW;
       const bool isk = p < 512;
       const int pv = p & 511;
-      const int tok = isk ? min(s0 + (pv >> 4), k_end - 1) : min(s0 + 8 * (pv & 3), ((k_end - 1) >> 3) << 3);
+      // K: the step's fragment-native tile is one contiguous 8 KiB (piece pv at pv * 8)
+      const int tok = isk ? s0 : min(s0 + 8 * (pv & 3), ((k_end - 1) >> 3) << 3);
       const int64_t base = static_cast<int64_t>(bt[tok / bs]) * blk_stride;
-      const bf16_t* src = isk ? kch + base + (tok % bs) * kHD + (pv & 15) * 8 : vch + base + (pv >> 2) * bs + tok % bs;
+      const bf16_t* src = isk ? kch + base + (tok % bs) * kHD + pv * 8 : vch + base + (pv >> 2) * bs + tok % bs;
       stage[i] = *reinterpret_cast<const u32x4*>(src);
     }
   };
@@ -533,7 +542,9 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
     for (int i = 0; i < NP; ++i) {
       const int p = threadIdx.x + i * 64 * NW;
       const int pv = p & 511;
-      bf16_t* dst = p < 512 ? &K_s[buf][k_lds_row(pv >> 4)][(pv & 15) * 8] : &V_s[buf][pv >> 2][(pv & 3) * 8];
+      // K piece pv = ((t * 4 + kk) * 64 + lane): key row t * 16 + (lane & 15), dims 32 (lane >> 4) + 8 kk
+      bf16_t* dst = p < 512 ? &K_s[buf][(pv >> 8) * 16 + (pv & 15)][32 * ((pv >> 4) & 3) + 8 * ((pv >> 6) & 3)]
+                            : &V_s[buf][pv >> 2][(pv & 3) * 8];
       *reinterpret_cast<u32x4*>(dst) = stage[i];
     }
   };
@@ -591,7 +602,7 @@ static int decode_launch(void* out, const void* q, const QkvIn& qi, const void* 
                          void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
                          int out_stride, float scale, int max_ctx, hipStream_t stream) {
   if (n_seqs <= 0) return 0;
-  if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
+  if (n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0) return -1;  // K tiles: 32 keys
   // max_ctx bounds the contexts of this launch (<= 0: the block-table capacity).  A launch
   // known to stay within one partition needs no partition grid and no merge kernel.
   if (max_ctx <= 0 || max_ctx > max_blocks * bs) max_ctx = max_blocks * bs;
@@ -664,7 +675,7 @@ PK_EXPORT int pk_paged_prefill(void* out, const void* q, const void* k_cache, co
                                int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride,
                                int max_q_len, float scale, hipStream_t stream) {
   if (n_seqs <= 0 || max_q_len <= 0) return 0;
-  if (n_q % n_kv || n_q / n_kv > 16 || bs % 8 || bs <= 0) return -1;
+  if (n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0) return -1;  // K tiles: 32 keys
   const int G = n_q / n_kv;
   if (g_prefill_lds && (G == 1 || G == 2 || G == 4 || G == 8)) {
     // 16-query column tiles per workgroup: 4 (64 queries: more waves share each K/V tile) for

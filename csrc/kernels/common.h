@@ -47,6 +47,24 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return r;
 }
 
+// ---- paged K-cache layout --------------------------------------------------------------
+// A K-cache block of one KV head ([bs][128] bf16, bs a multiple of 32) is stored as bs/32
+// fragment-native 8 KiB tiles: inside a 32-token tile, element (token k, dim d) sits at
+//     ((t * 4 + kk) * 64 + lane) * 8 + j,   t = (k >> 2) & 1, kk = (d >> 3) & 3, j = d & 7,
+//     lane = 16 * (d >> 5) + 4 * (k >> 3) + (k & 3)
+// -- the order in which the attention kernels' S^T = K.Q^T MFMA A-fragments (key tile t,
+// k-step kk) are held by the 64 lanes (attention.hip load_kv).  Every fragment load of a wave is
+// then one contiguous 1 KiB (eight full 128-B lines) instead of 16 rows x 64 B, so the decode
+// stream reads whole lines (tools/attn_layout_lab.py at 384 keys: 20.9 -> 20.1 us, 17.9 us with
+// non-temporal loads -- which lose in the captured decode step, so they are off).
+// Writers scatter one token's 128 dims with 8-dim (16-byte) granules; RoPE halves d and d+64
+// stay 16-byte aligned.
+__host__ __device__ __forceinline__ int kcache_off(int k_in_block, int d) {
+  const int k = k_in_block & 31;
+  const int lane = 16 * (d >> 5) + 4 * (k >> 3) + (k & 3);
+  return (k_in_block >> 5) * 4096 + ((((k >> 2) & 1) * 4 + ((d >> 3) & 3)) * 64 + lane) * 8 + (d & 7);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -213,7 +213,11 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
           } else {
             const int slot = args.slots[m];
             if (slot < 0) continue;
-            d = args.k_cache + ((static_cast<int64_t>(slot / bs) * nkv + (nb - nq)) * bs + slot % bs) * 128 + j;
+            // fragment-native K tile (common.h kcache_off; 4-dim groups stay contiguous)
+            bf16_t* kb = args.k_cache + (static_cast<int64_t>(slot / bs) * nkv + (nb - nq)) * bs * 128;
+            *reinterpret_cast<uint2*>(kb + kcache_off(slot % bs, j)) = va;
+            *reinterpret_cast<uint2*>(kb + kcache_off(slot % bs, j + 64)) = vb;
+            continue;
           }
           *reinterpret_cast<uint2*>(d) = va;
           *reinterpret_cast<uint2*>(d + 64) = vb;
@@ -815,10 +819,15 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
     b = rbf(b);
     const float* cs = cos_sin + static_cast<int64_t>(positions[m]) * 128;
     const float co = cs[lane], si = cs[64 + lane];
-    bf16_t* d = h < nq ? q_out + static_cast<int64_t>(m) * nq * 128 + h * 128
-                       : kc + ((static_cast<int64_t>(slot / bs) * nkv + (h - nq)) * bs + slot % bs) * 128;
-    d[lane] = f2bf(a * co - b * si);
-    d[lane + 64] = f2bf(b * co + a * si);
+    if (h < nq) {
+      bf16_t* d = q_out + static_cast<int64_t>(m) * nq * 128 + h * 128;
+      d[lane] = f2bf(a * co - b * si);
+      d[lane + 64] = f2bf(b * co + a * si);
+    } else {  // fragment-native K tile (common.h kcache_off)
+      bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * nkv + (h - nq)) * bs * 128;
+      d[kcache_off(slot % bs, lane)] = f2bf(a * co - b * si);
+      d[kcache_off(slot % bs, lane + 64)] = f2bf(b * co + a * si);
+    }
   } else {
     bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * nkv + (h - nq - nkv)) * 128 * bs + slot % bs;
     d[static_cast<int64_t>(lane) * bs] = f2bf(a);
@@ -898,7 +907,7 @@ int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
       if (norm || a.counters == nullptr || a.residual == nullptr || a.sumsq_parts == nullptr) return -1;
       return launch_pk<kAddResNorm, false>(a, packed, nt, stream);
     case kQkvRope:
-      if (a.counters == nullptr || a.N != (a.nq + 2 * a.nkv) * 128 || a.bs <= 0) return -1;
+      if (a.counters == nullptr || a.N != (a.nq + 2 * a.nkv) * 128 || a.bs <= 0 || a.bs % 32) return -1;
       return norm ? launch_pk<kQkvRope, true>(a, packed, nt, stream) : launch_pk<kQkvRope, false>(a, packed, nt, stream);
     default: return -1;
   }
@@ -1020,7 +1029,7 @@ PK_EXPORT int pk_qkv_reduce_rope_cache(void* q_out, const void* partial, int S, 
                                        const void* positions, const void* cos_sin, void* k_cache, void* v_cache,
                                        const void* slots, int bs, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (bs <= 0 || S < 1) return -1;
+  if (bs <= 0 || bs % 32 || S < 1) return -1;
   const int grid = (M * (nq + 2 * nkv) + 3) / 4;
   auto go = [&](auto ss) {
     qkv_reduce_rope_cache_kernel<decltype(ss)::value><<<grid, 256, 0, stream>>>(

@@ -47,9 +47,9 @@ __global__ void __launch_bounds__(256) rope_and_cache_kernel(bf16_t* __restrict_
     *reinterpret_cast<u32x4*>(x + c + kHalf) = vb;
     if (head >= nq && slot >= 0) {
       const int kh = head - nq;
-      bf16_t* dst = kc + ((static_cast<int64_t>(slot / bs) * nkv + kh) * bs + slot % bs) * kHD;
-      *reinterpret_cast<u32x4*>(dst + c) = va;
-      *reinterpret_cast<u32x4*>(dst + c + kHalf) = vb;
+      bf16_t* dst = kc + (static_cast<int64_t>(slot / bs) * nkv + kh) * bs * kHD;  // fragment-native tile
+      *reinterpret_cast<u32x4*>(dst + kcache_off(slot % bs, c)) = va;
+      *reinterpret_cast<u32x4*>(dst + kcache_off(slot % bs, c + kHalf)) = vb;
     }
   }
   if (slot < 0) return;
@@ -68,7 +68,7 @@ PK_EXPORT int pk_rope_and_cache(void* qkv, const void* positions, const void* co
                                 const void* slot_mapping, int T, int nq, int nkv, int hd, int bs, int q_stride,
                                 int unused, hipStream_t stream) {
   if (T <= 0) return 0;
-  if (hd != kHD || (bs % 8) != 0) return -1;
+  if (hd != kHD || (bs % 32) != 0) return -1;  // fragment-native K tiles of 32 tokens
   rope_and_cache_kernel<<<T, 256, 0, stream>>>(static_cast<bf16_t*>(qkv), static_cast<const int*>(positions),
                                                static_cast<const float*>(cos_sin), static_cast<bf16_t*>(k_cache),
                                                static_cast<bf16_t*>(v_cache), static_cast<const int*>(slot_mapping), nq,

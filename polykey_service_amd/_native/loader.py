@@ -57,7 +57,9 @@ def load_cdll(name: str) -> ctypes.CDLL:
         if name in _cache:
             return _cache[name]
         import torch  # noqa: F401
-        path = artifact_path(name)
+        # A/B runs of kernel-library builds (tools/ab_decode.py): POLYKEY_LIB_<NAME> = path of a
+        # variant build of the same sources
+        path = os.environ.get("POLYKEY_LIB_" + name.upper()) or artifact_path(name)
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         _cache[name] = lib
         return lib

@@ -42,6 +42,10 @@ class EngineConfig:
     watermark: float = 0.01
     device: str = ""
     overlap: bool = False  # pipelined steps (see LLMEngine.step); AsyncLLM turns it on
+    # scheduler policy (engine/scheduler.py): prefill_first | decode_first; POLYKEY_SCHED_POLICY
+    sched_policy: str = dataclasses.field(default_factory=lambda: os.environ.get("POLYKEY_SCHED_POLICY",
+                                                                                 "prefill_first"))
+    max_decode_stall: int = 4
     # automatic prefix caching (csrc/runtime/block_manager.h); POLYKEY_PREFIX_CACHING=0 disables
     prefix_caching: bool = dataclasses.field(
         default_factory=lambda: os.environ.get("POLYKEY_PREFIX_CACHING", "1") != "0")
@@ -62,6 +66,9 @@ class LLMEngine:
         if cfg.max_model_len > mcfg.max_position:
             cfg = dataclasses.replace(cfg, max_model_len=mcfg.max_position)
             self.cfg = cfg
+        if cfg.block_size <= 0 or cfg.block_size % 32:
+            # the K cache stores 32-token fragment-native tiles (csrc/kernels/common.h kcache_off)
+            raise ValueError(f"block_size must be a positive multiple of 32, got {cfg.block_size}")
         # DP attention + EP (ParallelState.dp_attention): every rank schedules its own requests
         # and the ranks step in lockstep because each MoE layer is an all-to-all over all of
         # them.  Steps are synchronous (no overlap / continuations) and eager: the dispatch
@@ -97,7 +104,8 @@ class LLMEngine:
         rt = load_extension("_pk_runtime")
         self.bm = rt.BlockManager(nblocks, cfg.block_size, int(nblocks * cfg.watermark), cfg.prefix_caching)
         self.runner.bm = self.bm
-        self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len)
+        self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.max_num_batched_tokens, cfg.max_model_len,
+                                   policy=cfg.sched_policy, max_decode_stall=cfg.max_decode_stall)
         if cfg.hip_graphs and dev.type == "cuda":
             self.runner.capture_graphs()
         self.step_count = 0
@@ -192,6 +200,8 @@ class LLMEngine:
         if (not self.overlap or batch.prefills or sch.waiting or len(batch.decodes) != len(sch.running)
                 or any(s.is_finished() for s in batch.decodes)):
             return None
+        if all(len(s.output_ids) + 1 >= s.params.max_tokens for s in batch.decodes):
+            return None  # the in-flight step ends every sequence: a continuation would be discarded
         return self.runner.launch_continuation(batch, handle)
 
     def _complete(self, batch, sampling, handle):

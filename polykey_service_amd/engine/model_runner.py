@@ -97,7 +97,8 @@ class ModelRunner:
         self.device = device
         self.bs = cfg.block_size
         self.max_blocks = (cfg.max_model_len + self.bs - 1) // self.bs
-        self.layout = _Layout(cfg.max_num_batched_tokens, cfg.max_num_seqs, self.max_blocks)
+        self.max_step_tokens = cfg.max_num_batched_tokens  # decodes count toward the budget
+        self.layout = _Layout(self.max_step_tokens, cfg.max_num_seqs, self.max_blocks)
         pin = device.type == "cuda"
         # two pinned staging buffers used alternately: a step may be packed while the previous
         # step's H2D copy is still queued behind the GPU (continuation launches, LLMEngine.step)
@@ -181,7 +182,7 @@ class ModelRunner:
 
     def activation_reserve_bytes(self) -> int:
         m = self.mcfg
-        T = self.cfg.max_num_batched_tokens
+        T = self.max_step_tokens
         tp = self.model.st.tp_size
         per_tok = 2 * (m.hidden_size * 4 + (m.q_size + 2 * m.kv_size) // tp + 3 * m.intermediate_size // tp)
         logits = self.cfg.max_num_seqs * m.vocab_size * 4 * 2

@@ -1,15 +1,21 @@
 """Continuous-batching scheduler (the L3 "Scheduler" of SURVEY.md §1.2 / §3.6).
 
-Every engine step builds one batch under a token budget (``max_num_batched_tokens``) and a
-sequence cap (``max_num_seqs``):
+Every engine step builds one batch under a prefill-token budget (``max_num_batched_tokens``)
+and a sequence cap (``max_num_seqs``):
 
-1. running sequences first, oldest first: a decode costs 1 token; a sequence still in a
-   chunked prefill takes ``min(pending, budget)`` tokens.  If the KV pool cannot grow a
+1. running sequences, oldest first: a decode costs 1 token; a sequence still in a chunked
+   prefill takes ``min(pending, budget)`` tokens.  If the KV pool cannot grow a
    running sequence, the *youngest* running sequence is preempted (blocks freed, state reset
    to recompute) and the step retries — the oldest requests keep their latency;
-2. then waiting sequences in FIFO order, admitted only when their (chunked) prefill fits
-   both the budget and the KV pool minus a watermark reserve; the first one that does not fit
-   blocks the queue (no overtaking → no starvation).
+2. waiting sequences in FIFO order, admitted only when their (chunked) prefill fits both the
+   budget and the KV pool minus a watermark reserve; the first one that does not fit blocks
+   the queue (no overtaking → no starvation).
+
+Policy ``prefill_first`` (default, throughput) runs 2 before 1 while prompts are queued —
+a wave of prompts is prefilled in whole budget-sized steps (GEMM rows a multiple of the
+budget, no small tail chunk needing an extra un-graphed step) — but never skips the running
+decodes for more than ``max_decode_stall`` consecutive steps; ``decode_first`` always runs 1
+first (lowest inter-token latency under mixed load).
 
 KV bookkeeping lives in the native :class:`_pk_runtime.BlockManager` (``csrc/runtime``).
 
@@ -39,7 +45,11 @@ class ScheduledBatch:
 
     @property
     def num_tokens(self) -> int:
-        return len(self.decodes) + sum(n for _, n in self.prefills)
+        return len(self.decodes) + self.num_prefill_tokens
+
+    @property
+    def num_prefill_tokens(self) -> int:
+        return sum(n for _, n in self.prefills)
 
     @property
     def empty(self) -> bool:
@@ -61,14 +71,31 @@ def _salt(s: Optional[str]) -> int:
     return int.from_bytes(hashlib.blake2b(s.encode(), digest_size=8).digest(), "little") or 1
 
 
+class _Step:
+    """One step's batch under construction."""
+
+    def __init__(self, budget: int):
+        self.budget = budget
+        self.decodes: List[Sequence] = []
+        self.prefills: List[Tuple[Sequence, int]] = []
+        self.preempted: List[Sequence] = []
+        self.scheduled = set()
+
+
 class Scheduler:
     def __init__(self, block_manager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
-                 max_model_len: int = 8192, max_prefill_chunk: Optional[int] = None):
+                 max_model_len: int = 8192, max_prefill_chunk: Optional[int] = None, policy: str = "prefill_first",
+                 max_decode_stall: int = 4):
         self.bm = block_manager
         self.max_num_seqs = max_num_seqs
         self.max_num_batched_tokens = max_num_batched_tokens
         self.max_model_len = max_model_len
         self.max_prefill_chunk = max_prefill_chunk or max_num_batched_tokens
+        if policy not in ("prefill_first", "decode_first"):
+            raise ValueError(f"unknown scheduling policy {policy!r}")
+        self.policy = policy
+        self.max_decode_stall = max_decode_stall
+        self._decode_stall = 0
         self.waiting: Deque[Sequence] = collections.deque()
         self.running: List[Sequence] = []
         self.by_request: Dict[str, Sequence] = {}
@@ -170,29 +197,44 @@ class Scheduler:
         return None
 
     def schedule(self) -> ScheduledBatch:
-        budget = self.max_num_batched_tokens
-        decodes: List[Sequence] = []
-        prefills: List[Tuple[Sequence, int]] = []
-        preempted: List[Sequence] = []
-        scheduled = set()
+        st = _Step(self.max_num_batched_tokens)
+        # prefill-first: new prompts are admitted ahead of the running decodes (those run with
+        # whatever budget is left), so a wave of prompts is prefilled in full budget-sized
+        # steps with no decode rows mixed in -- GEMM shapes stay multiples of the budget and no
+        # small tail chunk is left for an extra un-graphed step.  Decodes are skipped for at
+        # most max_decode_stall consecutive steps, then a decode-first step runs.
+        pf = (self.policy == "prefill_first" and bool(self.waiting) and bool(self.running)
+              and self._decode_stall < self.max_decode_stall)
+        if pf:
+            self._admit(st)
+        self._schedule_running(st)
+        if not pf:
+            self._admit(st)
+        skipped = any(s.num_pending == 1 and s.seq_id not in st.scheduled for s in self.running)
+        self._decode_stall = self._decode_stall + 1 if skipped else 0
+        return ScheduledBatch(st.decodes, st.prefills, st.preempted)
 
+    def _schedule_running(self, st: "_Step") -> None:
         i = 0
-        while i < len(self.running) and budget > 0:
+        while i < len(self.running) and st.budget > 0:
             seq = self.running[i]
+            if seq.seq_id in st.scheduled:  # admitted earlier in this step (prefill-first)
+                i += 1
+                continue
             pending = seq.num_pending
-            n = 1 if pending == 1 else min(pending, budget, self.max_prefill_chunk)
+            n = 1 if pending == 1 else min(pending, st.budget, self.max_prefill_chunk)
             while not self.bm.allocate(seq.seq_id, seq.num_computed + n):
                 victim = self._preempt_youngest(protect=seq)
                 if victim is None:
                     break
-                preempted.append(victim)
+                st.preempted.append(victim)
             else:
                 if pending == 1:
-                    decodes.append(seq)
+                    st.decodes.append(seq)
                 else:
-                    prefills.append((seq, n))
-                scheduled.add(seq.seq_id)
-                budget -= n
+                    st.prefills.append((seq, n))
+                st.scheduled.add(seq.seq_id)
+                st.budget -= n
                 i = self.running.index(seq) + 1  # preemption may have removed earlier entries
                 continue
             # could not even fit this sequence alone: preempt it too
@@ -204,20 +246,22 @@ class Scheduler:
             seq.num_preemptions += 1
             self.num_preemptions += 1
             self.waiting.appendleft(seq)
-            preempted.append(seq)
-
+            st.preempted.append(seq)
         # preempted sequences that were already scheduled this step are dropped from it
-        if preempted:
-            gone = {s.seq_id for s in preempted}
-            decodes = [s for s in decodes if s.seq_id not in gone]
-            prefills = [(s, n) for s, n in prefills if s.seq_id not in gone]
+        if st.preempted:
+            gone = {s.seq_id for s in st.preempted}
+            st.decodes = [s for s in st.decodes if s.seq_id not in gone]
+            st.prefills = [(s, n) for s, n in st.prefills if s.seq_id not in gone]
+            st.budget = self.max_num_batched_tokens - len(st.decodes) - sum(n for _, n in st.prefills)
 
-        while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
+    def _admit(self, st: "_Step") -> None:
+        preempted = {s.seq_id for s in st.preempted}
+        while self.waiting and st.budget > 0 and len(self.running) < self.max_num_seqs:
             seq = self.waiting[0]
-            if seq.seq_id in {s.seq_id for s in preempted}:
+            if seq.seq_id in preempted:
                 break  # do not thrash: re-admit preempted sequences next step
             self._match_prefix(seq)
-            n = min(seq.num_pending, budget, self.max_prefill_chunk)
+            n = min(seq.num_pending, st.budget, self.max_prefill_chunk)
             if not self.bm.can_allocate(seq.seq_id, seq.num_computed + n, True):
                 self._unmatch(seq)
                 break
@@ -231,9 +275,9 @@ class Scheduler:
                 seq.num_cached_tokens = min(seq.num_computed, len(seq.prompt_ids))
                 self.num_cached_tokens += seq.num_cached_tokens
             self.running.append(seq)
+            st.scheduled.add(seq.seq_id)
             if seq.num_pending == 1 and n == 1:
-                decodes.append(seq)
+                st.decodes.append(seq)
             else:
-                prefills.append((seq, n))
-            budget -= n
-        return ScheduledBatch(decodes, prefills, preempted)
+                st.prefills.append((seq, n))
+            st.budget -= n

@@ -81,6 +81,30 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) 
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
 
 
+_KIDX: dict = {}
+
+
+def kcache_index(bs: int, device=None) -> torch.Tensor:
+    """[bs, 128] flat position of K element (token, dim) inside one (block, kv head) slab of the
+    paged K cache: fragment-native 32-token tiles (csrc/kernels/common.h ``kcache_off``)."""
+    if bs % 32:
+        raise ValueError(f"the K-cache layout needs a block size that is a multiple of 32, got {bs}")
+    key = (bs, str(device))
+    if key not in _KIDX:
+        k = torch.arange(bs).view(bs, 1)
+        d = torch.arange(128).view(1, 128)
+        kt = k & 31
+        lane = 16 * (d >> 5) + 4 * (kt >> 3) + (kt & 3)
+        _KIDX[key] = ((k >> 5) * 4096 + ((((kt >> 2) & 1) * 4 + ((d >> 3) & 3)) * 64 + lane) * 8 + (d & 7)).to(device)
+    return _KIDX[key]
+
+
+def k_cache_logical(k_cache: torch.Tensor) -> torch.Tensor:
+    """The physical K cache [blocks, n_kv, bs, 128] as logical (token, dim) rows."""
+    nb, nkv, bs, hd = k_cache.shape
+    return k_cache.reshape(nb, nkv, bs * hd)[:, :, kcache_index(bs, k_cache.device).view(-1)].view(nb, nkv, bs, hd)
+
+
 def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
                    k_cache: Optional[torch.Tensor], v_cache: Optional[torch.Tensor],
                    slot_mapping: Optional[torch.Tensor], nq: int, nkv: int, hd: int) -> torch.Tensor:
@@ -97,7 +121,11 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
         if valid.any():
             s = sm[valid]
             blk, off = s // bs, s % bs
-            k_cache[blk, :, off, :] = k[valid].to(k_cache.dtype)
+            n, nkv_ = blk.numel(), k_cache.shape[1]
+            kflat = k_cache.view(k_cache.shape[0], nkv_, bs * hd)
+            pos = kcache_index(bs, k_cache.device)[off]  # [n, 128] fragment-native positions
+            kflat[blk.view(n, 1, 1), torch.arange(nkv_, device=k_cache.device).view(1, nkv_, 1),
+                  pos.view(n, 1, hd)] = k[valid].to(k_cache.dtype)
             v_cache[blk, :, :, off] = v[valid].to(v_cache.dtype)
     return q
 
@@ -108,7 +136,7 @@ def gather_kv(k_cache, v_cache, block_table, n_tokens):
     bs = k_cache.shape[2]
     nb = (n_tokens + bs - 1) // bs
     blocks = block_table[:nb].long()
-    k = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * bs, k_cache.shape[1], -1)[:n_tokens]
+    k = k_cache_logical(k_cache[blocks]).permute(0, 2, 1, 3).reshape(nb * bs, k_cache.shape[1], -1)[:n_tokens]
     v = v_cache[blocks].permute(0, 3, 1, 2).reshape(nb * bs, v_cache.shape[1], -1)[:n_tokens]
     return k, v
 

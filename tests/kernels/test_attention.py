@@ -30,7 +30,7 @@ def block_tables_for(ctxs, bs, num_blocks, max_blocks, seed=0):
     return bt
 
 
-@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 32), (32, 8, 16), (4, 4, 32), (16, 1, 64)])
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 32), (32, 8, 96), (4, 4, 32), (16, 1, 64)])
 @pytest.mark.parametrize("ctxs", [[1, 5, 32, 33, 100], [512, 513, 1200, 7], [2048, 1]])
 def test_decode(nq, nkv, bs, ctxs):
     max_blocks = (max(ctxs) + bs - 1) // bs + 3
@@ -77,7 +77,7 @@ def test_decode_zero_context_rows_are_zero():
     torch.testing.assert_close(out[1:2].float(), exp.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 32), (4, 1, 16), (16, 1, 32)])
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 32), (4, 1, 64), (16, 1, 32)])
 @pytest.mark.parametrize("qlens,ctxs", [([7, 16, 33], [7, 16, 33]), ([1, 20, 64], [100, 20, 300]),
                                         ([130], [130]), ([5, 1], [70, 1])])
 def test_prefill_with_prefix(nq, nkv, bs, qlens, ctxs):
@@ -124,7 +124,7 @@ def test_mixed_decode_and_prefill():
     torch.testing.assert_close(out[2:].float(), exp_p.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 16), (4, 2, 64)])
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 96), (4, 2, 64)])
 def test_rope_and_cache(nq, nkv, bs):
     T = 37
     qkv = torch.randn(T, (nq + 2 * nkv) * HD).to(torch.bfloat16)
@@ -145,7 +145,7 @@ def test_rope_and_cache(nq, nkv, bs):
     assert torch.equal(vc_d.cpu(), vc_r)
 
 
-@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 16), (16, 4, 32)])
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 64), (16, 4, 32)])
 @pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [512, 513, 1300, 0]])
 @pytest.mark.parametrize("S", [1, 4])
 def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S):

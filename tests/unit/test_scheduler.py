@@ -115,3 +115,30 @@ def test_everything_finishes_without_leaks(reqs, blocks, budget):
     for s in seqs:
         assert len(s.output_ids) == s.params.max_tokens
     assert bm.num_free == blocks
+
+
+def test_prefill_first_wave_and_decode_stall_cap():
+    """prefill_first: a wave of 4 prompts of 100 tokens (budget 200) admitted while 2 sequences
+    decode runs as two whole 200-token prefill steps; the decodes wait at most
+    max_decode_stall steps.  decode_first mixes the decodes in and leaves a tail chunk."""
+    def run(policy, stall=4):
+        bm = rt.BlockManager(1000, 16, 0)
+        sch = Scheduler(bm, max_num_seqs=8, max_num_batched_tokens=200, max_model_len=1024, policy=policy,
+                        max_decode_stall=stall)
+        old = [mk(10, 50), mk(10, 50)]
+        for s in old:
+            sch.add(s)
+        simulate_step(sch, sch.schedule())
+        for _ in range(4):
+            sch.add(mk(100, 5))
+        steps = []
+        for _ in range(3):
+            b = sch.schedule()
+            steps.append((len(b.decodes), [n for _, n in b.prefills]))
+            simulate_step(sch, b)
+        return steps
+    assert run("prefill_first") == [(0, [100, 100]), (0, [100, 100]), (6, [])]
+    assert run("prefill_first", stall=1) == [(0, [100, 100]), (4, [100, 96]), (5, [4])]
+    assert run("decode_first") == [(2, [100, 98]), (3, [2, 100, 95]), (5, [5])]
+    with pytest.raises(ValueError):
+        Scheduler(rt.BlockManager(10, 16, 0), policy="fastest")
