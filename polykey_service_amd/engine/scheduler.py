@@ -27,6 +27,7 @@ full blocks (:meth:`Scheduler.commit_prefix`) once the step that wrote their KV 
 """
 from __future__ import annotations
 
+import bisect
 import collections
 import dataclasses
 import time
@@ -274,7 +275,11 @@ class Scheduler:
                 seq.first_scheduled = time.monotonic()
                 seq.num_cached_tokens = min(seq.num_computed, len(seq.prompt_ids))
                 self.num_cached_tokens += seq.num_cached_tokens
-            self.running.append(seq)
+            # `running` stays in arrival order (seq ids are monotonic): a re-admitted preempted
+            # sequence keeps its age, so "youngest" in _preempt_youngest is the latest arrival
+            # (appending it made an old sequence the youngest and two sequences that do not fit
+            # together could preempt each other forever under prefill_first)
+            bisect.insort(self.running, seq, key=lambda s: s.seq_id)
             st.scheduled.add(seq.seq_id)
             if seq.num_pending == 1 and n == 1:
                 st.decodes.append(seq)

@@ -1,0 +1,122 @@
+"""Prefill-sized GEMMs on the hand-written MFMA kernel (``csrc/kernels/gemm_prefill.hip``).
+
+``y = x @ W^T`` (``W`` in PyTorch ``[N, K]`` layout), bf16 in / fp32 accumulate / bf16 out, for
+hundreds to tens of thousands of rows; dense, or grouped by expert with the group row offsets
+read on the device (MoE prefill: no host read-back, one launch per projection, graph
+capturable).  Optional fused SiLU(gate) * up for gate/up rows interleaved in blocks of 16
+(:func:`polykey_service_amd.ops.gemm.interleave_gate_up`).
+
+CPU tensors use the fp32 reference with the kernel's bf16 rounding points.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+from . import native
+
+BM = 256
+BN = 256
+# 0: BK 64 x 2 LDS stages, 1: BK 32 x 4 stages, 2: ping-pong quadrant phases (default: 6-8 %
+# faster than 0, tools/prefill_gemm_bench.py) -- csrc/kernels/gemm_prefill.hip
+VARIANT = int(os.environ.get("POLYKEY_PREFILL_GEMM_VARIANT", "2"))
+
+
+class PrefillGemmArgs(ctypes.Structure):
+    """Mirror of ``struct PrefillGemmArgs`` (checked against ``pk_prefill_gemm_args_size``)."""
+    _fields_ = [("C", ctypes.c_void_p), ("A", ctypes.c_void_p), ("W", ctypes.c_void_p),
+                ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int), ("lda", ctypes.c_int),
+                ("ldc", ctypes.c_int), ("row_offsets", ctypes.c_void_p), ("w_stride", ctypes.c_longlong),
+                ("groups", ctypes.c_int), ("tiles_m", ctypes.c_int), ("silu", ctypes.c_int)]
+
+
+_checked = False
+
+
+def supported(N: int, K: int) -> bool:
+    return N % BN == 0 and K % 64 == 0
+
+
+def _launch(a: PrefillGemmArgs, variant: Optional[int] = None) -> None:
+    global _checked
+    lib = native.lib()
+    if not _checked:
+        fn = lib.pk_prefill_gemm_args_size
+        fn.restype = ctypes.c_int
+        n = fn()
+        assert n == ctypes.sizeof(PrefillGemmArgs), f"PrefillGemmArgs mismatch: C {n} vs ctypes {ctypes.sizeof(PrefillGemmArgs)}"
+        f = lib.pk_prefill_gemm
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        f.restype = ctypes.c_int
+        _checked = True
+    native.check(lib.pk_prefill_gemm(ctypes.byref(a), VARIANT if variant is None else variant, native.stream_ptr()),
+                 "pk_prefill_gemm")
+
+
+def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
+    y = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    if silu:
+        v = y.view(y.shape[0], -1, 2, 16)
+        g, u = v[:, :, 0].reshape(y.shape[0], -1), v[:, :, 1].reshape(y.shape[0], -1)
+        y = torch.nn.functional.silu(g).to(torch.bfloat16).float() * u
+    return y.to(x.dtype)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, silu: bool = False,
+           variant: Optional[int] = None) -> torch.Tensor:
+    """x [M, K] @ w[N, K]^T -> [M, N] (SiLU: [M, N/2]), optionally into ``out``."""
+    M, K = x.shape
+    N = w.shape[0]
+    n_out = N // 2 if silu else N
+    if not x.is_cuda:
+        y = _ref(x, w, silu)
+        if out is None:
+            return y
+        out.copy_(y)
+        return out
+    if out is None:
+        out = torch.empty((M, n_out), dtype=x.dtype, device=x.device)
+    if M == 0:
+        return out
+    if not supported(N, K) or x.stride(1) != 1 or not w.is_contiguous() or out.stride(1) != 1:
+        raise ValueError(f"prefill GEMM: unsupported shape/layout M={M} N={N} K={K}")
+    a = PrefillGemmArgs()
+    a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), w.data_ptr()
+    a.M, a.N, a.K, a.lda, a.ldc = M, N, K, x.stride(0), out.stride(0)
+    a.groups, a.tiles_m, a.silu = 0, (M + BM - 1) // BM, int(silu)
+    _launch(a, variant)
+    return out
+
+
+def grouped_linear(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, silu: bool = False,
+                   out: Optional[torch.Tensor] = None, variant: Optional[int] = None) -> torch.Tensor:
+    """Rows [offsets[e], offsets[e+1]) of ``x`` times ``w[e]^T`` (w: [G, N, K], offsets int32 on
+    the device, rows past offsets[G] untouched).  One launch; the grid covers
+    ceil(rows / 256) + G tile rows and the kernel maps each to its group."""
+    T, K = x.shape
+    G, N, _ = w.shape
+    n_out = N // 2 if silu else N
+    if not x.is_cuda:
+        offs = offsets.tolist()
+        y = torch.zeros((T, n_out), dtype=x.dtype) if out is None else out
+        for e in range(G):
+            lo, hi = offs[e], offs[e + 1]
+            if hi > lo:
+                y[lo:hi] = _ref(x[lo:hi], w[e], silu)
+        return y
+    if out is None:
+        out = torch.empty((T, n_out), dtype=x.dtype, device=x.device)
+    if T == 0:
+        return out
+    if not supported(N, K) or x.stride(1) != 1 or not w.is_contiguous() or offsets.dtype != torch.int32:
+        raise ValueError(f"grouped prefill GEMM: unsupported shape/layout T={T} N={N} K={K}")
+    a = PrefillGemmArgs()
+    a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), w.data_ptr()
+    a.M, a.N, a.K, a.lda, a.ldc = T, N, K, x.stride(0), out.stride(0)
+    a.row_offsets, a.w_stride, a.groups = offsets.data_ptr(), N * K, G
+    a.tiles_m, a.silu = (T + BM - 1) // BM + G, int(silu)
+    _launch(a, variant)
+    return out

@@ -5,8 +5,9 @@ Decode (T <= 64 tokens): everything stays on the device and is graph-capturable 
 GEMM for w13 with the fused SiLU epilogue → grouped skinny GEMM for w2 → weighted
 ``unpermute``.  An expert that received no token is skipped without reading its weights.
 
-Prefill (T > 64): the same routing kernels, then one hipBLASLt GEMM per expert over its
-contiguous rows (expert row counts are read back once per layer; prefill is not graphed).
+Prefill (T > 64): the same routing kernels, then ONE launch per projection of the grouped MFMA
+GEMM of ``csrc/kernels/gemm_prefill.hip`` — it reads the expert row offsets on the device (no
+read-back, no per-expert launches) and fuses SiLU(gate)*up into the w13 epilogue.
 
 Expert parallelism: with ``e_lo, e_hi`` this rank only computes experts ``[e_lo, e_hi)``;
 slots routed elsewhere get ``inv = -1`` and contribute zero, and the caller all-reduces the
@@ -22,7 +23,7 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from . import gemm, native, reference
+from . import gemm, gemm_prefill, native, reference
 from .gemm import silu_and_mul_interleaved
 
 
@@ -112,7 +113,9 @@ def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_ro
         native.call("pk_moe_gemm", out.data_ptr(), a.data_ptr(), w.data_ptr(), offsets.data_ptr(), max_rows, N, K,
                     out.stride(0), E_local, 2 if silu else 0, native.stream_ptr())
         return out
-    offs = offsets.tolist()  # prefill: one read-back per layer, then a library GEMM per expert
+    if a.is_cuda and gemm_prefill.supported(N, K) and w.is_contiguous():
+        return gemm_prefill.grouped_linear(a, w, offsets, silu=silu, out=out)
+    offs = offsets.tolist()  # shapes the MFMA kernel does not tile: a library GEMM per expert
     for e in range(E_local):
         lo, hi = offs[e], offs[e + 1]
         if hi > lo:  # results land in their rows of `out` directly (no slice-assignment copy)
