@@ -63,6 +63,26 @@ __device__ __forceinline__ bf16x8_t pack_p(const float* p) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// Reductions over the 4 lane groups of a column (lanes r, r+16, r+32, r+48) with the gfx950
+// VALU lane swaps (v_permlane16/32_swap: rows 1<->0 / 3<->2, then halves) instead of
+// ds_bpermute round trips through the LDS crossbar (__shfl_xor): max(x, swapped x) and
+// x + swapped x are already the pairwise results in every lane (prefill attention 1-4 % faster,
+// profiles/r2_prefill_attention.txt).
+__device__ __forceinline__ float col_max(float x) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+// Total exp-sum of the lane's column (reduce the 4 lane groups).
+__device__ __forceinline__ float col_sum(float l) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+  l = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 struct WaveState {
   float m;        // running max (base-2 scaled) of this lane's column
   float l;        // partial exp-sum of this lane's 8 keys per step (summed over lane groups at the end)
@@ -125,8 +145,7 @@ __device__ __forceinline__ void attend_step(WaveState& st, const bf16x8_t (&qf)[
       sv[4 * t + i] = v;
       mx = fmaxf(mx, v);
     }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = col_max(mx);
   const float m_new = fmaxf(st.m, mx);
   const float alpha = exp2f(st.m - m_new);
   st.m = m_new;
@@ -181,12 +200,7 @@ __device__ __forceinline__ void load_q(bf16x8_t (&qf)[4], const bf16_t* q, bool 
   for (int kk = 0; kk < 4; ++kk) qf[kk] = valid ? ld8(q + 32 * g + 8 * kk) : zero8();
 }
 
-// Total exp-sum of the lane's column (reduce the 4 lane groups).
-__device__ __forceinline__ float col_sum(float l) {
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  return l;
-}
+
 
 // ------------------------------------------------------------------------------ decode
 #ifndef PK_DECODE_BT_PREFETCH

@@ -56,6 +56,7 @@ SP_MIN_TOKENS = int(os.environ.get("POLYKEY_SP_MIN_TOKENS", "256"))
 # by default).
 INLAUNCH_RESIDUAL = os.environ.get("POLYKEY_INLAUNCH_RESIDUAL", "0") == "1"
 INLAUNCH_SPLIT = int(os.environ.get("POLYKEY_INLAUNCH_SPLIT", "4"))
+HALF_O_SLABS = os.environ.get("POLYKEY_HALF_O_SLABS", "1") == "1"
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:
@@ -485,7 +486,10 @@ class LlamaForCausalLM(nn.Module):
                 parts = gemm.linear_add_residual(a, at.o, ws, ctr, residual, buf2, S=INLAUNCH_SPLIT, packed=at.o_p,
                                                  half=True)
             else:
-                parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p), residual, buf2)
+                # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode
+                # step, profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
+                parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=HALF_O_SLABS),
+                                            residual, buf2)
             h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf,
                                  rowscale=gemm.RowScale(parts, layer.eps))
             if inlaunch:

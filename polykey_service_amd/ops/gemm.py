@@ -210,6 +210,12 @@ _SPLIT_OVERRIDE = {tuple(int(v) for v in k.split("x")): int(s) for k, s in
                    (e.split(":") for e in os.environ.get("POLYKEY_SKINNY_SPLIT", "").split(",") if e)}
 
 
+# per-shape override of the 64-row n-block (KR = 1) split-K partials for A/B runs:
+# POLYKEY_SKINNY_HALF="4096x4096:4,4096x14336:4" (N x K : S)
+_HALF_SPLIT = {tuple(int(v) for v in k.split("x")): int(s) for k, s in
+               (e.split(":") for e in os.environ.get("POLYKEY_SKINNY_HALF", "").split(",") if e)}
+
+
 def choose_split(N: int, K: int, M: int, target: int = _TARGET_WGS) -> int:
     """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows each)."""
     if (N, K) in _SPLIT_OVERRIDE:
@@ -280,15 +286,22 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
 
 
 def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Optional[int] = None,
-                   packed: Optional[torch.Tensor] = None) -> Partial:
-    """Split-K fp32 slabs into workspace ``ws`` (fp32, >= S*M*N)."""
+                   packed: Optional[torch.Tensor] = None, half: bool = False) -> Partial:
+    """Split-K fp32 slabs into workspace ``ws`` (fp32, >= S*M*N).  ``half`` (packed W): 64-row
+    n-blocks at half the default split -- the same grid, half the slab bytes."""
     M, K = x.shape
     N = w.shape[0]
-    S = S or choose_split(N, K, M)
+    if S is None and packed is not None and (N, K) in _HALF_SPLIT:
+        half, S = True, _HALF_SPLIT[(N, K)]
+    half = half and packed is not None and packed.numel() * packed.element_size() < NT_MIN_BYTES
+    if S is None:
+        S = choose_split(N, K, M)
+        if half:
+            S = max(1, S // 2)
     assert ws.numel() >= S * M * N, "split-K workspace too small"
     src = packed if packed is not None else w
     native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), src.data_ptr(), M, N, K, x.stride(0), N, S,
-                1 | _wmode(packed), native.stream_ptr())
+                1 | _wmode(packed) | (HALF_BIT if half else 0), native.stream_ptr())
     return Partial(ws, S, M, N)
 
 

@@ -100,6 +100,10 @@ def test_fragment_packed_weights(M, N, K, S):
     if S > 1:
         p = gemm.linear_partial(x, w, ws, S, packed=wp)
         torch.testing.assert_close(p.view().sum(0), exp, atol=1e-2, rtol=1e-2)
+        # 64-row n-blocks (KR = 1) at half the split: same slab layout [S/2, M, N]
+        ph = gemm.linear_partial(x, w, ws, packed=wp, half=True)
+        assert ph.S == max(1, gemm.choose_split(N, K, M) // 2)
+        torch.testing.assert_close(ph.view().sum(0), exp, atol=1e-2, rtol=1e-2)
 
 
 def test_fragment_packed_silu():
