@@ -274,7 +274,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
            packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 out [M, N]; ``packed`` = :func:`pack_weight` (w) streamed instead of ``w`` when given."""
     if not skinny_ok(x, w):
-        return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
+        # torch.mm into a preallocated output: hipBLASLt picks a faster kernel for the 8B QKV
+        # prefill shape than through F.linear (288 vs 344 us at 8192 rows; the other
+        # projections are equal: profiles/r2_prefill_gemm_lab.txt)
+        if out is None:
+            out = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+        return torch.mm(x, w.t(), out=out)
     M, K = x.shape
     N = w.shape[0]
     if out is None:
