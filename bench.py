@@ -7,7 +7,9 @@ independent Llama-3-8B replica (request-level data parallel → weak scaling: pe
 fixed as N grows) that serves a real ``polykey.v2.PolykeyService`` gRPC server on
 127.0.0.1 and is driven by ``--concurrency`` concurrent ``ExecuteTool`` clients in the same
 process.  With ``--tp 8 --model llama3-70b`` the 8 ranks form one tensor-parallel replica
-(RCCL all-reduce over xGMI) and rank 0 serves the gRPC endpoint.
+(RCCL all-reduce over xGMI) and rank 0 serves the gRPC endpoint.  The clients run in a load
+generator process of their own per replica with ``--client process``
+(``polykey_service_amd.client.load_gen``); by default they run on the server's event loop.
 
 A "step" is one wave of ``--concurrency`` requests per replica, each a synthetic
 ``--prompt-len``-token prompt generating exactly ``--max-tokens`` tokens (``ignore_eos``,
@@ -55,6 +57,10 @@ def parse_args(argv=None):
     ap.add_argument("--port-base", type=int, default=int(os.environ.get("POLYKEY_BENCH_PORT", "0")),
                     help="gRPC port of rank 0 (rank r: base + r); 0: an ephemeral port per rank")
     ap.add_argument("--seed", type=int, default=0)
+    # measured on 1x MI355X (profiles/r2_bench_client_ab.txt): unary 12,879 tok/s with the clients on
+    # the server's event loop vs 12,299 from a separate load-generator process (streaming: 12,787)
+    ap.add_argument("--client", choices=["process", "inproc"], default="inproc",
+                    help="load generator on the server's event loop (default) or in its own process")
     return ap.parse_args(argv)
 
 
@@ -85,6 +91,11 @@ async def run_waves(args, engine, st, leaders_group):
     port = args.port_base + st.rank if args.port_base > 0 else 0
     srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
     port = await srv.start()
+    if args.client == "process":
+        try:
+            return await _drive_external(args, engine, st, leaders_group, port, srv, llm=router.llm)
+        finally:
+            await srv.server.stop(0)
     channel = grpc.aio.insecure_channel(f"127.0.0.1:{port}", options=[
         ("grpc.max_receive_message_length", 64 << 20), ("grpc.max_send_message_length", 64 << 20)])
     unary = channel.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
@@ -170,6 +181,55 @@ async def run_waves(args, engine, st, leaders_group):
     return tokens, elapsed, lats
 
 
+async def _drive_external(args, engine, st, leaders_group, port, srv, llm):
+    """Waves from a load-generator child process (no exec: a fresh interpreter via
+    create_subprocess_exec); the timed span is bracketed here by barrier + device sync."""
+    import torch
+    import torch.distributed as dist
+    cmd = [sys.executable, "-m", "polykey_service_amd.client.load_gen", "--addr", f"127.0.0.1:{port}",
+           "--tool", f"llm.generate:{args.model}", "--vocab", str(engine.mcfg.vocab_size),
+           "--concurrency", str(args.concurrency), "--prompt-len", str(args.prompt_len),
+           "--max-tokens", str(args.max_tokens), "--mode", args.mode, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--seed", str(args.seed * 1000 + st.rank)]
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(os.path.abspath(__file__)) + os.pathsep
+               + os.environ.get("PYTHONPATH", ""))
+    proc = await asyncio.create_subprocess_exec(*cmd, stdin=asyncio.subprocess.PIPE,
+                                                stdout=asyncio.subprocess.PIPE, env=env)
+    try:
+        ready = json.loads((await proc.stdout.readline()) or b"{}")
+        if not ready.get("ready"):
+            raise RuntimeError(f"load generator failed to start: {ready}")
+        dev = engine.device
+        if dist.is_initialized():
+            dist.barrier(group=leaders_group)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        proc.stdin.write(b"go\n")
+        await proc.stdin.drain()
+        res = json.loads((await proc.stdout.readline()) or b"{}")
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if dist.is_initialized():
+            dist.barrier(group=leaders_group)
+        elapsed = time.perf_counter() - t0
+        if "tokens" not in res:
+            raise RuntimeError(f"load generator failed: {res}")
+    finally:
+        if proc.returncode is None:
+            try:
+                proc.stdin.close()  # a generator still waiting for "go" reads EOF and exits
+            except Exception:
+                pass
+            try:
+                await asyncio.wait_for(proc.wait(), 30)
+            except asyncio.TimeoutError:
+                proc.kill()
+    if engine.lockstep:  # DP attention + EP: leave the lockstep loop together with the other ranks
+        await asyncio.get_running_loop().run_in_executor(None, llm.shutdown)
+    return res["tokens"], elapsed, res["lats"]
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -238,6 +298,7 @@ def main(argv=None) -> int:
                 else f"dp{st.world_size}" + (f"_ep{st.ep_size}_a2a" if st.ep_size > 1 else ""),
                 "concurrency_per_replica": args.concurrency,
                 "rpc": f"ExecuteTool ({args.mode})",
+                "clients": "load-generator process" if args.client == "process" else "server event loop",
                 "hip_graphs": not args.no_graphs,
                 # every prompt is unique, so the prefix cache must serve nothing (no skipped work)
                 "prefix_caching": ecfg.prefix_caching,

@@ -136,6 +136,16 @@ class LLMEngine:
     def has_unfinished(self) -> bool:
         return self.scheduler.has_work() or self._inflight is not None
 
+    def first_step_unfilled(self) -> bool:
+        """Idle engine (nothing running or in flight) whose waiting requests do not yet fill one
+        prefill step (token budget and sequence cap): a burst of arrivals may still be landing."""
+        sch = self.scheduler
+        if sch.running or self._inflight is not None or not sch.waiting:
+            return False
+        if len(sch.waiting) >= sch.max_num_seqs:
+            return False
+        return sum(s.num_pending for s in sch.waiting) < sch.max_num_batched_tokens
+
     def step(self) -> List[RequestOutput]:
         """One engine iteration.  With ``overlap`` the step is pipelined: the batch launched by
         the previous call is completed (wait for its sampled ids, advance sequence state, free
