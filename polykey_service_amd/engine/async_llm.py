@@ -55,6 +55,10 @@ class AsyncLLM:
         # request waits one gap.  0 disables.
         self.arrival_window_s = float(os.environ.get("POLYKEY_ARRIVAL_WINDOW_MS", "8")) / 1e3
         self.arrival_gap_s = float(os.environ.get("POLYKEY_ARRIVAL_GAP_MS", "2")) / 1e3
+        # "step": stop once the waiting requests fill one prefill step; "burst": keep collecting
+        # until the burst is over (the whole burst's prefill then runs without gRPC arrivals
+        # contending for the GIL with its kernel launches)
+        self.arrival_fill = os.environ.get("POLYKEY_ARRIVAL_FILL", "step")
         # The engine thread and the asyncio (gRPC) thread share the GIL.  CPython's default 5 ms
         # switch interval lets a burst of RPC handling hold the engine thread off for whole
         # decode steps (the GPU idles meanwhile); a short interval hands the GIL over promptly.
@@ -157,7 +161,8 @@ class AsyncLLM:
         eng = self.engine
         deadline = time.monotonic() + self.arrival_window_s
         self.stats["arrival_waits"] += 1
-        while not self._stop and eng.first_step_unfilled():
+        burst = self.arrival_fill == "burst"
+        while not self._stop and (eng.first_step_unfilled() or (burst and eng.idle_with_waiting())):
             left = deadline - time.monotonic()
             if left <= 0:
                 return
@@ -217,7 +222,7 @@ class AsyncLLM:
                     self._wake.wait(0.05)
                     self._wake.clear()
                     continue
-                if not eng.lockstep and self.arrival_window_s > 0 and eng.first_step_unfilled():
+                if not eng.lockstep and self.arrival_window_s > 0 and eng.idle_with_waiting():
                     self._coalesce_arrivals()
                 t0 = time.perf_counter()
                 outs = eng.step()

@@ -136,6 +136,11 @@ class LLMEngine:
     def has_unfinished(self) -> bool:
         return self.scheduler.has_work() or self._inflight is not None
 
+    def idle_with_waiting(self) -> bool:
+        sch = self.scheduler
+        return (not sch.running and self._inflight is None and bool(sch.waiting)
+                and len(sch.waiting) < sch.max_num_seqs)
+
     def first_step_unfilled(self) -> bool:
         """Idle engine (nothing running or in flight) whose waiting requests do not yet fill one
         prefill step (token budget and sequence cap): a burst of arrivals may still be landing."""
