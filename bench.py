@@ -59,6 +59,9 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     # measured on 1x MI355X (profiles/r2_bench_client_ab.txt): unary 12,879 tok/s with the clients on
     # the server's event loop vs 12,299 from a separate load-generator process (streaming: 12,787)
+    ap.add_argument("--frontend", choices=["replicas", "gateway"], default="replicas",
+                    help="N > 1, tp 1: every rank serves its own gRPC endpoint (replicas) or rank 0 serves ONE "
+                         "front end routing to every rank's engine process (gateway, engine/remote.py)")
     ap.add_argument("--client", choices=["process", "inproc"], default="inproc",
                     help="load generator on the server's event loop (default) or in its own process")
     return ap.parse_args(argv)
@@ -72,7 +75,7 @@ def relaunch_with_torchrun(args) -> int:
     return subprocess.call(cmd)
 
 
-async def run_waves(args, engine, st, leaders_group):
+async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
     import grpc
     import torch
     import torch.distributed as dist
@@ -87,13 +90,16 @@ async def run_waves(args, engine, st, leaders_group):
     logger = slog.Logger(open(os.devnull, "w"))
     router = ToolRouter()
     cfg = ServerConfig(model=args.model, backend="local")
-    attach_local_llm(router, cfg, logger, engine=engine)
+    attach_local_llm(router, cfg, logger, engine=engine, llm=llm)
     port = args.port_base + st.rank if args.port_base > 0 else 0
+    conc = args.concurrency * n_replicas  # gateway: one front end for every replica's clients
     srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
     port = await srv.start()
     if args.client == "process":
         try:
-            return await _drive_external(args, engine, st, leaders_group, port, srv, llm=router.llm)
+            return await _drive_external(args, engine, st, leaders_group if n_replicas == 1 else None, port, srv,
+                                         llm=router.llm, conc=args.concurrency * n_replicas,
+                                         stop_after=engine.lockstep or n_replicas > 1)
         finally:
             await srv.server.stop(0)
     channel = grpc.aio.insecure_channel(f"127.0.0.1:{port}", options=[
@@ -107,6 +113,8 @@ async def run_waves(args, engine, st, leaders_group):
     rng = random.Random(args.seed * 1000 + st.rank)
     tool = f"llm.generate:{args.model}"
     llm = router.llm
+    # gateway: the other ranks sit in their engine servers, so rank 0 times the waves alone
+    sync_ranks = dist.is_initialized() and n_replicas == 1
 
     timing = os.environ.get("POLYKEY_BENCH_TIMING") == "1"
     marks = []
@@ -153,13 +161,13 @@ async def run_waves(args, engine, st, leaders_group):
         return sum(r[0] for r in res), [r[1] for r in res]
 
     for _ in range(args.warmup):
-        await wave([build() for _ in range(args.concurrency)])
+        await wave([build() for _ in range(conc)])
     # the load generator prepares its synthetic requests up front, as a separate client
     # process would: building 64 x 256 random ids inside a wave would only steal the event
     # loop (and the GIL) from the server under test
-    waves = [[build() for _ in range(args.concurrency)] for _ in range(args.steps)]
+    waves = [[build() for _ in range(conc)] for _ in range(args.steps)]
     dev = engine.device
-    if dist.is_initialized():
+    if sync_ranks:
         dist.barrier(group=leaders_group)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
@@ -171,24 +179,26 @@ async def run_waves(args, engine, st, leaders_group):
         lats += l
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
-    if dist.is_initialized():
+    if sync_ranks:
         dist.barrier(group=leaders_group)
     elapsed = time.perf_counter() - t0
     await channel.close()
     await srv.server.stop(0)
-    if engine.lockstep:  # DP attention + EP: leave the lockstep loop together with the other ranks
+    if engine.lockstep or n_replicas > 1:
+        # DP attention + EP: leave the lockstep loop together with the other ranks; gateway:
+        # stop the other ranks' engine servers (they are waiting on the front end)
         await asyncio.get_running_loop().run_in_executor(None, llm.shutdown)
     return tokens, elapsed, lats
 
 
-async def _drive_external(args, engine, st, leaders_group, port, srv, llm):
+async def _drive_external(args, engine, st, leaders_group, port, srv, llm, conc, stop_after):
     """Waves from a load-generator child process (no exec: a fresh interpreter via
     create_subprocess_exec); the timed span is bracketed here by barrier + device sync."""
     import torch
     import torch.distributed as dist
     cmd = [sys.executable, "-m", "polykey_service_amd.client.load_gen", "--addr", f"127.0.0.1:{port}",
            "--tool", f"llm.generate:{args.model}", "--vocab", str(engine.mcfg.vocab_size),
-           "--concurrency", str(args.concurrency), "--prompt-len", str(args.prompt_len),
+           "--concurrency", str(conc), "--prompt-len", str(args.prompt_len),
            "--max-tokens", str(args.max_tokens), "--mode", args.mode, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--seed", str(args.seed * 1000 + st.rank)]
     env = dict(os.environ, PYTHONPATH=os.path.dirname(os.path.abspath(__file__)) + os.pathsep
@@ -200,7 +210,7 @@ async def _drive_external(args, engine, st, leaders_group, port, srv, llm):
         if not ready.get("ready"):
             raise RuntimeError(f"load generator failed to start: {ready}")
         dev = engine.device
-        if dist.is_initialized():
+        if dist.is_initialized() and leaders_group is not None:
             dist.barrier(group=leaders_group)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
@@ -210,7 +220,7 @@ async def _drive_external(args, engine, st, leaders_group, port, srv, llm):
         res = json.loads((await proc.stdout.readline()) or b"{}")
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
-        if dist.is_initialized():
+        if dist.is_initialized() and leaders_group is not None:
             dist.barrier(group=leaders_group)
         elapsed = time.perf_counter() - t0
         if "tokens" not in res:
@@ -225,7 +235,7 @@ async def _drive_external(args, engine, st, leaders_group, port, srv, llm):
                 await asyncio.wait_for(proc.wait(), 30)
             except asyncio.TimeoutError:
                 proc.kill()
-    if engine.lockstep:  # DP attention + EP: leave the lockstep loop together with the other ranks
+    if stop_after:  # DP attention + EP lockstep / gateway engine servers: stop with the other ranks
         await asyncio.get_running_loop().run_in_executor(None, llm.shutdown)
     return res["tokens"], elapsed, res["lats"]
 
@@ -254,7 +264,18 @@ def main(argv=None) -> int:
     init_s = time.perf_counter() - t_init
     leaders = list(range(0, st.world_size, st.tp_size))
     leaders_group = dist.new_group(leaders) if dist.is_initialized() else None
-    if st.tp_rank != 0:
+    gateway = args.frontend == "gateway" and st.world_size > 1 and st.tp_size == 1 and not engine.lockstep
+    if gateway:
+        from polykey_service_amd.engine.async_llm import AsyncLLM
+        from polykey_service_amd.engine.remote import dp_gateway
+        local = AsyncLLM(engine)
+        pool = dp_gateway(local, st)  # ranks > 0 serve their engine until rank 0 stops them
+        if pool is None:
+            local.shutdown()
+            tokens, elapsed, lats = 0, 0.0, []
+        else:
+            tokens, elapsed, lats = asyncio.run(run_waves(args, engine, st, None, llm=pool, n_replicas=st.world_size))
+    elif st.tp_rank != 0:
         engine.runner.worker_loop()
         tokens, elapsed, lats = 0, 0.0, []
     else:
@@ -295,7 +316,8 @@ def main(argv=None) -> int:
                 "output_len": args.max_tokens,
                 "parallelism": (f"tp{st.tp_size}" + (f"_dp{st.dp_size}" if st.dp_size > 1 else "")
                                 + (f"_ep{st.ep_size}" if st.ep_size > 1 else "")) if st.tp_size > 1
-                else f"dp{st.world_size}" + (f"_ep{st.ep_size}_a2a" if st.ep_size > 1 else ""),
+                else f"dp{st.world_size}" + (f"_ep{st.ep_size}_a2a" if st.ep_size > 1 else "")
+                + ("_gateway" if gateway else ""),
                 "concurrency_per_replica": args.concurrency,
                 "rpc": f"ExecuteTool ({args.mode})",
                 "clients": "load-generator process" if args.client == "process" else "server event loop",

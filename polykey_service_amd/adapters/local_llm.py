@@ -127,7 +127,9 @@ class LLMTool:
         toks: List[int] = []
         last = None
         text = ""
-        async for out in self.llm.generate(prompt, sp, request_id=ctx.request_id):
+        # without stop strings a unary call needs only the final result: a remote engine
+        # (engine/remote.py) then reports the request once instead of once per step
+        async for out in self.llm.generate(prompt, sp, request_id=ctx.request_id, final_only=not sp.stop):
             toks.extend(out.new_token_ids)
             last = out
             if sp.stop:
@@ -184,9 +186,12 @@ class LLMTool:
 
 
 class ReplicaPool:
-    """Request-level data parallelism inside one server process (SURVEY.md §2.3 "DP"):
-    one engine per GPU (each on its own thread and HIP device), every request goes to the
-    replica with the fewest unfinished sequences.  Duck-types :class:`AsyncLLM`."""
+    """Request-level data parallelism behind one front end (SURVEY.md §2.3 "DP"): every
+    request goes to the replica with the fewest unfinished requests.  Replicas are in-process
+    :class:`AsyncLLM` engines (one thread and HIP device each) or
+    :class:`~polykey_service_amd.engine.remote.RemoteEngine` handles of engine processes (one
+    rank per GPU: :func:`~polykey_service_amd.engine.remote.dp_gateway`); the first replica must
+    be local.  Duck-types :class:`AsyncLLM`."""
 
     def __init__(self, replicas):
         self.replicas = list(replicas)
@@ -196,10 +201,13 @@ class ReplicaPool:
         self.watchdog_s = 0.0
 
     def _pick(self):
-        return min(self.replicas, key=lambda r: r.engine.scheduler.num_unfinished() + len(r._cmds))
+        return min(self.replicas, key=lambda r: r.load())
 
-    def generate(self, prompt_ids, params, request_id=None):
-        return self._pick().generate(prompt_ids, params, request_id)
+    def load(self) -> int:
+        return sum(r.load() for r in self.replicas)
+
+    def generate(self, prompt_ids, params, request_id=None, final_only=False):
+        return self._pick().generate(prompt_ids, params, request_id, final_only=final_only)
 
     async def generate_all(self, prompt_ids, params, request_id=None):
         return await self._pick().generate_all(prompt_ids, params, request_id)
@@ -222,13 +230,16 @@ class ReplicaPool:
             await r.aclose()
 
 
-def attach_local_llm(router, cfg, logger, engine=None):
-    """Build (or reuse) the engine for ``cfg.model`` and register its tools."""
+def attach_local_llm(router, cfg, logger, engine=None, llm=None):
+    """Build (or reuse) the engine for ``cfg.model`` and register its tools (``llm``: an already
+    built AsyncLLM / ReplicaPool over ``engine``)."""
     from ..engine.async_llm import AsyncLLM
     from ..engine.llm_engine import EngineConfig, LLMEngine
     from ..parallel.state import init_parallel
 
-    if engine is None and getattr(cfg, "replicas", 1) > 1 and cfg.tp == 1:
+    if llm is not None:
+        pass
+    elif engine is None and getattr(cfg, "replicas", 1) > 1 and cfg.tp == 1:
         import dataclasses as _dc
 
         import torch
@@ -243,13 +254,24 @@ def attach_local_llm(router, cfg, logger, engine=None):
         llm = ReplicaPool([AsyncLLM(e) for e in engines])
         engine = engines[0]
     else:
-        if engine is None:
+        built = engine is None
+        if built:
             st = init_parallel(tp=cfg.tp, ep=cfg.ep)
             engine = LLMEngine(EngineConfig.from_server_config(cfg), st)
             if st.tp_rank != 0:
                 engine.runner.worker_loop()  # never returns until the leader stops
                 raise SystemExit(0)
         llm = AsyncLLM(engine)
+        st = engine.st
+        if built and st.world_size > 1 and st.tp_size == 1 and not engine.lockstep:
+            # DP under torchrun (one engine per GPU rank): ONE front end on rank 0 routes to every
+            # rank's engine process; the other ranks serve their engine until it stops them
+            from ..engine.remote import dp_gateway
+            pool = dp_gateway(llm, st)
+            if pool is None:
+                llm.shutdown()
+                raise SystemExit(0)
+            llm = pool
     name = cfg.model if isinstance(cfg.model, str) else "model"
     router.register_model_tool("llm.generate", name, LLMTool("llm.generate", name, llm, chat=False))
     chat_tool = LLMTool("llm.chat", name, llm, chat=True)

@@ -41,6 +41,10 @@ class AsyncLLM:
         self._cmds: Deque[Tuple[str, object]] = collections.deque()
         self._wake = threading.Event()
         self._streams: Dict[str, Tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
+        # requests submitted by another process's front end (engine/remote.py EngineServer):
+        # their outputs go to the external sink, called on the engine thread once per step
+        self._external: set = set()
+        self._external_sink: Optional[Callable[[list], None]] = None
         self._lock = threading.Lock()
         self._stop = False
         self.dead: Optional[BaseException] = None
@@ -67,8 +71,35 @@ class AsyncLLM:
         self._thread.start()
 
     # ---------------------------------------------------------------- client side
+    def load(self) -> int:
+        """Unfinished + queued requests (the DP router's least-loaded metric)."""
+        return self.engine.scheduler.num_unfinished() + len(self._cmds)
+
+    # ---------------------------------------------------------- remote front end
+    def set_external_sink(self, sink: Optional[Callable[[list], None]]) -> None:
+        self._external_sink = sink
+
+    def submit_external(self, rid: str, prompt_ids: List[int], params: SamplingParams) -> None:
+        if self.dead is not None:
+            sink = self._external_sink
+            if sink is not None:
+                sink([(rid, EngineDeadError(f"engine is dead: {self.dead}"))])
+            return
+        with self._lock:
+            self._external.add(rid)
+            self._cmds.append(("add", (rid, prompt_ids, params)))
+        self._wake.set()
+
+    def abort_external(self, rid: str) -> None:
+        with self._lock:
+            if rid not in self._external:
+                return
+            self._external.discard(rid)
+            self._cmds.append(("abort", rid))
+        self._wake.set()
+
     async def generate(self, prompt_ids: List[int], params: SamplingParams,
-                       request_id: Optional[str] = None) -> AsyncIterator[RequestOutput]:
+                       request_id: Optional[str] = None, final_only: bool = False) -> AsyncIterator[RequestOutput]:
         if self.dead is not None:
             raise EngineDeadError(f"engine is dead: {self.dead}")
         rid = request_id or uuid.uuid4().hex
@@ -176,11 +207,20 @@ class AsyncLLM:
 
     def _deliver(self, items) -> None:
         by_loop: Dict[asyncio.AbstractEventLoop, list] = {}
+        external = []
         with self._lock:
             for rid, item in items:
+                if rid in self._external:
+                    external.append((rid, item))
+                    if isinstance(item, BaseException) or item.finished:
+                        self._external.discard(rid)
+                    continue
                 ent = self._streams.get(rid)
                 if ent is not None:
                     by_loop.setdefault(ent[0], []).append((ent[1], item))
+        sink = self._external_sink
+        if external and sink is not None:
+            sink(external)
         for loop, batch in by_loop.items():
             try:
                 loop.call_soon_threadsafe(_fanout, batch)
@@ -241,7 +281,7 @@ class AsyncLLM:
             self.dead = e
             traceback.print_exc()
             with self._lock:
-                rids = list(self._streams)
+                rids = list(self._streams) + list(self._external)
             self._deliver([(r, EngineDeadError(f"engine loop failed: {e!r}")) for r in rids])
             if self.on_fatal is not None:
                 try:

@@ -13,11 +13,13 @@ ARGS = ["--model", "tiny-llama-gqa4", "--steps", "1", "--warmup", "1", "--concur
         "--max-tokens", "4", "--no-graphs"]
 
 
-@pytest.mark.parametrize("gpus,client", [(1, "process"), (2, "process"), (1, "inproc")])
-def test_bench_json_line(tmp_path, gpus, client):
+@pytest.mark.parametrize("gpus,client,frontend", [(1, "process", "replicas"), (2, "process", "replicas"),
+                                                 (1, "inproc", "replicas"), (2, "inproc", "gateway"),
+                                                 (3, "process", "gateway")])
+def test_bench_json_line(tmp_path, gpus, client, frontend):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--client", client]
-                       + ARGS, cwd=tmp_path,
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--client", client,
+                        "--frontend", frontend] + ARGS, cwd=tmp_path,
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -27,7 +29,8 @@ def test_bench_json_line(tmp_path, gpus, client):
     assert out["n_gpus"] == gpus and out["steps"] == 1 and out["warmup"] == 1
     assert out["value"] > 0 and out["ms_per_step"] > 0 and out["higher_is_better"] is True
     assert out["scaling"] == "weak" and out["dtype"] == "bf16"
-    assert out["config"]["parallelism"] == f"dp{gpus}" and out["config"]["global_batch"] == 4 * gpus
+    gw = "_gateway" if frontend == "gateway" and gpus > 1 else ""
+    assert out["config"]["parallelism"] == f"dp{gpus}{gw}" and out["config"]["global_batch"] == 4 * gpus
     assert out["config"]["clients"] == ("load-generator process" if client == "process" else "server event loop")
     # unique random prompts: the prefix cache serves nothing, so no prefill work is skipped
     assert out["config"]["prefix_caching"] is True and out["config"]["prefix_cache_hit_tokens"] == 0
