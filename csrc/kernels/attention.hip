@@ -597,7 +597,208 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
   }
 }
 
-int g_prefill_lds = 1;  // pk_set_prefill_impl: 1 = LDS-tiled kernel where it applies, 0 = per-wave kernel
+// ------------------------------------------- prefill on 32x32x16 MFMAs, P kept in registers
+// One wave owns 32 queries of one head against 64-key steps (guide Appendix B "Fused attention
+// prefill" structure):
+//   X_t = S^T (32 keys x 32 queries) = K_t . Q^T     (A = K rows, B = Q^T; 8 MFMAs per key tile t)
+//   softmax per query = per lane column: 16 keys in the lane's registers x 2 tiles, the other
+//   32 keys of the step in lane l ^ 32 (one permlane32_swap for the max)
+//   O^T (128 d x 32 queries) += V^T . P^T           (A = V^T rows, B = X_t converted to bf16)
+// The accumulator of the first product is the B operand of the second with no lane movement
+// (guide §3 "An accumulator tile as the next MFMA's operand"): registers 8s..8s+7 of X_t are
+// the k-step s fragment, whose element j of lane half h is X row 16s + 8(j>>2) + 4h + (j&3).
+// The K rows of the QK^T A operand are read with bits 2 and 3 of the key index swapped, so
+// X row rho holds key swap23(rho) and that permuted k order becomes the NATURAL key order
+// 16s + 8h + j -- V^T fragments are then plain 16-byte reads of 8 consecutive keys.
+// Per 64-key step and wave: 32 MFMAs of 32x32x16 against 32 KiB of LDS fragment reads (half the
+// bytes per FLOP of paged_prefill_lds_kernel) and 32 exp2 per lane.
+// Workgroup: 8 waves = G heads of the kv head's GQA group x (8 / G) 32-query groups; K / V
+// tiles staged through LDS (register staged, double buffered, one barrier per step).
+constexpr int kKS = 64;            // keys per step
+constexpr int kKRow32 = kHD + 8;   // K_s row (bf16): 272 B, 16 rows on distinct bank groups
+constexpr int kVRow32 = kKS + 8;   // V_s row (bf16): 144 B
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ int swap23(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
+
+template <int G>
+__global__ void __launch_bounds__(512) paged_prefill_mfma32_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
+    const int* __restrict__ cu_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride, float scale2) {
+  __shared__ __attribute__((aligned(16))) bf16_t K_s[2][kKS][kKRow32];
+  __shared__ __attribute__((aligned(16))) bf16_t V_s[2][kHD][kVRow32];
+  constexpr int kQG = 8 / G;           // 32-query groups per workgroup
+  constexpr int kPQ = 32 * kQG;        // queries per workgroup
+  const int qb = gridDim.x - 1 - blockIdx.x, seq = blockIdx.y, h = blockIdx.z;  // heaviest blocks first
+  const int q0 = cu_q[seq], L = cu_q[seq + 1] - q0;
+  if (qb * kPQ >= L) return;
+  const int ctx = context_lens[seq];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int hq = h * G + w % G;
+  const int qi = qb * kPQ + (w / G) * 32 + r;  // this lane's query (column of X and O^T)
+  const bool valid = qi < L;
+  const int qpos = valid ? ctx - L + qi : -1;
+  const int last_q = min(L - 1, qb * kPQ + kPQ - 1);
+  const int k_end = min(ctx, ctx - L + last_q + 1);
+  const int nsteps = (k_end + kKS - 1) / kKS;
+  const int wave_last_q = min(L - 1, qb * kPQ + (w / G) * 32 + 31);
+  const int wave_steps = (min(ctx, ctx - L + wave_last_q + 1) + kKS - 1) / kKS;
+  const int wave_first_pos = ctx - L + qb * kPQ + (w / G) * 32;  // position of the wave's first query
+  const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
+  const bf16_t* kch = kc + static_cast<int64_t>(h) * bs * kHD;
+  const bf16_t* vch = vc + static_cast<int64_t>(h) * kHD * bs;
+  const int* bt = block_tables + static_cast<int64_t>(seq) * max_blocks;
+
+  // ---- staging: per step 1024 K granules (16 B = 8 dims of one key) and 1024 V^T granules
+  // (8 keys of one channel); thread tid stages granules tid and tid + 512 of each
+  u32x4 ks[2], vs[2];
+  auto load_tile = [&](int step) {
+    const int s0 = min(step, nsteps - 1) * kKS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      // K: 32-token fragment-native tile t2 = i (keys s0 + 32 i ..), piece p = tid (common.h kcache_off)
+      const int tok = min(s0 + 32 * i, ((k_end - 1) >> 5) << 5);
+      const int64_t kb = static_cast<int64_t>(bt[tok / bs]) * blk_stride + (tok % bs) * kHD;
+      ks[i] = *reinterpret_cast<const u32x4*>(kch + kb + tid * 8);
+      // V^T: channel d = tid >> 2, keys 8 (tid & 3) of the same 32-token tile
+      const int64_t vb = static_cast<int64_t>(bt[tok / bs]) * blk_stride;
+      vs[i] = *reinterpret_cast<const u32x4*>(vch + vb + (tid >> 2) * bs + tok % bs + 8 * (tid & 3));
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      // invert kcache_off for piece p = tid: lane' = p & 63, (t, kk) = p >> 6
+      const int pl = tid & 63, tk = tid >> 6;
+      const int key = 32 * i + 8 * ((pl >> 2) & 3) + 4 * (tk >> 2) + (pl & 3);
+      const int d = 32 * (pl >> 4) + 8 * (tk & 3);
+      *reinterpret_cast<u32x4*>(&K_s[buf][key][d]) = ks[i];
+      *reinterpret_cast<u32x4*>(&V_s[buf][tid >> 2][32 * i + 8 * (tid & 3)]) = vs[i];
+    }
+  };
+
+  // Q^T B-fragments: k-step kk (dims 16 kk + 8 hh .. +8) of query qi
+  bf16x8_t qf[8];
+  {
+    const bf16_t* qp = q + static_cast<int64_t>(q0 + (valid ? qi : 0)) * q_stride + hq * kHD + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) qf[kk] = valid ? ld8(qp + 16 * kk) : zero8();
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  float m_run = kNegBig, l_run = 0.f;
+  const int krow = swap23(r);
+
+  auto compute = [&](int step, int buf) {
+    if (step >= wave_steps) return;
+    const int s0 = step * kKS;
+    // ---- X_t = S^T for the two 32-key tiles
+    f32x16 x[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[t][i] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(&K_s[buf][32 * t + krow][16 * kk + 8 * hh]);
+        x[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], x[t], 0, 0, 0);
+      }
+    }
+    // ---- online softmax over the lane's 32 keys (+ the other half in lane ^ 32).  The max is
+    // taken on raw scores (scale2 > 0) and the scale folded into the exponent's FMA; keys are
+    // masked only on steps that reach past the wave's first query or the context end.
+    float mx = kNegBig;
+    if (s0 + kKS - 1 > wave_first_pos || s0 + kKS > ctx) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = s0 + 32 * t + (i & 7) + 8 * hh + 16 * (i >> 3);  // swap23 of X row
+          const bool ok = key < ctx && key <= qpos;
+          x[t][i] = ok ? x[t][i] : -INFINITY;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, x[t][i]);
+    {
+      auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+    }
+    const float m_new = fmaxf(m_run, mx * scale2);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    const bool rescale = __any(m_new != m_run);  // wave-uniform: skip the O^T scaling if no max moved
+    m_run = m_new;
+    float psum = 0.f;
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float p[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          p[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[t][8 * s2 + j], scale2, -m_new));
+          psum += p[j];
+        }
+        pf[t][s2] = pack_p(p);
+      }
+    l_run = l_run * alpha + psum;
+    // ---- O^T += V^T . P^T
+    if (rescale) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8_t vf =
+              *reinterpret_cast<const bf16x8_t*>(&V_s[buf][32 * dt + r][32 * t + 16 * s2 + 8 * hh]);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][s2], o[dt], 0, 0, 0);
+        }
+    }
+  };
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int buf = step & 1;
+    load_tile(step + 1);  // the next step's global loads fly during this step's math
+    compute(step, buf);
+    store_tile(buf ^ 1);  // every wave finished reading buf ^ 1 before the previous barrier
+    __syncthreads();
+  }
+  // ---- O = O^T / l: lane holds query qi, dims dt*32 + (i&3) + 8 (i>>2) + 4 hh
+  {
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
+    l_run = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  }
+  if (!valid) return;
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  bf16_t* op = out + static_cast<int64_t>(q0 + qi) * out_stride + hq * kHD + 4 * hh;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      uint2 v;
+      v.x = pack2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+      v.y = pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+      *reinterpret_cast<uint2*>(op + 32 * dt + 8 * g4) = v;
+    }
+}
+
+int g_prefill_lds = 2;  // pk_set_prefill_impl: 2 = 32x32-MFMA kernel (default), 1 = LDS-tiled 16x16 kernel, 0 = per-wave kernel
 
 #ifndef PK_DECODE_PART
 #define PK_DECODE_PART 512  // keys per decode partition (ops/attention.py _PART must match)
@@ -674,7 +875,8 @@ PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, 
 }
 
 PK_EXPORT int pk_set_prefill_impl(int lds) {
-  g_prefill_lds = lds != 0;
+  if (lds < 0 || lds > 2) return -1;
+  g_prefill_lds = lds;
   return 0;
 }
 
@@ -691,6 +893,19 @@ PK_EXPORT int pk_paged_prefill(void* out, const void* q, const void* k_cache, co
   if (n_seqs <= 0 || max_q_len <= 0) return 0;
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0) return -1;  // K tiles: 32 keys
   const int G = n_q / n_kv;
+  if (g_prefill_lds == 2 && (G == 1 || G == 2 || G == 4 || G == 8)) {
+    const int pq = 32 * 8 / G;  // queries per workgroup (8 waves: G heads x 8/G 32-query groups)
+    const dim3 grid((max_q_len + pq - 1) / pq, n_seqs, n_kv);
+#define PK_PREFILL_M32(GG)                                                                                       paged_prefill_mfma32_kernel<GG><<<grid, 512, 0, stream>>>(                                                         static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),                static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables),                                    static_cast<const int*>(context_lens), static_cast<const int*>(cu_q), n_kv, bs, max_blocks, q_stride,          out_stride, scale * kLog2e)
+    switch (G) {
+      case 1: PK_PREFILL_M32(1); break;
+      case 2: PK_PREFILL_M32(2); break;
+      case 4: PK_PREFILL_M32(4); break;
+      default: PK_PREFILL_M32(8); break;
+    }
+#undef PK_PREFILL_M32
+    return PK_CHECK_LAUNCH();
+  }
   if (g_prefill_lds && (G == 1 || G == 2 || G == 4 || G == 8)) {
     // 16-query column tiles per workgroup: 4 (64 queries: more waves share each K/V tile) for
     // G <= 4 and prompts < 2K; 2 otherwise (the 1024-thread cap; long causal prompts balance

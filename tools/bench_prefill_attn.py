@@ -27,7 +27,7 @@ for n_seqs, qlen, prefix in ((32, 256, 0), (8, 1024, 0), (2, 4096, 0), (16, 256,
     flops = 4.0 * D * keys * NQ
     row = f"{n_seqs:3d} seqs x {qlen:5d} q (+{prefix} cached):"
     outs = {}
-    for impl in (0, 1):
+    for impl in (0, 1, 2):
         native.lib().pk_set_prefill_impl(impl)
         for _ in range(3):
             outs[impl] = A.paged_attention(q, kc, vc, md, 0.088)
@@ -39,7 +39,7 @@ for n_seqs, qlen, prefix in ((32, 256, 0), (8, 1024, 0), (2, 4096, 0), (16, 256,
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 10 * 1000
-        row += f" | {['per-wave', 'lds'][impl]} {us:8.1f} us {flops / us / 1e6:6.0f} TF/s"
-    diff = max((outs[0].float() - outs[i].float()).abs().max().item() for i in (1,))
+        row += f" | {['per-wave', 'lds', 'mfma32'][impl]} {us:8.1f} us {flops / us / 1e6:6.0f} TF/s"
+    diff = max((outs[0].float() - outs[i].float()).abs().max().item() for i in (1, 2))
     print(row + f" | max|diff| {diff:.3g}", flush=True)
-native.lib().pk_set_prefill_impl(1)
+native.lib().pk_set_prefill_impl(2)
