@@ -622,16 +622,20 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 __device__ __forceinline__ int swap23(int r) { return (r & ~12) | ((r & 4) << 1) | ((r & 8) >> 1); }
 
-template <int G>
-__global__ void __launch_bounds__(512) paged_prefill_mfma32_kernel(
+template <int G, int NW>
+__global__ void __launch_bounds__(64 * NW, 2) paged_prefill_mfma32_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
     const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
     const int* __restrict__ cu_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride, float scale2) {
   __shared__ __attribute__((aligned(16))) bf16_t K_s[2][kKS][kKRow32];
   __shared__ __attribute__((aligned(16))) bf16_t V_s[2][kHD][kVRow32];
-  constexpr int kQG = 8 / G;           // 32-query groups per workgroup
+  static_assert(NW % G == 0, "a workgroup holds whole GQA groups");
+  constexpr int kQG = NW / G;          // 32-query groups per workgroup
+  constexpr int NJ = 1024 / (64 * NW); // K (and V^T) granules staged per thread per step
   constexpr int kPQ = 32 * kQG;        // queries per workgroup
-  const int qb = gridDim.x - 1 - blockIdx.x, seq = blockIdx.y, h = blockIdx.z;  // heaviest blocks first
+  // grid (n_kv, n_seqs, q blocks) with the q block slowest: dispatch order is x fastest, so every
+  // (head, sequence) pair's LAST -- heaviest, causal -- query block is launched first
+  const int qb = gridDim.z - 1 - blockIdx.z, seq = blockIdx.y, h = blockIdx.x;
   const int q0 = cu_q[seq], L = cu_q[seq + 1] - q0;
   if (qb * kPQ >= L) return;
   const int ctx = context_lens[seq];
@@ -654,29 +658,38 @@ __global__ void __launch_bounds__(512) paged_prefill_mfma32_kernel(
 
   // ---- staging: per step 1024 K granules (16 B = 8 dims of one key) and 1024 V^T granules
   // (8 keys of one channel); thread tid stages granules tid and tid + 512 of each
-  u32x4 ks[2], vs[2];
+  // Which granule a lane stages is permuted inside its wave's 1 KiB (loads stay whole lines) so
+  // that the LDS stores -- ds_write_b128 banks over 8 contiguous lanes, (a/4) mod 32
+  // (MI355X_MICROARCH.md §LDS) -- hit 8 distinct 4-bank groups: K piece lane' takes lane bit 2 at
+  // its bit 4 (dims +32: +16 banks) and lane bits 3-4 at its bits 2-3; V^T channel bit 2 comes
+  // from lane bit 2 (+4 rows = +16 banks) and channel bits 0-1 / 3 from lane bits 3-4 / 5.
+  const int kpl = (lane & 3) | (((lane >> 3) & 3) << 2) | (((lane >> 2) & 1) << 4) | (lane & 32);
+  const int vdl = (((lane >> 2) & 1) << 2) | ((lane >> 3) & 3) | (((lane >> 5) & 1) << 3);
+  const int vkg = lane & 3;
+  // granule g = j * 64 NW + tid (j < NJ): 32-token tile g >> 9, wave chunk (g >> 6) & 7 of it
+  u32x4 ks[NJ], vs[NJ];
   auto load_tile = [&](int step) {
     const int s0 = min(step, nsteps - 1) * kKS;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      // K: 32-token fragment-native tile t2 = i (keys s0 + 32 i ..), piece p = tid (common.h kcache_off)
+    for (int j = 0; j < NJ; ++j) {
+      const int g = j * 64 * NW + tid, i = g >> 9, ch = (g >> 6) & 7;
       const int tok = min(s0 + 32 * i, ((k_end - 1) >> 5) << 5);
-      const int64_t kb = static_cast<int64_t>(bt[tok / bs]) * blk_stride + (tok % bs) * kHD;
-      ks[i] = *reinterpret_cast<const u32x4*>(kch + kb + tid * 8);
-      // V^T: channel d = tid >> 2, keys 8 (tid & 3) of the same 32-token tile
-      const int64_t vb = static_cast<int64_t>(bt[tok / bs]) * blk_stride;
-      vs[i] = *reinterpret_cast<const u32x4*>(vch + vb + (tid >> 2) * bs + tok % bs + 8 * (tid & 3));
+      const int64_t base = static_cast<int64_t>(bt[tok / bs]) * blk_stride;
+      // K: fragment-native tile of 32 tokens, piece (ch, kpl) (common.h kcache_off)
+      ks[j] = *reinterpret_cast<const u32x4*>(kch + base + (tok % bs) * kHD + ((ch << 6) | kpl) * 8);
+      // V^T: channel 16 ch + vdl, keys 8 vkg .. of the same 32-token tile
+      vs[j] = *reinterpret_cast<const u32x4*>(vch + base + (16 * ch + vdl) * bs + tok % bs + 8 * vkg);
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      // invert kcache_off for piece p = tid: lane' = p & 63, (t, kk) = p >> 6
-      const int pl = tid & 63, tk = tid >> 6;
-      const int key = 32 * i + 8 * ((pl >> 2) & 3) + 4 * (tk >> 2) + (pl & 3);
-      const int d = 32 * (pl >> 4) + 8 * (tk & 3);
-      *reinterpret_cast<u32x4*>(&K_s[buf][key][d]) = ks[i];
-      *reinterpret_cast<u32x4*>(&V_s[buf][tid >> 2][32 * i + 8 * (tid & 3)]) = vs[i];
+    for (int j = 0; j < NJ; ++j) {
+      const int g = j * 64 * NW + tid, i = g >> 9, ch = (g >> 6) & 7;
+      // invert kcache_off for piece (ch, kpl): lane' = kpl, (t, kk) = ch
+      const int kkey = 8 * ((kpl >> 2) & 3) + 4 * (ch >> 2) + (kpl & 3);
+      const int kd = 32 * (kpl >> 4) + 8 * (ch & 3);
+      *reinterpret_cast<u32x4*>(&K_s[buf][32 * i + kkey][kd]) = ks[j];
+      *reinterpret_cast<u32x4*>(&V_s[buf][16 * ch + vdl][32 * i + 8 * vkg]) = vs[j];
     }
   };
 
@@ -798,6 +811,7 @@ __global__ void __launch_bounds__(512) paged_prefill_mfma32_kernel(
     }
 }
 
+int g_attn_nw = 0;  // waves per 32x32-MFMA prefill workgroup: 0 = default (4; 8 when G = 8), else 4 / 8
 int g_prefill_lds = 2;  // pk_set_prefill_impl: 2 = 32x32-MFMA kernel (default), 1 = LDS-tiled 16x16 kernel, 0 = per-wave kernel
 
 #ifndef PK_DECODE_PART
@@ -874,6 +888,12 @@ PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, 
                        n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
 }
 
+PK_EXPORT int pk_set_attn_waves(int nw) {  // A/B knob: waves per 32x32-MFMA prefill workgroup (0 auto, 4, 8)
+  if (nw != 0 && nw != 4 && nw != 8) return -1;
+  g_attn_nw = nw;
+  return 0;
+}
+
 PK_EXPORT int pk_set_prefill_impl(int lds) {
   if (lds < 0 || lds > 2) return -1;
   g_prefill_lds = lds;
@@ -894,14 +914,26 @@ PK_EXPORT int pk_paged_prefill(void* out, const void* q, const void* k_cache, co
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0) return -1;  // K tiles: 32 keys
   const int G = n_q / n_kv;
   if (g_prefill_lds == 2 && (G == 1 || G == 2 || G == 4 || G == 8)) {
-    const int pq = 32 * 8 / G;  // queries per workgroup (8 waves: G heads x 8/G 32-query groups)
-    const dim3 grid((max_q_len + pq - 1) / pq, n_seqs, n_kv);
-#define PK_PREFILL_M32(GG)                                                                                       paged_prefill_mfma32_kernel<GG><<<grid, 512, 0, stream>>>(                                                         static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),                static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables),                                    static_cast<const int*>(context_lens), static_cast<const int*>(cu_q), n_kv, bs, max_blocks, q_stride,          out_stride, scale * kLog2e)
-    switch (G) {
-      case 1: PK_PREFILL_M32(1); break;
-      case 2: PK_PREFILL_M32(2); break;
-      case 4: PK_PREFILL_M32(4); break;
-      default: PK_PREFILL_M32(8); break;
+    // 4-wave workgroups (two per CU: independent barriers let one workgroup's MFMAs overlap the
+    // other's softmax) where the GQA group fits; G = 8 needs all 8 waves for one query group
+    // (profiles/r2_prefill_attention.txt: 4 waves >= 8 waves at every measured shape)
+    const int nw = G == 8 || g_attn_nw == 8 ? 8 : 4;
+    const int pq = 32 * nw / G;  // queries per workgroup (nw waves: G heads x nw/G 32-query groups)
+    const dim3 grid(n_kv, n_seqs, (max_q_len + pq - 1) / pq);
+#define PK_PREFILL_M32(GG, NWW)                                                                                \
+  paged_prefill_mfma32_kernel<GG, NWW><<<grid, 64 * NWW, 0, stream>>>(                                         \
+      static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),          \
+      static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables),                              \
+      static_cast<const int*>(context_lens), static_cast<const int*>(cu_q), n_kv, bs, max_blocks, q_stride,    \
+      out_stride, scale * kLog2e)
+    switch (G * 16 + nw) {
+      case 1 * 16 + 4: PK_PREFILL_M32(1, 4); break;
+      case 2 * 16 + 4: PK_PREFILL_M32(2, 4); break;
+      case 4 * 16 + 4: PK_PREFILL_M32(4, 4); break;
+      case 1 * 16 + 8: PK_PREFILL_M32(1, 8); break;
+      case 2 * 16 + 8: PK_PREFILL_M32(2, 8); break;
+      case 4 * 16 + 8: PK_PREFILL_M32(4, 8); break;
+      default: PK_PREFILL_M32(8, 8); break;
     }
 #undef PK_PREFILL_M32
     return PK_CHECK_LAUNCH();
