@@ -262,6 +262,12 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_kernel(const Prefill
 // phase p is retired by the vmcnt(2) at the R of phase p + 2 and read from phase p + 3 on; its
 // LDS slot was last read in phase p - 2 or earlier (both checked for all four pieces), so two
 // LDS buffers suffice and the loads of ~1.5 phases stay in flight across the barriers.
+// PW: W is block-packed (ops/gemm.py pack_weight, the decode GEMM's layout): per 128-row
+// n-block and 128-deep k-step, 32 row-tile x k-block fragments of 1 KiB in MFMA lane order.  A
+// 64-deep half of a k-step is 16 such fragments; they are copied linearly into the W piece
+// (fragment f = 2 tile + k-block at f KiB) and every W fragment read is one lane-linear 16-byte
+// ds_read -- conflict-free without a swizzle.  So one weight layout serves decode and prefill.
+template <bool PW>
 __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_pp_kernel(const PrefillGemmArgs args) {
   constexpr int BK = 64, kChunks = 8, kPiece = 128 * BK, kStage = 4 * kPiece, kSwz = 1;
   constexpr int kRowsPerInstr = kThreads / kChunks;  // 64
@@ -282,14 +288,20 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_pp_kernel(const Pref
       if (p < 2) {
         const int m = min(tl.m0 + p * 128 + row, tl.rows - 1);
         src[p][j] = args.A + static_cast<long long>(tl.row0 + m) * args.lda + logical * 8;
+      } else if constexpr (PW) {
+        const int f = j * 8 + w;  // fragment of the 64-deep half: row tile f >> 1, k-block f & 1
+        src[p][j] = tl.W + static_cast<long long>((tl.n0 >> 7) + (p - 2)) * 128 * K + ((f >> 1) * 4 + (f & 1)) * 512 +
+                    lane * 8;
       } else {
         src[p][j] = tl.W + static_cast<long long>(tl.n0 + (p - 2) * 128 + row) * K + logical * 8;
       }
     }
   auto stage_piece = [&](int p, int kt) {
     bf16_t* base = lds + (kt & 1) * kStage + p * kPiece + w * 64 * 8;
-    glds16(src[p][0] + kt * BK, base);
-    glds16(src[p][1] + kt * BK, base + kRowsPerInstr * BK);
+    // packed W: k-step kt >> 1 (128 x 128 block of 16384 elements), half kt & 1 (k-blocks 2, 3)
+    const long long off = PW && p >= 2 ? (kt >> 1) * 16384LL + (kt & 1) * 1024 : static_cast<long long>(kt) * BK;
+    glds16(src[p][0] + off, base);
+    glds16(src[p][1] + off, base + kRowsPerInstr * BK);
   };
 
   const int wr = w >> 2, wc = w & 3;
@@ -337,7 +349,9 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_pp_kernel(const Pref
         for (int nf = 0; nf < 2; ++nf)
 #pragma unroll
           for (int s = 0; s < 2; ++s)
-            wf[nf][s] = *reinterpret_cast<const bf16x8_t*>(base + frag(2 + kWh[q], wc * 32 + nf * 16 + r, s));
+            wf[nf][s] = *reinterpret_cast<const bf16x8_t*>(
+                base + (PW ? (2 + kWh[q]) * kPiece + ((wc * 2 + nf) * 2 + s) * 512 + lane * 8
+                           : frag(2 + kWh[q], wc * 32 + nf * 16 + r, s)));
       }
       if (more) stage_piece(kStagePiece[q], kt + 1);
       barrier();
@@ -393,7 +407,8 @@ int launch(const PrefillGemmArgs& a, int variant, hipStream_t stream) {
   switch (variant) {
     case 0: prefill_gemm_kernel<64, 2><<<grid, kThreads, 0, stream>>>(a); break;
     case 1: prefill_gemm_kernel<32, 4><<<grid, kThreads, 0, stream>>>(a); break;
-    case 2: prefill_gemm_pp_kernel<<<grid, kThreads, 0, stream>>>(a); break;
+    case 2: prefill_gemm_pp_kernel<false><<<grid, kThreads, 0, stream>>>(a); break;
+    case 3: prefill_gemm_pp_kernel<true><<<grid, kThreads, 0, stream>>>(a); break;  // block-packed W
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
@@ -401,11 +416,13 @@ int launch(const PrefillGemmArgs& a, int variant, hipStream_t stream) {
 
 }  // namespace
 
-// variant: 0 = BK 64 x 2 stages, 1 = BK 32 x 4 stages, 2 = ping-pong quadrant phases (BK 64).  Requires N % 256 == 0, K % 64 == 0,
+// variant: 0 = BK 64 x 2 stages, 1 = BK 32 x 4 stages, 2 = ping-pong quadrant phases (BK 64),
+// 3 = variant 2 reading block-packed W (K % 128 == 0).  Requires N % 256 == 0, K % 64 == 0,
 // 16-byte aligned rows (lda % 8 == 0, K % 8 == 0, ldc % 4 == 0).
 PK_EXPORT int pk_prefill_gemm(const PrefillGemmArgs* a, int variant, hipStream_t stream) {
   if (a->M <= 0 || a->tiles_m <= 0) return 0;
   if (a->N % kBN || a->K % 64 || a->lda % 8 || a->ldc % 4) return -1;
+  if (variant == 3 && a->K % 128) return -1;
   if (a->row_offsets != nullptr && a->groups <= 0) return -1;
   if (a->row_offsets == nullptr && a->tiles_m != (a->M + kBM - 1) / kBM) return -1;
   return launch(*a, variant, stream);

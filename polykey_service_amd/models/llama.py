@@ -83,7 +83,8 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
             return gemm.linear_partial(x, w, ws, S, packed=wp)
     if x.shape[0] > gemm.SKINNY_MAX_M:
         # prefill: the all-reduce of one row chunk overlaps the GEMM of the next
-        return comm.tp_row_parallel_overlapped(x, w.shape[0], lambda rows, out: gemm.linear(rows, w, out=out))
+        return comm.tp_row_parallel_overlapped(x, w.shape[0],
+                                               lambda rows, out: gemm.linear(rows, w, out=out, packed=wp))
     return comm.tp_all_reduce(_proj(x, w, ws, wp))
 
 
@@ -529,31 +530,58 @@ class LlamaForCausalLM(nn.Module):
         """Give every dense projection and the LM head a block-packed copy
         (:func:`gemm.pack_weight`) for the decode GEMM, which streams it faster than row-major
         (tools/bench_gemm.py, tools/gemm_lab.hip).  Prefill keeps using the row-major weight
-        through hipBLASLt, so this doubles projection memory: ``auto`` packs only when both
-        copies fit in 75 % of HBM (8B: +16 GB of 288 GB; Mixtral-8x7B: +90 GB; 70B on one GPU:
-        skipped).  ``POLYKEY_PACKED_WEIGHTS`` = auto | 1 | 0."""
+        through hipBLASLt, so this doubles projection memory: ``auto`` packs when both copies fit
+        in 75 % of HBM (8B: +16 GB of 288 GB; Mixtral-8x7B: +90 GB).  When they do not (70B on
+        one GPU) the projections are kept ONLY packed: prefill then reads the same layout through
+        the hand-written MFMA GEMM (``csrc/kernels/gemm_prefill.hip`` variant 3) and the
+        row-major attributes become shape-only (meta) placeholders.
+        ``POLYKEY_PACKED_WEIGHTS`` = auto | 1 (both copies) | packed (packed only) | 0."""
         mode = mode or os.environ.get("POLYKEY_PACKED_WEIGHTS", "auto")
         if mode == "0" or self.device.type != "cuda" or not gemm.SKINNY_ENABLED:
             return False
         head_bytes = self.lm_head.numel() * self.lm_head.element_size()
+        packed_only = mode == "packed"
         if mode == "auto":
             total = torch.cuda.get_device_properties(self.device).total_memory
             proj = sum(w.numel() * w.element_size() for w in self.layers.parameters())
             if 2 * proj + 2 * head_bytes > 0.75 * total:
-                return False
-        fold = FOLD_NORM and self.st.tp_size == 1 and isinstance(self.layers[0].mlp, LlamaMLP)
+                packed_only = True
+        if packed_only and not self._packed_prefill_ok():
+            return False
+        fold = FOLD_NORM and self.st.tp_size == 1 and isinstance(self.layers[0].mlp, LlamaMLP) and not packed_only
+
+        def pack(owner, name: str, dst: str, w: Optional[torch.Tensor] = None) -> None:
+            src = getattr(owner, name)
+            setattr(owner, dst, gemm.pack_weight(src if w is None else w))
+            if packed_only:  # free the row-major copy now: peak memory is one projection over
+                setattr(owner, name, _p(torch.empty(src.shape, dtype=src.dtype, device="meta")))
+
         for layer in self.layers:
             if fold:
                 layer.attn.qkv_pf = gemm.pack_weight(gemm.fold_norm(layer.attn.qkv, layer.ln1))
                 layer.mlp.gate_up_pf = gemm.pack_weight(gemm.fold_norm(layer.mlp.gate_up, layer.ln2))
                 layer.mlp.down_p = gemm.pack_weight(layer.mlp.down)
             else:
-                layer.attn.qkv_p = gemm.pack_weight(layer.attn.qkv)
-                self._pack_mlp(layer.mlp)
-            layer.attn.o_p = gemm.pack_weight(layer.attn.o)
+                pack(layer.attn, "qkv", "qkv_p")
+                if isinstance(layer.mlp, LlamaMLP):
+                    pack(layer.mlp, "gate_up", "gate_up_p")
+                    pack(layer.mlp, "down", "down_p")
+                else:
+                    self._pack_mlp(layer.mlp)
+            pack(layer.attn, "o", "o_p")
         if self.lm_head.shape[0] % 128 == 0 and self.lm_head.shape[1] % 256 == 0:
             self.lm_head_p = gemm.pack_weight(self.lm_head)
+        self.packed_only = packed_only
         return True
+
+    def _packed_prefill_ok(self) -> bool:
+        """Every dense projection is a shape the packed-W prefill GEMM tiles (TP = 1, Llama MLP)."""
+        from ..ops import gemm_prefill
+        l0 = self.layers[0]
+        if self.st.tp_size != 1 or not isinstance(l0.mlp, LlamaMLP):
+            return False
+        return all(gemm_prefill.supported(w.shape[0], w.shape[1]) and w.shape[1] % 128 == 0
+                   for w in (l0.attn.qkv, l0.attn.o, l0.mlp.gate_up, l0.mlp.down))
 
     def _pack_mlp(self, mlp) -> None:
         mlp.gate_up_p = gemm.pack_weight(mlp.gate_up)

@@ -274,6 +274,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
            packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bf16 out [M, N]; ``packed`` = :func:`pack_weight` (w) streamed instead of ``w`` when given."""
     if not skinny_ok(x, w):
+        if w.is_meta:  # packed-only weights (LlamaForCausalLM.pack_decode_weights): prefill on them
+            from . import gemm_prefill
+            return gemm_prefill.linear(x, w, out=out, packed=packed)
         # torch.mm into a preallocated output: hipBLASLt picks a faster kernel for the 8B QKV
         # prefill shape than through F.linear (288 vs 344 us at 8192 rows; the other
         # projections are equal: profiles/r2_prefill_gemm_lab.txt)
@@ -323,6 +326,9 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         _launch_ex(MODE_SILU, x, w_gu_interleaved, packed, 1, out=out, norm=norm, rowscale=rowscale)
         return out
     if not skinny_ok(x, w_gu_interleaved):
+        if w_gu_interleaved.is_meta:  # packed-only weights: fused SiLU in the prefill GEMM epilogue
+            from . import gemm_prefill
+            return gemm_prefill.linear(x, w_gu_interleaved, packed=packed, silu=True)
         return silu_and_mul_interleaved(linear(x, w_gu_interleaved))
     M, K = x.shape
     N = w_gu_interleaved.shape[0]

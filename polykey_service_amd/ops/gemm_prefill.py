@@ -65,13 +65,21 @@ def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
     return y.to(x.dtype)
 
 
+PACKED_VARIANT = 3  # ping-pong kernel reading the decode GEMM's block-packed W
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, silu: bool = False,
-           variant: Optional[int] = None) -> torch.Tensor:
-    """x [M, K] @ w[N, K]^T -> [M, N] (SiLU: [M, N/2]), optionally into ``out``."""
+           variant: Optional[int] = None, packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [M, K] @ w[N, K]^T -> [M, N] (SiLU: [M, N/2]), optionally into ``out``.  ``packed``:
+    :func:`~polykey_service_amd.ops.gemm.pack_weight` of ``w`` is read instead (``w`` then only
+    gives the shape: a model holding only the packed copy passes a placeholder)."""
     M, K = x.shape
     N = w.shape[0]
     n_out = N // 2 if silu else N
     if not x.is_cuda:
+        if packed is not None:
+            from .gemm import unpack_weight
+            w = unpack_weight(packed)
         y = _ref(x, w, silu)
         if out is None:
             return y
@@ -81,10 +89,14 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
         out = torch.empty((M, n_out), dtype=x.dtype, device=x.device)
     if M == 0:
         return out
-    if not supported(N, K) or x.stride(1) != 1 or not w.is_contiguous() or out.stride(1) != 1:
+    src = packed if packed is not None else w
+    if (not supported(N, K) or x.stride(1) != 1 or not src.is_contiguous() or out.stride(1) != 1
+            or (packed is not None and (K % 128 or tuple(packed.shape) != (N, K)))):
         raise ValueError(f"prefill GEMM: unsupported shape/layout M={M} N={N} K={K}")
+    if packed is not None:
+        variant = PACKED_VARIANT
     a = PrefillGemmArgs()
-    a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), w.data_ptr()
+    a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), src.data_ptr()
     a.M, a.N, a.K, a.lda, a.ldc = M, N, K, x.stride(0), out.stride(0)
     a.groups, a.tiles_m, a.silu = 0, (M + BM - 1) // BM, int(silu)
     _launch(a, variant)

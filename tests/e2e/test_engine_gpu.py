@@ -191,3 +191,30 @@ def test_folded_norm_decode_matches_normalised(monkeypatch):
         with torch.inference_mode():
             outs.append(gpu.forward(ids, pos, md, [(k.clone(), v.clone()) for k, v in kv0]).float())
     torch.testing.assert_close(outs[0], outs[1], atol=0.1, rtol=0.05)
+
+
+def test_packed_only_weights_match_row_major(monkeypatch):
+    """70B-on-one-GPU mode: projections kept ONLY block-packed (row-major attributes become meta
+    placeholders); prefill reads the packed layout through the MFMA prefill GEMM, decode through
+    the skinny GEMM.  Prefill logits match the engine holding row-major weights."""
+    _, ref_model = _models("tiny-llama-gqa4")
+    _, pk_model = _models("tiny-llama-gqa4")
+    prompts = [[1] + list(range(5, 5 + n)) for n in (70, 130, 257)]  # > 64-row prefill GEMMs
+    logits = {}
+    outs = {}
+    for tag, model, mode in (("rowmajor", ref_model, "0"), ("packed", pk_model, "packed")):
+        monkeypatch.setenv("POLYKEY_PACKED_WEIGHTS", mode)
+        e = LLMEngine(EngineConfig(model="tiny-llama-gqa4", max_num_seqs=8, max_num_batched_tokens=512,
+                                   max_model_len=1024, hip_graphs=True, device="cuda"),
+                      ParallelState(device=torch.device("cuda")), model=model)
+        e.runner.keep_logits = True
+        for p in prompts:
+            e.add_request(p, SamplingParams(max_tokens=5))
+        e.step()  # one prefill step of all three prompts
+        logits[tag] = e.runner.last_logits.float().cpu().clone()
+        while e.has_unfinished():
+            e.step()
+        outs[tag] = e
+    assert pk_model.packed_only and pk_model.layers[0].attn.qkv.is_meta and pk_model.layers[0].mlp.down.is_meta
+    assert pk_model.layers[0].attn.qkv_p is not None and not getattr(ref_model, "packed_only", False)
+    torch.testing.assert_close(logits["packed"], logits["rowmajor"], atol=5e-2, rtol=5e-2)

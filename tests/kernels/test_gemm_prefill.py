@@ -76,6 +76,19 @@ def test_repeatable_bitwise(variant):
     torch.testing.assert_close(ys[0].float(), other.float(), atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("M,N,K,silu", [(300, 512, 4096, False), (4100, 1280, 8192, False), (513, 1024, 4096, True)])
+def test_block_packed_weights(M, N, K, silu):
+    """The decode GEMM's block-packed layout read directly (variant 3): same result as the
+    row-major weight through the row-major kernel."""
+    x, w = rnd(M, K), rnd(N, K, scale=0.02)
+    wp = gemm.pack_weight(w)
+    y = gemm_prefill.linear(x, torch.empty(N, K, dtype=torch.bfloat16, device="meta"), packed=wp, silu=silu)
+    ref = gemm_prefill.linear(x, w, silu=silu, variant=2)
+    torch.testing.assert_close(y.float(), ref.float(), atol=1e-2, rtol=1e-2)
+    if not silu:
+        torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+
+
 def test_native_library_has_prefill_gemm():
     from polykey_service_amd.ops import native
     assert native.has("pk_prefill_gemm")
