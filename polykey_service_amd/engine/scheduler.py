@@ -185,17 +185,19 @@ class Scheduler:
 
     # ------------------------------------------------------------------ policy
     def _preempt_youngest(self, protect: Sequence) -> Optional[Sequence]:
-        for cand in reversed(self.running):
-            if cand is not protect:
-                self.running.remove(cand)
-                self.bm.free_seq(cand.seq_id)
-                cand.num_computed = 0
-                cand.status = SeqStatus.WAITING
-                cand.num_preemptions += 1
-                self.num_preemptions += 1
-                self.waiting.appendleft(cand)
-                return cand
-        return None
+        """Free the youngest running sequence that is younger than ``protect``; None when
+        ``protect`` is itself the youngest (it then yields instead: an older sequence is never
+        evicted for a younger one, or two that do not fit together evict each other forever)."""
+        if not self.running or self.running[-1] is protect:
+            return None
+        cand = self.running.pop()
+        self.bm.free_seq(cand.seq_id)
+        cand.num_computed = 0
+        cand.status = SeqStatus.WAITING
+        cand.num_preemptions += 1
+        self.num_preemptions += 1
+        self.waiting.appendleft(cand)
+        return cand
 
     def schedule(self) -> ScheduledBatch:
         st = _Step(self.max_num_batched_tokens)

@@ -11,6 +11,8 @@ from __future__ import annotations
 import os
 from typing import Dict, List, Optional
 
+import numpy as np
+
 from .chat_template import LLAMA3, ChatTemplate, load_chat_template
 
 
@@ -28,6 +30,8 @@ class ByteTokenizer:
         return ([self.bos_token_id] if add_bos else []) + ids
 
     def decode(self, ids: List[int], keep_special: bool = False) -> str:
+        if len(ids) >= 32:
+            return self._decode_np(ids)
         out = bytearray()
         for i in ids:
             b = i - self.offset
@@ -37,6 +41,21 @@ class ByteTokenizer:
                 # random-weight models emit ids outside the byte range: render deterministically
                 out.extend(b"\xc2\xb7")  # '·'
         return out.decode("utf-8", errors="replace")
+
+    def _decode_np(self, ids) -> str:
+        """:meth:`decode` in one numpy pass (a 256-token completion: ~10x fewer Python steps
+        on the serving event loop): each id becomes its byte, '·' (2 bytes), or nothing."""
+        a = np.asarray(ids, dtype=np.int64)
+        b = a - self.offset
+        byte = (b >= 0) & (b < 256)
+        special = ~byte & ((a == self.bos_token_id) | (a == self.eos_token_id))
+        out = np.empty((a.size, 2), dtype=np.uint8)
+        out[:, 0], out[:, 1] = 0xC2, 0xB7
+        out[byte, 0] = b[byte]
+        keep = np.ones((a.size, 2), dtype=bool)
+        keep[byte, 1] = False
+        keep[special] = False
+        return out[keep].tobytes().decode("utf-8", errors="replace")
 
     def apply_chat_template(self, messages: List[Dict[str, str]], tools=None) -> str:
         return self.chat_template.render(messages, tools)

@@ -5,6 +5,7 @@ field names map to the reference's Go usage.
 """
 import math
 
+import numpy as np
 from google.protobuf import struct_pb2
 from google.protobuf.json_format import MessageToDict  # noqa: F401  (re-exported for callers)
 
@@ -55,8 +56,29 @@ def _value_to_py(v):
     if kind == "struct_value":
         return {k: _value_to_py(x) for k, x in v.struct_value.fields.items()}
     if kind == "list_value":
-        return _list_to_py(v.list_value.values)
+        nums = _number_list(v.list_value)
+        return nums if nums is not None else _list_to_py(v.list_value.values)
     return None
+
+
+def _number_list(lv):
+    """All-number ListValue (e.g. prompt_token_ids) -> floats straight from its wire bytes:
+    every element serialises as ``0a 09 11 <8-byte little-endian double>`` (field 1 = a 9-byte
+    Value whose field 2 is the double), so one numpy pass replaces a Python call per element
+    (~5x faster for 256 ids).  None when the list holds anything else."""
+    n = len(lv.values)
+    if n < 16:
+        return None
+    data = lv.SerializeToString()
+    if len(data) != 11 * n:
+        return None
+    a = np.frombuffer(data, dtype=np.uint8).reshape(n, 11)
+    if not ((a[:, 0] == 0x0A).all() and (a[:, 1] == 0x09).all() and (a[:, 2] == 0x11).all()):
+        return None
+    x = np.ascontiguousarray(a[:, 3:]).view("<f8").ravel()
+    if not np.isfinite(x).all():
+        raise ValueError("Fail to serialize non-finite Value.number_value")
+    return x.tolist()
 
 
 def _list_to_py(values) -> list:

@@ -15,6 +15,7 @@ import io
 import json
 import sys
 import threading
+import time as _time
 from typing import IO, Any, Optional
 
 DEBUG, INFO, WARN, ERROR = -4, 0, 4, 8
@@ -92,20 +93,28 @@ def parse_go_duration(text: str) -> float:
     return sign * total
 
 
+_SEC_CACHE: list = [None, "", ""]  # whole second -> its "YYYY-MM-DDTHH:MM:SS" and zone suffix
+
+
 def _rfc3339nano(ts: Optional[float] = None) -> str:
-    now = _dt.datetime.now(_dt.timezone.utc).astimezone() if ts is None else \
-        _dt.datetime.fromtimestamp(ts, _dt.timezone.utc).astimezone()
-    off = now.utcoffset() or _dt.timedelta(0)
-    base = now.strftime("%Y-%m-%dT%H:%M:%S")
-    frac = f".{now.microsecond:06d}".rstrip("0").rstrip(".")
-    if off == _dt.timedelta(0):
-        tz = "Z"
-    else:
-        mins = int(off.total_seconds() // 60)
-        sign = "+" if mins >= 0 else "-"
-        mins = abs(mins)
-        tz = f"{sign}{mins // 60:02d}:{mins % 60:02d}"
-    return base + frac + tz
+    """Go's time.RFC3339Nano (trailing zeros of the fraction dropped).  The date/zone part is
+    formatted once per second: every RPC logs three records on the serving event loop."""
+    t = _time.time() if ts is None else ts
+    us = int(round(t * 1e6))
+    sec, micro = divmod(us, 1_000_000)
+    if _SEC_CACHE[0] != sec:
+        now = _dt.datetime.fromtimestamp(sec, _dt.timezone.utc).astimezone()
+        off = now.utcoffset() or _dt.timedelta(0)
+        if off == _dt.timedelta(0):
+            tz = "Z"
+        else:
+            mins = int(off.total_seconds() // 60)
+            sign = "+" if mins >= 0 else "-"
+            mins = abs(mins)
+            tz = f"{sign}{mins // 60:02d}:{mins % 60:02d}"
+        _SEC_CACHE[:] = [sec, now.strftime("%Y-%m-%dT%H:%M:%S"), tz]
+    frac = f".{micro:06d}".rstrip("0").rstrip(".")
+    return _SEC_CACHE[1] + frac + _SEC_CACHE[2]
 
 
 def _jsonable(v: Any) -> Any:

@@ -142,3 +142,22 @@ def test_prefill_first_wave_and_decode_stall_cap():
     assert run("decode_first") == [(2, [100, 98]), (3, [2, 100, 95]), (5, [5])]
     with pytest.raises(ValueError):
         Scheduler(rt.BlockManager(10, 16, 0), policy="fastest")
+
+
+def test_younger_sequence_never_evicts_an_older_one():
+    """Two sequences that cannot both hold their KV (5 + 5 blocks of 9): the younger one must
+    yield to the older, or under prefill-first they preempt each other forever."""
+    reqs = [(51, 4), (46, 5), (50, 8), (33, 10), (30, 9), (41, 5), (18, 4), (2, 2), (40, 12)]
+    bm = rt.BlockManager(9, 8, 0)
+    sch = Scheduler(bm, 6, 19, 512)
+    seqs = []
+    for p, m in reqs:
+        s = mk(p, m)
+        sch.add(s)
+        seqs.append(s)
+    for _ in range(2000):
+        if not sch.has_work():
+            break
+        simulate_step(sch, sch.schedule())
+    assert not sch.has_work() and all(s.is_finished() for s in seqs)
+    assert bm.num_free == 9

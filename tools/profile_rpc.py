@@ -32,7 +32,7 @@ class StubLLM:
     def __init__(self):
         self.tokenizer = get_tokenizer("", 128256, 128000, 128001)
 
-    async def generate(self, prompt_ids, params, request_id=None):
+    async def generate(self, prompt_ids, params, request_id=None, final_only=False):
         yield RequestOutput(request_id or "r", list(range(params.max_tokens)), True, "length", len(prompt_ids),
                             params.max_tokens, {"queue_s": 0.0, "ttft_s": 0.0, "e2e_s": 0.0})
 
