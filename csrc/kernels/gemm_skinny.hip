@@ -671,6 +671,21 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __rest
   bf16_t* res = residual + static_cast<int64_t>(m) * H;
   const int64_t slab = static_cast<int64_t>(M) * H;
   const float* base = partial + static_cast<int64_t>(m) * H;
+  // the norm weight and (ROUTE) the router rows do not depend on the slabs: request them first,
+  // so their round trips overlap the slab loads instead of following the row reduction
+  constexpr int kRouteE = 8;  // router experts per pass (E <= 8: all of them, prefetched)
+  uint2 wpre[PER];
+  uint2 rpre[ROUTE ? PER : 1][ROUTE ? kRouteE : 1];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = 4 * (threadIdx.x + i * blockDim.x);
+    wpre[i] = *reinterpret_cast<const uint2*>(w + c);
+    if constexpr (ROUTE) {
+#pragma unroll
+      for (int e = 0; e < kRouteE; ++e)
+        if (e < ra.E) rpre[i][e] = *reinterpret_cast<const uint2*>(ra.router + static_cast<int64_t>(e) * H + c);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = 4 * (threadIdx.x + i * blockDim.x);
@@ -700,10 +715,11 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __rest
   }
   const float rinv = rsqrtf(block_sum(ss, red) / H + eps);
   bf16_t* xo = x + static_cast<int64_t>(m) * H;
+  float xr[ROUTE ? PER : 1][4];  // the written (bf16-rounded) x values, kept for the router
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = 4 * (threadIdx.x + i * blockDim.x);
-    const uint2 ww = *reinterpret_cast<const uint2*>(w + c);
+    const uint2 ww = wpre[i];
     float y[4];
     y[0] = bf2f(f2bf(v[i][0] * rinv)) * bf2f(static_cast<bf16_t>(ww.x & 0xffff));
     y[1] = bf2f(f2bf(v[i][1] * rinv)) * bf2f(static_cast<bf16_t>(ww.x >> 16));
@@ -713,28 +729,44 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __rest
     o.x = pack2(y[0], y[1]);
     o.y = pack2(y[2], y[3]);
     *reinterpret_cast<uint2*>(xo + c) = o;
+    if constexpr (ROUTE) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xr[i][j] = bf2f(f2bf(y[j]));
+    }
   }
   if constexpr (ROUTE) {
-    // x row is in registers (normalised, bf16-rounded values y of this thread's columns)
+    // router logits from the x row still in registers: kRouteE experts per pass, every router
+    // load of the pass issued together and the kRouteE wave reductions independent of each
+    // other (one expert at a time re-derived x and serialised 8 load + reduce round trips)
     __shared__ float part_s[16][64];
     __shared__ float logit_s[64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int e = 0; e < ra.E; ++e) {
-      float acc = 0.f;
+    for (int e0 = 0; e0 < ra.E; e0 += kRouteE) {
+      float acc[kRouteE];
+#pragma unroll
+      for (int e = 0; e < kRouteE; ++e) acc[e] = 0.f;
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int c = 4 * (threadIdx.x + i * blockDim.x);
-        const uint2 ww = *reinterpret_cast<const uint2*>(w + c);
-        const uint2 rr = *reinterpret_cast<const uint2*>(ra.router + static_cast<int64_t>(e) * H + c);
-        const float y0 = bf2f(f2bf(bf2f(f2bf(v[i][0] * rinv)) * bf2f(static_cast<bf16_t>(ww.x & 0xffff))));
-        const float y1 = bf2f(f2bf(bf2f(f2bf(v[i][1] * rinv)) * bf2f(static_cast<bf16_t>(ww.x >> 16))));
-        const float y2 = bf2f(f2bf(bf2f(f2bf(v[i][2] * rinv)) * bf2f(static_cast<bf16_t>(ww.y & 0xffff))));
-        const float y3 = bf2f(f2bf(bf2f(f2bf(v[i][3] * rinv)) * bf2f(static_cast<bf16_t>(ww.y >> 16))));
-        acc += y0 * bf2f(static_cast<bf16_t>(rr.x & 0xffff)) + y1 * bf2f(static_cast<bf16_t>(rr.x >> 16)) +
-               y2 * bf2f(static_cast<bf16_t>(rr.y & 0xffff)) + y3 * bf2f(static_cast<bf16_t>(rr.y >> 16));
+#pragma unroll
+        for (int e = 0; e < kRouteE; ++e) {
+          if (e0 + e < ra.E) {
+            const uint2 rr = e0 == 0 ? rpre[i][e]
+                                     : *reinterpret_cast<const uint2*>(ra.router + static_cast<int64_t>(e0 + e) * H + c);
+            acc[e] += xr[i][0] * bf2f(static_cast<bf16_t>(rr.x & 0xffff)) +
+                      xr[i][1] * bf2f(static_cast<bf16_t>(rr.x >> 16)) +
+                      xr[i][2] * bf2f(static_cast<bf16_t>(rr.y & 0xffff)) +
+                      xr[i][3] * bf2f(static_cast<bf16_t>(rr.y >> 16));
+          }
+        }
       }
-      acc = wave_sum(acc);
-      if (lane == 0) part_s[wid][e] = acc;
+#pragma unroll
+      for (int e = 0; e < kRouteE; ++e) acc[e] = wave_sum(acc[e]);
+      if (lane == 0) {
+#pragma unroll
+        for (int e = 0; e < kRouteE; ++e)
+          if (e0 + e < ra.E) part_s[wid][e0 + e] = acc[e];
+      }
     }
     __syncthreads();
     if (threadIdx.x < ra.E) {
@@ -743,29 +775,34 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __rest
       logit_s[threadIdx.x] = bf2f(f2bf(t));  // the router GEMM's bf16 output
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    // softmax + top-k with no serial thread: lane e reads every logit, finds its own rank (value
+    // descending, lower expert first on ties -- the order a greedy arg-max scan picks) and, when
+    // it ranks below k, owns output slot `rank`; the renormalisation sum adds the chosen
+    // probabilities in rank order, as the scan did
+    __shared__ float psel_s[64];
+    const int E = ra.E, e = threadIdx.x;
+    int rank = E;
+    float pr = 0.f;
+    if (e < E) {
       float mx = -INFINITY;
-      for (int e = 0; e < ra.E; ++e) mx = fmaxf(mx, logit_s[e]);
+      for (int q = 0; q < E; ++q) mx = fmaxf(mx, logit_s[q]);
       float sum = 0.f;
-      for (int e = 0; e < ra.E; ++e) sum += __expf(logit_s[e] - mx);
-      unsigned long long taken = 0ull;
-      float wsum = 0.f;
-      for (int j = 0; j < ra.k; ++j) {
-        int best = 0;
-        float bv = -INFINITY;
-        for (int e = 0; e < ra.E; ++e)
-          if (!((taken >> e) & 1ull) && logit_s[e] > bv) {
-            bv = logit_s[e];
-            best = e;
-          }
-        taken |= 1ull << best;
-        const float pr = __expf(bv - mx) / sum;
-        ra.ids[m * ra.k + j] = best;
-        ra.w[m * ra.k + j] = pr;
-        wsum += pr;
+      for (int q = 0; q < E; ++q) sum += __expf(logit_s[q] - mx);
+      const float le = logit_s[e];
+      rank = 0;
+      for (int q = 0; q < E; ++q) {
+        const float lq = logit_s[q];
+        rank += (lq > le || (lq == le && q < e)) ? 1 : 0;
       }
-      if (ra.renorm)
-        for (int j = 0; j < ra.k; ++j) ra.w[m * ra.k + j] /= wsum;
+      pr = __expf(le - mx) / sum;
+      if (rank < ra.k) psel_s[rank] = pr;
+    }
+    __syncthreads();
+    if (rank < ra.k) {
+      float wsum = 0.f;
+      for (int j = 0; j < ra.k; ++j) wsum += psel_s[j];
+      ra.ids[m * ra.k + rank] = e;
+      ra.w[m * ra.k + rank] = ra.renorm ? pr / wsum : pr;
     }
   }
 }

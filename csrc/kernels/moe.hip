@@ -139,6 +139,9 @@ __global__ void __launch_bounds__(1024) combine_add_rmsnorm_kernel(bf16_t* __res
   float v[PER][4];
   float ss = 0.f;
   bf16_t* res = residual + static_cast<int64_t>(t) * H;
+  uint2 wpre[PER];  // the norm weight, requested before the expert rows (independent of them)
+#pragma unroll
+  for (int i = 0; i < PER; ++i) wpre[i] = *reinterpret_cast<const uint2*>(nw + 4 * (threadIdx.x + i * blockDim.x));
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = 4 * (threadIdx.x + i * blockDim.x);
@@ -169,7 +172,7 @@ __global__ void __launch_bounds__(1024) combine_add_rmsnorm_kernel(bf16_t* __res
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = 4 * (threadIdx.x + i * blockDim.x);
-    const uint2 ww = *reinterpret_cast<const uint2*>(nw + c);
+    const uint2 ww = wpre[i];
     float o4[4];
     o4[0] = bf2f(f2bf(v[i][0] * rinv)) * bf2f(static_cast<bf16_t>(ww.x & 0xffff));
     o4[1] = bf2f(f2bf(v[i][1] * rinv)) * bf2f(static_cast<bf16_t>(ww.x >> 16));

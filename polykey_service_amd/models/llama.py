@@ -74,12 +74,16 @@ def _proj(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor],
     return gemm.linear(x, w, packed=wp)
 
 
-def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: Optional[torch.Tensor] = None):
+def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: Optional[torch.Tensor] = None,
+              half: bool = False):
     """Row-parallel projection feeding a residual add + RMSNorm.  TP=1 decode returns the
-    split-K partial slabs unreduced (the norm kernel sums them); TP>1 all-reduces bf16."""
+    split-K partial slabs unreduced (the norm kernel sums them); TP>1 all-reduces bf16.
+    ``half``: slabs from 64-row n-blocks at half the split (the o-projection, HALF_O_SLABS)."""
     if get_state().tp_size == 1 and ws is not None and gemm.skinny_ok(x, w) and gemm.norm_fusable(w.shape[0]):
         S = gemm.choose_split(w.shape[0], x.shape[1], x.shape[0])
         if ws.numel() >= S * x.shape[0] * w.shape[0]:
+            if half:
+                return gemm.linear_partial(x, w, ws, packed=wp, half=True)
             return gemm.linear_partial(x, w, ws, S, packed=wp)
     if x.shape[0] > gemm.SKINNY_MAX_M:
         # prefill: the all-reduce of one row chunk overlaps the GEMM of the next
@@ -125,7 +129,7 @@ class LlamaAttention(nn.Module):
                 # and writes the new k / v into the paged cache
                 a = attn_ops.paged_decode_from_qkv(p, positions, cos_sin, k_cache, v_cache, md, self.scale,
                                                    self.nq, self.nkv)
-                return _proj_out(a, self.o, ws, self.o_p)
+                return _proj_out(a, self.o, ws, self.o_p, half=HALF_O_SLABS)
             # split-K QKV whose epilogue kernel also applies RoPE and writes the KV cache
             q = gemm.qkv_reduce_rope_cache(p, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq,
                                            self.nkv)
@@ -133,7 +137,7 @@ class LlamaAttention(nn.Module):
             return _proj_out(self.attend(gemm.linear(x, self.qkv, packed=self.qkv_p), positions, md, cos_sin, kv),
                              self.o, ws, self.o_p)
         a = attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
-        return _proj_out(a, self.o, ws, self.o_p)
+        return _proj_out(a, self.o, ws, self.o_p, half=HALF_O_SLABS)
 
     def attend(self, qkv: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
                kv: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
