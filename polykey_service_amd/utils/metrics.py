@@ -36,8 +36,8 @@ class Metrics:
         self.kv_util = Gauge("polykey_engine_kv_utilization", "fraction of KV blocks in use", registry=r)
         self.step_seconds = Histogram("polykey_engine_step_seconds", "engine step wall time", buckets=_TOK_BUCKETS,
                                       registry=r)
-        self.preemptions = Gauge("polykey_engine_preemptions", "preemptions so far", registry=r)
         # cumulative engine counts exported as Counters (advanced by the delta since the last step)
+        self.preemptions = Counter("polykey_engine_preemptions", "sequences preempted (KV recompute)", registry=r)
         self.cached_tokens = Counter("polykey_engine_prefix_cache_hit_tokens", "prompt tokens served from the "
                                      "prefix cache", registry=r)
         self.prefix_queries = Counter("polykey_engine_prefix_cache_queries", "full prompt blocks looked up in the "
@@ -77,7 +77,7 @@ class Metrics:
         self.waiting.set(len(sch.waiting))
         bm = engine.bm
         self.kv_util.set(1.0 - bm.num_free / max(bm.num_blocks, 1))
-        self.preemptions.set(sch.num_preemptions)
+        self._advance(self.preemptions, "preemptions", sch.num_preemptions)
         self._advance(self.cached_tokens, "tokens", getattr(sch, "num_cached_tokens", 0))
         self._advance(self.prefix_queries, "queries", getattr(bm, "prefix_queries", 0))
         self._advance(self.prefix_hits, "hits", getattr(bm, "prefix_hits", 0))
