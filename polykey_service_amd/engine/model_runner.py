@@ -315,9 +315,12 @@ class ModelRunner:
     def _check_comm(self) -> None:
         """Fail loudly once a custom all-reduce of this step (or an earlier one) timed out: the
         step's tokens were computed from incomplete sums (parallel/custom_ar.py)."""
-        car = self.model.st.custom_ar
-        if car is not None:
-            car.check()
+        st = self.model.st
+        if st.custom_ar is not None:
+            st.custom_ar.check()
+        for rc in (getattr(st, "rccl_tp", None), getattr(st, "rccl_ep", None)):
+            if rc is not None:  # RCCL's asynchronous error word (non-blocking poll)
+                rc.check()
 
     def launch_continuation(self, batch: ScheduledBatch, prev) -> Optional[tuple]:
         """Decode step k+1 of ``batch.decodes`` enqueued while step k (``prev``) may still run:

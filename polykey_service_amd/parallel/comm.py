@@ -1,7 +1,9 @@
 """Tensor-parallel / expert-parallel collectives.
 
-Device collectives go through ``torch.distributed`` on the TP group, which is RCCL over
-xGMI on MI355X (backend "nccl"); the same code runs on gloo in CPU tests.  Per-call sizes
+Device collectives are RCCL over xGMI on MI355X: the direct communicators of
+``parallel/rccl.py`` (one RCCL call on the caller's stream) when ``init_parallel`` created them,
+else ``torch.distributed`` on the TP / EP group (backend "nccl"); the same code runs on gloo in
+CPU tests.  Small decode all-reduces / gathers take the one-shot xGMI kernel instead.  Per-call sizes
 for the north-star configs (SURVEY.md §2.3 collective table): 70B TP8 decode all-reduces
 [B, 8192] bf16 = 16 KiB·B twice per layer — latency-bound, hence HIP-graph capture of the
 whole decode step (RCCL collectives are graph-capturable); prefill all-reduces are tens of
@@ -26,8 +28,16 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     car = st.custom_ar
     if car is not None and car.supports(x):
         return car.all_reduce(x, out=x)  # one-shot xGMI kernel (small decode messages)
+    rc = _direct(st.rccl_tp, x)
+    if rc is not None and x.is_contiguous():
+        return rc.all_reduce(x, out=x)
     dist.all_reduce(x, group=st.tp_group)
     return x
+
+
+def _direct(comm, x: torch.Tensor):
+    """The direct RCCL communicator for a device tensor, or None (torch.distributed / gloo)."""
+    return comm if comm is not None and x.is_cuda else None
 
 
 _COMM_STREAMS = {}
@@ -105,6 +115,10 @@ class SPLayout:
 
 def _reduce_scatter(out: torch.Tensor, x: torch.Tensor) -> None:
     st = get_state()
+    rc = _direct(st.rccl_tp, x)
+    if rc is not None and out.is_contiguous():
+        rc.reduce_scatter(x, out=out)
+        return
     if dist.get_backend(st.tp_group) != "gloo":
         dist.reduce_scatter_tensor(out, x, group=st.tp_group)
         return
@@ -160,16 +174,23 @@ def sp_all_gather(shard: torch.Tensor, lay: SPLayout, fn=None) -> torch.Tensor:
     events = []
     if overlap:
         cs.wait_stream(main)
+    rc = _direct(st.rccl_tp, shard)
+
+    def gather(dst, src):
+        if rc is not None:
+            rc.all_gather(src, out=dst)
+        else:
+            dist.all_gather_into_tensor(dst, src, group=st.tp_group)
     for c in range(lay.chunks):
         lo, hi, slo, shi = lay.chunk(c)
         if overlap:
             with torch.cuda.stream(cs):
-                dist.all_gather_into_tensor(full[lo:hi], shard[slo:shi], group=st.tp_group)
+                gather(full[lo:hi], shard[slo:shi])
                 ev = torch.cuda.Event()
                 ev.record(cs)
             events.append(ev)
         else:
-            dist.all_gather_into_tensor(full[lo:hi], shard[slo:shi], group=st.tp_group)
+            gather(full[lo:hi], shard[slo:shi])
     if overlap:
         full.record_stream(cs)
         shard.record_stream(cs)
@@ -209,7 +230,11 @@ def tp_all_gather_last(x: torch.Tensor) -> torch.Tensor:
     if car is not None and car.supports_gather(x):
         return car.all_gather_last(x)
     out = torch.empty((st.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x, group=st.tp_group)
+    rc = _direct(st.rccl_tp, x)
+    if rc is not None:
+        rc.all_gather(x, out=out)
+    else:
+        dist.all_gather_into_tensor(out, x, group=st.tp_group)
     out = out.view((st.tp_size,) + tuple(x.shape))
     return out.movedim(0, -2).reshape(*x.shape[:-1], x.shape[-1] * st.tp_size)
 
@@ -219,6 +244,9 @@ def tp_all_to_all(x: torch.Tensor, out_splits: List[int], in_splits: List[int]) 
     st = get_state()
     if st.tp_size == 1:
         return x
+    rc = _direct(st.rccl_tp, x)
+    if rc is not None:
+        return rc.all_to_allv(x, out_splits, in_splits)
     out = torch.empty((sum(out_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_to_all_single(out, x.contiguous(), out_splits, in_splits, group=st.tp_group)
     return out
@@ -229,6 +257,9 @@ def tp_all_to_all_counts(counts: torch.Tensor) -> torch.Tensor:
     st = get_state()
     if st.tp_size == 1:
         return counts
+    rc = _direct(st.rccl_tp, counts)
+    if rc is not None:
+        return rc.all_to_allv(counts.reshape(-1, 1), [1] * st.tp_size, [1] * st.tp_size).view(-1)
     out = torch.empty_like(counts)
     dist.all_to_all_single(out, counts.contiguous(), group=st.tp_group)
     return out
@@ -242,6 +273,9 @@ def ep_all_to_all(x: torch.Tensor, out_splits: List[int], in_splits: List[int]) 
     if x.is_cuda and dist.get_backend(st.ep_group) == "gloo":
         # ranks sharing one GPU (rehearsal / tests): gloo moves host copies
         return ep_all_to_all(x.cpu(), out_splits, in_splits).to(x.device)
+    rc = _direct(st.rccl_ep, x)
+    if rc is not None:  # one group of ncclSend/ncclRecv pairs on the compute stream
+        return rc.all_to_allv(x, out_splits, in_splits)
     out = torch.empty((sum(out_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_to_all_single(out, x.contiguous(), out_splits, in_splits, group=st.ep_group)
     return out
@@ -254,6 +288,9 @@ def ep_all_to_all_counts(counts: torch.Tensor) -> torch.Tensor:
         return counts
     if counts.is_cuda and dist.get_backend(st.ep_group) == "gloo":
         return ep_all_to_all_counts(counts.cpu()).to(counts.device)
+    rc = _direct(st.rccl_ep, counts)
+    if rc is not None:
+        return rc.all_to_allv(counts.reshape(-1, 1), [1] * st.ep_size, [1] * st.ep_size).view(-1)
     out = torch.empty_like(counts)
     dist.all_to_all_single(out, counts.contiguous(), group=st.ep_group)
     return out
@@ -294,6 +331,9 @@ def tp_broadcast_tensor(t: torch.Tensor) -> torch.Tensor:
     st = get_state()
     if st.tp_size == 1:
         return t
+    rc = _direct(st.rccl_tp, t)
+    if rc is not None and t.is_contiguous():
+        return rc.broadcast(t, root=0)  # the group's first rank is its leader
     dist.broadcast(t, src=st.dp_rank * st.tp_size, group=st.tp_cpu_group if not t.is_cuda else st.tp_group)
     return t
 

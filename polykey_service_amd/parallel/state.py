@@ -17,11 +17,14 @@ from __future__ import annotations
 
 import dataclasses
 import datetime
+import logging
 import os
 from typing import Optional
 
 import torch
 import torch.distributed as dist
+
+log = logging.getLogger(__name__)
 
 
 @dataclasses.dataclass
@@ -40,6 +43,8 @@ class ParallelState:
     tp_group: Optional[object] = None      # device collectives (RCCL / gloo on CPU)
     tp_cpu_group: Optional[object] = None  # gloo: control-plane broadcast of step metadata
     custom_ar: Optional[object] = None     # one-shot xGMI all-reduce (parallel/custom_ar.py)
+    rccl_tp: Optional[object] = None       # direct RCCL communicator of the TP group (parallel/rccl.py)
+    rccl_ep: Optional[object] = None       # ... of the EP group (the TP one when EP runs inside TP)
     backend: str = "none"
     device: torch.device = dataclasses.field(default_factory=lambda: torch.device("cpu"))
 
@@ -132,14 +137,33 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
         if be == "nccl" or (os.environ.get("POLYKEY_CUSTOM_AR") == "force" and dev.type == "cuda"):
             from .custom_ar import maybe_create
             st.custom_ar = maybe_create(st)
+        if be == "nccl" and os.environ.get("POLYKEY_RCCL_DIRECT", "1") == "1":
+            _create_rccl(st)
     set_state(st)
     return st
 
 
+def _create_rccl(st: ParallelState) -> None:
+    """Direct RCCL communicators for the TP and EP groups (collective over each group; the
+    unique ids travel over the gloo groups).  Any failure leaves torch.distributed in charge."""
+    from . import rccl
+    try:
+        if st.tp_size > 1:
+            st.rccl_tp = rccl.RcclComm.create(st.tp_group, st.device, cpu_group=st.tp_cpu_group)
+        if st.ep_size > 1:
+            st.rccl_ep = (st.rccl_tp if st.ep_group is st.tp_group
+                          else rccl.RcclComm.create(st.ep_group, st.device, cpu_group=st.ep_cpu_group))
+    except (rccl.RcclError, OSError) as e:  # pragma: no cover - needs several GPUs
+        log.warning("direct RCCL communicators unavailable (%s); collectives stay on torch.distributed", e)
+        st.rccl_tp = st.rccl_ep = None
+
+
 def destroy_parallel() -> None:
-    car = get_state().custom_ar
-    if car is not None:
-        car.close()
+    st = get_state()
+    if st.custom_ar is not None:
+        st.custom_ar.close()
+    for c in {id(c): c for c in (st.rccl_tp, st.rccl_ep) if c is not None}.values():
+        c.close()
     if dist.is_initialized():
         dist.destroy_process_group()
     set_state(ParallelState())
