@@ -147,3 +147,42 @@ def test_keepalive_enforcement_allows_10s_pings():
     assert opts["grpc.http2.min_recv_ping_interval_without_data_ms"] <= 10_000
     assert opts["grpc.keepalive_permit_without_calls"] == 1
     assert opts["grpc.max_connection_idle_ms"] == 300_000 and opts["grpc.keepalive_time_ms"] == 7_200_000
+
+
+class SlowStreamService(ToolRouter):
+    """A stream of 5 chunks, 0.1 s apart (an LLM stream in flight when the server stops)."""
+
+    def __init__(self):
+        super().__init__()
+        self.started = threading.Event()
+
+    async def execute_tool_stream(self, ctx, tool_name, parameters=None, secret_id=None, metadata=None):
+        for i in range(5):
+            self.started.set()
+            yield proto.ExecuteToolResponse(string_output=f"chunk{i}")
+            await asyncio.sleep(0.1)
+
+
+def test_graceful_shutdown_lets_in_flight_streams_finish():
+    """SIGTERM path (R7): health flips to NOT_SERVING first, new calls are refused, and a stream
+    already in flight still delivers every chunk within the grace period."""
+    svc = SlowStreamService()
+    with ServerThread(svc) as s, grpc.insecure_channel(s.addr) as ch:
+        st = ch.unary_stream(proto.EXECUTE_TOOL_STREAM, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                             response_deserializer=proto.ExecuteToolResponse.FromString)
+        got = []
+        reader = threading.Thread(target=lambda: got.extend(
+            r.string_output for r in st(proto.ExecuteToolRequest(tool_name="slow"), timeout=10)))
+        reader.start()
+        assert svc.started.wait(5)
+        stopper = threading.Thread(target=s.stop, args=(5.0,))
+        stopper.start()
+        reader.join(10)
+        stopper.join(10)
+        assert got == [f"chunk{i}" for i in range(5)]
+        assert s.srv.health.get("") == NOT_SERVING
+        with pytest.raises(grpc.RpcError):
+            unary(ch, proto.EXECUTE_TOOL, proto.ExecuteToolRequest, proto.ExecuteToolResponse)(
+                proto.ExecuteToolRequest(tool_name="example_tool"), timeout=2)
+        msgs = [r["msg"] for r in s.records()]
+    assert msgs.index("server shutting down") < msgs.index("server stopped")
