@@ -48,6 +48,7 @@ __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
@@ -402,6 +403,158 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_pp_kernel(const Pref
     }
 }
 
+// ---- deep variant (4 / 5): the ping-pong phases with three 16 KiB pieces in flight instead of
+// about one and a half (guide §5 T3+T4: counted vmcnt letting loads span phases is the lever).
+// Every wave keeps BOTH W halves of a k-tile in registers (+16 VGPRs), so each operand half is
+// read from LDS exactly once per k-tile -- quadrant order A0W0, A0W1, A1W0, A1W1 reads A0+W0,
+// W1, A1, nothing -- and its LDS slot frees early: A0 / W0 after phase 0, W1 after 1, A1 after 2.
+// The next tiles' pieces go into those slots as soon as the 2-phase WAR distance allows:
+//   phase q0: W1(t+1)   q1: A1(t+1)   q2: A0(t+2)   q3: W0(t+2)
+// (W1 / A1 of t+1 into the other buffer, last read in phases 1 / 2 of tile t-1; A0 / W0 of t+2
+// into this tile's buffer, last read in phase 0).  Each piece is read 5-6 phases after it is
+// issued; the R of phase p retires what phase p+1 reads, and in steady state exactly three
+// younger pieces (6 loads) have been issued since the oldest one needed: vmcnt(6) everywhere
+// (vmcnt(0) in the last two k-tiles, where fewer younger loads exist).  The prologue stages
+// tile 0 and A0 / W0 of tile 1 and retires tile 0 (vmcnt(4)).
+template <bool PW>
+__global__ void __launch_bounds__(kThreads, 1) prefill_gemm_deep_kernel(const PrefillGemmArgs args) {
+  constexpr int BK = 64, kChunks = 8, kPiece = 128 * BK, kStage = 4 * kPiece, kSwz = 1;
+  constexpr int kRowsPerInstr = kThreads / kChunks;  // 64
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kStage];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  Tile tl;
+  if (!tile_of(args, tl)) return;
+  const int K = args.K, nk = K / BK;
+
+  // piece order in LDS: 0 = A rows 0-127, 1 = A 128-255, 2 = W 0-127, 3 = W 128-255
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = j * kRowsPerInstr + tid / kChunks;
+      const int logical = (tid % kChunks) ^ ((row >> kSwz) & (kChunks - 1));
+      if (p < 2) {
+        const int m = min(tl.m0 + p * 128 + row, tl.rows - 1);
+        src[p][j] = args.A + static_cast<long long>(tl.row0 + m) * args.lda + logical * 8;
+      } else if constexpr (PW) {
+        const int f = j * 8 + w;
+        src[p][j] = tl.W + static_cast<long long>((tl.n0 >> 7) + (p - 2)) * 128 * K + ((f >> 1) * 4 + (f & 1)) * 512 +
+                    lane * 8;
+      } else {
+        src[p][j] = tl.W + static_cast<long long>(tl.n0 + (p - 2) * 128 + row) * K + logical * 8;
+      }
+    }
+  auto stage_piece = [&](int p, int kt) {
+    bf16_t* base = lds + (kt & 1) * kStage + p * kPiece + w * 64 * 8;
+    const long long off = PW && p >= 2 ? (kt >> 1) * 16384LL + (kt & 1) * 1024 : static_cast<long long>(kt) * BK;
+    glds16(src[p][0] + off, base);
+    glds16(src[p][1] + off, base + kRowsPerInstr * BK);
+  };
+
+  const int wr = w >> 2, wc = w & 3;
+  const int r = lane & 15, g = lane >> 4;
+  auto frag = [&](int piece, int row, int s) {
+    return piece * kPiece + row * BK + (((4 * s + g) ^ ((row >> kSwz) & (kChunks - 1))) * 8);
+  };
+  typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+  bf16x8_t af[4][2], wf[2][2][2];  // wf[W half][n frag][k step]
+  f32x4 acc[4][2][4];              // [quadrant][n frag][m frag]
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < 4; ++p) stage_piece(p, 0);
+  if (nk > 1) {
+    stage_piece(0, 1);
+    stage_piece(2, 1);
+    wait_vm<4>();
+  } else {
+    wait_vm<0>();
+  }
+  barrier();
+  if (wr == 1) barrier();  // the second M-half runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  constexpr int kAh[4] = {0, 0, 1, 1}, kWh[4] = {0, 1, 0, 1};
+  constexpr int kStagePiece[4] = {3, 1, 0, 2}, kStageAhead[4] = {1, 1, 2, 2};  // W1, A1 of t+1; A0, W0 of t+2
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16_t* base = lds + (kt & 1) * kStage;
+    const bool steady = kt + 2 < nk;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // ---- R: retire what the next phase reads, read this phase's new operand halves, stage
+      if (steady) wait_vm<6>();
+      else wait_vm<0>();
+      if (q == 0 || q == 2) {
+#pragma unroll
+        for (int mf = 0; mf < 4; ++mf)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            af[mf][s] = *reinterpret_cast<const bf16x8_t*>(base + frag(kAh[q], wr * 64 + mf * 16 + r, s));
+      }
+      if (q < 2) {
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            wf[q][nf][s] = *reinterpret_cast<const bf16x8_t*>(
+                base + (PW ? (2 + q) * kPiece + ((wc * 2 + nf) * 2 + s) * 512 + lane * 8
+                           : frag(2 + q, wc * 32 + nf * 16 + r, s)));
+      }
+      if (kt + kStageAhead[q] < nk) stage_piece(kStagePiece[q], kt + kStageAhead[q]);
+      barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- M
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+          for (int mf = 0; mf < 4; ++mf)
+            acc[q][nf][mf] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kWh[q]][nf][s], af[mf][s], acc[q][nf][mf], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (wr == 0) barrier();  // equal barrier counts for both halves
+
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int mf = 0; mf < 4; ++mf) {
+      const int m = tl.m0 + kAh[q] * 128 + wr * 64 + mf * 16 + r;
+      if (m >= tl.rows) continue;
+      bf16_t* crow = args.C + static_cast<long long>(tl.row0 + m) * args.ldc;
+      const int nb = tl.n0 + kWh[q] * 128 + wc * 32;
+      if (args.silu) {
+        float y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = rbf(silu(rbf(acc[q][0][mf][i]))) * rbf(acc[q][1][mf][i]);
+        uint2 v;
+        v.x = pack2(y[0], y[1]);
+        v.y = pack2(y[2], y[3]);
+        *reinterpret_cast<uint2*>(crow + nb / 2 + 4 * g) = v;
+      } else {
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+          uint2 v;
+          v.x = pack2(acc[q][nf][mf][0], acc[q][nf][mf][1]);
+          v.y = pack2(acc[q][nf][mf][2], acc[q][nf][mf][3]);
+          *reinterpret_cast<uint2*>(crow + nb + nf * 16 + 4 * g) = v;
+        }
+      }
+    }
+}
+
 int launch(const PrefillGemmArgs& a, int variant, hipStream_t stream) {
   const int grid = a.tiles_m * (a.N / kBN);
   switch (variant) {
@@ -409,6 +562,8 @@ int launch(const PrefillGemmArgs& a, int variant, hipStream_t stream) {
     case 1: prefill_gemm_kernel<32, 4><<<grid, kThreads, 0, stream>>>(a); break;
     case 2: prefill_gemm_pp_kernel<false><<<grid, kThreads, 0, stream>>>(a); break;
     case 3: prefill_gemm_pp_kernel<true><<<grid, kThreads, 0, stream>>>(a); break;  // block-packed W
+    case 4: prefill_gemm_deep_kernel<false><<<grid, kThreads, 0, stream>>>(a); break;
+    case 5: prefill_gemm_deep_kernel<true><<<grid, kThreads, 0, stream>>>(a); break;  // block-packed W
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
@@ -417,12 +572,12 @@ int launch(const PrefillGemmArgs& a, int variant, hipStream_t stream) {
 }  // namespace
 
 // variant: 0 = BK 64 x 2 stages, 1 = BK 32 x 4 stages, 2 = ping-pong quadrant phases (BK 64),
-// 3 = variant 2 reading block-packed W (K % 128 == 0).  Requires N % 256 == 0, K % 64 == 0,
+// 3 = variant 2 reading block-packed W (K % 128 == 0), 4 / 5 = variants 2 / 3 with three pieces in flight.  Requires N % 256 == 0, K % 64 == 0,
 // 16-byte aligned rows (lda % 8 == 0, K % 8 == 0, ldc % 4 == 0).
 PK_EXPORT int pk_prefill_gemm(const PrefillGemmArgs* a, int variant, hipStream_t stream) {
   if (a->M <= 0 || a->tiles_m <= 0) return 0;
   if (a->N % kBN || a->K % 64 || a->lda % 8 || a->ldc % 4) return -1;
-  if (variant == 3 && a->K % 128) return -1;
+  if ((variant == 3 || variant == 5) && a->K % 128) return -1;
   if (a->row_offsets != nullptr && a->groups <= 0) return -1;
   if (a->row_offsets == nullptr && a->tiles_m != (a->M + kBM - 1) / kBM) return -1;
   return launch(*a, variant, stream);

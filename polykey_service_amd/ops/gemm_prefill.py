@@ -20,9 +20,11 @@ from . import native
 
 BM = 256
 BN = 256
-# 0: BK 64 x 2 LDS stages, 1: BK 32 x 4 stages, 2: ping-pong quadrant phases (default: 6-8 %
+# 0: BK 64 x 2 LDS stages, 1: BK 32 x 4 stages, 2: ping-pong quadrant phases (6-8 %
 # faster than 0, tools/prefill_gemm_bench.py) -- csrc/kernels/gemm_prefill.hip
-VARIANT = int(os.environ.get("POLYKEY_PREFILL_GEMM_VARIANT", "2"))
+# 4: ping-pong quadrant phases with three LDS-DMA pieces in flight (tools/prefill_gemm_ab.py, same
+# process: grouped MoE w13 +3.2 %, w2 +4.8 %, dense gate_up / down +2.3-2.5 % over variant 2)
+VARIANT = int(os.environ.get("POLYKEY_PREFILL_GEMM_VARIANT", "4"))
 
 
 class PrefillGemmArgs(ctypes.Structure):
@@ -65,7 +67,8 @@ def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
     return y.to(x.dtype)
 
 
-PACKED_VARIANT = 3  # ping-pong kernel reading the decode GEMM's block-packed W
+# ping-pong kernel reading the decode GEMM's block-packed W (5: its deep-pipelined form)
+PACKED_VARIANT = int(os.environ.get("POLYKEY_PREFILL_GEMM_PACKED_VARIANT", "5"))
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, silu: bool = False,
@@ -93,7 +96,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
     if (not supported(N, K) or x.stride(1) != 1 or not src.is_contiguous() or out.stride(1) != 1
             or (packed is not None and (K % 128 or tuple(packed.shape) != (N, K)))):
         raise ValueError(f"prefill GEMM: unsupported shape/layout M={M} N={N} K={K}")
-    if packed is not None:
+    if packed is not None and variant not in (3, 5):
         variant = PACKED_VARIANT
     a = PrefillGemmArgs()
     a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), src.data_ptr()

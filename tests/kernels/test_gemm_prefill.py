@@ -13,7 +13,7 @@ def rnd(*shape, scale=1.0):
     return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 4096), (1000, 768, 1024), (4100, 1280, 8192),
                                    (8192, 4096, 4096), (77, 256, 14336)])
 def test_dense(M, N, K, variant):
@@ -33,7 +33,7 @@ def test_dense_strided_out_and_input():
     assert torch.count_nonzero(out_full[:, 512:]) == 0
 
 
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 4])
 @pytest.mark.parametrize("M,I,K", [(513, 512, 4096), (256, 14336, 4096)])
 def test_silu_epilogue(M, I, K, variant):
     x = rnd(M, K)
@@ -45,7 +45,7 @@ def test_silu_epilogue(M, I, K, variant):
     torch.testing.assert_close(y.float(), exp, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4])
 @pytest.mark.parametrize("silu", [False, True])
 def test_grouped(silu, variant):
     G, N, K = 6, 512, 1024
@@ -63,7 +63,7 @@ def test_grouped(silu, variant):
     assert torch.all(out[lo:] == 7.0)  # rows past the last group are never written
 
 
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 4])
 def test_repeatable_bitwise(variant):
     """Race screen for the LDS-DMA pipelines (guide §5: an early read passes reference checks
     whenever the DMA happens to land first): repeated launches on a busy chip give identical
@@ -72,17 +72,20 @@ def test_repeatable_bitwise(variant):
     ys = [gemm_prefill.linear(x, w, variant=variant) for _ in range(6)]
     for y in ys[1:]:
         assert torch.equal(y, ys[0])
-    other = gemm_prefill.linear(x, w, variant=2 - variant)
+    other = gemm_prefill.linear(x, w, variant=0 if variant else 2)
     torch.testing.assert_close(ys[0].float(), other.float(), atol=1e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("M,N,K,silu", [(300, 512, 4096, False), (4100, 1280, 8192, False), (513, 1024, 4096, True)])
-def test_block_packed_weights(M, N, K, silu):
+@pytest.mark.parametrize("variant", [3, 5])
+@pytest.mark.parametrize("M,N,K,silu", [(300, 512, 4096, False), (4100, 1280, 8192, False), (513, 1024, 4096, True),
+                                        (256, 256, 128, False), (700, 512, 256, True)])
+def test_block_packed_weights(M, N, K, silu, variant):
     """The decode GEMM's block-packed layout read directly (variant 3): same result as the
     row-major weight through the row-major kernel."""
     x, w = rnd(M, K), rnd(N, K, scale=0.02)
     wp = gemm.pack_weight(w)
-    y = gemm_prefill.linear(x, torch.empty(N, K, dtype=torch.bfloat16, device="meta"), packed=wp, silu=silu)
+    y = gemm_prefill.linear(x, torch.empty(N, K, dtype=torch.bfloat16, device="meta"), packed=wp, silu=silu,
+                            variant=variant)
     ref = gemm_prefill.linear(x, w, silu=silu, variant=2)
     torch.testing.assert_close(y.float(), ref.float(), atol=1e-2, rtol=1e-2)
     if not silu:
