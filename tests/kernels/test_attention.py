@@ -155,6 +155,35 @@ def test_rope_and_cache(nq, nkv, bs):
     assert torch.equal(vc_d.cpu(), vc_r)
 
 
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 2, 64)])
+def test_rope_and_cache_aligned_runs(nq, nkv, bs):
+    """Prefill layout: 32-token groups that fill an aligned 32-slot run of a block take the
+    transposed V-tile path; a misaligned group, a group with a padding row and a short tail
+    take the per-token path -- both bit-exact against the reference."""
+    nb = 12
+    runs = [list(range(2 * bs, 2 * bs + 32)),               # aligned, block 2
+            list(range(5 * bs + bs - 32, 5 * bs + bs)),     # aligned, last 32 slots of block 5
+            list(range(7 * bs + 3, 7 * bs + 35)),           # misaligned start
+            list(range(9 * bs, 9 * bs + 32)),               # aligned but one padding row
+            list(range(11 * bs, 11 * bs + 5))]              # tail of 5 tokens
+    runs[3][7] = -1
+    slots = torch.tensor(sum(runs, []), dtype=torch.int32)
+    T = slots.numel()
+    qkv = torch.randn(T, (nq + 2 * nkv) * HD).to(torch.bfloat16)
+    pos = torch.arange(T, dtype=torch.int32)
+    cs = ref.rope_cos_sin_cache(4096, HD, 500000.0)
+    kc = torch.zeros(nb, nkv, bs, HD, dtype=torch.bfloat16)
+    vc = torch.zeros(nb, nkv, HD, bs, dtype=torch.bfloat16)
+    qkv_r, kc_r, vc_r = qkv.clone(), kc.clone(), vc.clone()
+    ref.rope_and_cache(qkv_r, pos, cs, kc_r, vc_r, slots, nq, nkv, HD)
+    d = "cuda"
+    qkv_d, kc_d, vc_d = qkv.to(d), kc.to(d), vc.to(d)
+    A.rope_and_cache(qkv_d, pos.to(d), cs.to(d), kc_d, vc_d, slots.to(d), nq, nkv, HD)
+    torch.testing.assert_close(qkv_d.cpu().float(), qkv_r.float(), atol=1.6e-2, rtol=1e-2)
+    torch.testing.assert_close(kc_d.cpu().float(), kc_r.float(), atol=1.6e-2, rtol=1e-2)
+    assert torch.equal(vc_d.cpu(), vc_r)
+
+
 @pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 64), (16, 4, 32)])
 @pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [512, 513, 1300, 0]])
 @pytest.mark.parametrize("S", [1, 4])
