@@ -917,7 +917,13 @@ int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
   const bool half = (mode & 128) != 0;   // bit 7: 64-row n-blocks (KR = 1)
   if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr || a.M > 64)) return -1;
   if (half) {  // split-K projections only: fp32 slabs or the in-launch residual update
-    if (grouped || norm || a.row_scale || nt) return -1;
+    if (grouped || norm || nt) return -1;
+    if (a.row_scale) {  // folded-norm QKV slabs (packed W only)
+      if ((mode & 7) != kPartial || !packed || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64 ||
+          a.M > 64)
+        return -1;
+      return launch<kPartial, true, false, false, true, 1>(a, stream);
+    }
     if ((mode & 7) == kPartial)
       return packed ? launch<kPartial, true, false, false, false, 1>(a, stream)
                     : launch<kPartial, false, false, false, false, 1>(a, stream);

@@ -57,6 +57,7 @@ SP_MIN_TOKENS = int(os.environ.get("POLYKEY_SP_MIN_TOKENS", "256"))
 INLAUNCH_RESIDUAL = os.environ.get("POLYKEY_INLAUNCH_RESIDUAL", "0") == "1"
 INLAUNCH_SPLIT = int(os.environ.get("POLYKEY_INLAUNCH_SPLIT", "4"))
 HALF_O_SLABS = os.environ.get("POLYKEY_HALF_O_SLABS", "1") == "1"
+HALF_QKV_SLABS = os.environ.get("POLYKEY_HALF_QKV_SLABS", "0") == "1"
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:
@@ -481,7 +482,8 @@ class LlamaForCausalLM(nn.Module):
         for i, layer in enumerate(self.layers):
             at, mlp = layer.attn, layer.mlp
             kc, vc = kv_caches[i]
-            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf)
+            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf,
+                                             half=HALF_QKV_SLABS)
             if md.num_prefill == 0 and FUSED_QKV_ATTENTION:
                 a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
             else:

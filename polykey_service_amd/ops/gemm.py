@@ -345,13 +345,19 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
 
 
 def linear_partial_rowscale(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, rowscale: RowScale,
-                            S: Optional[int] = None, packed: Optional[torch.Tensor] = None) -> Partial:
-    """:func:`linear_partial` of a folded-norm projection: slabs of rinv[m] * (x @ W'^T)."""
+                            S: Optional[int] = None, packed: Optional[torch.Tensor] = None,
+                            half: bool = False) -> Partial:
+    """:func:`linear_partial` of a folded-norm projection: slabs of rinv[m] * (x @ W'^T).
+    ``half`` (packed W): 64-row n-blocks at half the default split."""
     M, K = x.shape
     N = w.shape[0]
-    S = S or choose_split(N, K, M)
+    half = half and packed is not None and packed.numel() * packed.element_size() < NT_MIN_BYTES
+    if S is None:
+        S = choose_split(N, K, M)
+        if half:
+            S = max(1, S // 2)
     assert ws.numel() >= S * M * N, "split-K workspace too small"
-    _launch_ex(MODE_PARTIAL, x, w, packed, S, ws=ws, rowscale=rowscale)
+    _launch_ex(MODE_PARTIAL | (HALF_BIT if half else 0), x, w, packed, S, ws=ws, rowscale=rowscale)
     return Partial(ws, S, M, N)
 
 

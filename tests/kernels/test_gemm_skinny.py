@@ -289,3 +289,21 @@ def test_rowscale_folded_norm(M):
     # |silu(g) u| reaches ~90, so compare against the output scale rather than per element
     err = (y.float() - exp).abs().max().item()
     assert err <= 0.025 * exp.abs().max().item(), err
+
+
+@pytest.mark.parametrize("M", [1, 64])
+def test_rowscale_half_blocks(M):
+    """Folded-norm QKV slabs from 64-row n-blocks at half the split (POLYKEY_HALF_QKV_SLABS):
+    S/2 slabs summing to the same rinv-scaled product as the 128-row-block split."""
+    H, N = 4096, 6144
+    res = rnd(M, H)
+    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    w = rnd(N, H, scale=0.02)
+    wp = gemm.pack_weight(gemm.fold_norm(w, nw))
+    parts = gemm.residual_parts(None, res.clone(), torch.empty(4 * 64, device="cuda"))
+    rs = gemm.RowScale(parts, 1e-5)
+    ws = torch.empty(2 * 4 * M * N, dtype=torch.float32, device="cuda")
+    a = gemm.linear_partial_rowscale(res, w, ws[: 4 * M * N], rs, packed=wp)
+    b = gemm.linear_partial_rowscale(res, w, ws[4 * M * N:], rs, packed=wp, half=True)
+    assert a.S == 4 and b.S == 2
+    torch.testing.assert_close(a.view().sum(0), b.view().sum(0), atol=2e-3, rtol=2e-3)
