@@ -329,11 +329,17 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
   }
 
   // the grid's z dimension is small (<= 4); a workgroup walks partitions z, z + gridDim.z, ...
+  // carrying its online-softmax state across them (the order of key blocks does not matter to
+  // the softmax), so it combines its waves and writes ONE partial at the end: no LDS combine /
+  // partial store between partitions and gridDim.z partials to merge instead of n_parts.
+  const int n_eff = min(n_used, static_cast<int>(gridDim.z));  // partials of this sequence
+  WaveState st;
+  init_state(st);
   for (int part = blockIdx.z; part < n_used; part += gridDim.z) {
     const int begin = part * kPart;
     const int end = min(ctx, begin + kPart);
     const int b0 = begin / bs, nblk = (end - 1) / bs - b0 + 1;
-    __syncthreads();  // the previous partition's LDS readers are done
+    __syncthreads();  // the previous partition's block-table readers are done
 #if PK_DECODE_BT_PREFETCH
     if (part == static_cast<int>(blockIdx.z) && kPart % bs == 0) {  // nblk <= kPart / bs <= 64 * NW
       if (static_cast<int>(threadIdx.x) < nblk) bt_s[threadIdx.x] = bt_pre;
@@ -342,79 +348,76 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
       for (int i = threadIdx.x; i < nblk; i += 64 * NW)
         bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
     __syncthreads();
-    WaveState st;
-    init_state(st);
     KVFrag fa;
     attend(st, qf, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w, end, NW * kStep, ctx, ctx - 1, scale2, fa);
-    const float lsum = col_sum(st.l);
+  }
+  const float lsum = col_sum(st.l);
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
+  for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o_lds[w][r][16 * dt + 4 * g + i] = st.o[dt][i];
-    if (g == 0) {
-      ml_lds[w][r][0] = st.m;
-      ml_lds[w][r][1] = lsum;
+    for (int i = 0; i < 4; ++i) o_lds[w][r][16 * dt + 4 * g + i] = st.o[dt][i];
+  if (g == 0) {
+    ml_lds[w][r][0] = st.m;
+    ml_lds[w][r][1] = lsum;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
+    const int c = idx / kHD, d = idx % kHD;
+    float M = kNegBig;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
+    float O = 0.f, L = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) {
+      const float f = exp2f(ml_lds[ww][c][0] - M);
+      O += f * o_lds[ww][c][d];
+      L += f * ml_lds[ww][c][1];
     }
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
-      const int c = idx / kHD, d = idx % kHD;
-      float M = kNegBig;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
-      float O = 0.f, L = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) {
-        const float f = exp2f(ml_lds[ww][c][0] - M);
-        O += f * o_lds[ww][c][d];
-        L += f * ml_lds[ww][c][1];
-      }
-      const int hq = h * G + c;
-      if (n_used == 1) {
-        out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
-      } else {
-        const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + part;
-        part_o[pi * kHD + d] = O;
-        if (d == 0) {
-          part_ml[2 * pi] = M;
-          part_ml[2 * pi + 1] = L;
-        }
-      }
-    }
-    if (n_used == 1 || counters == nullptr) continue;
-    // ---- in-launch split-K merge: the last partition to arrive combines all of them
-    // (guide §5 "In-launch split-K reduction": plain slab stores, every wave drains, one agent
-    // release + ticket; the last arriver acquires, merges and re-arms the counter).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int* ctr = counters + seq * n_kv + h;
-      const int t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = (t == n_used - 1);
-      if (last) {
-        __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-    if (!last) continue;
-    for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
-      const int c = idx / kHD, d = idx % kHD;
-      const int hq = h * G + c;
-      const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
-      float M = kNegBig;
-      for (int p = 0; p < n_used; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
-      float O = 0.f, L = 0.f;
-      for (int p = 0; p < n_used; ++p) {
-        const float f = exp2f(part_ml[2 * (base + p)] - M);
-        O += f * part_o[(base + p) * kHD + d];
-        L += f * part_ml[2 * (base + p) + 1];
-      }
+    const int hq = h * G + c;
+    if (n_eff == 1) {
       out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
+    } else {
+      const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + blockIdx.z;
+      part_o[pi * kHD + d] = O;
+      if (d == 0) {
+        part_ml[2 * pi] = M;
+        part_ml[2 * pi + 1] = L;
+      }
     }
-    return;  // every partition has arrived
+  }
+  if (n_eff == 1 || counters == nullptr) return;
+  // ---- in-launch split-K merge: the last workgroup to arrive combines the partials
+  // (guide §5 "In-launch split-K reduction": plain slab stores, every wave drains, one agent
+  // release + ticket; the last arriver acquires, merges and re-arms the counter).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* ctr = counters + seq * n_kv + h;
+    const int t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == n_eff - 1);
+    if (last) {
+      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
+    const int c = idx / kHD, d = idx % kHD;
+    const int hq = h * G + c;
+    const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
+    float M = kNegBig;
+    for (int p = 0; p < n_eff; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
+    float O = 0.f, L = 0.f;
+    for (int p = 0; p < n_eff; ++p) {
+      const float f = exp2f(part_ml[2 * (base + p)] - M);
+      O += f * part_o[(base + p) * kHD + d];
+      L += f * part_ml[2 * (base + p) + 1];
+    }
+    out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
   }
 }
 
@@ -424,10 +427,10 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(bf16_t* __rest
                                                                   const float* __restrict__ part_o,
                                                                   const float* __restrict__ part_ml,
                                                                   const int* __restrict__ context_lens, int n_q,
-                                                                  int out_stride, int n_parts) {
+                                                                  int out_stride, int n_parts, int z) {
   const int hq = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
   const int ctx = context_lens[seq];
-  const int n_used = (ctx + kPart - 1) / kPart;
+  const int n_used = min((ctx + kPart - 1) / kPart, z);  // one partial per partition workgroup
   bf16_t* o = out + static_cast<int64_t>(seq) * out_stride + hq * kHD;
   if (ctx <= 0) {
     o[d] = 0;
@@ -860,7 +863,7 @@ static int decode_launch(void* out, const void* q, const QkvIn& qi, const void* 
   dim3 g2(n_q, n_seqs);
   paged_decode_reduce_kernel<kDecodePart><<<g2, 128, 0, stream>>>(
       static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
-      static_cast<const int*>(context_lens), n_q, out_stride, n_parts);
+      static_cast<const int*>(context_lens), n_q, out_stride, n_parts, static_cast<int>(grid.z));
   return PK_CHECK_LAUNCH();
 }
 

@@ -31,7 +31,7 @@ def block_tables_for(ctxs, bs, num_blocks, max_blocks, seed=0):
 
 
 @pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 32), (32, 8, 96), (4, 4, 32), (16, 1, 64)])
-@pytest.mark.parametrize("ctxs", [[1, 5, 32, 33, 100], [512, 513, 1200, 7], [2048, 1]])
+@pytest.mark.parametrize("ctxs", [[1, 5, 32, 33, 100], [512, 513, 1200, 7], [2048, 1], [5000, 3, 2600]])
 def test_decode(nq, nkv, bs, ctxs):
     max_blocks = (max(ctxs) + bs - 1) // bs + 3
     nb = sum((c + bs - 1) // bs for c in ctxs) + 4
