@@ -230,6 +230,11 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
   __shared__ float ml_lds[NW][16][2];
   __shared__ int last;
   __shared__ int bt_s[kPart / 8 + 2];  // this partition's block-table window (LDS: lookups use lgkmcnt)
+  // FROM_QKV, new token folded in (see below): its rotated k, its v and its G scores
+  __shared__ __attribute__((aligned(16))) bf16_t kn_s[kHD];
+  __shared__ float vn_s[kHD];
+  __shared__ float sn_s[16];
+  static_assert(64 * NW >= 256, "the new-token scores use 16 lanes per query head, G <= 16");
   const int h = blockIdx.x, seq = blockIdx.y;
 #if PK_DECODE_BT_PREFETCH
   // the first partition's block-table window, requested before anything else so its round
@@ -260,14 +265,22 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
   // (prefetching the first K/V step across the q preparation below was measured: it pushes
   // the kernel to 256 VGPRs + AGPRs, one wave per SIMD, and is slower overall)
   bf16x8_t qf[4];
+  // fold: the workgroup holding the new token (key ctx - 1) keeps its k / v in LDS, attends to
+  // keys [0, ctx - 1) from the cache and adds key ctx - 1 from LDS in the final combine; the
+  // cache write goes out at the end of the kernel.  Writing the row first and reading it back
+  // through the cache cost 4-5 us per launch at 384-512 keys (the scattered 2-byte V^T stores
+  // and the K tile stores land on lines the waves are about to stream).
+  bool fold = false;
+  int slot = -1;
   if constexpr (FROM_QKV) {
     __shared__ __attribute__((aligned(16))) bf16_t q_s[16][kHD];
     const int N = (n_q + 2 * n_kv) * kHD;
     const int64_t slab = static_cast<int64_t>(qi.M) * N;
     const float* base = qi.partial + static_cast<int64_t>(seq) * N;
     const float* cs = qi.cos_sin + static_cast<int64_t>(qi.positions[seq]) * kHD;
-    const int slot = qi.slots[seq];
+    slot = qi.slots[seq];
     const bool writer = slot >= 0 && static_cast<int>(blockIdx.z) == (n_used - 1) % static_cast<int>(gridDim.z);
+    fold = writer && qi.positions[seq] == ctx - 1;
     const int n_items = G * 64 + (writer ? 128 : 0);
     for (int it = threadIdx.x; it < n_items; it += 64 * NW) {
       int col, j;
@@ -308,22 +321,38 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
         if (it < G * 64) {
           q_s[it >> 6][j] = ra;
           q_s[it >> 6][j + 64] = rb;
+        } else if (fold) {
+          kn_s[j] = ra;
+          kn_s[j + 64] = rb;
         } else {
           bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * n_kv + h) * bs * kHD;
           d[kcache_off(slot % bs, j)] = ra;
           d[kcache_off(slot % bs, j + 64)] = rb;
         }
+      } else if (fold) {
+        vn_s[j] = bf2f(f2bf(a));
+        vn_s[j + 64] = bf2f(f2bf(b));
       } else {
         bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs + slot % bs;
         d[static_cast<int64_t>(j) * bs] = f2bf(a);
         d[static_cast<int64_t>(j + 64) * bs] = f2bf(b);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new k/v rows are in L2 before any wave reads them
+    if (!fold) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new k/v rows are in L2 before any wave reads them
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
       qf[kk] = r < G ? *reinterpret_cast<const bf16x8_t*>(&q_s[r][32 * g + 8 * kk]) : zero8();
+    if (fold) {  // scores of the new key, 16 lanes per query head (read after the combine's barrier)
+      const int c = threadIdx.x >> 4, part = threadIdx.x & 15;
+      float sdot = 0.f;
+      if (c < G)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sdot += bf2f(q_s[c][8 * part + e]) * bf2f(kn_s[8 * part + e]);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) sdot += __shfl_xor(sdot, o, 64);
+      if (c < G && part == 0) sn_s[c] = sdot * scale2;
+    }
   } else {
     load_q(qf, q + static_cast<int64_t>(seq) * q_stride + (h * G + r) * kHD, r < G);
   }
@@ -333,11 +362,12 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
   // the softmax), so it combines its waves and writes ONE partial at the end: no LDS combine /
   // partial store between partitions and gridDim.z partials to merge instead of n_parts.
   const int n_eff = min(n_used, static_cast<int>(gridDim.z));  // partials of this sequence
+  const int ctx_c = fold ? ctx - 1 : ctx;  // keys read from the cache
   WaveState st;
   init_state(st);
   for (int part = blockIdx.z; part < n_used; part += gridDim.z) {
     const int begin = part * kPart;
-    const int end = min(ctx, begin + kPart);
+    const int end = min(ctx_c, begin + kPart);
     const int b0 = begin / bs, nblk = (end - 1) / bs - b0 + 1;
     __syncthreads();  // the previous partition's block-table readers are done
 #if PK_DECODE_BT_PREFETCH
@@ -349,7 +379,9 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
         bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
     __syncthreads();
     KVFrag fa;
-    attend(st, qf, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w, end, NW * kStep, ctx, ctx - 1, scale2, fa);
+    if (end > begin)
+      attend(st, qf, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w, end, NW * kStep, ctx_c, ctx_c - 1, scale2,
+             fa);
   }
   const float lsum = col_sum(st.l);
 #pragma unroll
@@ -366,12 +398,19 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     float M = kNegBig;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
+    const float sn = fold ? sn_s[c] : kNegBig;
+    M = fmaxf(M, sn);
     float O = 0.f, L = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) {
       const float f = exp2f(ml_lds[ww][c][0] - M);
       O += f * o_lds[ww][c][d];
       L += f * ml_lds[ww][c][1];
+    }
+    if (fold) {  // key ctx - 1: P rounded to bf16 for the PV product as in attend_step
+      const float f = exp2f(sn - M);
+      O += bf2f(f2bf(f)) * vn_s[d];
+      L += f;
     }
     const int hq = h * G + c;
     if (n_eff == 1) {
@@ -383,6 +422,16 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
         part_ml[2 * pi] = M;
         part_ml[2 * pi + 1] = L;
       }
+    }
+  }
+  if (fold) {  // the new token's row into the paged cache, off the attention's critical path
+    const int t = threadIdx.x;
+    if (t < kHD) {
+      bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * n_kv + h) * bs * kHD;
+      d[kcache_off(slot % bs, t)] = kn_s[t];
+    } else if (t < 2 * kHD) {
+      bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs + slot % bs;
+      d[static_cast<int64_t>(t - kHD) * bs] = f2bf(vn_s[t - kHD]);
     }
   }
   if (n_eff == 1 || counters == nullptr) return;

@@ -59,17 +59,21 @@ def main():
         N = (NQ + 2 * NKV) * D
         slab = torch.randn(4 * B * N, device="cuda") * 0.05
         gb = B * ctx * NKV * D * 2 * 2 / 1e9
+        # split-partition builds (PK_DECODE_PART < 512) need the partial buffers; q path merges in-launch
+        part_o = torch.empty(B * NQ * 8 * D, device="cuda")
+        part_ml = torch.empty(B * NQ * 8 * 2, device="cuda")
+        ctrs = torch.zeros(B * NKV, dtype=torch.int32, device="cuda")
 
         def call_q(f, i):
             k, v = layers[i % 4]
-            rc = f(out.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), bt.data_ptr(), cl.data_ptr(), None, None,
-                   None, B, NQ, NKV, BS, maxb, NQ * D, NQ * D, 0.088, 512, st())
+            rc = f(out.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), bt.data_ptr(), cl.data_ptr(), part_o.data_ptr(),
+                   part_ml.data_ptr(), ctrs.data_ptr(), B, NQ, NKV, BS, maxb, NQ * D, NQ * D, 0.088, 512, st())
             assert rc == 0, rc
 
         def call_qkv(g_, i):
             k, v = layers[i % 4]
             rc = g_(out.data_ptr(), slab.data_ptr(), 4, B, pos.data_ptr(), cs.data_ptr(), slots.data_ptr(),
-                    k.data_ptr(), v.data_ptr(), bt.data_ptr(), cl.data_ptr(), None, None, B, NQ, NKV, BS, maxb,
+                    k.data_ptr(), v.data_ptr(), bt.data_ptr(), cl.data_ptr(), part_o.data_ptr(), part_ml.data_ptr(), B, NQ, NKV, BS, maxb,
                     NQ * D, 0.088, 512, st())
             assert rc == 0, rc
 
