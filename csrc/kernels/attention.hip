@@ -99,8 +99,8 @@ struct KVFrag {
 // bt[i - bt_base] = physical block of logical block i; `lim` bounds the tokens a load may touch
 // (past it the address is clamped, the data never used), so the block lookups stay inside the
 // caller's block-table window.  K comes from the fragment-native cache tile of step s (common.h
-// kcache_off: one contiguous KiB per load instruction); V^T rows are 64 B of 32 keys, lane group
-// g reading keys 8g..8g+7 (ldkv: plain loads; PK_DECODE_KV_NT=1 makes them non-temporal).
+// kcache_off: one contiguous KiB per load instruction); V likewise (common.h vcache_off): lane
+// (r, g) reads keys 8g..8g+7 of channel 16 dt + r, one contiguous KiB per d-tile (ldkv: plain loads; PK_DECODE_KV_NT=1 makes them non-temporal).
 __device__ __forceinline__ void load_kv(KVFrag& f, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                                         int64_t blk_stride, const int* __restrict__ bt, int bt_base, int bs, int s,
                                         int lim) {
@@ -116,9 +116,9 @@ __device__ __forceinline__ void load_kv(KVFrag& f, const bf16_t* __restrict__ kc
   int tok0 = s + 8 * g;
   tok0 = min(tok0, ((lim - 1) >> 3) << 3);
   const int blk = bt[tok0 / bs - bt_base];
-  const bf16_t* p = vc + blk * blk_stride + r * bs + (tok0 % bs);
+  const bf16_t* p = vc + blk * blk_stride + vcache_off(tok0 % bs, r);  // + 512 per 16-channel tile
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt) f.v[dt] = ldkv(p + dt * 16 * bs);
+  for (int dt = 0; dt < 8; ++dt) f.v[dt] = ldkv(p + dt * 512);
 }
 
 __device__ __forceinline__ void attend_step(WaveState& st, const bf16x8_t (&qf)[4], const KVFrag& f, int s,
@@ -333,9 +333,9 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
         vn_s[j] = bf2f(f2bf(a));
         vn_s[j + 64] = bf2f(f2bf(b));
       } else {
-        bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs + slot % bs;
-        d[static_cast<int64_t>(j) * bs] = f2bf(a);
-        d[static_cast<int64_t>(j + 64) * bs] = f2bf(b);
+        bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs;
+        d[vcache_off(slot % bs, j)] = f2bf(a);
+        d[vcache_off(slot % bs, j + 64)] = f2bf(b);
       }
     }
     if (!fold) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new k/v rows are in L2 before any wave reads them
@@ -430,8 +430,8 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
       bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * n_kv + h) * bs * kHD;
       d[kcache_off(slot % bs, t)] = kn_s[t];
     } else if (t < 2 * kHD) {
-      bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs + slot % bs;
-      d[static_cast<int64_t>(t - kHD) * bs] = f2bf(vn_s[t - kHD]);
+      bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs;
+      d[vcache_off(slot % bs, t - kHD)] = f2bf(vn_s[t - kHD]);
     }
   }
   if (n_eff == 1 || counters == nullptr) return;
@@ -599,7 +599,7 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
       // K: the step's fragment-native tile is one contiguous 8 KiB (piece pv at pv * 8)
       const int tok = isk ? s0 : min(s0 + 8 * (pv & 3), ((k_end - 1) >> 3) << 3);
       const int64_t base = static_cast<int64_t>(bt[tok / bs]) * blk_stride;
-      const bf16_t* src = isk ? kch + base + (tok % bs) * kHD + pv * 8 : vch + base + (pv >> 2) * bs + tok % bs;
+      const bf16_t* src = isk ? kch + base + (tok % bs) * kHD + pv * 8 : vch + base + vcache_off(tok % bs, pv >> 2);
       stage[i] = *reinterpret_cast<const u32x4*>(src);
     }
   };
@@ -729,8 +729,8 @@ __global__ void __launch_bounds__(64 * NW, 2) paged_prefill_mfma32_kernel(
       const int64_t base = static_cast<int64_t>(bt[tok / bs]) * blk_stride;
       // K: fragment-native tile of 32 tokens, piece (ch, kpl) (common.h kcache_off)
       ks[j] = *reinterpret_cast<const u32x4*>(kch + base + (tok % bs) * kHD + ((ch << 6) | kpl) * 8);
-      // V^T: channel 16 ch + vdl, keys 8 vkg .. of the same 32-token tile
-      vs[j] = *reinterpret_cast<const u32x4*>(vch + base + (16 * ch + vdl) * bs + tok % bs + 8 * vkg);
+      // V: channel 16 ch + vdl, keys 8 vkg .. of the same 32-token tile (common.h vcache_off)
+      vs[j] = *reinterpret_cast<const u32x4*>(vch + base + vcache_off(tok % bs + 8 * vkg, 16 * ch + vdl));
     }
   };
   auto store_tile = [&](int buf) {

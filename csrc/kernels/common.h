@@ -59,6 +59,17 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
 // non-temporal loads -- which lose in the captured decode step, so they are off).
 // Writers scatter one token's 128 dims with 8-dim (16-byte) granules; RoPE halves d and d+64
 // stay 16-byte aligned.
+// V cache, fragment-native like K: per 32-token tile, [d / 16][key / 8][d % 16][key % 8], so the
+// 8 consecutive keys of one channel (a PV MFMA operand) are 16 contiguous bytes, a wave's 64
+// operand loads of one 16-channel tile are one contiguous KiB, and a decode token's 128 channels
+// land in 16 cache lines (8 runs of 16 two-byte stores 16 bytes apart) instead of 128 separate
+// 64-byte V^T rows (those per-token stores cost 2.6-2.9 us per decode-attention launch at 384-512
+// keys, profiles/r2_decode_ab.txt).
+__host__ __device__ __forceinline__ int vcache_off(int k_in_block, int d) {
+  const int k = k_in_block & 31;
+  return (k_in_block >> 5) * 4096 + ((((d >> 4) << 2) + (k >> 3)) * 16 + (d & 15)) * 8 + (k & 7);
+}
+
 __host__ __device__ __forceinline__ int kcache_off(int k_in_block, int d) {
   const int k = k_in_block & 31;
   const int lane = 16 * (d >> 5) + 4 * (k >> 3) + (k & 3);

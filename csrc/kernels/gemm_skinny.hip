@@ -239,11 +239,12 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
           if (m >= M) break;
           const int slot = args.slots[m];
           if (slot < 0) continue;
-          bf16_t* d = args.v_cache + ((static_cast<int64_t>(slot / bs) * nkv + kh) * 128 + d0) * bs + slot % bs;
-          d[0] = f2bf(a[i].x);
-          d[bs] = f2bf(a[i].y);
-          d[2 * bs] = f2bf(a[i].z);
-          d[3 * bs] = f2bf(a[i].w);
+          bf16_t* d = args.v_cache + (static_cast<int64_t>(slot / bs) * nkv + kh) * 128 * bs;
+          const int vo = vcache_off(slot % bs, d0);  // channels d0 .. d0 + 3 are 8 elements apart
+          d[vo] = f2bf(a[i].x);
+          d[vo + 8] = f2bf(a[i].y);
+          d[vo + 16] = f2bf(a[i].z);
+          d[vo + 24] = f2bf(a[i].w);
         }
       }
     }
@@ -866,9 +867,9 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
       d[kcache_off(slot % bs, lane + 64)] = f2bf(b * co + a * si);
     }
   } else {
-    bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * nkv + (h - nq - nkv)) * 128 * bs + slot % bs;
-    d[static_cast<int64_t>(lane) * bs] = f2bf(a);
-    d[static_cast<int64_t>(lane + 64) * bs] = f2bf(b);
+    bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * nkv + (h - nq - nkv)) * 128 * bs;
+    d[vcache_off(slot % bs, lane)] = f2bf(a);
+    d[vcache_off(slot % bs, lane + 64)] = f2bf(b);
   }
 }
 

@@ -87,9 +87,10 @@ __global__ void __launch_bounds__(256) rope_and_cache_kernel(bf16_t* __restrict_
         const uint32_t hi = v0[static_cast<int64_t>(2 * j + 1) * q_stride + u];
         w[j] = lo | (hi << 16);
       }
-      u32x4* dst = reinterpret_cast<u32x4*>(vc + ((static_cast<int64_t>(blk) * nkv + kh) * kHD + d) * bs + k0);
+      bf16_t* vb = vc + (static_cast<int64_t>(blk) * nkv + kh) * kHD * bs;  // 8 keys per 16-byte piece
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dst[q] = u32x4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<u32x4*>(vb + vcache_off(k0 + 8 * q, d)) = u32x4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
     }
     return;
   }
@@ -98,7 +99,7 @@ __global__ void __launch_bounds__(256) rope_and_cache_kernel(bf16_t* __restrict_
     const int slot = slot_s[tt];
     if (slot < 0) continue;
     const int kh = e / kHD, d = e % kHD;
-    vc[((static_cast<int64_t>(slot / bs) * nkv + kh) * kHD + d) * bs + slot % bs] =
+    vc[(static_cast<int64_t>(slot / bs) * nkv + kh) * kHD * bs + vcache_off(slot % bs, d)] =
         qkv[static_cast<int64_t>(t0 + tt) * q_stride + voff + e];
   }
 }

@@ -99,6 +99,29 @@ def kcache_index(bs: int, device=None) -> torch.Tensor:
     return _KIDX[key]
 
 
+_VIDX: dict = {}
+
+
+def vcache_index(bs: int, device=None) -> torch.Tensor:
+    """[bs, 128] flat position of V element (token, dim) inside one (block, kv head) slab of the
+    paged V cache: per 32-token tile [d / 16][key / 8][d % 16][key % 8] (common.h ``vcache_off``)."""
+    if bs % 32:
+        raise ValueError(f"the V-cache layout needs a block size that is a multiple of 32, got {bs}")
+    key = (bs, str(device))
+    if key not in _VIDX:
+        k = torch.arange(bs).view(bs, 1)
+        d = torch.arange(128).view(1, 128)
+        kt = k & 31
+        _VIDX[key] = ((k >> 5) * 4096 + ((((d >> 4) << 2) + (kt >> 3)) * 16 + (d & 15)) * 8 + (kt & 7)).to(device)
+    return _VIDX[key]
+
+
+def v_cache_logical(v_cache: torch.Tensor) -> torch.Tensor:
+    """The physical V cache [blocks, n_kv, 128, bs] as logical (token, dim) rows [blocks, n_kv, bs, 128]."""
+    nb, nkv, hd, bs = v_cache.shape
+    return v_cache.reshape(nb, nkv, bs * hd)[:, :, vcache_index(bs, v_cache.device).view(-1)].view(nb, nkv, bs, hd)
+
+
 def k_cache_logical(k_cache: torch.Tensor) -> torch.Tensor:
     """The physical K cache [blocks, n_kv, bs, 128] as logical (token, dim) rows."""
     nb, nkv, bs, hd = k_cache.shape
@@ -126,7 +149,10 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
             pos = kcache_index(bs, k_cache.device)[off]  # [n, 128] fragment-native positions
             kflat[blk.view(n, 1, 1), torch.arange(nkv_, device=k_cache.device).view(1, nkv_, 1),
                   pos.view(n, 1, hd)] = k[valid].to(k_cache.dtype)
-            v_cache[blk, :, :, off] = v[valid].to(v_cache.dtype)
+            vflat = v_cache.view(v_cache.shape[0], nkv_, bs * hd)
+            vpos = vcache_index(bs, v_cache.device)[off]
+            vflat[blk.view(n, 1, 1), torch.arange(nkv_, device=v_cache.device).view(1, nkv_, 1),
+                  vpos.view(n, 1, hd)] = v[valid].to(v_cache.dtype)
     return q
 
 
@@ -137,7 +163,7 @@ def gather_kv(k_cache, v_cache, block_table, n_tokens):
     nb = (n_tokens + bs - 1) // bs
     blocks = block_table[:nb].long()
     k = k_cache_logical(k_cache[blocks]).permute(0, 2, 1, 3).reshape(nb * bs, k_cache.shape[1], -1)[:n_tokens]
-    v = v_cache[blocks].permute(0, 3, 1, 2).reshape(nb * bs, v_cache.shape[1], -1)[:n_tokens]
+    v = v_cache_logical(v_cache[blocks]).permute(0, 2, 1, 3).reshape(nb * bs, v_cache.shape[1], -1)[:n_tokens]
     return k, v
 
 
