@@ -15,8 +15,9 @@
 //     lane reads 64 contiguous bytes of its key row (K) and of its query row (Q);
 //   * keys: tile t, row r holds key 8*(r>>2) + 4t + (r&3), so after QK^T lane group g holds
 //     keys 8g..8g+7 of its column -- exactly the P^T B-fragment layout -- and the matching
-//     V^T A-fragment is 8 consecutive tokens of one channel: one 16-byte load from the
-//     transposed V cache [block][kv_head][d][block_size].
+//     V^T A-fragment is 8 consecutive tokens of one channel: one 16-byte load from the V
+//     cache, stored per (block, kv head) in fragment-native 32-token tiles
+//     [d / 16][key / 8][d % 16][key % 8] (common.h vcache_off: a wave's d-tile is one KiB).
 // Softmax runs in base 2 with the 1/sqrt(d) scale folded into one multiply.  K/V go straight
 // from global memory to VGPRs (decode is HBM-bound: guide §5 "GEMV / M <= 16" row); waves of a
 // workgroup that read the same K/V tile hit the CU's L1.
