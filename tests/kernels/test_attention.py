@@ -187,9 +187,12 @@ def test_rope_and_cache_aligned_runs(nq, nkv, bs):
 @pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 64), (16, 4, 32)])
 @pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [512, 513, 1300, 0]])
 @pytest.mark.parametrize("S", [1, 4])
-def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S):
+@pytest.mark.parametrize("pos_last", [True, False])
+def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S, pos_last):
     """Attention kernel fed by the QKV split-K slabs (reduce + RoPE + cache write folded in) vs
-    the unfused kernels: same output, same K/V cache contents; ctx 0 = padded row (slot -1)."""
+    the unfused kernels: same output, same K/V cache contents; ctx 0 = padded row (slot -1).
+    pos_last: the new token's position is ctx - 1 (its key is folded in from LDS and the cache
+    row stored at the end); otherwise the kernel writes the row first and attends through the cache."""
     from polykey_service_amd.ops import gemm
     d = "cuda"
     B = len(ctxs)
@@ -199,7 +202,7 @@ def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S):
     kc, vc = make_cache(nb, nkv, bs, seed=3)
     bt = block_tables_for([max(c, 1) for c in ctxs], bs, nb, max_blocks, seed=3)
     cl = torch.tensor(ctxs, dtype=torch.int32)
-    pos = (cl - 1).clamp(min=0)
+    pos = (cl - 1).clamp(min=0) if pos_last else (cl // 2).clamp(min=0)
     slots = torch.tensor([int(bt[i, (c - 1) // bs]) * bs + (c - 1) % bs if c > 0 else -1 for i, c in enumerate(ctxs)],
                          dtype=torch.int32)
     g = torch.Generator().manual_seed(5)
