@@ -34,7 +34,10 @@ constexpr int kHD = 128;
 constexpr int kStep = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1e30f;
-constexpr int kDecodeWaves = 4;  // waves per (seq, kv head, partition); 8 measured ~10 % slower at 384 keys
+#ifndef PK_DECODE_WAVES
+#define PK_DECODE_WAVES 4
+#endif
+constexpr int kDecodeWaves = PK_DECODE_WAVES;  // waves per (seq, kv head, partition); 8 measured ~10 % slower at 384 keys
 int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
