@@ -24,7 +24,7 @@ from .. import proto
 from ..engine.sequence import SamplingParams
 from ..engine.tokenizer import IncrementalDetokenizer
 from ..service.base import RequestContext, ToolError, ok_status
-from ..service.tool_calls import run_chat, validate_tools
+from ..service.tool_calls import run_chat, tool_rounds, validate_tools
 
 
 def _status():
@@ -100,9 +100,13 @@ class LLMTool:
         if not isinstance(msgs, list) or not msgs:
             raise ToolError("INVALID_ARGUMENT", "llm.chat requires a non-empty 'messages' list")
         sp = self._sampling(params)
+        try:
+            rounds = tool_rounds(params.get("max_tool_rounds"))
+        except ValueError as e:
+            raise ToolError("INVALID_ARGUMENT", str(e))
         oc = await run_chat(self.llm, self.tok.chat_template, msgs, sp, tc[0], tc[1], router=self.router,
                             execute=bool(params.get("execute_tools")), secret_id=params.get("tool_secret_id"),
-                            max_rounds=int(params.get("max_tool_rounds", 3)), request_id=ctx.request_id)
+                            max_rounds=rounds, request_id=ctx.request_id)
         resp = proto.ExecuteToolResponse(status=_status())
         if params.get("return") == "struct" or oc.tool_calls or oc.executed:
             m = oc.metrics or {}

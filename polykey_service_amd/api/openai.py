@@ -21,7 +21,7 @@ from typing import Any, Dict, List, Optional
 
 from ..engine.sequence import SamplingParams
 from ..service.base import ToolError
-from ..service.tool_calls import run_chat, validate_tools
+from ..service.tool_calls import run_chat, tool_rounds, validate_tools
 
 _SAMPLING_KEYS = ("max_tokens", "temperature", "top_p", "top_k", "min_p", "seed", "stop", "ignore_eos",
                   "stop_token_ids", "cache_salt")
@@ -161,9 +161,10 @@ def create_app(router):
         rid = "chatcmpl-" + uuid.uuid4().hex[:24]
         created = int(time.time())
         try:
+            rounds = tool_rounds(body.get("max_tool_rounds"))
             oc = await run_chat(llm, llm.tokenizer.chat_template, msgs, sp, tools, choice, router=router,
                                 execute=bool(body.get("execute_tools")), secret_id=body.get("tool_secret_id"),
-                                max_rounds=int(body.get("max_tool_rounds", 3)), request_id=rid)
+                                max_rounds=rounds, request_id=rid)
         except (ValueError, TypeError) as e:
             return err(400, str(e))
         usage = _usage(oc.prompt_tokens, oc.completion_tokens, oc.metrics)

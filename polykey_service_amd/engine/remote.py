@@ -71,10 +71,12 @@ class EngineServer:
     engine until a "stop" frame (or the connection closing); outputs go back from the engine
     thread through :meth:`AsyncLLM.set_external_sink`."""
 
-    def __init__(self, llm, host: str = "127.0.0.1", port: int = 0):
+    def __init__(self, llm, host: str = "127.0.0.1", port: int = 0, token: Optional[str] = None):
         self.llm = llm
         self.lsock = socket.create_server((host, port))
         self.port = self.lsock.getsockname()[1]
+        # shared secret the front end must present in its first frame (None: no check)
+        self.token = token
         self._wlock = threading.Lock()
         self._conn: Optional[socket.socket] = None
         self._final: Dict[str, List] = {}  # rid -> tokens so far (final-only requests)
@@ -104,8 +106,24 @@ class EngineServer:
             except OSError:
                 pass  # front end gone: serve() sees the closed connection and stops
 
+    def _accept(self) -> socket.socket:
+        """The first connection whose hello frame carries the shared token (others are closed)."""
+        while True:
+            conn, _ = self.lsock.accept()
+            if self.token is None:
+                return conn
+            conn.settimeout(10.0)
+            try:
+                hello = _recv(conn)
+            except (OSError, ValueError, msgpack.exceptions.ExtraData, msgpack.exceptions.UnpackException):
+                hello = None
+            if isinstance(hello, dict) and hello.get("op") == "hello" and hello.get("token") == self.token:
+                conn.settimeout(None)
+                return conn
+            conn.close()
+
     def serve(self) -> None:
-        conn, _ = self.lsock.accept()
+        conn = self._accept()
         conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self._conn = conn
         self.llm.set_external_sink(self._sink)
@@ -119,6 +137,7 @@ class EngineServer:
                         self._final[msg["rid"]] = []
                     self.llm.submit_external(msg["rid"], msg["prompt"], SamplingParams(**msg["params"]))
                 elif msg["op"] == "abort":
+                    self._final.pop(msg["rid"], None)  # the engine reports nothing more for it
                     self.llm.abort_external(msg["rid"])
         finally:
             self.llm.set_external_sink(None)
@@ -134,7 +153,8 @@ class RemoteEngine:
     """Front-end handle of an engine in another process; duck-types ``AsyncLLM`` for the
     router (:class:`~polykey_service_amd.adapters.local_llm.ReplicaPool`) and the tools."""
 
-    def __init__(self, addr: Tuple[str, int], tokenizer, name: str = "remote", connect_timeout: float = 120.0):
+    def __init__(self, addr: Tuple[str, int], tokenizer, name: str = "remote", connect_timeout: float = 120.0,
+                 token: Optional[str] = None):
         self.tokenizer = tokenizer
         self.name = name
         self.on_fatal = None
@@ -152,6 +172,8 @@ class RemoteEngine:
         self.sock.settimeout(None)
         self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self._wlock = threading.Lock()
+        if token is not None:
+            _send(self.sock, self._wlock, {"op": "hello", "token": token})
         self._lock = threading.Lock()
         self._streams: Dict[str, Tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
         self._closed = False
@@ -271,16 +293,28 @@ def dp_gateway(llm, st, group=None):
     front end and blocks until the front end stops it (returns None); rank 0 returns a
     :class:`~polykey_service_amd.adapters.local_llm.ReplicaPool` over its own ``llm`` and a
     :class:`RemoteEngine` per other rank."""
+    import os
+    import secrets
+
     import torch.distributed as dist
 
     from ..adapters.local_llm import ReplicaPool
-    server = EngineServer(llm) if st.rank != 0 else None
-    ports: List = [None] * st.world_size
-    dist.all_gather_object(ports, server.port if server is not None else 0, group=group)
+    # one node: loopback only; several nodes: every rank listens on all interfaces and
+    # advertises its host name (POLYKEY_GATEWAY_HOST overrides what it advertises)
+    single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(st.world_size))) == st.world_size
+    bind = "127.0.0.1" if single_node else "0.0.0.0"
+    advertise = os.environ.get("POLYKEY_GATEWAY_HOST") or ("127.0.0.1" if single_node else socket.gethostname())
+    # rank 0 draws the shared token; every engine server accepts only a front end that presents it
+    tok = [secrets.token_hex(16) if st.rank == 0 else None]
+    dist.broadcast_object_list(tok, src=0, group=group)
+    server = EngineServer(llm, host=bind, token=tok[0]) if st.rank != 0 else None
+    addrs: List = [None] * st.world_size
+    dist.all_gather_object(addrs, (advertise, server.port) if server is not None else None, group=group)
     if server is not None:
         server.serve()
         return None
-    remotes = [RemoteEngine(("127.0.0.1", ports[r]), llm.tokenizer, name=f"rank{r}") for r in range(1, st.world_size)]
+    remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0])
+               for r in range(1, st.world_size)]
     return ReplicaPool([llm] + remotes)
 
 

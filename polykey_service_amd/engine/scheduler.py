@@ -238,10 +238,10 @@ class Scheduler:
                     st.prefills.append((seq, n))
                 st.scheduled.add(seq.seq_id)
                 st.budget -= n
-                i = self.running.index(seq) + 1  # preemption may have removed earlier entries
+                i = self._index(seq) + 1  # preemption may have removed earlier entries
                 continue
             # could not even fit this sequence alone: preempt it too
-            i = self.running.index(seq)
+            i = self._index(seq)
             self.running.remove(seq)
             self.bm.free_seq(seq.seq_id)
             seq.num_computed = 0
@@ -256,6 +256,10 @@ class Scheduler:
             st.decodes = [s for s in st.decodes if s.seq_id not in gone]
             st.prefills = [(s, n) for s, n in st.prefills if s.seq_id not in gone]
             st.budget = self.max_num_batched_tokens - len(st.decodes) - sum(n for _, n in st.prefills)
+
+    def _index(self, seq) -> int:
+        """Position of ``seq`` in ``running`` (kept sorted by seq id): O(log n), not a scan."""
+        return bisect.bisect_left(self.running, seq.seq_id, key=lambda s: s.seq_id)
 
     def _admit(self, st: "_Step") -> None:
         preempted = {s.seq_id for s in st.preempted}

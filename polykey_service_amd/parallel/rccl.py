@@ -18,6 +18,7 @@ error without blocking and raises; :meth:`RcclComm.abort` tears a hung communica
 from __future__ import annotations
 
 import ctypes
+import math
 import threading
 from typing import List, Optional, Sequence
 
@@ -198,7 +199,7 @@ class RcclComm:
         if sum(in_splits) != x.shape[0]:
             raise ValueError("all_to_allv: in_splits must cover dim 0 of x")
         x = x.contiguous()
-        row = x[0].numel() if x.dim() > 1 else 1
+        row = math.prod(x.shape[1:])  # 0-row inputs (an idle EP rank) are valid
         out = torch.empty((sum(out_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
         sc = [s * row for s in in_splits]
         rc = [s * row for s in out_splits]

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import dataclasses
 import json
+import os
 import uuid
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -129,6 +130,22 @@ def forced_call(generated: str, name: Optional[str], allowed: List[str], family:
                 raw = raw[:-len(tail)].rstrip()
                 break
         return _call(name, raw)
+
+
+# server-side cap on client-requested tool rounds (each round is a full generation that may run
+# gateway tools with model-written arguments)
+MAX_TOOL_ROUNDS = int(os.environ.get("POLYKEY_MAX_TOOL_ROUNDS", "8"))
+
+
+def tool_rounds(value: Any, default: int = 3, cap: Optional[int] = None) -> int:
+    """Validate a client's ``max_tool_rounds``: an integer >= 1, clamped to the server cap."""
+    if value is None:
+        value = default
+    if isinstance(value, bool) or not isinstance(value, (int, float)) or int(value) != value:
+        raise ValueError("max_tool_rounds must be an integer")
+    if value < 1:
+        raise ValueError("max_tool_rounds must be >= 1")
+    return min(int(value), MAX_TOOL_ROUNDS if cap is None else cap)
 
 
 def tool_names(tools: Optional[List[Dict[str, Any]]]) -> List[str]:

@@ -265,3 +265,13 @@ def test_forced_tool_choice_grpc(model_router):
                                "tool_choice": "required", "max_tokens": 4, "temperature": 0})
         d = proto.struct_to_dict(call(req, timeout=60).struct_output)
     assert d["finish_reason"] == "tool_calls" and d["tool_calls"][0]["function"]["name"] == "get_weather"
+
+
+def test_tool_rounds_are_validated_and_clamped():
+    from polykey_service_amd.service import tool_calls
+    assert tool_calls.tool_rounds(None) == 3
+    assert tool_calls.tool_rounds(2) == 2
+    assert tool_calls.tool_rounds(10 ** 6) == tool_calls.MAX_TOOL_ROUNDS
+    for bad in (0, -1, "3", 2.5, True, [1]):
+        with pytest.raises(ValueError):
+            tool_calls.tool_rounds(bad)

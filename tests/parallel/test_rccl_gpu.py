@@ -35,6 +35,15 @@ def test_collectives_one_rank(comm):
     comm.check()
 
 
+def test_all_to_allv_empty_rows(comm):
+    """An idle EP rank sends and receives [0, H]: zero counts everywhere must be a no-op."""
+    empty = torch.zeros((0, 4096), dtype=torch.bfloat16, device="cuda")
+    out = comm.all_to_allv(empty, [0], [0])
+    torch.cuda.synchronize()
+    assert out.shape == (0, 4096)
+    comm.check()
+
+
 def test_bad_arguments_raise(comm):
     x = torch.zeros(8, 8, device="cuda")
     with pytest.raises(ValueError):

@@ -102,3 +102,50 @@ def test_dead_engine_fails_requests():
     asyncio.run(go())
     remote.shutdown()
     llm.shutdown()
+
+
+def test_engine_server_rejects_a_front_end_without_the_token():
+    """The engine server serves only the front end presenting the shared token (dp_gateway draws
+    it on rank 0); an unauthenticated connection is closed and the server keeps listening."""
+    import socket as _socket
+    llm = _llm()
+    srv = EngineServer(llm, token="s3cret")
+    th = threading.Thread(target=srv.serve, daemon=True)
+    th.start()
+    intruder = _socket.create_connection(("127.0.0.1", srv.port))
+    intruder.sendall(b"\x05\x00\x00\x00hello")  # not a valid hello frame
+    intruder.settimeout(10)
+    assert intruder.recv(16) == b""  # closed by the server
+    intruder.close()
+    remote = RemoteEngine(("127.0.0.1", srv.port), llm.tokenizer, name="t", token="s3cret")
+    sp = SamplingParams(max_tokens=3, ignore_eos=True)
+    toks, _ = asyncio.run(remote.generate_all(PROMPT, sp))
+    assert len(toks) == 3
+    remote.shutdown()
+    th.join(10)
+    llm.shutdown()
+
+
+def test_abort_of_a_final_only_request_drops_its_buffer(served):
+    llm, remote = served
+
+    async def go():
+        agen = remote.generate(PROMPT, SamplingParams(max_tokens=200, ignore_eos=True), request_id="r-final",
+                               final_only=True)
+        task = asyncio.ensure_future(agen.__anext__())
+        await asyncio.sleep(0.3)
+        task.cancel()
+        try:
+            await task
+        except (asyncio.CancelledError, StopAsyncIteration):
+            pass
+        await agen.aclose()
+    asyncio.run(go())
+    import time as _t
+    deadline = _t.monotonic() + 5
+    # the EngineServer behind the fixture is reachable through the remote's peer: find it via gc
+    import gc
+    servers = [o for o in gc.get_objects() if isinstance(o, EngineServer)]
+    while _t.monotonic() < deadline and any("r-final" in s._final for s in servers):
+        _t.sleep(0.05)
+    assert not any("r-final" in s._final for s in servers)
