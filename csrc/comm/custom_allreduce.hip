@@ -14,7 +14,13 @@
 //      a fixed rank order (bit-identical on every rank) and writes bf16 output.
 //
 // No grid-wide barrier: chunk b only depends on the W workgroups b of the W ranks.  The epoch
-// lives in device memory (per workgroup), so the kernel replays correctly inside HIP graphs.
+// lives in device memory, so the kernels replay correctly inside HIP graphs.  It is ONE call
+// counter for every collective of the context (all-reduce, all-gather, fused reduce): every
+// workgroup of a call advances its share of the epoch array to the same value, so workgroup b
+// of the next call -- whatever its grid -- starts from the epoch every rank agrees on, and the
+// data-slot parity alternates per call.  A rank can run at most one call ahead of a peer (its
+// wait needs the peer's flag of that call), so a write into slot parity (e & 1) can never hit a
+// region a slow peer is still reading from call e - 1.
 // IPC buffers are allocated uncached (hipDeviceMallocUncached): peers' stores become visible
 // to polling loads without cache maintenance, and remote data reads are never served stale.
 // Failure: a peer that does not arrive within the wall-clock timeout sets the
@@ -33,13 +39,14 @@
 namespace {
 
 constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 256;
+constexpr int kMaxBlocks = 1024;  // workgroups of one call (flag rows)
+constexpr int kArBlocks = 256;    // grid cap of the one-shot / two-shot all-reduce and all-gather
 constexpr int kThreads = 512;
 
 struct Signals {                                 // at the start of every rank's IPC buffer
   uint32_t flag[kMaxBlocks][kMaxRanks];          // written by peers (remote stores)
   uint32_t flag2[kMaxBlocks][kMaxRanks];         // two-shot: reduce-scatter results published
-  uint32_t epoch[kMaxBlocks];                    // this rank's per-workgroup call counter
+  uint32_t epoch[kMaxBlocks];                    // this rank's call counter (all entries equal between calls)
   uint32_t error;                                // device-side copy of the sticky error word
 };
 
@@ -80,6 +87,14 @@ __device__ __forceinline__ void spin_wait(uint32_t* flag, uint32_t e, Signals* m
       break;
     }
   }
+}
+
+// Call epilogue: workgroup b stores the call's epoch into entries b, b + nb, ... of the epoch
+// array, so every entry holds the same value whatever grid the next call launches.
+__device__ __forceinline__ void end_call(Signals* my_sig, uint32_t e) {
+  for (int i = blockIdx.x + static_cast<int>(threadIdx.x) * static_cast<int>(gridDim.x); i < kMaxBlocks;
+       i += static_cast<int>(blockDim.x * gridDim.x))
+    my_sig->epoch[i] = e;
 }
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
@@ -147,7 +162,7 @@ __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __re
     }
     out[i] = make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
   }
-  if (threadIdx.x == 0) my_sig->epoch[b] = e;
+  end_call(my_sig, e);
 }
 
 // Bounded relaxed poll of this rank's flag[b][j] for every peer j, then one system acquire.
@@ -249,7 +264,7 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
     const uint4* res = reinterpret_cast<const uint4*>(peers->base[s] + res_slot);
     for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) out[i] = res[i];
   }
-  if (threadIdx.x == 0) my_sig->epoch[b] = e;
+  end_call(my_sig, e);
 }
 
 // All-gather along the last dim: every rank contributes rows x row16 16-byte units and receives
@@ -288,7 +303,128 @@ __global__ void __launch_bounds__(kThreads) allgather_1shot(const PeerPtrs* __re
 #pragma unroll
     for (int j = 0; j < W; ++j) out[(row * W + j) * row16 + col] = v[j];
   }
-  if (threadIdx.x == 0) my_sig->epoch[b] = e;
+  end_call(my_sig, e);
+}
+
+// Fused TP decode collective of a row-parallel projection (Llama o / down under TP; VERDICT r2
+// "fused TP decode collective"): in ONE launch
+//   1. sum this rank's split-K slabs [S, M, N] fp32 of the projection (or take its bf16 [M, N]
+//      partial when S == 0) and write the bf16 partial straight into this rank's IPC slot,
+//   2. publish, wait for the peers' flags of the same workgroup,
+//   3. sum the W partials over xGMI in rank order (bit-identical on every rank), round to bf16
+//      (the all-reduce's output), add it into the bf16 residual stream in place, and
+//   4. write per-(1024-column chunk, row) sums of squares of the new residual: the parts the
+//      NEXT projection's folded RMSNorm (RowScale) turns into rinv -- no normalised copy.
+// It replaces split-K reduce + one-shot all-reduce (with its copy-in) + residual/norm kernel.
+// Work items are (row, 1024-column chunk); workgroup b takes items b, b + nb, ...  A workgroup
+// is 128 threads x 8 columns.  Grid size is a host choice (<= kMaxBlocks): a shared-GPU
+// rehearsal keeps it small so every rank's grid is resident at once.
+__device__ __forceinline__ void unpack8f(const uint4& v, float* f) {
+  const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = bf2f(static_cast<uint16_t>(w4[q] & 0xffffu));
+    f[2 * q + 1] = bf2f(static_cast<uint16_t>(w4[q] >> 16));
+  }
+}
+
+__device__ __forceinline__ float rbf(float x) { return bf2f(static_cast<uint16_t>(pack2(x, 0.f) & 0xffffu)); }
+
+__device__ __forceinline__ float wave_sum64(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int W>
+__global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __restrict__ peers, int rank,
+                                                               size_t data_bytes, const float* __restrict__ slabs,
+                                                               int S, const uint4* __restrict__ partial,
+                                                               uint16_t* __restrict__ residual,
+                                                               float* __restrict__ parts, int M, int N,
+                                                               const Fail fail) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
+  __shared__ uint32_t e_s, err_s;
+  __shared__ float red[2];
+  if (threadIdx.x == 0) {
+    e_s = my_sig->epoch[b] + 1;
+    err_s = my_sig->error;
+  }
+  __syncthreads();
+  if (err_s) return;
+  const uint32_t e = e_s;
+  const size_t slot = kSigBytes + (e & 1u) * data_bytes;
+  const int nchunk = N >> 10;
+  const int items = M * nchunk;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + slot);
+  // 1. local split-K reduction -> bf16 partial in this rank's slot
+  for (int it = b; it < items; it += nb) {
+    const int r = it / nchunk, c = it - r * nchunk;
+    const int64_t off = static_cast<int64_t>(r) * N + (c << 10) + threadIdx.x * 8;  // element offset
+    uint4 pk;
+    if (S > 0) {
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int sidx = 0; sidx < S; ++sidx) {
+        const float4 p0 = *reinterpret_cast<const float4*>(slabs + sidx * slab + off);
+        const float4 p1 = *reinterpret_cast<const float4*>(slabs + sidx * slab + off + 4);
+        a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w;
+        a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
+      }
+      pk = make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
+    } else {
+      pk = partial[off >> 3];
+    }
+    mine[off >> 3] = pk;
+  }
+  // 2. publish (same protocol as the one-shot all-reduce), wait for every peer's workgroup b
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < W) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
+    __hip_atomic_store(&ps->flag[b][rank], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x < W) {
+    spin_wait(&my_sig->flag[b][threadIdx.x], e, my_sig, fail);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (__hip_atomic_load(&my_sig->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) err_s = 1u;
+  }
+  __syncthreads();
+  if (err_s) return;  // a peer never arrived: residual untouched, the engine fails the step
+  // 3./4. rank-ordered sum over xGMI, residual add, per-chunk sums of squares
+  const uint4* src[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) src[j] = reinterpret_cast<const uint4*>(peers->base[j] + slot);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int it = b; it < items; it += nb) {
+    const int r = it / nchunk, c = it - r * nchunk;
+    const int64_t off = static_cast<int64_t>(r) * N + (c << 10) + threadIdx.x * 8;
+    uint4 v[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) v[j] = src[j][off >> 3];
+    const uint4 rr = *reinterpret_cast<const uint4*>(residual + off);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc8(acc, v[j]);
+    float res[8];
+    unpack8f(rr, res);
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      res[q] = rbf(rbf(acc[q]) + res[q]);
+      ss += res[q] * res[q];
+    }
+    *reinterpret_cast<uint4*>(residual + off) =
+        make_uint4(pack2(res[0], res[1]), pack2(res[2], res[3]), pack2(res[4], res[5]), pack2(res[6], res[7]));
+    ss = wave_sum64(ss);
+    if (lane == 0) red[wid] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) parts[static_cast<int64_t>(c) * M + r] = red[0] + red[1];
+    __syncthreads();
+  }
+  end_call(my_sig, e);
 }
 
 }  // namespace
@@ -397,8 +533,8 @@ PK_EXPORT int pk_car_allreduce_bf16_algo(void* ctx, const void* inp, void* out, 
   if (bytes <= 0) return 0;
   if (bytes % 16 || static_cast<size_t>(bytes) > c->data_bytes) return -2;
   const int64_t n16 = bytes / 16;
-  if (blocks <= 0) blocks = static_cast<int>(std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, n16 / (kThreads * 2))));
-  blocks = std::min(blocks, kMaxBlocks);
+  if (blocks <= 0) blocks = static_cast<int>(std::min<int64_t>(kArBlocks, std::max<int64_t>(1, n16 / (kThreads * 2))));
+  blocks = std::min(blocks, kArBlocks);
   const uint4* in4 = static_cast<const uint4*>(inp);
   uint4* out4 = static_cast<uint4*>(out);
   if (algo == 0) algo = bytes <= kOneShotMax ? 1 : 2;
@@ -466,8 +602,8 @@ PK_EXPORT int pk_car_allgather(void* ctx, const void* inp, void* out, long long 
   if (rows <= 0 || row_bytes <= 0) return 0;
   if (row_bytes % 16 || static_cast<size_t>(rows * row_bytes) > c->data_bytes) return -2;
   const int64_t row16 = row_bytes / 16, n16 = rows * row16;
-  if (blocks <= 0) blocks = static_cast<int>(std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, n16 / (kThreads * 2))));
-  blocks = std::min(blocks, kMaxBlocks);
+  if (blocks <= 0) blocks = static_cast<int>(std::min<int64_t>(kArBlocks, std::max<int64_t>(1, n16 / (kThreads * 2))));
+  blocks = std::min(blocks, kArBlocks);
   const Fail fail{c->d_err, c->timeout_ticks};
   const uint4* in4 = static_cast<const uint4*>(inp);
   uint4* out4 = static_cast<uint4*>(out);
@@ -485,6 +621,48 @@ PK_EXPORT int pk_car_allgather(void* ctx, const void* inp, void* out, long long 
     PK_CAG_CASE(7)
     PK_CAG_CASE(8)
 #undef PK_CAG_CASE
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+// Fused reduce-scatter-free TP collective of a row-parallel decode projection (see
+// reduce_residual_kernel): residual[M, N] (bf16, in place) += allreduce_over_ranks(bf16(sum_s
+// slabs[s])) and parts[N / 1024, M] = per-chunk sums of squares of the new residual rows.
+// slabs: fp32 [S, M, N] (S >= 1), or S == 0 and `partial` a bf16 [M, N] partial.
+// N % 1024 == 0, M * N * 2 <= data_bytes; blocks <= 0: one workgroup per (row, chunk) item up to
+// 512 workgroups.
+PK_EXPORT int pk_car_reduce_residual(void* ctx, const void* slabs, int S, const void* partial, void* residual,
+                                     void* parts, int M, int N, int blocks, hipStream_t stream) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr || c->d_peers == nullptr) return -1;
+  if (M <= 0) return 0;
+  if (N <= 0 || N % 1024 || S < 0 || (S == 0 && partial == nullptr) || (S > 0 && slabs == nullptr) ||
+      residual == nullptr || parts == nullptr)
+    return -2;
+  if (static_cast<size_t>(M) * N * 2 > c->data_bytes) return -2;
+  const int items = M * (N / 1024);
+  if (blocks <= 0) blocks = std::min(items, 512);
+  blocks = std::max(1, std::min({blocks, items, kMaxBlocks}));
+  const Fail fail{c->d_err, c->timeout_ticks};
+  const float* sl = static_cast<const float*>(slabs);
+  const uint4* pt = static_cast<const uint4*>(partial);
+  uint16_t* rs = static_cast<uint16_t*>(residual);
+  float* ps = static_cast<float*>(parts);
+  switch (c->world) {
+#define PK_CRR_CASE(WW)                                                                                          \
+  case WW:                                                                                                     \
+    reduce_residual_kernel<WW><<<blocks, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, sl, S, pt, rs, ps, M, \
+                                                           N, fail);                                           \
+    break;
+    PK_CRR_CASE(2)
+    PK_CRR_CASE(3)
+    PK_CRR_CASE(4)
+    PK_CRR_CASE(5)
+    PK_CRR_CASE(6)
+    PK_CRR_CASE(7)
+    PK_CRR_CASE(8)
+#undef PK_CRR_CASE
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;

@@ -32,6 +32,9 @@ class ModelConfig:
     bos_token_id: int = 128000
     eos_token_id: int = 128001
     init_std: float = 0.02
+    # random-init std of the MoE router (None: init_std).  The tiny test MoEs use a wide router so
+    # top-2 routing has no near-ties that bf16 reduction-order noise could flip between TP layouts
+    router_init_std: Optional[float] = None
 
     @property
     def is_moe(self) -> bool:
@@ -69,7 +72,7 @@ PRESETS: Dict[str, ModelConfig] = {
                                    init_std=0.05, bos_token_id=1, eos_token_id=2),
     "tiny-mixtral": ModelConfig("tiny-mixtral", 1024, 512, 768, 2, 8, 2, rope_theta=1e6, max_position=2048,
                                 num_experts=4, experts_per_token=2, init_std=0.05, bos_token_id=1,
-                                eos_token_id=2),
+                                eos_token_id=2, router_init_std=0.5),
     # the 70B TP=8 per-rank shape at test size: 8 KV heads (one per rank at TP=8), GQA group 8,
     # vocab not divisible by 8 (padded shards, like 128256 / 8 = 16032 rows), hidden % 1024 == 0
     "tiny-llama-g8": ModelConfig("tiny-llama-g8", 1003, 1024, 2048, 2, 64, 8, max_position=2048, init_std=0.05,
@@ -77,7 +80,7 @@ PRESETS: Dict[str, ModelConfig] = {
     # Mixtral's expert count and attention shape (8 experts: one per rank at EP=8, 8 KV heads)
     "tiny-mixtral-e8": ModelConfig("tiny-mixtral-e8", 1000, 1024, 1024, 2, 32, 8, rope_theta=1e6,
                                    max_position=2048, num_experts=8, experts_per_token=2, init_std=0.05,
-                                   bos_token_id=1, eos_token_id=2),
+                                   bos_token_id=1, eos_token_id=2, router_init_std=0.5),
     "small-llama": ModelConfig("small-llama", 32000, 2048, 5632, 8, 16, 4, init_std=0.02,
                                bos_token_id=1, eos_token_id=2),
 }

@@ -33,7 +33,7 @@ from ..ops import reference
 from ..parallel import comm
 from ..parallel.state import ParallelState, get_state
 from .config import ModelConfig
-from .weights import SafetensorsIndex, random_full, shard_cols, shard_rows
+from .weights import SafetensorsIndex, random_full, random_shard, shard_cols, shard_rows
 
 
 # decode attention consumes the QKV split-K slabs directly (POLYKEY_FUSED_QKV_ATTN=0: separate
@@ -91,6 +91,23 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
         return comm.tp_row_parallel_overlapped(x, w.shape[0],
                                                lambda rows, out: gemm.linear(rows, w, out=out, packed=wp))
     return comm.tp_all_reduce(_proj(x, w, ws, wp))
+
+
+def ranks_per_device() -> int:
+    """Local ranks sharing one GPU (1 on a real node; 8 in a one-GPU TP=8 rehearsal)."""
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    n_dev = max(torch.cuda.device_count(), 1) if torch.cuda.is_available() else 1
+    return max(1, (local + n_dev - 1) // n_dev)
+
+
+def pack_folded(owner, name: str, norm_w: torch.Tensor, packed_only: bool) -> torch.Tensor:
+    """Block-packed copy of ``owner.<name>`` with ``norm_w`` folded into its columns; with
+    ``packed_only`` the row-major weight becomes a meta placeholder (freed before the next)."""
+    src = getattr(owner, name)
+    out = gemm.pack_weight(gemm.fold_norm(src, norm_w))
+    if packed_only:
+        setattr(owner, name, _p(torch.empty(src.shape, dtype=src.dtype, device="meta")))
+    return out
 
 
 def add_norm(pending, residual: torch.Tensor, w: torch.Tensor, eps: float):
@@ -187,6 +204,11 @@ class LlamaForCausalLM(nn.Module):
         tp = self.st.tp_size
         assert cfg.num_heads % tp == 0 and cfg.num_kv_heads % tp == 0 and cfg.intermediate_size % tp == 0
         self.vocab_local = (cfg.vocab_size + tp - 1) // tp
+        if tp > 1:
+            # vocab shards padded to 128 rows: the LM-head shard stays on the block-packed decode
+            # GEMM (128256 / 8 = 16032 rows -> 16128; Mixtral 32000 / 8 -> 4096); the zero rows
+            # give logits past the vocabulary that compute_logits drops
+            self.vocab_local = (self.vocab_local + 127) // 128 * 128
         self.vocab_start = self.st.tp_rank * self.vocab_local
         self.layers = nn.ModuleList([LlamaLayer(cfg, self.st, self._make_mlp(i)) for i in range(cfg.num_layers)])
         self.embed = None
@@ -207,35 +229,39 @@ class LlamaForCausalLM(nn.Module):
         return torch.cat([t, t.new_zeros((pad,) + t.shape[1:])]) if pad else t
 
     def init_random(self, seed: int = 0) -> "LlamaForCausalLM":
+        """Random weights, drawn shard-locally (``weights.random_shard``): every TP degree holds
+        slices of the same logical tensors, and a rank draws only its own shard."""
         cfg, st, dev, dt = self.cfg, self.st, self.device, self.dtype
         H, hd, std = cfg.hidden_size, cfg.head_dim, cfg.init_std
         tp, r = st.tp_size, st.tp_rank
-        rnd = lambda name, shape: random_full(name, shape, std, seed, dev, dt)
-        self.embed = _p(shard_rows(self._vocab_pad(rnd("embed", (cfg.vocab_size, H))), r, tp).contiguous())
+        self._seed = seed
+        rows = lambda name, shape: random_shard(name, shape, std, seed, dev, dt, r, tp, 0)
+        cols = lambda name, shape: random_shard(name, shape, std, seed, dev, dt, r, tp, 1)
+        vocab = lambda name: random_shard(name, (cfg.vocab_size, H), std, seed, dev, dt, r, tp, 0,
+                                          pad_to=self.vocab_local)
+        self.embed = _p(vocab("embed").contiguous())
         self.norm = _p(torch.ones(H, dtype=dt, device=dev))
-        if cfg.tie_embeddings:
-            self.lm_head = self.embed
-        else:
-            self.lm_head = _p(shard_rows(self._vocab_pad(rnd("lm_head", (cfg.vocab_size, H))), r, tp).contiguous())
+        self.lm_head = self.embed if cfg.tie_embeddings else _p(vocab("lm_head").contiguous())
         for i, layer in enumerate(self.layers):
-            q = rnd(f"l{i}.q", (cfg.num_heads * hd, H))
-            k = rnd(f"l{i}.k", (cfg.num_kv_heads * hd, H))
-            v = rnd(f"l{i}.v", (cfg.num_kv_heads * hd, H))
-            layer.attn.qkv = _p(torch.cat([shard_rows(q, r, tp), shard_rows(k, r, tp), shard_rows(v, r, tp)]).contiguous())
+            q = rows(f"l{i}.q", (cfg.num_heads * hd, H))
+            k = rows(f"l{i}.k", (cfg.num_kv_heads * hd, H))
+            v = rows(f"l{i}.v", (cfg.num_kv_heads * hd, H))
+            layer.attn.qkv = _p(torch.cat([q, k, v]).contiguous())
             del q, k, v
-            layer.attn.o = _p(shard_cols(rnd(f"l{i}.o", (H, cfg.num_heads * hd)), r, tp).contiguous())
+            layer.attn.o = _p(cols(f"l{i}.o", (H, cfg.num_heads * hd)).contiguous())
             layer.ln1 = _p(torch.ones(H, dtype=dt, device=dev))
             layer.ln2 = _p(torch.ones(H, dtype=dt, device=dev))
-            self._init_mlp_random(i, layer.mlp, rnd)
+            self._init_mlp_random(i, layer.mlp, rows, cols)
         return self
 
-    def _init_mlp_random(self, i: int, mlp: nn.Module, rnd) -> None:
-        cfg, tp, r = self.cfg, self.st.tp_size, self.st.tp_rank
+    def _init_mlp_random(self, i: int, mlp: nn.Module, rows, cols) -> None:
+        cfg = self.cfg
         H, I = cfg.hidden_size, cfg.intermediate_size
-        g = shard_rows(rnd(f"l{i}.gate", (I, H)), r, tp)
-        u = shard_rows(rnd(f"l{i}.up", (I, H)), r, tp)
+        g = rows(f"l{i}.gate", (I, H))
+        u = rows(f"l{i}.up", (I, H))
         mlp.gate_up = _p(gemm.interleave_gate_up(g, u).contiguous())
-        mlp.down = _p(shard_cols(rnd(f"l{i}.down", (H, I)), r, tp).contiguous())
+        del g, u
+        mlp.down = _p(cols(f"l{i}.down", (H, I)).contiguous())
 
     def load_hf(self, path: str) -> "LlamaForCausalLM":
         idx = SafetensorsIndex(path)
@@ -370,12 +396,12 @@ class LlamaForCausalLM(nn.Module):
         h = ops.rms_norm(residual, self.layers[0].ln1, self.layers[0].eps)
         for i, layer in enumerate(self.layers):
             at = layer.attn
-            qkv = comm.sp_all_gather(h, lay, comm.RowsFn(lambda r, o, w=at.qkv: gemm.linear(r, w, out=o),
-                                                         at.qkv.shape[0]))
+            qkv = comm.sp_all_gather(h, lay, comm.RowsFn(
+                lambda r, o, w=at.qkv, wp=at.qkv_p: gemm.linear(r, w, out=o, packed=wp), at.qkv.shape[0]))
             a = at.attend(qkv, positions, md, self.cos_sin, kv_caches[i])
             del qkv
-            o = comm.sp_reduce_scatter(a, lay, comm.RowsFn(lambda r, out, w=at.o: gemm.linear(r, w, out=out),
-                                                           at.o.shape[0]))
+            o = comm.sp_reduce_scatter(a, lay, comm.RowsFn(
+                lambda r, out, w=at.o, wp=at.o_p: gemm.linear(r, w, out=out, packed=wp), at.o.shape[0]))
             h, residual = ops.fused_add_rms_norm(o, residual, layer.ln2, layer.eps)
             m = self._sp_mlp(layer, h, lay)
             nxt = self.layers[i + 1].ln1 if i + 1 < len(self.layers) else self.norm
@@ -386,10 +412,10 @@ class LlamaForCausalLM(nn.Module):
         """Dense MLP on the SP shard: all-gather → gate_up + SiLU → down → reduce-scatter."""
         mlp = layer.mlp
         g = comm.sp_all_gather(h, lay, comm.RowsFn(
-            lambda r, o, w=mlp.gate_up: gemm.silu_and_mul_interleaved(gemm.linear(r, w), out=o),
-            mlp.gate_up.shape[0] // 2))
-        return comm.sp_reduce_scatter(g, lay, comm.RowsFn(lambda r, o, w=mlp.down: gemm.linear(r, w, out=o),
-                                                          mlp.down.shape[0]))
+            lambda r, o, w=mlp.gate_up, wp=mlp.gate_up_p: o.copy_(gemm.linear_silu(r, w, packed=wp))
+            if w.is_meta else gemm.silu_and_mul_interleaved(gemm.linear(r, w), out=o), mlp.gate_up.shape[0] // 2))
+        return comm.sp_reduce_scatter(g, lay, comm.RowsFn(
+            lambda r, o, w=mlp.down, wp=mlp.down_p: gemm.linear(r, w, out=o, packed=wp), mlp.down.shape[0]))
 
     # ------------------------------------------------------------------ fused decode chain
     # Off by default: measured slower on MI355X (tools/bench_gemm.py "fused decode chain": the
@@ -455,7 +481,13 @@ class LlamaForCausalLM(nn.Module):
     # ------------------------------------------------------------------ folded-norm decode chain
     def _rowscale_ok(self, x: torch.Tensor) -> bool:
         l0 = self.layers[0]
-        return (self.st.tp_size == 1 and l0.attn.qkv_pf is not None and getattr(l0.mlp, "gate_up_pf", None) is not None
+        if self.st.tp_size > 1:
+            # TP: every row-parallel projection ends in the fused IPC collective (slab reduce +
+            # xGMI peer sum + residual add + norm parts in one launch)
+            car = self.st.custom_ar
+            if car is None or not car.supports_reduce_residual(x.shape[0], self.cfg.hidden_size):
+                return False
+        return (l0.attn.qkv_pf is not None and getattr(l0.mlp, "gate_up_pf", None) is not None
                 and self.cfg.hidden_size % 1024 == 0 and gemm.norm_fusable(self.cfg.hidden_size)
                 and gemm.skinny_ok(x, l0.attn.qkv))
 
@@ -477,6 +509,8 @@ class LlamaForCausalLM(nn.Module):
         residual = x
         parts = gemm.residual_parts(None, residual, buf)
         last = len(self.layers) - 1
+        if self.st.tp_size > 1:
+            return self._forward_rowscale_tp(residual, parts, positions, md, kv_caches, ws, buf, buf2)
         inlaunch = INLAUNCH_RESIDUAL and H % 64 == 0
         ctr = self._fused_buffers()[0] if inlaunch else None
         for i, layer in enumerate(self.layers):
@@ -512,6 +546,35 @@ class LlamaForCausalLM(nn.Module):
                 x, _ = gemm.partial_add_rms_norm(d, residual, self.norm, self.cfg.rms_eps)
         return x
 
+    def _forward_rowscale_tp(self, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
+                             md: attn_ops.AttnMetadata, kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
+                             ws: torch.Tensor, buf: torch.Tensor, buf2: torch.Tensor) -> torch.Tensor:
+        """TP decode step of the folded-norm chain: per layer four launches plus attention,
+
+            qkv   = rinv1 * (residual @ (Wqkv_local diag ln1)^T)   split-K slabs -> attention
+            o     = split-K slabs of attn @ Wo_local^T  -> fused collective: slab sum, xGMI
+                    peer sum, residual += , norm parts (parallel/custom_ar.py reduce_residual)
+            h     = silu / mul of rinv2 * (residual @ (Wgu_local diag ln2)^T)
+            down  = split-K slabs -> fused collective
+
+        so each row-parallel projection costs its GEMM and ONE collective launch (SURVEY.md
+        §2.3: 2 x 80 all-reduces per 70B TP=8 step)."""
+        car = self.st.custom_ar
+        for i, layer in enumerate(self.layers):
+            at, mlp = layer.attn, layer.mlp
+            kc, vc = kv_caches[i]
+            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf)
+            if md.num_prefill == 0 and FUSED_QKV_ATTENTION:
+                a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
+            else:
+                q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
+                a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
+            parts = car.reduce_residual(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=HALF_O_SLABS),
+                                        residual, buf2)
+            h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf, rowscale=gemm.RowScale(parts, layer.eps))
+            parts = car.reduce_residual(gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p), residual, buf)
+        return gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
+
     def workspace(self, M: int) -> Optional[torch.Tensor]:
         """fp32 split-K slab buffer for decode-sized batches (fixed address: graph-safe)."""
         if self.device.type != "cuda" or M > gemm.SKINNY_MAX_M:
@@ -537,10 +600,13 @@ class LlamaForCausalLM(nn.Module):
         (:func:`gemm.pack_weight`) for the decode GEMM, which streams it faster than row-major
         (tools/bench_gemm.py, tools/gemm_lab.hip).  Prefill keeps using the row-major weight
         through hipBLASLt, so this doubles projection memory: ``auto`` packs when both copies fit
-        in 75 % of HBM (8B: +16 GB of 288 GB; Mixtral-8x7B: +90 GB).  When they do not (70B on
+        in 75 % of this rank's share of HBM (8B: +16 GB of 288 GB; Mixtral-8x7B: +90 GB; ranks
+        sharing one GPU split it).  When they do not (70B on one GPU, an 8-rank TP=8 rehearsal on
         one GPU) the projections are kept ONLY packed: prefill then reads the same layout through
-        the hand-written MFMA GEMM (``csrc/kernels/gemm_prefill.hip`` variant 3) and the
-        row-major attributes become shape-only (meta) placeholders.
+        the hand-written MFMA GEMM (``csrc/kernels/gemm_prefill.hip``) and the row-major
+        attributes become shape-only (meta) placeholders.  With folded norms (Llama MLP) the
+        packed-only copies of QKV and gate/up carry their RMSNorm weight, and prefill normalises
+        with unit weights (``ln1`` / ``ln2`` become ones; the originals stay as ``ln*_folded``).
         ``POLYKEY_PACKED_WEIGHTS`` = auto | 1 (both copies) | packed (packed only) | 0."""
         mode = mode or os.environ.get("POLYKEY_PACKED_WEIGHTS", "auto")
         if mode == "0" or self.device.type != "cuda" or not gemm.SKINNY_ENABLED:
@@ -548,13 +614,13 @@ class LlamaForCausalLM(nn.Module):
         head_bytes = self.lm_head.numel() * self.lm_head.element_size()
         packed_only = mode == "packed"
         if mode == "auto":
-            total = torch.cuda.get_device_properties(self.device).total_memory
+            total = torch.cuda.get_device_properties(self.device).total_memory / ranks_per_device()
             proj = sum(w.numel() * w.element_size() for w in self.layers.parameters())
             if 2 * proj + 2 * head_bytes > 0.75 * total:
                 packed_only = True
         if packed_only and not self._packed_prefill_ok():
             return False
-        fold = FOLD_NORM and self.st.tp_size == 1 and isinstance(self.layers[0].mlp, LlamaMLP) and not packed_only
+        fold = FOLD_NORM and isinstance(self.layers[0].mlp, LlamaMLP)
 
         def pack(owner, name: str, dst: str, w: Optional[torch.Tensor] = None) -> None:
             src = getattr(owner, name)
@@ -564,9 +630,14 @@ class LlamaForCausalLM(nn.Module):
 
         for layer in self.layers:
             if fold:
-                layer.attn.qkv_pf = gemm.pack_weight(gemm.fold_norm(layer.attn.qkv, layer.ln1))
-                layer.mlp.gate_up_pf = gemm.pack_weight(gemm.fold_norm(layer.mlp.gate_up, layer.ln2))
-                layer.mlp.down_p = gemm.pack_weight(layer.mlp.down)
+                layer.attn.qkv_pf = pack_folded(layer.attn, "qkv", layer.ln1, packed_only)
+                layer.mlp.gate_up_pf = pack_folded(layer.mlp, "gate_up", layer.ln2, packed_only)
+                if packed_only:  # prefill reads the folded copies: normalise with unit weights
+                    layer.attn.qkv_p, layer.mlp.gate_up_p = layer.attn.qkv_pf, layer.mlp.gate_up_pf
+                    layer.ln1_folded, layer.ln2_folded = layer.ln1, layer.ln2
+                    layer.ln1 = _p(torch.ones_like(layer.ln1))
+                    layer.ln2 = _p(torch.ones_like(layer.ln2))
+                pack(layer.mlp, "down", "down_p")
             else:
                 pack(layer.attn, "qkv", "qkv_p")
                 if isinstance(layer.mlp, LlamaMLP):
@@ -581,10 +652,12 @@ class LlamaForCausalLM(nn.Module):
         return True
 
     def _packed_prefill_ok(self) -> bool:
-        """Every dense projection is a shape the packed-W prefill GEMM tiles (TP = 1, Llama MLP)."""
+        """Every dense projection is a shape the packed-W prefill GEMM tiles (Llama MLP; per-rank
+        shapes under TP, e.g. 70B TP=8: QKV 1280 x 8192, o 8192 x 1024, gate/up 7168 x 8192,
+        down 8192 x 3584)."""
         from ..ops import gemm_prefill
         l0 = self.layers[0]
-        if self.st.tp_size != 1 or not isinstance(l0.mlp, LlamaMLP):
+        if not isinstance(l0.mlp, LlamaMLP):
             return False
         return all(gemm_prefill.supported(w.shape[0], w.shape[1]) and w.shape[1] % 128 == 0
                    for w in (l0.attn.qkv, l0.attn.o, l0.mlp.gate_up, l0.mlp.down))

@@ -26,7 +26,7 @@ from ..ops import gemm, moe
 from ..parallel import comm, ep as ep_comm
 from ..parallel.state import get_state
 from .llama import LlamaForCausalLM, _p
-from .weights import shard_cols, shard_rows
+from .weights import random_shard, shard_cols, shard_rows
 
 
 class MixtralMoE(nn.Module):
@@ -92,17 +92,21 @@ class MixtralForCausalLM(LlamaForCausalLM):
     def _mlp_weights(self, mlp) -> tuple:
         return ()
 
-    def _init_mlp_random(self, i: int, mlp: MixtralMoE, rnd) -> None:
+    def _init_mlp_random(self, i: int, mlp: MixtralMoE, rows, cols) -> None:
         cfg, st = self.cfg, self.st
         H, I = cfg.hidden_size, cfg.intermediate_size
         tp_shard = st.ep_size == 1 and st.tp_size > 1
-        mlp.router = _p(rnd(f"l{i}.router", (cfg.num_experts, H)).contiguous())
+        std, seed, dev, dt = cfg.init_std, self._seed, self.device, self.dtype
+        # blocks of the logical tensor run along the dim TP shards (rows of w1 / w3, columns of w2)
+        full = lambda name, shape, dim=0: random_shard(name, shape, std, seed, dev, dt, 0, 1, dim)
+        rstd = cfg.router_init_std if cfg.router_init_std is not None else std
+        mlp.router = _p(random_shard(f"l{i}.router", (cfg.num_experts, H), rstd, seed, dev, dt, 0, 1).contiguous())
         w13, w2 = [], []
         for e in range(mlp.e_lo, mlp.e_hi):
-            g, u, d = rnd(f"l{i}.e{e}.w1", (I, H)), rnd(f"l{i}.e{e}.w3", (I, H)), rnd(f"l{i}.e{e}.w2", (H, I))
-            if tp_shard:
-                g, u, d = shard_rows(g, st.tp_rank, st.tp_size), shard_rows(u, st.tp_rank, st.tp_size), \
-                    shard_cols(d, st.tp_rank, st.tp_size)
+            if tp_shard:  # attention TP without EP: every expert sharded Megatron-style
+                g, u, d = rows(f"l{i}.e{e}.w1", (I, H)), rows(f"l{i}.e{e}.w3", (I, H)), cols(f"l{i}.e{e}.w2", (H, I))
+            else:
+                g, u, d = full(f"l{i}.e{e}.w1", (I, H)), full(f"l{i}.e{e}.w3", (I, H)), full(f"l{i}.e{e}.w2", (H, I), 1)
             w13.append(gemm.interleave_gate_up(g, u))
             w2.append(d.contiguous())
         mlp.w13 = _p(torch.stack(w13).contiguous())

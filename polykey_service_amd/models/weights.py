@@ -34,6 +34,47 @@ def random_full(name: str, shape: Sequence[int], std: float, seed: int, device, 
     return t.to(dtype)
 
 
+RANDOM_BLOCK = 128
+
+
+def random_slice(name: str, shape: Sequence[int], std: float, seed: int, device, dtype, dim: int = 0,
+                 lo: int = 0, hi: Optional[int] = None, block: int = RANDOM_BLOCK) -> torch.Tensor:
+    """Indices [lo, hi) along ``dim`` of the logical random tensor ``shape`` without drawing the
+    rest: the tensor is cut into ``block``-wide slabs along ``dim``, each drawn from its own
+    seeded generator, so every rank of any TP degree materialises exactly its own shard and the
+    shards of TP = 8 concatenate to the TP = 1 tensor (a 70B rank draws 17.6 GB, not 141 GB)."""
+    n = shape[dim]
+    hi = n if hi is None else min(hi, n)
+    shp = list(shape)
+    shp[dim] = max(hi - lo, 0)
+    out = torch.empty(shp, dtype=dtype, device=device)
+    b = lo // block
+    while b * block < hi:
+        bl, bh = b * block, min(n, (b + 1) * block)
+        sub = list(shape)
+        sub[dim] = bh - bl
+        t = random_full(f"{name}#{b}", sub, std, seed, device, dtype)
+        a, z = max(lo, bl), min(hi, bh)
+        out.narrow(dim, a - lo, z - a).copy_(t.narrow(dim, a - bl, z - a))
+        b += 1
+    return out
+
+
+def random_shard(name: str, shape: Sequence[int], std: float, seed: int, device, dtype, rank: int, world: int,
+                 dim: int = 0, pad_to: Optional[int] = None) -> torch.Tensor:
+    """Rank ``rank``'s 1/``world`` shard along ``dim`` (``pad_to``: shard size after zero-padding
+    the logical dimension, e.g. vocab shards rounded up to 128 rows)."""
+    n = shape[dim]
+    k = pad_to if pad_to is not None else n // world
+    assert pad_to is not None or n % world == 0, (shape, world)
+    t = random_slice(name, shape, std, seed, device, dtype, dim, rank * k, (rank + 1) * k)
+    if t.shape[dim] < k:
+        pad = list(t.shape)
+        pad[dim] = k - t.shape[dim]
+        t = torch.cat([t, t.new_zeros(pad)], dim)
+    return t
+
+
 def shard_rows(t: torch.Tensor, rank: int, world: int) -> torch.Tensor:
     n = t.shape[0]
     assert n % world == 0, (t.shape, world)

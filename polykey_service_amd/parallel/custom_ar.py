@@ -40,6 +40,7 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_allreduce_bf16.argtypes = [_P, _P, _P, _LL, _I, _P]
         lib.pk_car_allreduce_bf16_algo.argtypes = [_P, _P, _P, _LL, _I, _I, _P]
         lib.pk_car_allgather.argtypes = [_P, _P, _P, _LL, _LL, _I, _P]
+        lib.pk_car_reduce_residual.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _P]
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_clear_error.argtypes = [_P]
         lib.pk_car_set_timeout_ms.argtypes = [_P, _LL]
@@ -60,6 +61,10 @@ class CustomAllReduce:
         self.rank, self.world, self.device = rank, world, device
         self.max_bytes = max_bytes
         self.blocks = blocks
+        # grid of the fused decode collective (0: one workgroup per (row, 1024-column chunk), up
+        # to 512).  Ranks sharing ONE GPU (rehearsals, tests) need every rank's grid resident at
+        # once -- POLYKEY_CUSTOM_AR_FUSED_BLOCKS caps it there.
+        self.fused_blocks = int(os.environ.get("POLYKEY_CUSTOM_AR_FUSED_BLOCKS", "0"))
         with torch.cuda.device(device):
             self.ctx = self.lib.pk_car_create(rank, world, max_bytes)
         if not self.ctx:
@@ -111,6 +116,33 @@ class CustomAllReduce:
             raise RuntimeError(f"custom all-gather launch failed ({rc})")
         return out
 
+    def supports_reduce_residual(self, M: int, N: int) -> bool:
+        """Shapes the fused decode collective takes (:meth:`reduce_residual`)."""
+        return M > 0 and N % 1024 == 0 and M * N * 2 <= self.max_bytes
+
+    def reduce_residual(self, pending, residual: torch.Tensor, parts: torch.Tensor) -> torch.Tensor:
+        """Fused TP collective of a row-parallel decode projection, one launch: this rank's
+        split-K slabs (a :class:`~polykey_service_amd.ops.gemm.Partial`) or bf16 partial [M, N]
+        are reduced locally, summed over the group through the IPC slots (rank order), added
+        into ``residual`` in place, and ``parts`` receives the per-1024-column sums of squares of
+        the new residual ([N / 1024, M] view returned) for the next folded-norm projection."""
+        M, N = residual.shape
+        if not (residual.is_contiguous() and residual.dtype == torch.bfloat16 and self.supports_reduce_residual(M, N)):
+            raise ValueError(f"reduce_residual: unsupported residual {tuple(residual.shape)} {residual.dtype}")
+        nparts = N // 1024
+        assert parts.numel() >= nparts * M and parts.dtype == torch.float32
+        if isinstance(pending, torch.Tensor):
+            assert pending.shape == (M, N) and pending.is_contiguous() and pending.dtype == torch.bfloat16
+            slabs, S, partial = 0, 0, pending.data_ptr()
+        else:
+            assert pending.M == M and pending.N == N and pending.buf.numel() >= pending.S * M * N
+            slabs, S, partial = pending.buf.data_ptr(), pending.S, 0
+        rc = self.lib.pk_car_reduce_residual(self.ctx, slabs, S, partial, residual.data_ptr(), parts.data_ptr(), M, N,
+                                             self.fused_blocks, torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"fused TP reduce launch failed ({rc})")
+        return parts.view(-1)[: nparts * M].view(nparts, M)
+
     def set_timeout(self, seconds: float) -> None:
         self.lib.pk_car_set_timeout_ms(self.ctx, max(1, int(seconds * 1000)))
 
@@ -154,6 +186,10 @@ def maybe_create(st) -> Optional[CustomAllReduce]:
         return None
     try:
         car = CustomAllReduce(st.tp_cpu_group, st.tp_rank, st.tp_size, st.device)
+        n_dev = max(torch.cuda.device_count(), 1)
+        shared = int(os.environ.get("LOCAL_WORLD_SIZE", str(st.tp_size))) > n_dev
+        if shared and "POLYKEY_CUSTOM_AR_FUSED_BLOCKS" not in os.environ:
+            car.fused_blocks = 64  # ranks share a GPU: every rank's grid must be resident at once
         good = car.self_test()
         votes = [None] * st.tp_size
         dist.all_gather_object(votes, good, group=st.tp_cpu_group)

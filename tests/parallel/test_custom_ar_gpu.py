@@ -63,6 +63,7 @@ def _worker(rank, world, port, q):
             want = float(sum(r + it for r in range(world)))
             assert bool((yg.float() == want).all()), (it, yg[:4])
         assert car.error() == 0
+        _fused_phase(car, rank, world, dev)
         # a rank that skips a call: every rank that waits for it times out and fails loudly
         # (sticky error word, read without a GPU sync), and later calls return at once
         car.set_timeout(1.0)
@@ -90,6 +91,85 @@ def _worker(rank, world, port, q):
         q.put((rank, "ok"))
     except BaseException as e:  # noqa: BLE001
         q.put((rank, repr(e)))
+
+
+def _rr_reference(slabs_all, partials_all, res, S):
+    """Sequential fp32 reference of pk_car_reduce_residual (same summation order)."""
+    world = len(partials_all)
+    parts_bf = []
+    for j in range(world):
+        if S == 0:
+            parts_bf.append(partials_all[j].float())
+        else:
+            a = torch.zeros_like(slabs_all[j][0])
+            for s_ in range(S):
+                a = a + slabs_all[j][s_]
+            parts_bf.append(a.to(torch.bfloat16).float())
+    acc = torch.zeros_like(parts_bf[0])
+    for j in range(world):
+        acc = acc + parts_bf[j]
+    new = (acc.to(torch.bfloat16).float() + res.float()).to(torch.bfloat16)
+    M, N = res.shape
+    sq = new.float().view(M, N // 1024, 1024).pow(2).sum(-1).t().contiguous()
+    return new, sq
+
+
+def _fused_phase(car, rank, world, dev):
+    """Fused TP decode collective: slab reduce + peer sum + residual add + norm parts, eager and
+    graph-replayed, interleaved with all-gathers and all-reduces of other grid sizes (one call
+    epoch for every collective of the context)."""
+    car.fused_blocks = 32  # every rank's grid resident at once on the shared GPU
+    g = torch.Generator().manual_seed(7)  # same residual on every rank
+    gr = torch.Generator().manual_seed(1000 + rank)
+    for M, N, S in ((1, 1024, 2), (3, 4096, 0), (64, 8192, 4), (17, 2048, 1)):
+        res = (torch.randn(M, N, generator=g) * 2).to(torch.bfloat16)
+        slabs = torch.randn(max(S, 1), M, N, generator=gr) if S else None
+        partial = torch.randn(M, N, generator=gr).to(torch.bfloat16) if S == 0 else None
+        all_slabs = [torch.empty(max(S, 1), M, N) for _ in range(world)] if S else None
+        all_part = [torch.empty(M, N, dtype=torch.bfloat16) for _ in range(world)]
+        if S:
+            dist.all_gather(all_slabs, slabs)
+        else:
+            dist.all_gather(all_part, partial)
+        want, want_sq = _rr_reference(all_slabs, all_part, res, S)
+        from polykey_service_amd.ops.gemm import Partial
+        r_dev = res.to(dev)
+        parts = torch.zeros(8 * 64, dtype=torch.float32, device=dev)
+        pend = Partial(slabs.to(dev).reshape(-1), S, M, N) if S else partial.to(dev)
+        out_parts = car.reduce_residual(pend, r_dev, parts)
+        torch.cuda.synchronize()
+        assert torch.equal(r_dev.cpu(), want), (M, N, S)
+        torch.testing.assert_close(out_parts.cpu(), want_sq, rtol=1e-5, atol=1e-3)
+        # an all-gather and an all-reduce with other grids in between (epoch consistency)
+        lg = torch.full((M, 256), float(rank), dtype=torch.bfloat16, device=dev)
+        got = car.all_gather_last(lg)
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu().view(M, world, 256)[:, :, 0].float(),
+                           torch.arange(world, dtype=torch.float32).expand(M, world))
+    # graph replay of the fused collective
+    M, N = 8, 4096
+    res0 = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    part_in = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+    r_dev = res0.to(dev)
+    parts = torch.zeros(4 * M, dtype=torch.float32, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        car.reduce_residual(part_in, r_dev, parts)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        car.reduce_residual(part_in, r_dev, parts)
+    for it in range(3):
+        part_in.fill_(float(rank + 1))
+        r_dev.copy_(res0.to(dev))
+        dist.barrier()
+        graph.replay()
+        torch.cuda.synchronize()
+        inc = torch.tensor(float(sum(r + 1 for r in range(world)))).to(torch.bfloat16).float()
+        want = (res0.float() + inc).to(torch.bfloat16)
+        assert torch.equal(r_dev.cpu(), want), it
+    assert car.error() == 0
 
 
 @pytest.mark.parametrize("world", [2, 8])

@@ -73,7 +73,16 @@ def test_tp_matches_tp1(tmp_path, model, world, ep, sp):
     got = torch.load(out, weights_only=True)
     # bf16 row-parallel partials are rounded per rank before the all-reduce: ~1 bf16 ulp noise
     torch.testing.assert_close(got["logits"], ref_logits, atol=1e-1, rtol=5e-2)
-    assert [t[0] for t in got["tokens"]] == [t[0] for t in ref_toks]
+    _same_first_tokens(got["tokens"], ref_toks, ref_logits)
+
+
+def _same_first_tokens(got_toks, ref_toks, ref_logits, tie=0.1):
+    """First (prefill) tokens equal, except where the reference itself has a near-tie (random
+    weights: two logits within bf16 noise of each other may flip under a different reduction)."""
+    for row, (g, r) in enumerate(zip(got_toks, ref_toks)):
+        if g[0] != r[0]:
+            lg = ref_logits[row].float()
+            assert lg[g[0]] >= lg.max() - tie, (row, g[0], r[0], float(lg[g[0]]), float(lg.max()))
 
 
 def _comm_worker(rank, world, port, out_path):
