@@ -74,12 +74,16 @@ struct Ctx {
   long long timeout_ticks = 0;
 };
 
-// Bounded wait for flags[b][j] == e of every peer j (one lane per peer).  On timeout the lane
-// records the failure in the device copy and the host-mapped word and stops waiting.
+// Bounded wait for flags[b][j] >= e of every peer j (one lane per peer).  ">=", not "==": a
+// peer that has finished call e may already have started call e + 1 and stamped e + 1 over
+// its e before this (slower, or time-sliced) rank polled -- it can never be further ahead, as
+// call e + 1 needs this rank's own flag.  Serial comparison (signed difference) survives the
+// 32-bit wrap.  On timeout the lane records the failure in the device copy and the
+// host-mapped word and stops waiting.
 __device__ __forceinline__ void spin_wait(uint32_t* flag, uint32_t e, Signals* my_sig, const Fail& f) {
   const long long t0 = wall_clock64();
   uint32_t it = 0;
-  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+  while (static_cast<int32_t>(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
     __builtin_amdgcn_s_sleep(1);
     if ((++it & 255u) == 0 && wall_clock64() - t0 > f.timeout) {
       __hip_atomic_store(&my_sig->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -578,6 +582,15 @@ PK_EXPORT int pk_car_clear_error(void* ctx) {
   Signals* s = reinterpret_cast<Signals*>(c->local);
   if (hipMemcpy(&s->error, &z, sizeof(z), hipMemcpyHostToDevice) != hipSuccess) return -3;
   __atomic_store_n(c->h_err, 0u, __ATOMIC_RELEASE);
+  return 0;
+}
+
+// Failure path (watchdog / peer death): set the sticky host error word, so check() raises on
+// every rank's next poll.  No device call: the device may be the thing that hangs.
+PK_EXPORT int pk_car_set_error(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr) return -1;
+  __atomic_store_n(c->h_err, 1u, __ATOMIC_RELEASE);
   return 0;
 }
 

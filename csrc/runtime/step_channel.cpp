@@ -1,8 +1,10 @@
 // Step channel implementation + pybind11 face (see step_channel.h).
 #include "runtime/step_channel.h"
 
+#include <errno.h>
 #include <fcntl.h>
 #include <immintrin.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -41,12 +43,18 @@ class Backoff {
     std::this_thread::sleep_for(std::chrono::microseconds(20));
     return true;
   }
+  // true every ~10 ms of sleeping: time for a (cheap, but not free) peer liveness probe
+  bool probe_due() const { return n_ >= 4096 && (n_ - 4096) % 512 == 0; }
 
  private:
   std::chrono::steady_clock::time_point t0_;
   std::chrono::milliseconds timeout_;
   uint64_t n_ = 0;
 };
+
+// A process exists (same node: every rank of a TP group shares the host).  EPERM means it
+// exists but belongs to another user.
+bool pid_alive(int32_t pid) { return pid <= 0 || kill(pid, 0) == 0 || errno != ESRCH; }
 }  // namespace
 
 StepChannelCore::StepChannelCore(const std::string& name, bool create, int nslots, int nconsumers,
@@ -85,6 +93,8 @@ StepChannelCore::StepChannelCore(const std::string& name, bool create, int nslot
     hdr_->nslots = static_cast<uint32_t>(nslots);
     hdr_->nconsumers = static_cast<uint32_t>(nconsumers);
     hdr_->slot_bytes = slot_bytes;
+    hdr_->producer_pid = static_cast<int32_t>(getpid());
+    for (auto& c : hdr_->consumer_pid) c.store(0, std::memory_order_relaxed);
     hdr_->seq.store(0, std::memory_order_relaxed);
     hdr_->closed.store(0, std::memory_order_relaxed);
     for (auto& a : hdr_->acked) a.store(0, std::memory_order_relaxed);
@@ -101,6 +111,7 @@ StepChannelCore::StepChannelCore(const std::string& name, bool create, int nslot
     }
     // a consumer that attaches late starts at the next step to be published
     next_ = hdr_->seq.load(std::memory_order_acquire) + 1;
+    hdr_->consumer_pid[consumer_index].store(static_cast<int32_t>(getpid()), std::memory_order_release);
   }
 }
 
@@ -125,8 +136,10 @@ bool StepChannelCore::publish(const void* data, uint64_t nbytes, int64_t timeout
     const uint64_t need = s - hdr_->nslots;
     Backoff bo(timeout_ms);
     for (uint32_t c = 0; c < hdr_->nconsumers; ++c)
-      while (hdr_->acked[c].load(std::memory_order_acquire) < need)
+      while (hdr_->acked[c].load(std::memory_order_acquire) < need) {
         if (!bo.wait()) return false;
+        if (bo.probe_due() && !pid_alive(hdr_->consumer_pid[c].load(std::memory_order_acquire))) return false;
+      }
   }
   SlotHead* sh = slot(s);
   std::memcpy(reinterpret_cast<char*>(sh) + sizeof(SlotHead), data, nbytes);
@@ -141,7 +154,8 @@ int64_t StepChannelCore::consume(void* dst, uint64_t cap, int64_t timeout_ms) {
   Backoff bo(timeout_ms);
   while (hdr_->seq.load(std::memory_order_acquire) < next_) {
     if (hdr_->closed.load(std::memory_order_acquire)) return -2;
-    if (!bo.wait()) return -1;
+    if (!bo.wait()) return pid_alive(hdr_->producer_pid) ? -1 : -3;
+    if (bo.probe_due() && !pid_alive(hdr_->producer_pid)) return -3;
   }
   const SlotHead* sh = slot(next_);
   if (sh->seq != next_) throw std::runtime_error("step channel overrun (consumer fell a full ring behind)");
@@ -152,6 +166,16 @@ int64_t StepChannelCore::consume(void* dst, uint64_t cap, int64_t timeout_ms) {
   ++next_;
   return n;
 }
+
+int StepChannelCore::dead_consumer() const {
+  for (uint32_t c = 0; c < hdr_->nconsumers; ++c) {
+    const int32_t pid = hdr_->consumer_pid[c].load(std::memory_order_acquire);
+    if (pid > 0 && !pid_alive(pid)) return static_cast<int>(c);
+  }
+  return -1;
+}
+
+bool StepChannelCore::producer_alive() const { return pid_alive(hdr_->producer_pid); }
 
 void StepChannelCore::close() {
   if (owner_) hdr_->closed.store(1, std::memory_order_release);
@@ -185,6 +209,8 @@ void bind_step_channel(py::module_& m) {
           },
           py::arg("buf"), py::arg("timeout_ms") = 1000)
       .def("close", &pk::StepChannelCore::close)
+      .def("dead_consumer", &pk::StepChannelCore::dead_consumer)
+      .def_property_readonly("producer_alive", &pk::StepChannelCore::producer_alive)
       .def_property_readonly("published", &pk::StepChannelCore::published)
       .def_property_readonly("next_to_consume", &pk::StepChannelCore::next_to_consume)
       .def_property_readonly("slot_bytes", &pk::StepChannelCore::slot_bytes)

@@ -28,9 +28,11 @@ struct alignas(64) StepChannelHeader {
   uint64_t magic;
   uint32_t nslots, nconsumers;
   uint64_t slot_bytes;
+  int32_t producer_pid;                     // liveness: a rank that dies is seen by its peers
   alignas(64) std::atomic<uint64_t> seq;    // last published step (1-based; 0 = none)
   alignas(64) std::atomic<uint32_t> closed; // producer gone
   alignas(64) std::atomic<uint64_t> acked[kMaxConsumers];  // per consumer: last step copied out
+  alignas(64) std::atomic<int32_t> consumer_pid[kMaxConsumers];  // 0 until that consumer attached
 };
 
 struct alignas(64) SlotHead {
@@ -48,11 +50,16 @@ class StepChannelCore {
   StepChannelCore& operator=(const StepChannelCore&) = delete;
 
   // Producer: copy `nbytes` into the next slot and publish it.  Waits (spinning, then sleeping)
-  // while the slot is still unread by some consumer; returns false after `timeout_ms`.
+  // while the slot is still unread by some consumer; returns false after `timeout_ms`, or at
+  // once when that consumer's process has died.
   bool publish(const void* data, uint64_t nbytes, int64_t timeout_ms);
   // Consumer: wait for the next step and copy it into `dst` (capacity `cap`).  Returns the
-  // byte count, -1 on timeout (call again), -2 when the producer closed the channel.
+  // byte count, -1 on timeout (call again), -2 when the producer closed the channel, -3 when
+  // the producer process no longer exists (died without closing: SIGKILL, OOM, crash).
   int64_t consume(void* dst, uint64_t cap, int64_t timeout_ms);
+  // Producer side: index of an attached consumer whose process no longer exists, else -1.
+  int dead_consumer() const;
+  bool producer_alive() const;
   void close();  // producer: wake every consumer with "closed"
 
   uint64_t published() const;

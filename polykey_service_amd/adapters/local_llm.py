@@ -263,7 +263,15 @@ def attach_local_llm(router, cfg, logger, engine=None, llm=None):
             st = init_parallel(tp=cfg.tp, ep=cfg.ep)
             engine = LLMEngine(EngineConfig.from_server_config(cfg), st)
             if st.tp_rank != 0:
-                engine.runner.worker_loop()  # never returns until the leader stops
+                try:
+                    engine.runner.worker_loop()  # never returns until the leader stops
+                except BaseException as e:  # noqa: BLE001 - leader died / collective failed
+                    logger.error("TP worker failed", error=repr(e), rank=st.rank)
+                    try:
+                        engine.runner.abort_comms()
+                    finally:
+                        from ..server.app import hard_exit
+                        hard_exit(1)
                 raise SystemExit(0)
         llm = AsyncLLM(engine)
         st = engine.st

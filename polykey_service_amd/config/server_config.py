@@ -33,6 +33,7 @@ class ServerConfig:
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 8192
     max_model_len: int = 8192
+    num_layers: int = 0            # > 0: truncate the preset's depth (rehearsals)
     kv_block_size: int = 32
     gpu_mem_fraction: float = 0.90
     num_kv_blocks: int = 0         # 0 → size from free HBM
@@ -65,6 +66,7 @@ _ENV = {
     "max_num_seqs": "POLYKEY_MAX_NUM_SEQS",
     "max_num_batched_tokens": "POLYKEY_MAX_BATCHED_TOKENS",
     "max_model_len": "POLYKEY_MAX_MODEL_LEN",
+    "num_layers": "POLYKEY_NUM_LAYERS",
     "kv_block_size": "POLYKEY_KV_BLOCK_SIZE",
     "gpu_mem_fraction": "POLYKEY_GPU_MEM_FRACTION",
     "num_kv_blocks": "POLYKEY_NUM_KV_BLOCKS",

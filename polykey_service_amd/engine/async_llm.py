@@ -67,8 +67,11 @@ class AsyncLLM:
         # switch interval lets a burst of RPC handling hold the engine thread off for whole
         # decode steps (the GPU idles meanwhile); a short interval hands the GIL over promptly.
         sys.setswitchinterval(float(os.environ.get("POLYKEY_GIL_SWITCH_S", "0.002")))
+        self._fatal_sent = False
         self._thread = threading.Thread(target=self._run, name="polykey-engine", daemon=True)
         self._thread.start()
+        self._watchdog = threading.Thread(target=self._watch, name="polykey-watchdog", daemon=True)
+        self._watchdog.start()
 
     # ---------------------------------------------------------------- client side
     def load(self) -> int:
@@ -164,6 +167,39 @@ class AsyncLLM:
 
     async def aclose(self) -> None:
         await asyncio.get_running_loop().run_in_executor(None, self.shutdown)
+
+    def _watch(self) -> None:
+        """Step watchdog: a step stuck for ``watchdog_s`` while work is pending
+        (a collective hung on a dead peer, a wedged GPU) kills the engine: its communicators
+        are aborted (the hung RCCL call returns, IPC collectives stop waiting), every stream
+        gets the error and ``on_fatal`` fires -- the server goes NOT_SERVING and exits non-zero
+        for its supervisor to restart the group.  Disabled while ``watchdog_s`` is 0."""
+        while not self._stop and self.dead is None:
+            time.sleep(0.5 if self.watchdog_s else 1.0)
+            w = self.watchdog_s
+            if not w or self.dead is not None or self._stop:
+                continue
+            if self.engine.has_unfinished() and time.monotonic() - self.last_step_time > w:
+                err = TimeoutError(f"engine step stalled for more than {w:.0f} s (hung collective or GPU)")
+                self.dead = err
+                try:
+                    self.engine.runner.abort_comms()
+                except Exception:  # noqa: BLE001
+                    pass
+                with self._lock:
+                    rids = list(self._streams) + list(self._external)
+                self._deliver([(r, EngineDeadError(f"engine stalled: {err}")) for r in rids])
+                self._fatal(err)
+
+    def _fatal(self, e: BaseException) -> None:
+        if self._fatal_sent:
+            return
+        self._fatal_sent = True
+        if self.on_fatal is not None:
+            try:
+                self.on_fatal(e)
+            except Exception:
+                pass
 
     def healthy(self) -> bool:
         if self.dead is not None:
@@ -278,16 +314,17 @@ class AsyncLLM:
                     self.stats["output_tokens"] += sum(len(o.new_token_ids) for o in outs)
                     self._deliver([(o.request_id, o) for o in outs])
         except BaseException as e:  # noqa: BLE001
-            self.dead = e
+            if self.dead is None:
+                self.dead = e
             traceback.print_exc()
+            try:  # a peer failed: let collectives of this rank stop waiting on it
+                eng.runner.abort_comms()
+            except Exception:  # noqa: BLE001
+                pass
             with self._lock:
                 rids = list(self._streams) + list(self._external)
             self._deliver([(r, EngineDeadError(f"engine loop failed: {e!r}")) for r in rids])
-            if self.on_fatal is not None:
-                try:
-                    self.on_fatal(e)
-                except Exception:
-                    pass
+            self._fatal(e)
         finally:
             if prof is not None:
                 prof.stop()

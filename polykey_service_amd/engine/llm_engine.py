@@ -46,6 +46,9 @@ class EngineConfig:
     sched_policy: str = dataclasses.field(default_factory=lambda: os.environ.get("POLYKEY_SCHED_POLICY",
                                                                                  "prefill_first"))
     max_decode_stall: int = 4
+    # > 0: keep only the first num_layers decoder layers of the preset (rehearsals of a large
+    # model's per-rank shapes with fewer layers, tests); 0: the preset's depth
+    num_layers: int = 0
     # automatic prefix caching (csrc/runtime/block_manager.h); POLYKEY_PREFIX_CACHING=0 disables
     prefix_caching: bool = dataclasses.field(
         default_factory=lambda: os.environ.get("POLYKEY_PREFIX_CACHING", "1") != "0")
@@ -55,7 +58,8 @@ class EngineConfig:
         return cls(model=sc.model, model_path=sc.model_path, tokenizer=sc.tokenizer, dtype=sc.dtype, seed=sc.seed,
                    block_size=sc.kv_block_size, max_num_seqs=sc.max_num_seqs,
                    max_num_batched_tokens=sc.max_num_batched_tokens, max_model_len=sc.max_model_len,
-                   num_kv_blocks=sc.num_kv_blocks, gpu_mem_fraction=sc.gpu_mem_fraction, hip_graphs=sc.hip_graphs)
+                   num_kv_blocks=sc.num_kv_blocks, gpu_mem_fraction=sc.gpu_mem_fraction, hip_graphs=sc.hip_graphs,
+                   num_layers=getattr(sc, "num_layers", 0))
 
 
 class LLMEngine:
@@ -63,6 +67,8 @@ class LLMEngine:
         self.cfg = cfg
         self.st = st or get_state()
         mcfg: ModelConfig = get_config(cfg.model_path or cfg.model)
+        if cfg.num_layers > 0 and cfg.num_layers != mcfg.num_layers:
+            mcfg = dataclasses.replace(mcfg, num_layers=cfg.num_layers)
         if cfg.max_model_len > mcfg.max_position:
             cfg = dataclasses.replace(cfg, max_model_len=mcfg.max_position)
             self.cfg = cfg

@@ -88,6 +88,15 @@ class _Layout:
         return v
 
 
+class TPPeerError(RuntimeError):
+    """A rank of this TP group died or stopped responding: the group cannot continue."""
+
+
+def peer_timeout_ms() -> int:
+    """Bound of every wait on a TP peer (step ring slot, IPC collective): POLYKEY_CUSTOM_AR_TIMEOUT_S."""
+    return int(float(os.environ.get("POLYKEY_CUSTOM_AR_TIMEOUT_S", "30")) * 1000)
+
+
 class ModelRunner:
     def __init__(self, model, cfg: RunnerConfig, device: torch.device, block_manager=None):
         self.model = model
@@ -369,11 +378,14 @@ class ModelRunner:
 
     def _publish(self, n_bt_rows: Optional[int] = None) -> None:
         """Hand the step inputs to the TP workers (shared-memory ring, host to host) and stage
-        them on this rank's device."""
+        them on this rank's device.  The wait for a slot is bounded by the collectives' timeout:
+        a worker that died (its pid is gone) or stopped consuming fails the step loudly."""
         n = self._staged_words(n_bt_rows)
         if self.channel is not None and self.model.st.tp_rank == 0:
-            if not self.channel.publish(self._hnp[self._cur], n * 4, 600000):
-                raise RuntimeError("TP step channel: a worker stopped consuming steps")
+            if not self.channel.publish(self._hnp[self._cur], n * 4, peer_timeout_ms()):
+                dead = self.channel.dead_consumer()
+                who = f"TP rank {dead + 1} died" if dead >= 0 else "a TP worker stopped consuming steps"
+                raise TPPeerError(f"TP step channel: {who}")
         self._stage_local(n)
 
     def _stage_local(self, n: int) -> None:
@@ -403,6 +415,8 @@ class ModelRunner:
                 continue  # idle leader: poll again (and re-check the comm error word)
             if nbytes == -2:
                 return
+            if nbytes == -3:  # the leader's process is gone (SIGKILL, OOM, crash): end this rank
+                raise TPPeerError("TP leader process died; this worker exits for its supervisor to restart the group")
             mode, T, n, nd, ns, max_q, g, short, cont = (int(v) for v in self.h["header"][:9])
             if mode == self.MODE_STOP:
                 return
@@ -416,6 +430,20 @@ class ModelRunner:
             if toks is not None:
                 self._prev_toks = toks
             self.stats["steps"] += 1
+
+    def abort_comms(self) -> None:
+        """Watchdog / failure path: tear down this rank's RCCL communicators (a collective hung on
+        a dead peer returns) and mark the IPC collectives failed (every later call skips its
+        waits), so the process can exit instead of blocking in a GPU wait."""
+        st = self.model.st
+        for rc in {id(c): c for c in (getattr(st, "rccl_tp", None), getattr(st, "rccl_ep", None))
+                   if c is not None}.values():
+            try:
+                rc.abort()
+            except Exception:  # noqa: BLE001 - best effort on the way down
+                pass
+        if st.custom_ar is not None:
+            st.custom_ar.fail()
 
     def stop_workers(self) -> None:
         if self.channel is not None and self.model.st.tp_rank == 0:

@@ -43,6 +43,7 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_reduce_residual.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _P]
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_clear_error.argtypes = [_P]
+        lib.pk_car_set_error.argtypes = [_P]
         lib.pk_car_set_timeout_ms.argtypes = [_P, _LL]
         lib.pk_car_destroy.argtypes = [_P]
         lib.pk_car_destroy.restype = None
@@ -155,6 +156,12 @@ class CustomAllReduce:
         if self.ctx and self.lib.pk_car_check_error(self.ctx):
             raise CustomAllReduceError(f"custom all-reduce: a TP peer of rank {self.rank} did not arrive within "
                                        "the timeout (group failed; restart the job)")
+
+    def fail(self) -> None:
+        """Mark this rank's group failed (the failure path's abort): every later call returns at
+        once without waiting and :meth:`check` raises."""
+        if self.ctx:
+            self.lib.pk_car_set_error(self.ctx)
 
     def clear_error(self) -> None:
         """Tests only: re-arm after a deliberately provoked timeout."""

@@ -210,7 +210,22 @@ async def amain(argv=None) -> int:
         await http.shutdown()
     if rc:
         logger.error("exiting after engine failure", error=repr(srv.fatal_error))
+        hard_exit(rc)
     return rc
+
+
+def hard_exit(rc: int) -> None:
+    """Leave NOW with ``rc``: after an engine failure the GPU runtime may still hold a kernel
+    that waits on a dead peer, and the interpreter's normal teardown (device sync, process-group
+    destruction) would block on it; the supervisor restarts the process (compose
+    ``restart: unless-stopped``).  Not an exec: the process just ends."""
+    import os
+    import sys
+    try:
+        sys.stdout.flush()
+        sys.stderr.flush()
+    finally:
+        os._exit(rc)
 
 
 def main(argv=None) -> int:

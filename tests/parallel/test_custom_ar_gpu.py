@@ -90,7 +90,8 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
         q.put((rank, "ok"))
     except BaseException as e:  # noqa: BLE001
-        q.put((rank, repr(e)))
+        import traceback
+        q.put((rank, repr(e) + " " + traceback.format_exc()[-1500:]))
 
 
 def _rr_reference(slabs_all, partials_all, res, S):
@@ -138,14 +139,21 @@ def _fused_phase(car, rank, world, dev):
         pend = Partial(slabs.to(dev).reshape(-1), S, M, N) if S else partial.to(dev)
         out_parts = car.reduce_residual(pend, r_dev, parts)
         torch.cuda.synchronize()
-        assert torch.equal(r_dev.cpu(), want), (M, N, S)
+        gotr = r_dev.cpu()
+        if not torch.equal(gotr, want):
+            bad = (gotr != want)
+            idx = bad.nonzero()[:4].tolist()
+            raise AssertionError((M, N, S, "err", car.error(), "nbad", int(bad.sum()),
+                                  [(i, float(gotr[i[0], i[1]]), float(want[i[0], i[1]]), float(res[i[0], i[1]]))
+                                   for i in idx]))
         torch.testing.assert_close(out_parts.cpu(), want_sq, rtol=1e-5, atol=1e-3)
         # an all-gather and an all-reduce with other grids in between (epoch consistency)
         lg = torch.full((M, 256), float(rank), dtype=torch.bfloat16, device=dev)
         got = car.all_gather_last(lg)
         torch.cuda.synchronize()
-        assert torch.equal(got.cpu().view(M, world, 256)[:, :, 0].float(),
-                           torch.arange(world, dtype=torch.float32).expand(M, world))
+        gv = got.cpu().view(M, world, 256).float()
+        assert torch.equal(gv, torch.arange(world, dtype=torch.float32).view(1, world, 1).expand(M, world, 256)), \
+            (M, N, S, gv[0, :, 0].tolist(), gv[-1, :, -1].tolist(), car.error())
     # graph replay of the fused collective
     M, N = 8, 4096
     res0 = torch.randn(M, N, generator=g).to(torch.bfloat16)

@@ -61,11 +61,9 @@ def _worker(rank, port, model, out_path, sp=False):
 @pytest.mark.parametrize("model,sp", [("tiny-llama-gqa4", False), ("tiny-mixtral", False),
                                       ("tiny-llama-gqa4", True), ("tiny-mixtral", True)])
 def test_tp2_on_gpu_matches_tp1(tmp_path, model, sp, monkeypatch):
-    from polykey_service_amd.models import llama
     from polykey_service_amd.parallel.state import ParallelState
-    # like for like: TP > 1 keeps normalised activations, so the TP=1 reference does not fold
-    # the RMSNorm weights into its decode projections (that path has its own e2e test)
-    monkeypatch.setattr(llama, "FOLD_NORM", False)
+    # like for like: TP = 1 and TP = 2 both fold the RMSNorm weights into their decode
+    # projections (TP = 2 ends each row-parallel projection in the fused IPC collective)
     ref_logits, ref_toks = _run(_engine(model, ParallelState(device=torch.device("cuda:0"))))
     out = str(tmp_path / "tp.pt")
     mp.start_processes(_worker, args=(_port(), model, out, sp), nprocs=2, join=True, start_method="spawn")
