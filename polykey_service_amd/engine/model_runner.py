@@ -136,6 +136,10 @@ class ModelRunner:
         self.stats = {"steps": 0, "graph_steps": 0, "short_graph_steps": 0, "tokens": 0}
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None
+        # diagnostics (tools/tp_rehearsal.py): every step's logits, graphed steps included (a copy
+        # captured into each graph); read last_logits right after the step, before the next one
+        self.debug_logits = os.environ.get("POLYKEY_DEBUG_LOGITS") == "1"
+        self._graph_logits: Dict[Tuple[int, int], torch.Tensor] = {}
         self.channel = None
         self._prev_toks = None  # worker: last step's sampled ids (device), for continuations
         if model.st.tp_size > 1:
@@ -293,9 +297,12 @@ class ModelRunner:
         return self._handle(toks, ns)
 
     def _short(self, g: int, nd: int) -> int:
-        """1 when the step can replay bucket ``g``'s short-context graph."""
-        return int(bool(g and g in self.short_graphs and nd and
-                        int(self.h["context_lens"][:nd].max()) <= self.short_ctx))
+        """1 when every decode context fits one attention partition: the step replays bucket
+        ``g``'s short-context graph, or (eager, g = 0) launches the same one-workgroup-per-
+        (seq, kv head) decode attention -- so eager and graphed steps compute identical sums."""
+        if not (self.short_ctx and nd) or (g and g not in self.short_graphs):
+            return 0
+        return int(int(self.h["context_lens"][:nd].max()) <= self.short_ctx)
 
     def _handle(self, toks, ns: int):
         self.stats["steps"] += 1
@@ -463,14 +470,16 @@ class ModelRunner:
                 self.graphs[g].replay()
                 out = self.graph_out[g]
             self.stats["graph_steps"] += 1
+            if self.debug_logits:
+                self.last_logits = self._graph_logits[(g, int(bool(short)))]
             return out
-        md = self._metadata(nd, n, T, max_q)
+        md = self._metadata(nd, n, T, max_q, bool(short))
         hidden = self.model(d["input_ids"][:T], d["positions"][:T], md, self.kv_caches)
         if ns == 0:
             return None
         rows = hidden if ns == T else hidden.index_select(0, d["sample_idx"][:ns].long())
         logits = self.model.compute_logits(rows)
-        if self.keep_logits:
+        if self.keep_logits or self.debug_logits:
             self.last_logits = logits
         return sampler_ops.sample(logits, d["temperature"][:ns], d["top_k"][:ns], d["top_p"][:ns],
                                   d["min_p"][:ns], d["seeds"][:ns], d["offsets"][:ns])
@@ -524,6 +533,8 @@ class ModelRunner:
             def run():
                 hidden = self.model(d["input_ids"][:g], d["positions"][:g], md, self.kv_caches)
                 logits = self.model.compute_logits(hidden)
+                if self.debug_logits:
+                    self._graph_logits[(g, int(short))] = logits.clone()
                 return sampler_ops.sample(logits, d["temperature"][:g], d["top_k"][:g], d["top_p"][:g],
                                           d["min_p"][:g], d["seeds"][:g], d["offsets"][:g])
 

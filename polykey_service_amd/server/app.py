@@ -199,7 +199,8 @@ async def amain(argv=None) -> int:
                         tls_key=cfg.tls_key)
     await srv.start()
     if getattr(service, "llm", None) is not None:
-        service.llm.watchdog_s = 60.0
+        import os
+        service.llm.watchdog_s = float(os.environ.get("POLYKEY_WATCHDOG_S", "60"))
         srv.watch_backend(service.llm)
     http = None
     if cfg.http_addr:

@@ -25,9 +25,10 @@ def test_llama3_70b_tp8_shapes_on_one_gpu(tmp_path):
     logs = "".join(open(os.path.join(out, f)).read()[-3000:] for f in sorted(os.listdir(out)) if f.endswith(".log"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:] + logs
     res = json.load(open(os.path.join(out, "result.json")))
+    print(json.dumps(res))
     assert res["layers"] == 4 and res["tp"] == 8
     assert res["vocab_local"] == 16128 and res["lm_head_packed"], res
-    assert res["fused_tp_decode"], "decode did not take the fused TP collective chain"
+    assert res["fused_tp_decode"], ("decode did not take the fused TP collective chain", json.dumps(res))
     assert res["car_err"] == 0
     assert res["graph_steps"] > 0 and res["continuations"] > 0, res
     assert res["graph_equals_eager"], res

@@ -33,11 +33,27 @@ def _run(eng):
     eng.runner.keep_logits = True
     seqs = [eng.add_request(p, SamplingParams(max_tokens=4)) for p in PROMPTS]
     eng.step()
-    eng.step()  # first decode step (skinny GEMMs + all-reduce)
+    prefill = eng.runner.last_logits.float().cpu().clone()
+    eng.step()  # first decode step (skinny GEMMs + fused TP collective)
     logits = eng.runner.last_logits.float().cpu().clone()
     while eng.has_unfinished():
         eng.step()
-    return logits, [s.output_ids for s in seqs]
+    return (prefill, logits), [s.output_ids for s in seqs]
+
+
+def _compare(got_logits, got_toks, ref_logits, ref_toks):
+    """Prefill logits close; first tokens equal unless the reference has a near-tie (random
+    weights); first-decode-step logits close on every row that decoded the same token."""
+    (gp, gd), (rp, rd) = got_logits, ref_logits
+    torch.testing.assert_close(gp, rp, atol=1e-1, rtol=5e-2)
+    same = []
+    for row, (g, r) in enumerate(zip(got_toks, ref_toks)):
+        if g[0] == r[0]:
+            same.append(row)
+        else:
+            assert float(rp[row, g[0]]) >= float(rp[row].max()) - 0.1, (row, g[0], r[0])
+    assert same, "no row decoded the reference's first token"
+    torch.testing.assert_close(gd[same], rd[same], atol=1e-1, rtol=5e-2)
 
 
 def _worker(rank, port, model, out_path, sp=False):
@@ -69,10 +85,8 @@ def test_tp2_on_gpu_matches_tp1(tmp_path, model, sp, monkeypatch):
     mp.start_processes(_worker, args=(_port(), model, out, sp), nprocs=2, join=True, start_method="spawn")
     got = torch.load(out, weights_only=True)
     assert got["car_err"] == 0
-    # decode-step logits agree to bf16 noise (row-parallel partials are rounded per rank);
-    # random weights give near-ties, so only the prefill tokens must match exactly
-    torch.testing.assert_close(got["logits"], ref_logits, atol=1e-1, rtol=5e-2)
-    assert [t[0] for t in got["tokens"]] == [t[0] for t in ref_toks]
+    # logits agree to bf16 noise (row-parallel partials are rounded per rank)
+    _compare(got["logits"], got["tokens"], ref_logits, ref_toks)
 
 
 def _engine2(model, st, graphs):

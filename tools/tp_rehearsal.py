@@ -46,7 +46,9 @@ def _engine(a, st, graphs: bool, device: str):
     return LLMEngine(EngineConfig(model=a.model, num_layers=a.layers, max_num_seqs=max(a.batch, len(CMP_PROMPTS)),
                                   max_num_batched_tokens=a.max_batched, max_model_len=1024, num_kv_blocks=blocks,
                                   hip_graphs=graphs, overlap=graphs, graph_batch_sizes=(len(CMP_PROMPTS), a.batch),
-                                  device=device), st)
+                                  device=device, prefix_caching=False), st)
+    # prefix caching off: the comparison runs repeat the same prompts, and a prefill over a cached
+    # prefix rounds differently from a full one (bf16 logits of random weights have exact ties)
 
 
 def _greedy(eng, prompts, n, keep_first=False):
@@ -86,6 +88,36 @@ def _near_tie_ok(got, ref, logits, tie=0.15):
     return bad
 
 
+def _steps_logits(eng, prompts, n):
+    import torch
+    from polykey_service_amd.engine import SamplingParams
+    seqs = [eng.add_request(list(p), SamplingParams(max_tokens=n, ignore_eos=True, temperature=0.0)) for p in prompts]
+    out = []
+    while eng.has_unfinished():
+        eng.step()
+        torch.cuda.synchronize()
+        out.append(eng.runner.last_logits.float().cpu().clone())
+    return out, [list(s.output_ids) for s in seqs]
+
+
+def _debug_compare(eng, a):
+    """Eager vs graphed, step by step: max |diff| of the logits and each row's top-2 gap."""
+    graphs, short = eng.runner.graphs, eng.runner.short_graphs
+    eng.runner.graphs, eng.runner.short_graphs = {}, {}
+    le, te = _steps_logits(eng, CMP_PROMPTS, a.cmp_tokens)
+    eng.runner.graphs, eng.runner.short_graphs = graphs, short
+    lg, tg = _steps_logits(eng, CMP_PROMPTS, a.cmp_tokens)
+    rows = []
+    for k, (x, y) in enumerate(zip(le, lg)):
+        n = min(x.shape[0], y.shape[0])
+        d = (x[:n] - y[:n]).abs()
+        top = x[:n].topk(2, -1).values
+        rows.append({"step": k, "max_abs_diff": round(float(d.max()), 5),
+                     "row_max_diff": [round(float(v), 4) for v in d.max(-1).values],
+                     "top2_gap": [round(float(v), 4) for v in (top[:, 0] - top[:, 1])]})
+    return {"steps": rows, "tokens_equal": te == tg}
+
+
 def role_rank(a) -> int:
     import torch
     from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
@@ -108,10 +140,17 @@ def role_rank(a) -> int:
     eager, first = _greedy(eng, CMP_PROMPTS, a.cmp_tokens, keep_first=True)
     eng.runner.graphs, eng.runner.short_graphs = graphs, short
     # (2) the same prompts through the decode graphs, with pipelined continuations
+    eng.overlap = False  # graphs, one scheduled step at a time (no continuations)
+    if eng.runner.debug_logits:  # step-by-step logits, eager vs graphed
+        res["debug"] = _debug_compare(eng, a)
+    graphed_nc, _ = _greedy(eng, CMP_PROMPTS, a.cmp_tokens)
+    eng.overlap = True
     g0, c0 = eng.runner.stats["graph_steps"], eng.continuation_steps
     graphed, _ = _greedy(eng, CMP_PROMPTS, a.cmp_tokens)
-    res.update(graph_equals_eager=graphed == eager, graph_steps=eng.runner.stats["graph_steps"] - g0,
-               continuations=eng.continuation_steps - c0, tokens0=[t[:6] for t in eager])
+    res.update(graph_equals_eager=graphed == eager, graph_no_continuation_equals_eager=graphed_nc == eager,
+               graph_steps=eng.runner.stats["graph_steps"] - g0,
+               continuations=eng.continuation_steps - c0, tokens0=[t[:6] for t in eager],
+               graph_tokens0=[t[:6] for t in graphed], graph_nc_tokens0=[t[:6] for t in graphed_nc])
     ref_path = os.path.join(a.out, "ref.pt")
     if os.path.exists(ref_path):
         ref = torch.load(ref_path, weights_only=True)
