@@ -204,6 +204,8 @@ def launch(a) -> int:
         e = dict(env, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(a.world),
                  LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(a.world), POLYKEY_CUSTOM_AR="force",
                  POLYKEY_CUSTOM_AR_TIMEOUT_S=os.environ.get("POLYKEY_CUSTOM_AR_TIMEOUT_S", "120"))
+        if a.hw_queues:
+            e["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
         cmd = me + common + ["--role", "rank", "--rank", str(r)]
         if a.prof:
             cmd = ["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", os.path.join(a.out, f"trace_r{r}"),
@@ -239,6 +241,10 @@ def main() -> int:
     ap.add_argument("--ref", choices=["none", "run", "file"], default="none")
     ap.add_argument("--prof", action="store_true", help="each rank under rocprofv3 --kernel-trace")
     ap.add_argument("--timeout", type=float, default=1000.0)
+    # one HW queue per rank: 8 processes x the default 4 queues oversubscribe the hardware scheduler,
+    # which then time-slices the ranks and every collective waits for a slice (4-layer 70B TP=8
+    # rehearsal: 7.4 ms / step at 1 queue per rank, 128 ms at 2, ~500 ms at the default)
+    ap.add_argument("--hw-queues", type=int, default=1, help="GPU_MAX_HW_QUEUES per rank (0: the box default)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tp_rehearsal"))
     a = ap.parse_args()
     if a.role == "ref":
