@@ -34,24 +34,13 @@ constexpr int kHD = 128;
 constexpr int kStep = 32;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1e30f;
-#ifndef PK_DECODE_WAVES
-#define PK_DECODE_WAVES 4
-#endif
-constexpr int kDecodeWaves = PK_DECODE_WAVES;  // waves per (seq, kv head, partition); 8 measured ~10 % slower at 384 keys
+constexpr int kDecodeWaves = 4;  // waves per (seq, kv head, partition); 8 measured ~10 % slower at 384 keys
 int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
-#ifndef PK_DECODE_KV_NT
-#define PK_DECODE_KV_NT 0  // in-situ decode step 4.43 (plain) vs 4.45 ms (NT): tools/ab_decode.py
-#endif
-// K/V stream loads (read once per step: non-temporal when PK_DECODE_KV_NT)
-__device__ __forceinline__ bf16x8_t ldkv(const bf16_t* p) {
-#if PK_DECODE_KV_NT
-  return __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(p));
-#else
-  return ld8(p);
-#endif
-}
+// K/V stream loads: plain (non-temporal measured slower: in-situ decode step 4.43 vs 4.45 ms,
+// tools/ab_decode.py)
+__device__ __forceinline__ bf16x8_t ldkv(const bf16_t* p) { return ld8(p); }
 
 __device__ __forceinline__ bf16x8_t zero8() {
   u32x4 z = {0u, 0u, 0u, 0u};
@@ -104,7 +93,7 @@ struct KVFrag {
 // (past it the address is clamped, the data never used), so the block lookups stay inside the
 // caller's block-table window.  K comes from the fragment-native cache tile of step s (common.h
 // kcache_off: one contiguous KiB per load instruction); V likewise (common.h vcache_off): lane
-// (r, g) reads keys 8g..8g+7 of channel 16 dt + r, one contiguous KiB per d-tile (ldkv: plain loads; PK_DECODE_KV_NT=1 makes them non-temporal).
+// (r, g) reads keys 8g..8g+7 of channel 16 dt + r, one contiguous KiB per d-tile (ldkv: plain loads).
 __device__ __forceinline__ void load_kv(KVFrag& f, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                                         int64_t blk_stride, const int* __restrict__ bt, int bt_base, int bs, int s,
                                         int lim) {
@@ -207,9 +196,6 @@ __device__ __forceinline__ void load_q(bf16x8_t (&qf)[4], const bf16_t* q, bool 
 
 
 // ------------------------------------------------------------------------------ decode
-#ifndef PK_DECODE_BT_PREFETCH
-#define PK_DECODE_BT_PREFETCH 1  // request the block-table window first (see paged_decode_kernel)
-#endif
 // grid (n_kv, n_seqs, min(n_parts, z)), block 64*NW (NW waves).  LDS: NW waves x 16 cols x 128 d fp32.
 // Decode attention fed straight from the QKV projection's split-K slabs (FROM_QKV): the
 // workgroup of (seq, kv head h) sums the S fp32 slabs of its G query heads and of k/v head h,
@@ -240,7 +226,6 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
   __shared__ float sn_s[16];
   static_assert(64 * NW >= 256, "the new-token scores use 16 lanes per query head, G <= 16");
   const int h = blockIdx.x, seq = blockIdx.y;
-#if PK_DECODE_BT_PREFETCH
   // the first partition's block-table window, requested before anything else so its round
   // trip overlaps the context / q preparation instead of following it (entries past the
   // sequence's blocks are in-bounds of the row and never used)
@@ -248,7 +233,6 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
   int bt_pre = 0;
   if (static_cast<int>(threadIdx.x) <= kPart / bs && pre_b0 + static_cast<int>(threadIdx.x) < max_blocks)
     bt_pre = block_tables[static_cast<int64_t>(seq) * max_blocks + pre_b0 + threadIdx.x];
-#endif
   const int ctx = context_lens[seq];
   const int G = n_q / n_kv;
   if (ctx <= 0) {
@@ -374,11 +358,9 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     const int end = min(ctx_c, begin + kPart);
     const int b0 = begin / bs, nblk = (end - 1) / bs - b0 + 1;
     __syncthreads();  // the previous partition's block-table readers are done
-#if PK_DECODE_BT_PREFETCH
     if (part == static_cast<int>(blockIdx.z) && kPart % bs == 0) {  // nblk <= kPart / bs <= 64 * NW
       if (static_cast<int>(threadIdx.x) < nblk) bt_s[threadIdx.x] = bt_pre;
     } else
-#endif
       for (int i = threadIdx.x; i < nblk; i += 64 * NW)
         bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
     __syncthreads();
@@ -547,112 +529,6 @@ __global__ void __launch_bounds__(512) paged_prefill_kernel(
   }
 }
 
-// ------------------------------------------------------- prefill with LDS-shared K/V tiles
-// grid (ceil(max_q_len / (16 QT)), n_seqs, n_kv), block 64 * NW with NW = QT * G (G = n_q / n_kv
-// <= 8): one workgroup per (16 QT-query block, sequence, kv head); wave w computes query head
-// h*G + w % G for the 16 queries of column tile w / G.  Every 32-key K / V tile of the kv head is staged in
-// LDS once per workgroup (register staged, double buffered, one barrier per tile) and consumed
-// by all QT*G waves — K/V bytes per MFMA drop QT*G-fold against paged_prefill_kernel, whose waves
-// each stream K/V from global — while each wave keeps the per-wave register footprint of one
-// 16-query tile, so two waves share every SIMD and hide each other's latencies.
-// LDS images are laid out for the fragment reads: K rows in the order the S^T = K.Q^T
-// A-fragments of key tile t read them (rows t*16 .. t*16+15 contiguous) with a 16-byte pad,
-// V^T rows (channel d, 32 keys) with a 16-byte pad.  The math is attend_step's.
-constexpr int kKRow = kHD + 8;     // K_s row, bf16 elements (272 B)
-constexpr int kVRow = kStep + 8;   // V_s row, bf16 elements (80 B)
-
-template <int NW, int QT>
-__global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
-    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc,
-    const bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
-    const int* __restrict__ cu_q, int n_kv, int bs, int max_blocks, int q_stride, int out_stride, float scale2) {
-  __shared__ __attribute__((aligned(16))) bf16_t K_s[2][kStep][kKRow];
-  __shared__ __attribute__((aligned(16))) bf16_t V_s[2][kHD][kVRow];
-  constexpr int G = NW / QT;             // query heads of the GQA group (QT 16-query tiles each)
-  constexpr int kPQ = 16 * QT;          // queries per workgroup
-  constexpr int NP = 1024 / (64 * NW);  // 16-byte pieces (512 of K, 512 of V^T) per thread per tile
-  const int qb = blockIdx.x, seq = blockIdx.y, h = blockIdx.z;
-  const int q0 = cu_q[seq], L = cu_q[seq + 1] - q0;
-  if (qb * kPQ >= L) return;
-  const int ctx = context_lens[seq];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int hq = h * G + w % G;
-  const int qi = qb * kPQ + (w / G) * 16 + r;
-  const bool valid = qi < L;
-  const int qpos = valid ? ctx - L + qi : -1;
-  const int last_q = min(L - 1, qb * kPQ + kPQ - 1);
-  const int k_end = min(ctx, ctx - L + last_q + 1);  // keys any query of the block can see
-  const int nsteps = (k_end + kStep - 1) / kStep;
-  const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
-  const bf16_t* kch = kc + static_cast<int64_t>(h) * bs * kHD;
-  const bf16_t* vch = vc + static_cast<int64_t>(h) * kHD * bs;
-  const int* bt = block_tables + static_cast<int64_t>(seq) * max_blocks;
-
-  // piece p < 512: K (key p >> 4, 16-byte chunk p & 15); p >= 512: V^T (channel (p-512) >> 2,
-  // keys 8 ((p-512) & 3) .. +8, contiguous in the transposed cache).  Keys past k_end are
-  // clamped to the last visible one (masked in the softmax); no load sits behind a branch.
-  u32x4 stage[NP];
-  auto load_tile = [&](int step) {
-    const int s0 = min(step, nsteps - 1) * kStep;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int p = threadIdx.x + i * 64 * NW;
-      const bool isk = p < 512;
-      const int pv = p & 511;
-      // K: the step's fragment-native tile is one contiguous 8 KiB (piece pv at pv * 8)
-      const int tok = isk ? s0 : min(s0 + 8 * (pv & 3), ((k_end - 1) >> 3) << 3);
-      const int64_t base = static_cast<int64_t>(bt[tok / bs]) * blk_stride;
-      const bf16_t* src = isk ? kch + base + (tok % bs) * kHD + pv * 8 : vch + base + vcache_off(tok % bs, pv >> 2);
-      stage[i] = *reinterpret_cast<const u32x4*>(src);
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int p = threadIdx.x + i * 64 * NW;
-      const int pv = p & 511;
-      // K piece pv = ((t * 4 + kk) * 64 + lane): key row t * 16 + (lane & 15), dims 32 (lane >> 4) + 8 kk
-      bf16_t* dst = p < 512 ? &K_s[buf][(pv >> 8) * 16 + (pv & 15)][32 * ((pv >> 4) & 3) + 8 * ((pv >> 6) & 3)]
-                            : &V_s[buf][pv >> 2][(pv & 3) * 8];
-      *reinterpret_cast<u32x4*>(dst) = stage[i];
-    }
-  };
-
-  bf16x8_t qf[4];
-  load_q(qf, q + static_cast<int64_t>(q0 + (valid ? qi : 0)) * q_stride + hq * kHD, valid);
-  WaveState st;
-  init_state(st);
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int step = 0; step < nsteps; ++step) {
-    const int buf = step & 1;
-    load_tile(step + 1);  // the next tile's global loads fly during this tile's math
-    KVFrag f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) f.k[t][kk] = *reinterpret_cast<const bf16x8_t*>(&K_s[buf][t * 16 + r][32 * g + 8 * kk]);
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) f.v[dt] = *reinterpret_cast<const bf16x8_t*>(&V_s[buf][16 * dt + r][8 * g]);
-    attend_step(st, qf, f, step * kStep, ctx, qpos, scale2);
-    store_tile(buf ^ 1);  // every wave finished reading buf ^ 1 before the previous barrier
-    __syncthreads();
-  }
-  const float lsum = col_sum(st.l);
-  if (!valid) return;
-  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-  bf16_t* o = out + static_cast<int64_t>(q0 + qi) * out_stride + hq * kHD;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    uint2 v;
-    v.x = pack2(st.o[dt][0] * inv, st.o[dt][1] * inv);
-    v.y = pack2(st.o[dt][2] * inv, st.o[dt][3] * inv);
-    *reinterpret_cast<uint2*>(o + 16 * dt + 4 * g) = v;
-  }
-}
-
 // ------------------------------------------- prefill on 32x32x16 MFMAs, P kept in registers
 // One wave owns 32 queries of one head against 64-key steps (guide Appendix B "Fused attention
 // prefill" structure):
@@ -666,8 +542,8 @@ __global__ void __launch_bounds__(64 * NW) paged_prefill_lds_kernel(
 // The K rows of the QK^T A operand are read with bits 2 and 3 of the key index swapped, so
 // X row rho holds key swap23(rho) and that permuted k order becomes the NATURAL key order
 // 16s + 8h + j -- V^T fragments are then plain 16-byte reads of 8 consecutive keys.
-// Per 64-key step and wave: 32 MFMAs of 32x32x16 against 32 KiB of LDS fragment reads (half the
-// bytes per FLOP of paged_prefill_lds_kernel) and 32 exp2 per lane.
+// Per 64-key step and wave: 32 MFMAs of 32x32x16 against 32 KiB of LDS fragment reads and 32
+// exp2 per lane.
 // Workgroup: 8 waves = G heads of the kv head's GQA group x (8 / G) 32-query groups; K / V
 // tiles staged through LDS (register staged, double buffered, one barrier per step).
 constexpr int kKS = 64;            // keys per step
@@ -867,13 +743,8 @@ __global__ void __launch_bounds__(64 * NW, 2) paged_prefill_mfma32_kernel(
     }
 }
 
-int g_attn_nw = 0;  // waves per 32x32-MFMA prefill workgroup: 0 = default (4; 8 when G = 8), else 4 / 8
-int g_prefill_lds = 2;  // pk_set_prefill_impl: 2 = 32x32-MFMA kernel (default), 1 = LDS-tiled 16x16 kernel, 0 = per-wave kernel
 
-#ifndef PK_DECODE_PART
-#define PK_DECODE_PART 512  // keys per decode partition (ops/attention.py _PART must match)
-#endif
-constexpr int kDecodePart = PK_DECODE_PART;
+constexpr int kDecodePart = 512;  // keys per decode partition (ops/attention.py _PART must match)
 
 }  // namespace
 
@@ -944,18 +815,6 @@ PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, 
                        n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
 }
 
-PK_EXPORT int pk_set_attn_waves(int nw) {  // A/B knob: waves per 32x32-MFMA prefill workgroup (0 auto, 4, 8)
-  if (nw != 0 && nw != 4 && nw != 8) return -1;
-  g_attn_nw = nw;
-  return 0;
-}
-
-PK_EXPORT int pk_set_prefill_impl(int lds) {
-  if (lds < 0 || lds > 2) return -1;
-  g_prefill_lds = lds;
-  return 0;
-}
-
 PK_EXPORT int pk_set_decode_z(int z) {
   if (z < 1) return -1;
   g_decode_z = z;
@@ -969,11 +828,11 @@ PK_EXPORT int pk_paged_prefill(void* out, const void* q, const void* k_cache, co
   if (n_seqs <= 0 || max_q_len <= 0) return 0;
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0) return -1;  // K tiles: 32 keys
   const int G = n_q / n_kv;
-  if (g_prefill_lds == 2 && (G == 1 || G == 2 || G == 4 || G == 8)) {
+  if (G == 1 || G == 2 || G == 4 || G == 8) {
     // 4-wave workgroups (two per CU: independent barriers let one workgroup's MFMAs overlap the
     // other's softmax) where the GQA group fits; G = 8 needs all 8 waves for one query group
     // (profiles/r2_prefill_attention.txt: 4 waves >= 8 waves at every measured shape)
-    const int nw = G == 8 || g_attn_nw == 8 ? 8 : 4;
+    const int nw = G == 8 ? 8 : 4;
     const int pq = 32 * nw / G;  // queries per workgroup (nw waves: G heads x nw/G 32-query groups)
     const dim3 grid(n_kv, n_seqs, (max_q_len + pq - 1) / pq);
 #define PK_PREFILL_M32(GG, NWW)                                                                                \
@@ -986,38 +845,12 @@ PK_EXPORT int pk_paged_prefill(void* out, const void* q, const void* k_cache, co
       case 1 * 16 + 4: PK_PREFILL_M32(1, 4); break;
       case 2 * 16 + 4: PK_PREFILL_M32(2, 4); break;
       case 4 * 16 + 4: PK_PREFILL_M32(4, 4); break;
-      case 1 * 16 + 8: PK_PREFILL_M32(1, 8); break;
-      case 2 * 16 + 8: PK_PREFILL_M32(2, 8); break;
-      case 4 * 16 + 8: PK_PREFILL_M32(4, 8); break;
       default: PK_PREFILL_M32(8, 8); break;
     }
 #undef PK_PREFILL_M32
     return PK_CHECK_LAUNCH();
   }
-  if (g_prefill_lds && (G == 1 || G == 2 || G == 4 || G == 8)) {
-    // 16-query column tiles per workgroup: 4 (64 queries: more waves share each K/V tile) for
-    // G <= 4 and prompts < 2K; 2 otherwise (the 1024-thread cap; long causal prompts balance
-    // better over more, smaller workgroups — tools/bench_prefill_attn.py)
-    const int qt = G <= 4 && max_q_len < 2048 ? 4 : 2;
-    const dim3 grid((max_q_len + 16 * qt - 1) / (16 * qt), n_seqs, n_kv);
-#define PK_PREFILL_LDS(NW, QT)                                                                                 \
-  paged_prefill_lds_kernel<NW, QT><<<grid, 64 * NW, 0, stream>>>(                                              \
-      static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<const bf16_t*>(k_cache),          \
-      static_cast<const bf16_t*>(v_cache), static_cast<const int*>(block_tables),                              \
-      static_cast<const int*>(context_lens), static_cast<const int*>(cu_q), n_kv, bs, max_blocks, q_stride,    \
-      out_stride, scale * kLog2e)
-    switch (G * 8 + qt) {
-      case 1 * 8 + 4: PK_PREFILL_LDS(4, 4); break;
-      case 1 * 8 + 2: PK_PREFILL_LDS(2, 2); break;
-      case 2 * 8 + 4: PK_PREFILL_LDS(8, 4); break;
-      case 2 * 8 + 2: PK_PREFILL_LDS(4, 2); break;
-      case 4 * 8 + 4: PK_PREFILL_LDS(16, 4); break;
-      case 4 * 8 + 2: PK_PREFILL_LDS(8, 2); break;
-      default: PK_PREFILL_LDS(16, 2); break;
-    }
-#undef PK_PREFILL_LDS
-    return PK_CHECK_LAUNCH();
-  }
+  // other GQA groups (3, 5, 6, 16, ...): one wave per query head, 16 queries per workgroup
   const int W = G > 8 ? 8 : G;
   if (G % W) return -1;
   dim3 grid((max_q_len + 15) / 16, n_seqs, n_kv * (G / W));

@@ -59,14 +59,11 @@ class AsyncLLM:
         # request waits one gap.  0 disables.
         self.arrival_window_s = float(os.environ.get("POLYKEY_ARRIVAL_WINDOW_MS", "8")) / 1e3
         self.arrival_gap_s = float(os.environ.get("POLYKEY_ARRIVAL_GAP_MS", "2")) / 1e3
-        # "step": stop once the waiting requests fill one prefill step; "burst": keep collecting
-        # until the burst is over (the whole burst's prefill then runs without gRPC arrivals
-        # contending for the GIL with its kernel launches)
-        self.arrival_fill = os.environ.get("POLYKEY_ARRIVAL_FILL", "step")
+
         # The engine thread and the asyncio (gRPC) thread share the GIL.  CPython's default 5 ms
         # switch interval lets a burst of RPC handling hold the engine thread off for whole
         # decode steps (the GPU idles meanwhile); a short interval hands the GIL over promptly.
-        sys.setswitchinterval(float(os.environ.get("POLYKEY_GIL_SWITCH_S", "0.002")))
+        sys.setswitchinterval(0.002)
         self._fatal_sent = False
         self._thread = threading.Thread(target=self._run, name="polykey-engine", daemon=True)
         self._thread.start()
@@ -228,8 +225,7 @@ class AsyncLLM:
         eng = self.engine
         deadline = time.monotonic() + self.arrival_window_s
         self.stats["arrival_waits"] += 1
-        burst = self.arrival_fill == "burst"
-        while not self._stop and (eng.first_step_unfilled() or (burst and eng.idle_with_waiting())):
+        while not self._stop and eng.first_step_unfilled():
             left = deadline - time.monotonic()
             if left <= 0:
                 return

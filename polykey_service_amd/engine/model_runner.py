@@ -51,16 +51,11 @@ class RunnerConfig:
     graph_batch_sizes: Tuple[int, ...] = ()
 
 
-# Long-context decode merges its partitions in a second kernel by default: the in-kernel
-# last-arriver merge needs an agent-scope release per partition (an L2 write-back on each XCD)
-# and measured 1.7-1.9x slower at 1-4K contexts (tools/bench_attn.py); contexts that fit one
-# partition need no merge either way.
-DECODE_INKERNEL_MERGE = os.environ.get("POLYKEY_DECODE_INKERNEL_MERGE", "0") == "1"
-# stage step inputs with a kernel reading pinned memory instead of an SDMA copy
-HOST_COPY_KERNEL = os.environ.get("POLYKEY_HOST_COPY_KERNEL", "1") == "1"
-# a second decode graph per bucket for steps whose contexts all fit one attention partition:
-# one workgroup per (seq, kv head) and no partition-merge kernel in each layer
-SHORT_DECODE_GRAPHS = os.environ.get("POLYKEY_SHORT_DECODE_GRAPHS", "1") == "1"
+# Long-context decode merges its partitions in a second kernel (an in-kernel last-arriver merge
+# needs an agent-scope release per partition and measured 1.7-1.9x slower at 1-4K contexts,
+# tools/bench_attn.py).  Step inputs are staged by a kernel reading pinned memory instead of an
+# SDMA copy.  Each decode bucket has a second graph for steps whose contexts all fit one attention
+# partition (one workgroup per (seq, kv head), no merge kernel).
 
 
 class _Layout:
@@ -128,11 +123,10 @@ class ModelRunner:
         self.graph_out: Dict[int, torch.Tensor] = {}
         self.short_graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self.short_graph_out: Dict[int, torch.Tensor] = {}
-        self.short_ctx = attn_ops._PART if SHORT_DECODE_GRAPHS and cfg.max_model_len > attn_ops._PART else 0
+        self.short_ctx = attn_ops._PART if cfg.max_model_len > attn_ops._PART else 0
         self.graph_pool = None
         a0 = model.layers[0].attn
-        self.part_o, self.part_ml, self.part_ctr = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks,
-                                                                             self.bs, device, n_kv=a0.nkv)
+        self.part_o, self.part_ml = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks, self.bs, device)
         self.stats = {"steps": 0, "graph_steps": 0, "short_graph_steps": 0, "tokens": 0}
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None
@@ -244,7 +238,7 @@ class ModelRunner:
             decode_block_tables=d["block_tables"][:nd] if nd else None,
             decode_context_lens=d["context_lens"][:nd] if nd else None,
             decode_part_o=self.part_o, decode_part_ml=self.part_ml,
-            decode_counters=self.part_ctr if DECODE_INKERNEL_MERGE else None,
+            decode_counters=None,
             decode_max_ctx=self.short_ctx if short else 0)
         if npf:
             md.prefill_block_tables = d["block_tables"][nd:n]
@@ -398,7 +392,7 @@ class ModelRunner:
     def _stage_local(self, n: int) -> None:
         """Copy the first ``n`` words of the current pinned staging buffer to the device.  On
         the GPU a kernel reads the pinned buffer directly (no SDMA hand-off)."""
-        if self.device.type == "cuda" and HOST_COPY_KERNEL:
+        if self.device.type == "cuda":
             native.call("pk_copy_from_host", self.dev_buf.data_ptr(), self.host_buf.data_ptr(), n * 4,
                         native.stream_ptr(self.device))
         else:

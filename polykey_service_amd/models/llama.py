@@ -36,28 +36,15 @@ from .config import ModelConfig
 from .weights import SafetensorsIndex, random_full, random_shard, shard_cols, shard_rows
 
 
-# decode attention consumes the QKV split-K slabs directly (POLYKEY_FUSED_QKV_ATTN=0: separate
-# reduce + RoPE + cache-write kernel, then attention)
-FUSED_QKV_ATTENTION = os.environ.get("POLYKEY_FUSED_QKV_ATTN", "1") == "1"
-# Decode (TP = 1, dense, block-packed weights): every RMSNorm weight is folded into the columns of
-# the projection that consumes it and that projection scales its output rows by rinv, so the
-# per-layer norm kernels shrink to residual updates (4x wider grid, no normalised copy written).
-# POLYKEY_FOLD_NORM=0: normalised activations as in prefill.
-FOLD_NORM = os.environ.get("POLYKEY_FOLD_NORM", "1") == "1"
+# Decode (dense, block-packed weights): every RMSNorm weight is folded into the columns of the
+# projection that consumes it and that projection scales its output rows by rinv, so the per-layer
+# norm kernels shrink to residual updates (TP = 1) or to the fused TP collective (TP > 1).  Tests
+# switch it off to compare against the normalised chain.
+FOLD_NORM = True
 # TP > 1 steps with at least SP_MIN_TOKENS tokens (prefill) run with a token-sharded residual
 # stream: reduce-scatter / all-gather around the norms instead of all-reduces (_forward_sp).
 SEQUENCE_PARALLEL = os.environ.get("POLYKEY_SEQUENCE_PARALLEL", "1") == "1"
 SP_MIN_TOKENS = int(os.environ.get("POLYKEY_SP_MIN_TOKENS", "256"))
-# Folded-norm decode: the o / down projections (64-row n-blocks, split-K INLAUNCH_SPLIT) reduce
-# their own split-K slabs in-launch -- the last split of each n-block to arrive adds the sum into
-# the residual and writes the row sums of squares the next projection's RowScale needs -- instead
-# of a separate residual-update kernel after each (tools/gemm_lab.hip o_res / down_res: -2 us per
-# projection in isolation; neutral on the graph-captured 8B step, profiles/r2_decode_ab.txt, so off
-# by default).
-INLAUNCH_RESIDUAL = os.environ.get("POLYKEY_INLAUNCH_RESIDUAL", "0") == "1"
-INLAUNCH_SPLIT = int(os.environ.get("POLYKEY_INLAUNCH_SPLIT", "4"))
-HALF_O_SLABS = os.environ.get("POLYKEY_HALF_O_SLABS", "1") == "1"
-HALF_QKV_SLABS = os.environ.get("POLYKEY_HALF_QKV_SLABS", "0") == "1"
 
 
 def _p(t: torch.Tensor) -> nn.Parameter:
@@ -79,7 +66,8 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
               half: bool = False):
     """Row-parallel projection feeding a residual add + RMSNorm.  TP=1 decode returns the
     split-K partial slabs unreduced (the norm kernel sums them); TP>1 all-reduces bf16.
-    ``half``: slabs from 64-row n-blocks at half the split (the o-projection, HALF_O_SLABS)."""
+    ``half``: slabs from 64-row n-blocks at half the split (the o-projection: -0.7..1.5 % decode
+    step, profiles/r2_decode_ab.txt)."""
     if get_state().tp_size == 1 and ws is not None and gemm.skinny_ok(x, w) and gemm.norm_fusable(w.shape[0]):
         S = gemm.choose_split(w.shape[0], x.shape[1], x.shape[0])
         if ws.numel() >= S * x.shape[0] * w.shape[0]:
@@ -142,12 +130,12 @@ class LlamaAttention(nn.Module):
         S = gemm.choose_split(self.qkv.shape[0], x.shape[1], T)
         if ws is not None and gemm.skinny_ok(x, self.qkv) and S > 1 and ws.numel() >= S * T * self.qkv.shape[0]:
             p = gemm.linear_partial(x, self.qkv, ws, S, packed=self.qkv_p)
-            if md.num_prefill == 0 and FUSED_QKV_ATTENTION:
+            if md.num_prefill == 0:
                 # pure decode: the attention kernel itself reduces the QKV slabs, applies RoPE
                 # and writes the new k / v into the paged cache
                 a = attn_ops.paged_decode_from_qkv(p, positions, cos_sin, k_cache, v_cache, md, self.scale,
                                                    self.nq, self.nkv)
-                return _proj_out(a, self.o, ws, self.o_p, half=HALF_O_SLABS)
+                return _proj_out(a, self.o, ws, self.o_p, half=True)
             # split-K QKV whose epilogue kernel also applies RoPE and writes the KV cache
             q = gemm.qkv_reduce_rope_cache(p, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq,
                                            self.nkv)
@@ -155,7 +143,7 @@ class LlamaAttention(nn.Module):
             return _proj_out(self.attend(gemm.linear(x, self.qkv, packed=self.qkv_p), positions, md, cos_sin, kv),
                              self.o, ws, self.o_p)
         a = attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
-        return _proj_out(a, self.o, ws, self.o_p, half=HALF_O_SLABS)
+        return _proj_out(a, self.o, ws, self.o_p, half=True)
 
     def attend(self, qkv: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
                kv: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
@@ -350,8 +338,6 @@ class LlamaForCausalLM(nn.Module):
             return self._forward_sp(input_ids, positions, md, kv_caches)
         x = self.embed_tokens(input_ids)
         ws = self.workspace(x.shape[0])
-        if ws is not None and self._fused_decode_ok(x):
-            return self._forward_fused(x, positions, md, kv_caches, ws)
         if ws is not None and self._rowscale_ok(x):
             return self._forward_rowscale(x, positions, md, kv_caches, ws)
         residual = None
@@ -417,67 +403,6 @@ class LlamaForCausalLM(nn.Module):
         return comm.sp_reduce_scatter(g, lay, comm.RowsFn(
             lambda r, o, w=mlp.down, wp=mlp.down_p: gemm.linear(r, w, out=o, packed=wp), mlp.down.shape[0]))
 
-    # ------------------------------------------------------------------ fused decode chain
-    # Off by default: measured slower on MI355X (tools/bench_gemm.py "fused decode chain": the
-    # last-arriver reduction of 256 KB of fp32 slabs per 128-column tile is serial, and the
-    # in-GEMM RMSNorm prologue re-normalises A in every workgroup) than GEMM + separate reduce.
-    FUSED_DECODE = os.environ.get("POLYKEY_FUSED_DECODE", "0") == "1"
-
-    def _fused_decode_ok(self, x: torch.Tensor) -> bool:
-        """TP=1 decode-sized batches run the 5-kernel-per-layer chain of :meth:`_forward_fused`."""
-        if not self.FUSED_DECODE or self.st.tp_size != 1 or self.cfg.head_dim != 128:
-            return False
-        l0 = self.layers[0]
-        if not isinstance(l0.mlp, LlamaMLP):
-            return False
-        H = self.cfg.hidden_size
-        return (H % 256 == 0 and gemm.skinny_ok(x, l0.attn.qkv) and gemm.skinny_ok(x, l0.mlp.gate_up)
-                and l0.attn.o.shape[1] % 256 == 0 and l0.mlp.down.shape[1] % 256 == 0)
-
-    def _fused_buffers(self):
-        """Fixed-address (graph-safe) split-K tickets and two sum-of-squares part buffers."""
-        if getattr(self, "_fbuf", None) is None:
-            H = self.cfg.hidden_size
-            n = (H // 128) * gemm.SKINNY_MAX_M
-            ctr = torch.zeros(4096, dtype=torch.int32, device=self.device)
-            self._fbuf = (ctr, torch.zeros(n, dtype=torch.float32, device=self.device),
-                          torch.zeros(n, dtype=torch.float32, device=self.device))
-        return self._fbuf
-
-    def _forward_fused(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata,
-                       kv_caches: List[Tuple[torch.Tensor, torch.Tensor]], ws: torch.Tensor) -> torch.Tensor:
-        """Decode step with every norm and split-K reduction folded into a GEMM:
-
-            qkv GEMM (prologue: RMSNorm(ln1); epilogue: reduce + RoPE + KV-cache write)
-            paged attention
-            o GEMM    (epilogue: reduce + residual add + row sum-of-squares parts)
-            gate_up   (prologue: RMSNorm(ln2); epilogue: SiLU(gate) * up)
-            down GEMM (epilogue: reduce + residual add + row sum-of-squares parts)
-
-        Layer 0's ln1 and the final norm are separate kernels.  The residual stream is updated
-        in place; a layer's norm weights are applied by the *consumer* GEMM from the producer's
-        per-(128-column block, row) sum-of-squares parts."""
-        T = x.shape[0]
-        H = self.cfg.hidden_size
-        ctr, pa, pb = self._fused_buffers()
-        parts_attn = pa[: (H // 128) * T].view(H // 128, T)  # written by o, read by gate_up
-        parts_mlp = pb[: (H // 128) * T].view(H // 128, T)   # written by down, read by next qkv
-        residual = x
-        h = ops.rms_norm(residual, self.layers[0].ln1, self.layers[0].eps)
-        for i, layer in enumerate(self.layers):
-            at, mlp = layer.attn, layer.mlp
-            kc, vc = kv_caches[i]
-            norm = None if i == 0 else gemm.NormIn(parts_mlp, layer.ln1, layer.eps)
-            q = gemm.linear_qkv_rope(residual if norm is not None else h, at.qkv, ws, ctr, positions,
-                                     self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv, packed=at.qkv_p,
-                                     norm=norm)
-            a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
-            gemm.linear_add_residual(a, at.o, ws, ctr, residual, parts_attn, packed=at.o_p)
-            h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_p,
-                                 norm=gemm.NormIn(parts_attn, layer.ln2, layer.eps))
-            gemm.linear_add_residual(h, mlp.down, ws, ctr, residual, parts_mlp, packed=mlp.down_p)
-        return gemm.norm_apply(residual, parts_mlp, self.norm, self.cfg.rms_eps)
-
     # ------------------------------------------------------------------ folded-norm decode chain
     def _rowscale_ok(self, x: torch.Tensor) -> bool:
         l0 = self.layers[0]
@@ -511,34 +436,20 @@ class LlamaForCausalLM(nn.Module):
         last = len(self.layers) - 1
         if self.st.tp_size > 1:
             return self._forward_rowscale_tp(residual, parts, positions, md, kv_caches, ws, buf, buf2)
-        inlaunch = INLAUNCH_RESIDUAL and H % 64 == 0
-        ctr = self._fused_buffers()[0] if inlaunch else None
         for i, layer in enumerate(self.layers):
             at, mlp = layer.attn, layer.mlp
             kc, vc = kv_caches[i]
-            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf,
-                                             half=HALF_QKV_SLABS)
-            if md.num_prefill == 0 and FUSED_QKV_ATTENTION:
+            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf)
+            if md.num_prefill == 0:
                 a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
             else:
                 q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
                 a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
-            if inlaunch:  # the o-projection's last splits add into the residual themselves
-                parts = gemm.linear_add_residual(a, at.o, ws, ctr, residual, buf2, S=INLAUNCH_SPLIT, packed=at.o_p,
-                                                 half=True)
-            else:
-                # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode
-                # step, profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
-                parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=HALF_O_SLABS),
-                                            residual, buf2)
+            # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
+            # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
+            parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True), residual, buf2)
             h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf,
                                  rowscale=gemm.RowScale(parts, layer.eps))
-            if inlaunch:
-                parts = gemm.linear_add_residual(h, mlp.down, ws, ctr, residual, buf, S=INLAUNCH_SPLIT,
-                                                 packed=mlp.down_p, half=True)
-                if i == last:
-                    x = gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
-                continue
             d = gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p)
             if i < last:
                 parts = gemm.residual_parts(d, residual, buf)
@@ -564,12 +475,12 @@ class LlamaForCausalLM(nn.Module):
             at, mlp = layer.attn, layer.mlp
             kc, vc = kv_caches[i]
             p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf)
-            if md.num_prefill == 0 and FUSED_QKV_ATTENTION:
+            if md.num_prefill == 0:
                 a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
             else:
                 q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
                 a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
-            parts = car.reduce_residual(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=HALF_O_SLABS),
+            parts = car.reduce_residual(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True),
                                         residual, buf2)
             h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf, rowscale=gemm.RowScale(parts, layer.eps))
             parts = car.reduce_residual(gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p), residual, buf)

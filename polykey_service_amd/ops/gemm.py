@@ -22,7 +22,7 @@ import os
 
 SKINNY_MAX_M = 64
 # measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
-_TARGET_WGS = int(os.environ.get("POLYKEY_SKINNY_TARGET_WGS", "192"))
+_TARGET_WGS = 192
 _ROWS_PER_WG = 128
 _KCHUNK = 256
 # The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see
@@ -205,21 +205,8 @@ def deinterleave_gate_up(w: torch.Tensor, block: int = 16):
     return v[:, 0].reshape(I2 // 2, K), v[:, 1].reshape(I2 // 2, K)
 
 
-# per-shape overrides for A/B runs: POLYKEY_SKINNY_SPLIT="6144x4096:8,4096x4096:4" (N x K : S)
-_SPLIT_OVERRIDE = {tuple(int(v) for v in k.split("x")): int(s) for k, s in
-                   (e.split(":") for e in os.environ.get("POLYKEY_SKINNY_SPLIT", "").split(",") if e)}
-
-
-# per-shape override of the 64-row n-block (KR = 1) split-K partials for A/B runs:
-# POLYKEY_SKINNY_HALF="4096x4096:4,4096x14336:4" (N x K : S)
-_HALF_SPLIT = {tuple(int(v) for v in k.split("x")): int(s) for k, s in
-               (e.split(":") for e in os.environ.get("POLYKEY_SKINNY_HALF", "").split(",") if e)}
-
-
 def choose_split(N: int, K: int, M: int, target: int = _TARGET_WGS) -> int:
     """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows each)."""
-    if (N, K) in _SPLIT_OVERRIDE:
-        return _SPLIT_OVERRIDE[(N, K)]
     blocks = N // _ROWS_PER_WG
     s = 1
     while blocks * s < target and s < 16 and K % (_KCHUNK * s * 2) == 0:
@@ -260,7 +247,7 @@ def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
 
 
 # weights at least this large are streamed with non-temporal loads (gate_up, MoE w13, LM head)
-NT_MIN_BYTES = int(os.environ.get("POLYKEY_NT_MIN_BYTES", str(160 << 20)))
+NT_MIN_BYTES = 160 << 20
 NT_BIT = 64
 
 
@@ -299,8 +286,6 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
     n-blocks at half the default split -- the same grid, half the slab bytes."""
     M, K = x.shape
     N = w.shape[0]
-    if S is None and packed is not None and (N, K) in _HALF_SPLIT:
-        half, S = True, _HALF_SPLIT[(N, K)]
     half = half and packed is not None and packed.numel() * packed.element_size() < NT_MIN_BYTES
     if S is None:
         S = choose_split(N, K, M)

@@ -24,7 +24,7 @@ BN = 256
 # faster than 0, tools/prefill_gemm_bench.py) -- csrc/kernels/gemm_prefill.hip
 # 4: ping-pong quadrant phases with three LDS-DMA pieces in flight (tools/prefill_gemm_ab.py, same
 # process: grouped MoE w13 +3.2 %, w2 +4.8 %, dense gate_up / down +2.3-2.5 % over variant 2)
-VARIANT = int(os.environ.get("POLYKEY_PREFILL_GEMM_VARIANT", "4"))
+VARIANT = 4
 
 
 class PrefillGemmArgs(ctypes.Structure):
@@ -68,7 +68,7 @@ def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
 
 
 # ping-pong kernel reading the decode GEMM's block-packed W (5: its deep-pipelined form)
-PACKED_VARIANT = int(os.environ.get("POLYKEY_PREFILL_GEMM_PACKED_VARIANT", "5"))
+PACKED_VARIANT = 5
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, silu: bool = False,

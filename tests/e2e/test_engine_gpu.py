@@ -82,35 +82,6 @@ def test_preemption_under_kv_pressure():
         assert seqs[i].output_ids == ref[i], i
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama-gqa4"])
-def test_fused_decode_chain_matches_unfused(name):
-    """The 5-kernel fused decode layer (norms / split-K reductions / RoPE folded into the GEMMs)
-    gives the same decode logits as the unfused kernel sequence."""
-    from polykey_service_amd.models.llama import LlamaForCausalLM
-    _, gpu = _models(name)
-    prompts = [[1] + list(range(5, 5 + n)) for n in (3, 17, 40)]
-    logits, toks = [], []
-    old = LlamaForCausalLM.FUSED_DECODE
-    try:
-        for fused in (False, True):
-            LlamaForCausalLM.FUSED_DECODE = fused
-            e = LLMEngine(EngineConfig(model=name, max_num_seqs=8, max_num_batched_tokens=256, max_model_len=512,
-                                       hip_graphs=False, device="cuda"), ParallelState(device=torch.device("cuda")),
-                          model=gpu)
-            e.runner.keep_logits = True
-            seqs = [e.add_request(p, SamplingParams(max_tokens=3)) for p in prompts]
-            e.step()  # prefill
-            e.step()  # first decode step
-            logits.append(e.runner.last_logits.float().cpu())
-            while e.has_unfinished():
-                e.step()
-            toks.append([s.output_ids[:2] for s in seqs])
-    finally:
-        LlamaForCausalLM.FUSED_DECODE = old
-    torch.testing.assert_close(logits[1], logits[0], atol=0.1, rtol=0.05)
-    assert toks[0] == toks[1]
-
-
 def test_continuation_steps_match_synchronous_engine():
     """Pipelined decode continuations (next step launched from the GPU-resident sampled ids
     before the host reads them) produce exactly the synchronous engine's tokens, for greedy and

@@ -77,20 +77,10 @@ def test_decode_zero_context_rows_are_zero():
     torch.testing.assert_close(out[1:2].float(), exp.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["per-wave", "lds", "mfma32", "mfma32-8w"])
-def prefill_impl(request):
-    from polykey_service_amd.ops import native
-    native.lib().pk_set_prefill_impl(min(request.param, 2))
-    native.lib().pk_set_attn_waves(8 if request.param == 3 else 4)
-    yield request.param
-    native.lib().pk_set_prefill_impl(2)
-    native.lib().pk_set_attn_waves(0)
-
-
 @pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (8, 1, 32), (4, 1, 64), (16, 1, 32), (64, 8, 32)])
 @pytest.mark.parametrize("qlens,ctxs", [([7, 16, 33], [7, 16, 33]), ([1, 20, 64], [100, 20, 300]),
                                         ([130], [130]), ([5, 1], [70, 1]), ([300, 77], [1000, 77])])
-def test_prefill_with_prefix(nq, nkv, bs, qlens, ctxs, prefill_impl):
+def test_prefill_with_prefix(nq, nkv, bs, qlens, ctxs):
     max_blocks = (max(ctxs) + bs - 1) // bs
     nb = sum((c + bs - 1) // bs for c in ctxs) + 2
     kc, vc = make_cache(nb, nkv, bs, seed=3)

@@ -26,23 +26,15 @@ for n_seqs, qlen, prefix in ((32, 256, 0), (8, 1024, 0), (2, 4096, 0), (16, 256,
     keys = sum(prefix + i + 1 for i in range(qlen)) * n_seqs
     flops = 4.0 * D * keys * NQ
     row = f"{n_seqs:3d} seqs x {qlen:5d} q (+{prefix} cached):"
-    outs = {}
-    for impl in (1, 2, 3, 4):
-        # 2 / 3 / 4: the 32x32-MFMA kernel with 4 / 8 waves per workgroup / by prompt length (default)
-        native.lib().pk_set_prefill_impl(min(impl, 2))
-        native.lib().pk_set_attn_waves({2: 4, 3: 8}.get(impl, 0))
-        for _ in range(3):
-            outs[impl] = A.paged_attention(q, kc, vc, md, 0.088)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(10):
-            A.paged_attention(q, kc, vc, md, 0.088)
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) / 10 * 1000
-        row += f" | {['per-wave', 'lds', 'mfma32-4w', 'mfma32-8w', 'mfma32'][impl]} {us:8.1f} us {flops / us / 1e6:6.0f} TF/s"
-    diff = max((outs[1].float() - outs[i].float()).abs().max().item() for i in (2, 3, 4))
-    print(row + f" | max|diff| {diff:.3g}", flush=True)
-native.lib().pk_set_prefill_impl(2)
-native.lib().pk_set_attn_waves(0)
+    for _ in range(3):
+        A.paged_attention(q, kc, vc, md, 0.088)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        A.paged_attention(q, kc, vc, md, 0.088)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 10 * 1000
+    print(row + f" {us:8.1f} us {flops / us / 1e6:6.0f} TF/s", flush=True)
+

@@ -130,6 +130,7 @@ def role_rank(a) -> int:
         eng.runner.worker_loop()
         destroy_parallel()
         return 0
+    print(json.dumps({"phase": "rank0 engine ready", "init_s": round(init_s, 1)}), flush=True)
     res = {"model": a.model, "layers": eng.mcfg.num_layers, "tp": a.world, "gpus": 1, "init_s": round(init_s, 1),
            "vocab_local": eng.model.vocab_local, "lm_head_packed": eng.model.lm_head_p is not None,
            "packed_only": bool(getattr(eng.model, "packed_only", False)),
@@ -194,6 +195,7 @@ def launch(a) -> int:
               "--max-batched", str(a.max_batched)]
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     if a.ref == "run":
+        print(json.dumps({"phase": "ref"}), flush=True)
         r = subprocess.run(me + common + ["--role", "ref"], env=env, timeout=a.timeout)
         if r.returncode != 0:
             print(json.dumps({"error": "reference run failed", "rc": r.returncode}), flush=True)
@@ -213,6 +215,15 @@ def launch(a) -> int:
         log = open(os.path.join(a.out, f"rank{r}.log"), "w")
         procs.append((subprocess.Popen(cmd, env=e, stdout=log, stderr=subprocess.STDOUT), log))
     deadline = time.monotonic() + a.timeout
+    t_start = time.monotonic()
+
+    def heartbeat():  # a long init (80 layers x 8 ranks) must not look like a hang to a supervisor
+        while any(p.poll() is None for p, _ in procs):
+            time.sleep(20)
+            print(json.dumps({"elapsed_s": round(time.monotonic() - t_start), "alive": sum(p.poll() is None for p, _ in procs)}),
+                  flush=True)
+    import threading
+    threading.Thread(target=heartbeat, daemon=True).start()
     rcs = []
     for p, log in procs:
         try:
