@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp
 cd $R
 OUT=gpurun_out/tp8_full
 timeout -k 10 1080 python -u tools/tp_rehearsal.py --world 8 --model llama3-70b --batch 64 --prompt 256 --steps 12 \
-  --cmp-tokens 8 --ref run --prof --timeout 1040 --out $OUT > gpurun_out/tp8_full.log 2>&1
+  --cmp-tokens 8 --ref ${REF:-run} --prof --timeout 1040 --out $OUT > gpurun_out/tp8_full.log 2>&1
 rc=$?
 echo "rehearsal rc=$rc"
 tail -3 gpurun_out/tp8_full.log

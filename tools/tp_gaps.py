@@ -37,7 +37,17 @@ def union_busy(iv, t0, t1):
 
 
 def short(name, n=70):
-    name = name.split("(")[0]
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "", 1)
+    depth, cut = 0, len(name)
+    for i, ch in enumerate(name):  # the name up to its argument list (template args may hold '(')
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+    name = name[:cut]
     return name if len(name) <= n else name[:n]
 
 

@@ -77,6 +77,37 @@ def role_ref(a) -> int:
     return 0
 
 
+def role_noise(a) -> int:
+    """Calibration for the TP = 8 vs TP = 1 logits comparison: the size of the difference two
+    equally valid TP = 1 computations of the same prefill give at this depth (random weights
+    amplify bf16 rounding-order noise layer by layer) -- each comparison prompt alone, in one
+    prefill step vs chunked into 64-token steps over its own cached prefix."""
+    import torch
+    from polykey_service_amd.parallel.state import ParallelState
+    eng = _engine(a, ParallelState(device=torch.device("cuda:0")), graphs=False, device="cuda:0")
+    out = {"layers": eng.mcfg.num_layers, "prompts": []}
+    for p in CMP_PROMPTS:
+        lg = []
+        for budget in (a.max_batched, 64):
+            eng.scheduler.max_num_batched_tokens = budget
+            eng.scheduler.max_prefill_chunk = budget
+            from polykey_service_amd.engine import SamplingParams
+            eng.runner.keep_logits = True
+            eng.add_request(list(p), SamplingParams(max_tokens=1, ignore_eos=True, temperature=0.0))
+            while eng.has_unfinished():
+                eng.step()  # the last step completes the prompt and samples from its logits
+            torch.cuda.synchronize()
+            lg.append(eng.runner.last_logits.float().cpu().clone())
+        d = (lg[0] - lg[1]).abs()
+        out["prompts"].append({"len": len(p), "chunks": -(-len(p) // 64), "max_abs_diff": round(float(d.max()), 4),
+                               "mean_abs_diff": round(float(d.mean()), 5), "scale": round(float(lg[0].abs().mean()), 4),
+                               "argmax_equal": int(lg[0].argmax()) == int(lg[1].argmax())})
+    print(json.dumps(out), flush=True)
+    with open(os.path.join(a.out, "noise.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    return 0
+
+
 def _near_tie_ok(got, ref, logits, tie=0.15):
     """Greedy first tokens equal, or the TP token is a near-tie of the reference's argmax."""
     bad = []
@@ -239,7 +270,7 @@ def launch(a) -> int:
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--role", choices=["launch", "ref", "rank"], default="launch")
+    ap.add_argument("--role", choices=["launch", "ref", "rank", "noise"], default="launch")
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--model", default="llama3-70b")
@@ -260,6 +291,9 @@ def main() -> int:
     a = ap.parse_args()
     if a.role == "ref":
         return role_ref(a)
+    if a.role == "noise":
+        os.makedirs(a.out, exist_ok=True)
+        return role_noise(a)
     if a.role == "rank":
         return role_rank(a)
     return launch(a)
