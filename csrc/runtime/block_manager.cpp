@@ -53,10 +53,12 @@ class BlockManager : public pk::BlockManagerCore {
 };
 
 void bind_step_channel(py::module_& m);  // step_channel.cpp
+void bind_vote_board(py::module_& m);    // vote_board.cpp
 
 PYBIND11_MODULE(_pk_runtime, m) {
   m.doc() = "polykey native runtime: paged KV block manager, step packer, TP step channel";
   bind_step_channel(m);
+  bind_vote_board(m);
   py::class_<BlockManager>(m, "BlockManager")
       .def(py::init<int64_t, int, int64_t, bool, uint64_t>(), py::arg("num_blocks"), py::arg("block_size"),
            py::arg("watermark_blocks") = 0, py::arg("prefix_caching") = false, py::arg("hash_key") = 0)

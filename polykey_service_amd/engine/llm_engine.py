@@ -77,13 +77,19 @@ class LLMEngine:
             raise ValueError(f"block_size must be a positive multiple of 32, got {cfg.block_size}")
         # DP attention + EP (ParallelState.dp_attention): every rank schedules its own requests
         # and the ranks step in lockstep because each MoE layer is an all-to-all over all of
-        # them.  Steps are synchronous (no overlap / continuations) and eager: the dispatch
-        # sizes are read back per layer, which a captured graph cannot do.
+        # them.  Steps are synchronous (no overlap / continuations).  With the IPC expert
+        # all-to-all (parallel/ep_ipc.py: device-side counts) decode steps replay HIP graphs;
+        # without it (multi-node, CPU) the dispatch sizes are read back per layer: eager only.
         self.lockstep = self.st.dp_attention
         if self.lockstep:
             if not mcfg.is_moe:
                 raise ValueError("DP attention + EP (tp=1, ep>1) needs an MoE model")
-            cfg = dataclasses.replace(cfg, hip_graphs=False, overlap=False)
+            from ..parallel import ep_ipc
+            if self.st.ep_a2a is None:
+                self.st.ep_a2a = ep_ipc.maybe_create(self.st, cfg.max_num_seqs * mcfg.experts_per_token,
+                                                     mcfg.hidden_size)
+            cfg = dataclasses.replace(cfg, overlap=False,
+                                      hip_graphs=cfg.hip_graphs and self.st.ep_a2a is not None)
             self.cfg = cfg
         self.mcfg = mcfg
         dev = torch.device(cfg.device) if cfg.device else self.st.device
@@ -186,12 +192,21 @@ class LLMEngine:
         return self._outputs(done) if done else []
 
     def _step_lockstep(self) -> List[RequestOutput]:
-        """DP attention + EP step: one host vote (gloo) per step decides whether the EP group
-        runs a forward; a rank with nothing scheduled joins it through the model's idle pass."""
+        """DP attention + EP step: one lockstep vote (shared memory on one node) per step decides
+        whether the EP group runs a forward and -- from the largest token count -- which expert
+        all-to-all every rank uses (IPC slots, graph-capturable, for decode-sized steps; RCCL
+        for prefill-sized ones); a rank with nothing scheduled joins through the idle pass."""
         from ..parallel import comm
         batch = self.scheduler.schedule()
-        if not comm.ep_any(not batch.empty):
+        ntok = len(batch.decodes) + sum(n for _, n in batch.prefills)
+        busy, _, max_tok = comm.ep_vote(not batch.empty, False, ntok)
+        if not busy:
             return []
+        # (graph buckets pad decode rows, but only buckets within the IPC capacity are captured)
+        a2a = self.st.ep_a2a
+        ipc = a2a is not None and a2a.fits(max_tok * self.mcfg.experts_per_token)
+        self.st.ep_step_rows = max_tok if ipc else (1 << 30)
+        self.runner.allow_graphs = ipc  # a replay holds the IPC path: only when every rank takes it
         if batch.empty:
             self.model.idle_forward()
             self.runner.stats["idle_steps"] = self.runner.stats.get("idle_steps", 0) + 1
@@ -202,7 +217,8 @@ class LLMEngine:
     def lockstep_vote(self, stopping: bool):
         """DP attention + EP loop vote → (any rank has work, every rank is stopping)."""
         from ..parallel import comm
-        return comm.ep_vote(self.has_unfinished(), stopping)
+        busy, all_stop, _ = comm.ep_vote(self.has_unfinished(), stopping)
+        return busy, all_stop
 
     def any_unfinished(self) -> bool:
         """Whether the engine loop must keep stepping: its own work, or (DP attention + EP) any

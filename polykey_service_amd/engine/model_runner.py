@@ -136,6 +136,7 @@ class ModelRunner:
         self._graph_logits: Dict[Tuple[int, int], torch.Tensor] = {}
         self.channel = None
         self._prev_toks = None  # worker: last step's sampled ids (device), for continuations
+        self.allow_graphs = True  # DP attention + EP: False for steps whose expert all-to-all is not IPC
         if model.st.tp_size > 1:
             self._open_channel()
 
@@ -280,7 +281,7 @@ class ModelRunner:
             rel = h["cu_q"][nd:n + 1] - h["cu_q"][nd]
             h["cu_rel"][:n - nd + 1] = rel
             max_q = int(np.max(np.diff(rel)))
-        elif self.graphs:
+        elif self.graphs and self.allow_graphs:
             g = self._graph_bucket(nd) or 0
             if g:
                 self._pad_decode(nd, g)
@@ -331,6 +332,8 @@ class ModelRunner:
         for rc in (getattr(st, "rccl_tp", None), getattr(st, "rccl_ep", None)):
             if rc is not None:  # RCCL's asynchronous error word (non-blocking poll)
                 rc.check()
+        if getattr(st, "ep_a2a", None) is not None:
+            st.ep_a2a.check()
 
     def launch_continuation(self, batch: ScheduledBatch, prev) -> Optional[tuple]:
         """Decode step k+1 of ``batch.decodes`` enqueued while step k (``prev``) may still run:
@@ -445,6 +448,8 @@ class ModelRunner:
                 pass
         if st.custom_ar is not None:
             st.custom_ar.fail()
+        if getattr(st, "ep_a2a", None) is not None:
+            st.ep_a2a.fail()
 
     def stop_workers(self) -> None:
         if self.channel is not None and self.model.st.tp_rank == 0:
@@ -510,6 +515,10 @@ class ModelRunner:
         if self.device.type != "cuda" or not self.cfg.hip_graphs:
             return
         sizes = sizes or self.default_graph_sizes()
+        st = self.model.st
+        if st.dp_attention:  # every replay sends bucket x top-k rows per peer: within the IPC capacity
+            k = self.mcfg.experts_per_token
+            sizes = [g for g in sizes if st.ep_a2a is not None and st.ep_a2a.fits(g * k)]
         d = self.d
         # a valid dummy decode state: every row points at block 0, context 1, no cache writes
         self.host_buf.zero_()
@@ -521,8 +530,11 @@ class ModelRunner:
         torch.cuda.synchronize(self.device)
         stream = torch.cuda.Stream(self.device)
         variants = (False, True) if self.short_ctx else (False,)
+        st = self.model.st
         for g, short in [(g, v) for g in sorted(sizes, reverse=True) for v in variants]:
             md = self._metadata(g, g, g, 0, short)
+            if st.dp_attention:  # capture the IPC expert all-to-all path (device-side counts)
+                st.ep_step_rows = g
 
             def run():
                 hidden = self.model(d["input_ids"][:g], d["positions"][:g], md, self.kv_caches)

@@ -296,24 +296,23 @@ def ep_all_to_all_counts(counts: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def ep_vote(busy: bool, stopping: bool = False, ntok: int = 0):
+    """Lockstep vote of the DP-attention ranks → (any rank busy, every rank stopping, the largest
+    token count).  One node: the shared-memory vote board (µs); else one gloo all-reduce."""
+    st = get_state()
+    if st.ep_size == 1 or st.ep_cpu_group is None:
+        return bool(busy), bool(stopping), int(ntok)
+    if st.ep_board is not None:
+        from ..engine.model_runner import peer_timeout_ms
+        return st.ep_board.vote(bool(busy), bool(stopping), int(ntok), max(peer_timeout_ms(), 600000))
+    t = torch.tensor([1 if busy else 0, 0 if stopping else 1, int(ntok)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=st.ep_cpu_group)
+    return bool(t[0].item()), not bool(t[1].item()), int(t[2].item())
+
+
 def ep_any(flag: bool) -> bool:
-    """Lockstep vote of the DP-attention ranks (gloo, host): True if any rank's flag is set."""
-    st = get_state()
-    if st.ep_size == 1 or st.ep_cpu_group is None:
-        return bool(flag)
-    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=st.ep_cpu_group)
-    return bool(t.item())
-
-
-def ep_vote(busy: bool, stopping: bool):
-    """One host all-reduce over the EP ranks → (any rank busy, every rank stopping)."""
-    st = get_state()
-    if st.ep_size == 1 or st.ep_cpu_group is None:
-        return bool(busy), bool(stopping)
-    t = torch.tensor([1 if busy else 0, 0 if stopping else 1], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=st.ep_cpu_group)
-    return bool(t[0].item()), not bool(t[1].item())
+    """True if any DP-attention rank's flag is set (one lockstep vote)."""
+    return ep_vote(flag)[0]
 
 
 def tp_broadcast_object(obj=None):

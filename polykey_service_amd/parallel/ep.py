@@ -37,16 +37,21 @@ from .state import get_state
 
 
 def _local_experts(recv_x: torch.Tensor, recv_e: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
-                   w13_p: Optional[torch.Tensor], w2_p: Optional[torch.Tensor]) -> torch.Tensor:
-    """Rows received from every rank × their local expert → outputs in arrival order."""
-    n = recv_x.shape[0]
+                   w13_p: Optional[torch.Tensor], w2_p: Optional[torch.Tensor], rows: Optional[int] = None,
+                   bound: Optional[int] = None) -> torch.Tensor:
+    """Rows received from every rank × their local expert → outputs in arrival order (rows whose
+    expert id is not local -- the IPC regions' -1 padding -- come out as zeros).  ``bound``: an
+    upper bound of any one expert's rows (the grouped GEMM's tile choice) when the counts live on
+    the device."""
+    n = recv_x.shape[0] if rows is None else rows
     if n == 0:
         return recv_x
     per = w13.shape[0]
     offsets, sorted_, inv = moe_ops.align(recv_e, per, 0, per)
     xs = moe_ops.permute(recv_x, sorted_, offsets, 1)
-    h = moe_ops.grouped_gemm(xs, w13, offsets, n, silu=True, packed=w13_p)
-    y = moe_ops.grouped_gemm(h, w2, offsets, n, silu=False, packed=w2_p)
+    mr = n if bound is None else bound
+    h = moe_ops.grouped_gemm(xs, w13, offsets, mr, silu=True, packed=w13_p)
+    y = moe_ops.grouped_gemm(h, w2, offsets, mr, silu=False, packed=w2_p)
     ones = torch.ones((n, 1), dtype=torch.float32, device=recv_x.device)
     return moe_ops.unpermute(y, inv, ones, n, 1)
 
@@ -55,8 +60,15 @@ def ep_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch
            routing: Optional[Tuple[torch.Tensor, torch.Tensor]] = None, w13_p: Optional[torch.Tensor] = None,
            w2_p: Optional[torch.Tensor] = None, defer_combine: bool = False):
     """x: this rank's tokens [T_local, H] (T_local may be 0); w13 / w2: this rank's experts.
-    Returns [T_local, H], or a :class:`~polykey_service_amd.ops.moe.PendingCombine`."""
+    Returns [T_local, H], or a :class:`~polykey_service_amd.ops.moe.PendingCombine`.
+
+    The step's path is uniform over the EP group (every rank must issue the same collectives):
+    the IPC all-to-all when the step's largest token count fits its capacity (``st.ep_step_rows``
+    from the lockstep vote), else the RCCL / gloo all-to-all with split lists on the host."""
     st = get_state()
+    a2a = st.ep_a2a
+    if a2a is not None and x.is_cuda and a2a.fits(st.ep_step_rows * k):
+        return _ep_moe_ipc(a2a, x, router_w, w13, w2, k, routing, w13_p, w2_p, defer_combine)
     ep = st.ep_size
     E = router_w.shape[0]
     per = E // ep
@@ -84,6 +96,38 @@ def ep_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch
     recv_e = comm.ep_all_to_all(send_e, rc, sc).view(-1, 1)
     y = _local_experts(recv_x, recv_e, w13, w2, w13_p, w2_p)
     back = comm.ep_all_to_all(y, sc, rc)  # [T*k, H] in the send (destination-sorted) order
+    pending = moe_ops.PendingCombine(back, inv, wts, T, k)
+    if defer_combine and T > 0:
+        return pending
+    return pending.combine() if T > 0 else x.new_zeros((0, H))
+
+
+def _ep_moe_ipc(a2a, x, router_w, w13, w2, k, routing, w13_p, w2_p, defer_combine):
+    """ep_moe over the IPC regions: device-side counts and offsets only (graph-capturable)."""
+    st = get_state()
+    ep = st.ep_size
+    E = router_w.shape[0]
+    per = E // ep
+    T, H = x.shape
+    dev = x.device
+    if T > 0:
+        ids, wts = routing if routing is not None else moe_ops.topk_softmax(F.linear(x, router_w), k)
+        dest = torch.div(ids, per, rounding_mode="floor").to(torch.int32)
+        offsets, sorted_, inv = moe_ops.align(dest, ep, 0, ep)  # destination-sorted (token, slot) rows
+        send_x = moe_ops.permute(x, sorted_, offsets, k)
+        sl = sorted_.long()
+        send_e = (ids.reshape(-1).long()[sl] - dest.reshape(-1).long()[sl] * per).to(torch.int32)
+    else:
+        wts = torch.zeros((0, k), dtype=torch.float32, device=dev)
+        inv = torch.zeros((0,), dtype=torch.int32, device=dev)
+        send_x = x
+        send_e = torch.zeros((0,), dtype=torch.int32, device=dev)
+        offsets = torch.zeros(ep + 1, dtype=torch.int32, device=dev)
+    a2a.dispatch(send_x.contiguous(), send_e, offsets)
+    # every rank's rows are in this rank's receive regions (padding ids -1: no local expert)
+    n = ep * a2a.C
+    y = _local_experts(a2a.recv_x, a2a.recv_e.view(-1, 1), w13, w2, w13_p, w2_p, rows=n, bound=a2a.C)
+    back = a2a.return_(y.contiguous())[: T * k]  # this rank's rows, in the order they were sent
     pending = moe_ops.PendingCombine(back, inv, wts, T, k)
     if defer_combine and T > 0:
         return pending

@@ -45,6 +45,9 @@ class ParallelState:
     custom_ar: Optional[object] = None     # one-shot xGMI all-reduce (parallel/custom_ar.py)
     rccl_tp: Optional[object] = None       # direct RCCL communicator of the TP group (parallel/rccl.py)
     rccl_ep: Optional[object] = None       # ... of the EP group (the TP one when EP runs inside TP)
+    ep_a2a: Optional[object] = None        # IPC expert all-to-all (parallel/ep_ipc.py; DP attention + EP)
+    ep_board: Optional[object] = None      # shared-memory lockstep vote (csrc/runtime/vote_board.cpp)
+    ep_step_rows: int = 1 << 30            # largest token count of the current lockstep step (vote)
     backend: str = "none"
     device: torch.device = dataclasses.field(default_factory=lambda: torch.device("cpu"))
 
@@ -132,6 +135,7 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
             # a dedicated gloo group: the engine thread's lockstep votes must never interleave
             # with another thread's collectives on WORLD
             st.ep_cpu_group = dist.new_group(list(range(world)), backend="gloo")
+            st.ep_board = _vote_board(st)
         elif ep > 1:
             st.ep_group, st.ep_cpu_group = st.tp_group, st.tp_cpu_group
         if be == "nccl" or (os.environ.get("POLYKEY_CUSTOM_AR") == "force" and dev.type == "cuda"):
@@ -141,6 +145,37 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
             _create_rccl(st)
     set_state(st)
     return st
+
+
+def _vote_board(st: ParallelState):
+    """Shared-memory lockstep vote for the DP-attention + EP ranks of ONE node (the gloo vote
+    stays for multi-node groups)."""
+    if int(os.environ.get("LOCAL_WORLD_SIZE", str(st.world_size))) != st.world_size:
+        return None
+    import uuid
+
+    from .._native.loader import load_extension
+    board, err = None, None
+    name = [None]
+    try:
+        rt = load_extension("_pk_runtime")
+        if st.rank == 0:  # created before its name is published: attaching can never race it
+            name[0] = f"/pk_vote_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+            board = rt.VoteBoard(name[0], True, st.world_size, 0)
+    except Exception as e:  # noqa: BLE001
+        err = e
+    dist.broadcast_object_list(name, src=0, group=st.ep_cpu_group)
+    if st.rank != 0 and name[0] is not None:
+        try:
+            board = rt.VoteBoard(name[0], False, st.world_size, st.rank)
+        except Exception as e:  # noqa: BLE001
+            err = e
+    ok = [None] * st.world_size
+    dist.all_gather_object(ok, board is not None, group=st.ep_cpu_group)  # all ranks or none
+    if not all(ok):
+        log.warning("shared-memory vote board unavailable (%s); lockstep votes over gloo", err)
+        return None
+    return board
 
 
 def _create_rccl(st: ParallelState) -> None:
@@ -162,6 +197,8 @@ def destroy_parallel() -> None:
     st = get_state()
     if st.custom_ar is not None:
         st.custom_ar.close()
+    if st.ep_a2a is not None:
+        st.ep_a2a.close()
     for c in {id(c): c for c in (st.rccl_tp, st.rccl_ep) if c is not None}.values():
         c.close()
     if dist.is_initialized():
