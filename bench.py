@@ -59,9 +59,10 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     # measured on 1x MI355X (profiles/r2_bench_client_ab.txt): unary 12,879 tok/s with the clients on
     # the server's event loop vs 12,299 from a separate load-generator process (streaming: 12,787)
-    ap.add_argument("--frontend", choices=["replicas", "gateway"], default="replicas",
-                    help="N > 1, tp 1: every rank serves its own gRPC endpoint (replicas) or rank 0 serves ONE "
-                         "front end routing to every rank's engine process (gateway, engine/remote.py)")
+    ap.add_argument("--frontend", choices=["replicas", "gateway", "single"], default="replicas",
+                    help="N > 1, tp 1: every rank serves its own gRPC endpoint (replicas); ONE gRPC address served "
+                         "by an acceptor in every rank (SO_REUSEPORT), each routing to the least-loaded engine "
+                         "(gateway, engine/remote.py dp_gateway); or rank 0 alone as the front end (single)")
     ap.add_argument("--client", choices=["process", "inproc"], default="inproc",
                     help="load generator on the server's event loop (default) or in its own process")
     return ap.parse_args(argv)
@@ -75,7 +76,7 @@ def relaunch_with_torchrun(args) -> int:
     return subprocess.call(cmd)
 
 
-async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
+async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, shared_port=0):
     import grpc
     import torch
     import torch.distributed as dist
@@ -91,7 +92,7 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
     router = ToolRouter()
     cfg = ServerConfig(model=args.model, backend="local")
     attach_local_llm(router, cfg, logger, engine=engine, llm=llm)
-    port = args.port_base + st.rank if args.port_base > 0 else 0
+    port = shared_port or (args.port_base + st.rank if args.port_base > 0 else 0)
     conc = args.concurrency * n_replicas  # gateway: one front end for every replica's clients
     srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
     port = await srv.start()
@@ -99,7 +100,7 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
         try:
             return await _drive_external(args, engine, st, leaders_group if n_replicas == 1 else None, port, srv,
                                          llm=router.llm, conc=args.concurrency * n_replicas,
-                                         stop_after=engine.lockstep or n_replicas > 1)
+                                         stop_after=engine.lockstep or n_replicas > 1 or bool(shared_port))
         finally:
             await srv.server.stop(0)
     channel = grpc.aio.insecure_channel(f"127.0.0.1:{port}", options=[
@@ -184,9 +185,10 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
     elapsed = time.perf_counter() - t0
     await channel.close()
     await srv.server.stop(0)
-    if engine.lockstep or n_replicas > 1:
-        # DP attention + EP: leave the lockstep loop together with the other ranks; gateway:
-        # stop the other ranks' engine servers (they are waiting on the front end)
+    if engine.lockstep or n_replicas > 1 or shared_port:
+        # DP attention + EP: leave the lockstep loop together with the other ranks; single front
+        # end: stop the other ranks' engine servers (they are waiting on it); SO_REUSEPORT gateway:
+        # every rank's waves are done (the barrier above) before any engine stops
         await asyncio.get_running_loop().run_in_executor(None, llm.shutdown)
     return tokens, elapsed, lats
 
@@ -264,8 +266,24 @@ def main(argv=None) -> int:
     init_s = time.perf_counter() - t_init
     leaders = list(range(0, st.world_size, st.tp_size))
     leaders_group = dist.new_group(leaders) if dist.is_initialized() else None
-    gateway = args.frontend == "gateway" and st.world_size > 1 and st.tp_size == 1 and not engine.lockstep
-    if gateway:
+    dp_front = st.world_size > 1 and st.tp_size == 1 and not engine.lockstep
+    gateway = args.frontend == "gateway" and dp_front
+    if gateway:  # one gRPC address, an acceptor per rank (SO_REUSEPORT), least-loaded routing
+        import socket as _socket
+
+        from polykey_service_amd.engine.async_llm import AsyncLLM
+        from polykey_service_amd.engine.remote import dp_gateway
+        local = AsyncLLM(engine)
+        pool = dp_gateway(local, st, reuseport=True)
+        port = [None]
+        if st.rank == 0:
+            s0 = _socket.socket()
+            s0.bind(("127.0.0.1", args.port_base or 0))
+            port[0] = s0.getsockname()[1]
+            s0.close()
+        dist.broadcast_object_list(port, src=0)
+        tokens, elapsed, lats = asyncio.run(run_waves(args, engine, st, leaders_group, llm=pool, shared_port=port[0]))
+    elif args.frontend == "single" and dp_front:
         from polykey_service_amd.engine.async_llm import AsyncLLM
         from polykey_service_amd.engine.remote import dp_gateway
         local = AsyncLLM(engine)
@@ -317,7 +335,8 @@ def main(argv=None) -> int:
                 "parallelism": (f"tp{st.tp_size}" + (f"_dp{st.dp_size}" if st.dp_size > 1 else "")
                                 + (f"_ep{st.ep_size}" if st.ep_size > 1 else "")) if st.tp_size > 1
                 else f"dp{st.world_size}" + (f"_ep{st.ep_size}_a2a" if st.ep_size > 1 else "")
-                + ("_gateway" if gateway else ""),
+                + ("_gateway" if gateway else "") + ("_single_frontend" if args.frontend == "single" and dp_front
+                                                          else ""),
                 "concurrency_per_replica": args.concurrency,
                 "rpc": f"ExecuteTool ({args.mode})",
                 "clients": "load-generator process" if args.client == "process" else "server event loop",

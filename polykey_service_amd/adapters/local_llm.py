@@ -226,8 +226,18 @@ class ReplicaPool:
                 setattr(r, k, v)
 
     def shutdown(self, timeout: float = 10.0) -> None:
-        for r in self.replicas:
+        # remote handles first (their "stop" frames release the other ranks' engine servers), then
+        # -- SO_REUSEPORT gateway -- wait until every other acceptor has released this rank's
+        # engine before stopping it
+        for r in self.replicas[1:]:
             r.shutdown(timeout)
+        th = self.__dict__.get("gateway_thread")
+        if th is not None:
+            th.join(timeout)
+        self.replicas[0].shutdown(timeout)
+        board = self.__dict__.get("load_board")
+        if board is not None:
+            board.close()
 
     async def aclose(self) -> None:
         for r in self.replicas:

@@ -65,11 +65,13 @@ def _params_dict(p: SamplingParams) -> dict:
 
 # --------------------------------------------------------------------------- engine side
 class EngineServer:
-    """Serves one :class:`~polykey_service_amd.engine.async_llm.AsyncLLM` to a front end.
+    """Serves one :class:`~polykey_service_amd.engine.async_llm.AsyncLLM` to front ends.
 
-    ``serve()`` blocks: it accepts the front end's connection and feeds its commands to the
-    engine until a "stop" frame (or the connection closing); outputs go back from the engine
-    thread through :meth:`AsyncLLM.set_external_sink`."""
+    ``serve(n)`` blocks: it accepts ``n`` authenticated front-end connections (the single
+    gateway: 1; the SO_REUSEPORT gateway: every other rank's acceptor), feeds their commands to
+    the engine, and returns once every one of them has sent "stop" or closed; outputs go back
+    from the engine thread through :meth:`AsyncLLM.set_external_sink`, each to the connection
+    that submitted the request."""
 
     def __init__(self, llm, host: str = "127.0.0.1", port: int = 0, token: Optional[str] = None):
         self.llm = llm
@@ -77,37 +79,47 @@ class EngineServer:
         self.port = self.lsock.getsockname()[1]
         # shared secret the front end must present in its first frame (None: no check)
         self.token = token
-        self._wlock = threading.Lock()
-        self._conn: Optional[socket.socket] = None
+        self._lock = threading.Lock()
+        self._conns: Dict[int, Tuple[socket.socket, threading.Lock]] = {}
+        self._owner: Dict[str, int] = {}   # rid -> connection that submitted it
         self._final: Dict[str, List] = {}  # rid -> tokens so far (final-only requests)
 
     def _sink(self, items) -> None:
-        """Engine thread: one frame with this step's outputs of remote requests."""
-        out = []
-        for rid, o in items:
-            if isinstance(o, BaseException):
-                self._final.pop(rid, None)
-                out.append([rid, [], True, "error", 0, 0, None, str(o)])
-                continue
-            acc = self._final.get(rid)
-            if acc is not None:
-                acc.extend(o.new_token_ids)
-                if not o.finished:
+        """Engine thread: one frame per front end with this step's outputs of its requests."""
+        per: Dict[int, list] = {}
+        with self._lock:
+            for rid, o in items:
+                cid = self._owner.get(rid)
+                if isinstance(o, BaseException):
+                    self._final.pop(rid, None)
+                    self._owner.pop(rid, None)
+                    per.setdefault(cid, []).append([rid, [], True, "error", 0, 0, None, str(o)])
                     continue
-                del self._final[rid]
-                ids = acc
-            else:
-                ids = o.new_token_ids
-            out.append([rid, list(ids), o.finished, o.finish_reason, o.num_prompt_tokens, o.num_output_tokens,
-                        o.metrics, None])
-        if out and self._conn is not None:
+                acc = self._final.get(rid)
+                if acc is not None:
+                    acc.extend(o.new_token_ids)
+                    if not o.finished:
+                        continue
+                    del self._final[rid]
+                    ids = acc
+                else:
+                    ids = o.new_token_ids
+                if o.finished:
+                    self._owner.pop(rid, None)
+                per.setdefault(cid, []).append([rid, list(ids), o.finished, o.finish_reason, o.num_prompt_tokens,
+                                                o.num_output_tokens, o.metrics, None])
+            conns = {cid: self._conns.get(cid) for cid in per}
+        for cid, out in per.items():
+            c = conns.get(cid)
+            if c is None:
+                continue
             try:
-                _send(self._conn, self._wlock, {"op": "out", "items": out})
+                _send(c[0], c[1], {"op": "out", "items": out})
             except OSError:
-                pass  # front end gone: serve() sees the closed connection and stops
+                pass  # front end gone: its reader sees the closed connection and stops
 
     def _accept(self) -> socket.socket:
-        """The first connection whose hello frame carries the shared token (others are closed)."""
+        """The next connection whose hello frame carries the shared token (others are closed)."""
         while True:
             conn, _ = self.lsock.accept()
             if self.token is None:
@@ -122,30 +134,52 @@ class EngineServer:
                 return conn
             conn.close()
 
-    def serve(self) -> None:
-        conn = self._accept()
-        conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-        self._conn = conn
-        self.llm.set_external_sink(self._sink)
+    def _read(self, cid: int, conn: socket.socket) -> None:
         try:
             while True:
                 msg = _recv(conn)
                 if msg is None or msg.get("op") == "stop":
                     break
                 if msg["op"] == "add":
-                    if msg.get("final"):
-                        self._final[msg["rid"]] = []
-                    self.llm.submit_external(msg["rid"], msg["prompt"], SamplingParams(**msg["params"]))
+                    rid = msg["rid"]
+                    with self._lock:
+                        self._owner[rid] = cid
+                        if msg.get("final"):
+                            self._final[rid] = []
+                    self.llm.submit_external(rid, msg["prompt"], SamplingParams(**msg["params"]))
                 elif msg["op"] == "abort":
-                    self._final.pop(msg["rid"], None)  # the engine reports nothing more for it
+                    with self._lock:
+                        self._final.pop(msg["rid"], None)  # the engine reports nothing more for it
+                        self._owner.pop(msg["rid"], None)
                     self.llm.abort_external(msg["rid"])
+        except OSError:
+            pass
         finally:
-            self.llm.set_external_sink(None)
-            self._conn = None
+            with self._lock:
+                self._conns.pop(cid, None)
             try:
                 conn.close()
-            finally:
-                self.lsock.close()
+            except OSError:
+                pass
+
+    def serve(self, n_clients: int = 1) -> None:
+        self.llm.set_external_sink(self._sink)
+        readers = []
+        try:
+            for cid in range(n_clients):
+                conn = self._accept()
+                conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                with self._lock:
+                    self._conns[cid] = (conn, threading.Lock())
+                t = threading.Thread(target=self._read, args=(cid, conn), name=f"polykey-engine-srv-{cid}",
+                                     daemon=True)
+                t.start()
+                readers.append(t)
+            for t in readers:
+                t.join()
+        finally:
+            self.llm.set_external_sink(None)
+            self.lsock.close()
 
 
 # ---------------------------------------------------------------------------- front end
@@ -154,9 +188,10 @@ class RemoteEngine:
     router (:class:`~polykey_service_amd.adapters.local_llm.ReplicaPool`) and the tools."""
 
     def __init__(self, addr: Tuple[str, int], tokenizer, name: str = "remote", connect_timeout: float = 120.0,
-                 token: Optional[str] = None):
+                 token: Optional[str] = None, load_fn=None):
         self.tokenizer = tokenizer
         self.name = name
+        self.load_fn = load_fn  # engine-wide load (shared-memory load board), else this handle's own
         self.on_fatal = None
         self.watchdog_s = 0.0
         self.dead: Optional[BaseException] = None
@@ -181,7 +216,7 @@ class RemoteEngine:
         self._reader.start()
 
     def load(self) -> int:
-        return len(self._streams)
+        return self.load_fn() if self.load_fn is not None else len(self._streams)
 
     def healthy(self) -> bool:
         return self.dead is None
@@ -286,13 +321,54 @@ class RemoteEngine:
         await asyncio.get_running_loop().run_in_executor(None, self.shutdown)
 
 
-def dp_gateway(llm, st, group=None):
-    """Wire the DP ranks (tp = 1, one engine per rank) to ONE front end on rank 0.
+class LoadBoard:
+    """Per-rank unfinished-request counts in POSIX shared memory: every front end of the
+    SO_REUSEPORT gateway routes by the engines' true loads, whoever submitted the requests."""
 
-    Collective over ``group`` (default: the world): every rank but 0 serves its ``llm`` to the
-    front end and blocks until the front end stops it (returns None); rank 0 returns a
+    def __init__(self, name: str, create: bool, world: int):
+        import numpy as np
+        from multiprocessing import resource_tracker, shared_memory
+        self.shm = shared_memory.SharedMemory(name=name, create=create, size=8 * world)
+        if not create:  # the creator owns (and unlinks) the segment
+            try:
+                resource_tracker.unregister(self.shm._name, "shared_memory")
+            except Exception:  # noqa: BLE001
+                pass
+        self.owner = create
+        self.arr = np.ndarray((world,), dtype=np.int64, buffer=self.shm.buf)
+        if create:
+            self.arr[:] = 0
+
+    def set(self, rank: int, v: int) -> None:
+        self.arr[rank] = v
+
+    def get(self, rank: int) -> int:
+        return int(self.arr[rank])
+
+    def close(self) -> None:
+        self.arr = None
+        self.shm.close()
+        if self.owner:
+            self.shm.unlink()
+
+
+def dp_gateway(llm, st, group=None, reuseport: bool = False):
+    """Wire the DP ranks (tp = 1, one engine per rank) to the gRPC front end.
+
+    Collective over ``group`` (default: the world).
+
+    ``reuseport=False`` (one front end): every rank but 0 serves its ``llm`` to rank 0 and blocks
+    until the front end stops it (returns None); rank 0 returns a
     :class:`~polykey_service_amd.adapters.local_llm.ReplicaPool` over its own ``llm`` and a
-    :class:`RemoteEngine` per other rank."""
+    :class:`RemoteEngine` per other rank.
+
+    ``reuseport=True`` (one front-end ADDRESS, N acceptor processes): every rank returns a
+    ReplicaPool over its own engine and every other rank's, serves its engine to the other ranks'
+    acceptors from a background thread, and publishes its load on a shared-memory board; each
+    rank then binds the SAME gRPC port (SO_REUSEPORT, grpc's default on Linux), the kernel spreads
+    client connections over the acceptors and each routes a request to the least-loaded engine --
+    request parsing and response building scale with the ranks instead of funnelling through one
+    Python process (profiles/r2_gateway_ab.txt)."""
     import os
     import secrets
 
@@ -307,15 +383,35 @@ def dp_gateway(llm, st, group=None):
     # rank 0 draws the shared token; every engine server accepts only a front end that presents it
     tok = [secrets.token_hex(16) if st.rank == 0 else None]
     dist.broadcast_object_list(tok, src=0, group=group)
-    server = EngineServer(llm, host=bind, token=tok[0]) if st.rank != 0 else None
-    addrs: List = [None] * st.world_size
-    dist.all_gather_object(addrs, (advertise, server.port) if server is not None else None, group=group)
-    if server is not None:
-        server.serve()
-        return None
-    remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0])
-               for r in range(1, st.world_size)]
-    return ReplicaPool([llm] + remotes)
+    if not reuseport:
+        server = EngineServer(llm, host=bind, token=tok[0]) if st.rank != 0 else None
+        addrs: List = [None] * st.world_size
+        dist.all_gather_object(addrs, (advertise, server.port) if server is not None else None, group=group)
+        if server is not None:
+            server.serve()
+            return None
+        remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0])
+                   for r in range(1, st.world_size)]
+        return ReplicaPool([llm] + remotes)
+    if not single_node:
+        raise ValueError("the SO_REUSEPORT gateway shares one address: its ranks must share a node")
+    server = EngineServer(llm, host=bind, token=tok[0])
+    addrs = [None] * st.world_size
+    dist.all_gather_object(addrs, (advertise, server.port), group=group)
+    name = [f"pk_load_{os.getpid()}_{secrets.token_hex(4)}" if st.rank == 0 else None]
+    board = LoadBoard(name[0], True, st.world_size) if st.rank == 0 else None
+    dist.broadcast_object_list(name, src=0, group=group)
+    if board is None:
+        board = LoadBoard(name[0], False, st.world_size)
+    llm.load_pub = lambda v, b=board, r=st.rank: b.set(r, v)
+    th = threading.Thread(target=server.serve, args=(st.world_size - 1,), name="polykey-engine-server", daemon=True)
+    th.start()
+    remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0],
+                            load_fn=lambda b=board, r=r: b.get(r)) for r in range(st.world_size) if r != st.rank]
+    dist.barrier(group=group)  # every acceptor connected before any rank serves clients
+    pool = ReplicaPool([llm] + remotes)
+    pool.gateway_thread, pool.load_board = th, board
+    return pool
 
 
 def _fanout(batch) -> None:
