@@ -76,6 +76,14 @@ def relaunch_with_torchrun(args) -> int:
     return subprocess.call(cmd)
 
 
+async def _abarrier(group) -> None:
+    """A barrier that keeps this rank's event loop running: with the SO_REUSEPORT gateway the
+    rank's acceptor serves other ranks' clients too, and blocking its loop in a collective
+    while their requests are in flight through it would deadlock the wave."""
+    import torch.distributed as dist
+    await asyncio.get_running_loop().run_in_executor(None, lambda: dist.barrier(group=group))
+
+
 async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, shared_port=0):
     import grpc
     import torch
@@ -92,10 +100,25 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, sha
     router = ToolRouter()
     cfg = ServerConfig(model=args.model, backend="local")
     attach_local_llm(router, cfg, logger, engine=engine, llm=llm)
-    port = shared_port or (args.port_base + st.rank if args.port_base > 0 else 0)
     conc = args.concurrency * n_replicas  # gateway: one front end for every replica's clients
-    srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
-    port = await srv.start()
+    if shared_port:
+        # SO_REUSEPORT gateway: rank 0's server takes a port from the kernel and holds it before the
+        # other ranks join it (a port picked, closed and re-bound later could be handed to another
+        # process meanwhile, whose reuseport listeners would then share our connections)
+        holder = [None]
+        if st.rank == 0:
+            srv = PolykeyServer(router, logger, f"127.0.0.1:{args.port_base or 0}")
+            holder[0] = await srv.start()
+        dist.broadcast_object_list(holder, src=0)
+        if st.rank != 0:
+            srv = PolykeyServer(router, logger, f"127.0.0.1:{holder[0]}")
+            await srv.start()
+        port = holder[0]
+        dist.barrier()  # every acceptor is listening before any client connects
+    else:
+        port = args.port_base + st.rank if args.port_base > 0 else 0
+        srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
+        port = await srv.start()
     if args.client == "process":
         try:
             return await _drive_external(args, engine, st, leaders_group if n_replicas == 1 else None, port, srv,
@@ -169,7 +192,7 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, sha
     waves = [[build() for _ in range(conc)] for _ in range(args.steps)]
     dev = engine.device
     if sync_ranks:
-        dist.barrier(group=leaders_group)
+        await _abarrier(leaders_group)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -181,7 +204,7 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, sha
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     if sync_ranks:
-        dist.barrier(group=leaders_group)
+        await _abarrier(leaders_group)
     elapsed = time.perf_counter() - t0
     await channel.close()
     await srv.server.stop(0)
@@ -213,7 +236,7 @@ async def _drive_external(args, engine, st, leaders_group, port, srv, llm, conc,
             raise RuntimeError(f"load generator failed to start: {ready}")
         dev = engine.device
         if dist.is_initialized() and leaders_group is not None:
-            dist.barrier(group=leaders_group)
+            await _abarrier(leaders_group)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -223,7 +246,7 @@ async def _drive_external(args, engine, st, leaders_group, port, srv, llm, conc,
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         if dist.is_initialized() and leaders_group is not None:
-            dist.barrier(group=leaders_group)
+            await _abarrier(leaders_group)
         elapsed = time.perf_counter() - t0
         if "tokens" not in res:
             raise RuntimeError(f"load generator failed: {res}")
@@ -269,20 +292,11 @@ def main(argv=None) -> int:
     dp_front = st.world_size > 1 and st.tp_size == 1 and not engine.lockstep
     gateway = args.frontend == "gateway" and dp_front
     if gateway:  # one gRPC address, an acceptor per rank (SO_REUSEPORT), least-loaded routing
-        import socket as _socket
-
         from polykey_service_amd.engine.async_llm import AsyncLLM
         from polykey_service_amd.engine.remote import dp_gateway
         local = AsyncLLM(engine)
         pool = dp_gateway(local, st, reuseport=True)
-        port = [None]
-        if st.rank == 0:
-            s0 = _socket.socket()
-            s0.bind(("127.0.0.1", args.port_base or 0))
-            port[0] = s0.getsockname()[1]
-            s0.close()
-        dist.broadcast_object_list(port, src=0)
-        tokens, elapsed, lats = asyncio.run(run_waves(args, engine, st, leaders_group, llm=pool, shared_port=port[0]))
+        tokens, elapsed, lats = asyncio.run(run_waves(args, engine, st, leaders_group, llm=pool, shared_port=True))
     elif args.frontend == "single" and dp_front:
         from polykey_service_amd.engine.async_llm import AsyncLLM
         from polykey_service_amd.engine.remote import dp_gateway

@@ -53,6 +53,8 @@ struct GemmArgs {
   int a_row_div;             //   into the A staging: a_rows = expert-sorted slots, a_row_div = top-k)
   int row_scale;             // output row m scaled by rinv[m] from nrm_parts (RMSNorm folded: A is the
                              //   residual stream, the norm weight is pre-multiplied into W's columns)
+  int row_tiles;             // set by dispatch: row tiles of M (> 1: M > 64, see skinny_gemm_kernel)
+  int tile_rows;             // set by dispatch: rows per row tile (64, or 128 for the MT = 8 variant)
 };
 
 namespace {
@@ -72,6 +74,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 //   kQkvRope:    128-column n-block = one head: RoPE (neox) for q / k heads, q -> out, k -> K
 //                cache, v -> transposed V cache at the token's slot (slot < 0: not cached).
 enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4 };
+constexpr int kMaxRows = 1024;  // decode batch bound of the row-tiled modes
 
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
@@ -262,11 +265,16 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
 constexpr int kKC = 256;           // k per LDS chunk
 constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows shift one 16-B slot)
 
+// MT = 8 (128 A rows, decode batches above 64): A is staged per 128-deep k-step instead of per
+// 256-deep chunk, so the double-buffered tile stays 68 KiB (two workgroups per CU) and the
+// register staging half as wide (no spills at 2 waves / SIMD).
 template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2>
 __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args) {
   constexpr int kR = KR;
-  __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kAStride];
-  __shared__ float rinv_s[64];
+  constexpr int kKA = MT > 4 ? 128 : kKC;  // k per staged A tile
+  constexpr int kPPR = kKA / 8;             // 16-byte pieces per A row
+  __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kKA + 8];
+  __shared__ float rinv_s[MT > 4 ? 16 * MT : 64];
 #if PK_LAB_LDS_PAD
   __shared__ char lab_pad[PK_LAB_LDS_PAD];  // timing only: force one workgroup per CU
   if (args.M < 0) lab_pad[threadIdx.x] = 1;
@@ -282,10 +290,29 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     if (M <= 0) return;  // no tokens routed to this expert: its weights are never read
     Wg += static_cast<int64_t>(blockIdx.y) * args.w_stride;
   }
+  // Row tiles (M > 64, not grouped): every (n-block, split) tile runs once per 64-row tile of M.
+  // The RT workgroups of one W tile are given consecutive dispatch slots of ONE XCD (workgroups
+  // go round-robin over the 8 XCDs), so they stream the same W bytes at the same time through
+  // that XCD's L2 and HBM sees each weight byte about once.
+  int bx = blockIdx.x;
+  if (args.row_offsets == nullptr && args.row_tiles > 1) {
+    const int RT = args.row_tiles, T = gridDim.x / RT;
+    int rt;
+    if ((T & 7) == 0) {
+      const int q = bx >> 3;
+      rt = q % RT;
+      bx = (q / RT) * 8 + (bx & 7);
+    } else {
+      rt = bx % RT;
+      bx /= RT;
+    }
+    row0 = rt * 16 * MT;
+    M = min(args.M - row0, 16 * MT);
+  }
   const bf16_t* __restrict__ A = args.a_rows != nullptr ? args.A : args.A + static_cast<int64_t>(row0) * args.lda;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
-  const int nb = blockIdx.x / S, split = blockIdx.x % S;
+  const int nb = bx / S, split = bx % S;
   const int kper = K / S;
   const int k0 = split * kper;
   const int r = lane & 15, g = lane >> 4;
@@ -302,13 +329,19 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   // RS (row scale): the sum-of-squares parts of row `tid` are requested before the weight
   // stream starts and consumed only after the main loop, so they never delay it (unconditional
   // loads from clamped addresses: a load behind a branch would make hipcc drain vmcnt)
-  // (up to 64 parts per row: 4 threads per row, 16 loads each)
-  constexpr int kRsLoads = 16;
-  float rs_p[RS ? kRsLoads : 1];
+  // (4 threads per row; up to 64 parts per row for 64 rows, 16 for 128 rows)
+  constexpr int kRsRows = MT > 4 ? 2 : 1;  // 64-row groups per thread
+  constexpr int kRsLoads = 16 / (kRsRows * kRsRows);
+  float rs_p[RS ? kRsRows * kRsLoads : 1];
   if constexpr (RS) {
-    const int np = min(args.nrm_nparts, 4 * kRsLoads), rr = min(tid >> 2, M - 1), sub = tid & 3;
+    const int np = min(args.nrm_nparts, 4 * kRsLoads), sub = tid & 3;
 #pragma unroll
-    for (int q = 0; q < kRsLoads; ++q) rs_p[q] = args.nrm_parts[min(sub + 4 * q, np - 1) * M + rr];
+    for (int h = 0; h < kRsRows; ++h) {
+      const int rr = min(64 * h + (tid >> 2), M - 1);
+#pragma unroll
+      for (int q = 0; q < kRsLoads; ++q)
+        rs_p[h * kRsLoads + q] = args.nrm_parts[min(sub + 4 * q, np - 1) * args.M + row0 + rr];
+    }
   }
 
   const bf16_t* wp[kR];
@@ -317,21 +350,21 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
     wp[t] = PK ? Wg + static_cast<int64_t>(n0 >> 7) * 128 * K + (((n0 & 127) >> 4) + t) * 4 * 512 + 8 * lane  // block-packed
                : Wg + static_cast<int64_t>(n0 + 16 * t + r) * K + 8 * g;                     // row-major [N, K]
 
-  // A staging: MT*16 rows x 256 cols = MT*512 16-byte pieces over 256 threads
-  constexpr int kPieces = (16 * MT * kKC / 8 + 255) / 256;
+  // A staging: MT*16 rows x kKA cols of 16-byte pieces over 256 threads
+  constexpr int kPieces = (16 * MT * kPPR + 255) / 256;
   u32x4 stage[kPieces];
   u32x4 stage_w[NORM ? kPieces : 1];
   const bf16_t* arow[kPieces];  // source row of each staged piece (fixed across k-chunks)
 #pragma unroll
   for (int p = 0; p < kPieces; ++p) {
-    const int src_row = min((tid + 256 * p) >> 5, M - 1);
+    const int src_row = min((tid + 256 * p) / kPPR, M - 1);
     const int r_a = args.a_rows != nullptr ? args.a_rows[row0 + src_row] / args.a_row_div : src_row;
     arow[p] = A + static_cast<int64_t>(r_a) * args.lda;
   }
   auto load_a = [&](int kc) {
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) {
-      const int col = ((tid + 256 * p) & 31) * 8;
+      const int col = ((tid + 256 * p) % kPPR) * 8;
       stage[p] = *reinterpret_cast<const u32x4*>(arow[p] + kc + col);
       if constexpr (NORM) stage_w[p] = *reinterpret_cast<const u32x4*>(args.nrm_w + kc + col);
     }
@@ -340,7 +373,7 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) {
       const int idx = tid + 256 * p;
-      const int row = idx >> 5, col = (idx & 31) * 8;
+      const int row = idx / kPPR, col = (idx % kPPR) * 8;
       u32x4 v = stage[p];
       if constexpr (NORM) {
         float x[8], wv[8];
@@ -399,7 +432,31 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   const int nchunks = kper / kKC;
   const int rot = (nb * 5) % nchunks;
   auto ck = [&](int c) { return k0 + ((min(c, nchunks - 1) + rot) % nchunks) * kKC; };
-  if constexpr (PK_W_DEPTH > 2) {
+  if constexpr (MT > 4) {
+    // one 128-deep k-step per staged A tile: W steps alternate wa / wb, two steps in flight
+    const int nsteps = 2 * nchunks;  // even
+    const int rot2 = 2 * rot;
+    auto ks = [&](int j) { return k0 + ((min(j, nsteps - 1) + rot2) % nsteps) * 128; };
+    load_a(ks(0));
+    load_w(wa, ks(0));
+    load_w(wb, ks(1));
+    store_a(0);
+    int buf = 0;
+    for (int j = 0; j < nsteps; j += 2) {
+      load_a(ks(j + 1));
+      __syncthreads();  // step j visible in a_lds[buf]; every wave is done with a_lds[buf^1]
+      mma_step(wa, buf, 0);
+      load_w(wa, ks(j + 2));
+      store_a(buf ^ 1);
+      buf ^= 1;
+      load_a(ks(j + 2));
+      __syncthreads();
+      mma_step(wb, buf, 0);
+      load_w(wb, ks(j + 3));
+      store_a(buf ^ 1);
+      buf ^= 1;
+    }
+  } else if constexpr (PK_W_DEPTH > 2) {
     // W register ring PK_W_DEPTH k-steps deep (step j = half j&1 of chunk j>>1)
     constexpr int WD = PK_W_DEPTH;
     bf16x8_t wr[WD][kR][4];
@@ -455,12 +512,16 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 
   if constexpr (RS) {
     const int np = min(args.nrm_nparts, 4 * kRsLoads), sub = tid & 3;
-    float ss = 0.f;
 #pragma unroll
-    for (int q = 0; q < kRsLoads; ++q) ss += sub + 4 * q < np ? rs_p[q] : 0.f;
-    ss += __shfl_xor(ss, 1, 4);
-    ss += __shfl_xor(ss, 2, 4);
-    if (sub == 0 && (tid >> 2) < M) rinv_s[tid >> 2] = rsqrtf(ss / K + args.eps);
+    for (int h = 0; h < kRsRows; ++h) {
+      float ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < kRsLoads; ++q) ss += sub + 4 * q < np ? rs_p[h * kRsLoads + q] : 0.f;
+      ss += __shfl_xor(ss, 1, 4);
+      ss += __shfl_xor(ss, 2, 4);
+      const int row = 64 * h + (tid >> 2);
+      if (sub == 0 && row < M) rinv_s[row] = rsqrtf(ss / K + args.eps);
+    }
     __syncthreads();
   }
 
@@ -875,8 +936,15 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
 
 template <int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2>
 int launch(const GemmArgs& a, hipStream_t stream) {
-  const dim3 grid((a.N / (64 * KR)) * a.S, a.row_offsets != nullptr ? a.groups : 1);
-  switch ((min(a.M, a.max_group_rows > 0 ? a.max_group_rows : a.M) + 15) / 16) {
+  const dim3 grid((a.N / (64 * KR)) * a.S * a.row_tiles, a.row_offsets != nullptr ? a.groups : 1);
+  if (a.tile_rows == 128) {  // row-tiled decode batches above 64 (dispatch: modes 0-2, no norm prologue)
+    if constexpr (MODE <= kSiluMul && !NORM) {
+      skinny_gemm_kernel<8, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a);
+      return PK_CHECK_LAUNCH();
+    }
+    return -1;
+  }
+  switch ((min(min(a.M, 64), a.max_group_rows > 0 ? a.max_group_rows : 64) + 15) / 16) {
     case 1: skinny_gemm_kernel<1, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a); break;
     case 2: skinny_gemm_kernel<2, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a); break;
     case 3: skinny_gemm_kernel<3, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a); break;
@@ -905,23 +973,31 @@ int launch_pk(const GemmArgs& a, bool packed, bool nt, hipStream_t stream) {
   return packed ? launch<MODE, true, NORM, false>(a, stream) : launch<MODE, false, NORM, false>(a, stream);
 }
 
-int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
-  if (a.M <= 0) return 0;
+int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
+  if (args.M <= 0) return 0;
+  GemmArgs a = args;
   const bool grouped = a.row_offsets != nullptr;
   if (grouped && (a.groups <= 0 || a.max_group_rows <= 0 || a.max_group_rows > 64 || (mode & 7) > kSiluMul ||
                   (mode & 32)))
     return -1;
-  if ((!grouped && a.M > 64) || a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;
+  // M > 64: row tiles of 128 (64 when the row scale has more than 16 parts per row) for the modes
+  // without an in-launch split-K reduction (its per-n-block tickets would be shared by the row
+  // tiles) and without the A-staging norm prologue
+  a.tile_rows = !grouped && a.M > 64 && !(a.row_scale && a.nrm_nparts > 16) ? 128 : 64;
+  a.row_tiles = grouped ? 1 : (a.M + a.tile_rows - 1) / a.tile_rows;
+  if (a.M > 64 && !grouped && (a.M > kMaxRows || (mode & 7) > kSiluMul || (mode & 32))) return -1;
+  if (a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;
   const bool packed = (mode & 16) != 0;  // bit 4: W in block-packed layout
   const bool norm = (mode & 32) != 0;    // bit 5: RMSNorm prologue on A
-  const bool nt = (mode & 64) != 0;      // bit 6: non-temporal weight loads (hint)
+  // bit 6: non-temporal weight loads (hint); not with several row tiles, whose workgroups of one
+  // W tile read it through the XCD's L2 one after another
+  const bool nt = (mode & 64) != 0 && a.row_tiles == 1;
   const bool half = (mode & 128) != 0;   // bit 7: 64-row n-blocks (KR = 1)
-  if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr || a.M > 64)) return -1;
+  if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr)) return -1;
   if (half) {  // split-K projections only: fp32 slabs or the in-launch residual update
     if (grouped || norm || nt) return -1;
     if (a.row_scale) {  // folded-norm QKV slabs (packed W only)
-      if ((mode & 7) != kPartial || !packed || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64 ||
-          a.M > 64)
+      if ((mode & 7) != kPartial || !packed || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64)
         return -1;
       return launch<kPartial, true, false, false, true, 1>(a, stream);
     }
@@ -935,7 +1011,7 @@ int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
     }
     return -1;
   }
-  if (a.row_scale && (grouped || norm || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64 || a.M > 64))
+  if (a.row_scale && (grouped || norm || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64))
     return -1;
   switch (mode & 7) {
     case kBF16:
@@ -961,7 +1037,7 @@ int dispatch(const GemmArgs& a, int mode, hipStream_t stream) {
 
 // mode 0: out bf16 [M, ldo] (S must be 1); 1: partial fp32 [S, M, N]; 2: SiLU-mul of interleaved
 // gate/up rows -> out bf16 [M, N/2] (S must be 1); bit 4: block-packed W; bit 6: non-temporal W.
-// Requires M <= 64, N % 128 == 0, K % (256 S) == 0.
+// Requires M <= kMaxRows (> 64: 64-row tiles), N % 128 == 0, K % (256 S) == 0.
 PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void* W, int M, int N, int K, int lda,
                              int ldo, int S, int mode, hipStream_t stream) {
   GemmArgs a{};

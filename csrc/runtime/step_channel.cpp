@@ -117,7 +117,7 @@ StepChannelCore::StepChannelCore(const std::string& name, bool create, int nslot
 
 StepChannelCore::~StepChannelCore() {
   if (hdr_ != nullptr) munmap(hdr_, bytes_);
-  if (owner_) shm_unlink(name_.c_str());
+  if (owner_ && !unlinked_) shm_unlink(name_.c_str());
 }
 
 SlotHead* StepChannelCore::slot(uint64_t seq) const {
@@ -177,6 +177,11 @@ int StepChannelCore::dead_consumer() const {
 
 bool StepChannelCore::producer_alive() const { return pid_alive(hdr_->producer_pid); }
 
+void StepChannelCore::unlink() {
+  if (owner_ && !unlinked_) shm_unlink(name_.c_str());
+  unlinked_ = true;
+}
+
 void StepChannelCore::close() {
   if (owner_) hdr_->closed.store(1, std::memory_order_release);
 }
@@ -209,6 +214,7 @@ void bind_step_channel(py::module_& m) {
           },
           py::arg("buf"), py::arg("timeout_ms") = 1000)
       .def("close", &pk::StepChannelCore::close)
+      .def("unlink", &pk::StepChannelCore::unlink)
       .def("dead_consumer", &pk::StepChannelCore::dead_consumer)
       .def_property_readonly("producer_alive", &pk::StepChannelCore::producer_alive)
       .def_property_readonly("published", &pk::StepChannelCore::published)

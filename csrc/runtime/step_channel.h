@@ -61,6 +61,7 @@ class StepChannelCore {
   int dead_consumer() const;
   bool producer_alive() const;
   void close();  // producer: wake every consumer with "closed"
+  void unlink();  // producer, once every consumer attached: drop the /dev/shm name
 
   uint64_t published() const;
   uint64_t next_to_consume() const { return next_; }
@@ -72,6 +73,7 @@ class StepChannelCore {
   SlotHead* slot(uint64_t seq) const;
   std::string name_;
   bool owner_ = false;
+  bool unlinked_ = false;
   int index_ = -1;  // consumer index (producer: -1)
   size_t bytes_ = 0;
   StepChannelHeader* hdr_ = nullptr;

@@ -86,10 +86,17 @@ class VoteBoard {
   }
   ~VoteBoard() {
     if (h_ != nullptr) munmap(h_, sizeof(VoteHeader));
-    if (owner_) shm_unlink(name_.c_str());
+    if (owner_ && !unlinked_) shm_unlink(name_.c_str());
   }
   VoteBoard(const VoteBoard&) = delete;
   VoteBoard& operator=(const VoteBoard&) = delete;
+
+  // Owner, once every rank has attached: drop the name so a killed group leaves nothing in
+  // /dev/shm (the mappings stay valid).
+  void unlink() {
+    if (owner_ && !unlinked_) shm_unlink(name_.c_str());
+    unlinked_ = true;
+  }
 
   // Post this rank's step numbers and wait for every rank's.  Returns (any busy, all stopping,
   // max ntok).  Throws on timeout or when a peer process has died.
@@ -133,6 +140,7 @@ class VoteBoard {
  private:
   std::string name_;
   bool owner_;
+  bool unlinked_ = false;
   int rank_;
   int n_ = 0;
   VoteHeader* h_ = nullptr;
@@ -147,6 +155,7 @@ void bind_vote_board(py::module_& m) {
   py::class_<pk::VoteBoard>(m, "VoteBoard")
       .def(py::init<const std::string&, bool, int, int>(), py::arg("name"), py::arg("create"), py::arg("nranks"),
            py::arg("rank"))
+      .def("unlink", &pk::VoteBoard::unlink)
       .def(
           "vote",
           [](pk::VoteBoard& b, bool busy, bool stopping, int64_t ntok, int64_t timeout_ms) {

@@ -26,6 +26,7 @@ from __future__ import annotations
 import dataclasses
 import math
 import os
+import threading
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -159,6 +160,8 @@ class ModelRunner:
             name = comm.tp_broadcast_object(None)
             self.channel = rt.StepChannel(name, False, consumer_index=st.tp_rank - 1)
         comm.barrier(st.tp_cpu_group)  # every consumer attached before the first publish
+        if st.tp_rank == 0:
+            self.channel.unlink()  # nothing left in /dev/shm if the group is killed
 
     # ---------------------------------------------------------------- KV cache
     def kv_bytes_per_block(self) -> int:
@@ -411,6 +414,32 @@ class ModelRunner:
         staging buffer, read its header on the host and launch the same work — the worker never
         waits for its own GPU (only, through the double-buffered staging, for a step two back)."""
         chan = self.channel
+        done = threading.Event()
+        watch = threading.Thread(target=self._leader_watch, args=(done,), name="pk-leader-watch", daemon=True)
+        watch.start()
+        try:
+            self._worker_steps(chan)
+        finally:
+            done.set()
+            watch.join(5.0)
+
+    def _leader_watch(self, done: threading.Event, grace_s: float = 10.0) -> None:
+        """A worker blocked on its GPU (a collective waiting for the dead leader, an RCCL kernel
+        that never times out) cannot reach the step channel's dead-producer check: this thread
+        sees the leader's pid vanish, aborts the communicators (the waits return), and if the
+        main loop has not ended the process ``grace_s`` later, exits it non-zero itself."""
+        while not done.wait(1.0):
+            if self.channel.producer_alive:
+                continue
+            self.abort_comms()
+            if done.wait(grace_s):
+                return
+            import sys
+            print("TP leader process died and this worker is still blocked on the GPU: exiting",
+                  file=sys.stderr, flush=True)
+            os._exit(1)
+
+    def _worker_steps(self, chan) -> None:
         while True:
             self._next_staging()
             nbytes = chan.consume(self._hnp[self._cur], 1000)

@@ -345,11 +345,19 @@ class LoadBoard:
     def get(self, rank: int) -> int:
         return int(self.arr[rank])
 
+    def unlink(self) -> None:
+        """Owner, once every rank has attached: drop the /dev/shm name (mappings stay valid)."""
+        if self.owner:
+            self.owner = False
+            try:
+                self.shm.unlink()
+            except FileNotFoundError:
+                pass
+
     def close(self) -> None:
         self.arr = None
         self.shm.close()
-        if self.owner:
-            self.shm.unlink()
+        self.unlink()
 
 
 def dp_gateway(llm, st, group=None, reuseport: bool = False):
@@ -409,6 +417,7 @@ def dp_gateway(llm, st, group=None, reuseport: bool = False):
     remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0],
                             load_fn=lambda b=board, r=r: b.get(r)) for r in range(st.world_size) if r != st.rank]
     dist.barrier(group=group)  # every acceptor connected before any rank serves clients
+    board.unlink()  # every rank attached the load board
     pool = ReplicaPool([llm] + remotes)
     pool.gateway_thread, pool.load_board = th, board
     return pool

@@ -20,7 +20,10 @@ from . import native, reference
 
 import os
 
-SKINNY_MAX_M = 64
+# decode batches above 64 rows run the kernel in 64-row tiles whose workgroups share each W tile
+# through one XCD's L2 (csrc/kernels/gemm_skinny.hip "Row tiles")
+SKINNY_MAX_M = 512
+SKINNY_TILE_M = 128  # rows per row tile above 64 (the kernel's MT = 8 variant)
 # measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
 _TARGET_WGS = 192
 _ROWS_PER_WG = 128
@@ -47,7 +50,8 @@ class GemmArgs(ctypes.Structure):
                 ("v_cache", ctypes.c_void_p), ("slots", ctypes.c_void_p), ("nq", ctypes.c_int),
                 ("nkv", ctypes.c_int), ("bs", ctypes.c_int), ("row_offsets", ctypes.c_void_p),
                 ("w_stride", ctypes.c_longlong), ("groups", ctypes.c_int), ("max_group_rows", ctypes.c_int),
-                ("a_rows", ctypes.c_void_p), ("a_row_div", ctypes.c_int), ("row_scale", ctypes.c_int)]
+                ("a_rows", ctypes.c_void_p), ("a_row_div", ctypes.c_int), ("row_scale", ctypes.c_int),
+                ("row_tiles", ctypes.c_int)]
 
 
 _ARGS_CHECKED = False
@@ -206,8 +210,8 @@ def deinterleave_gate_up(w: torch.Tensor, block: int = 16):
 
 
 def choose_split(N: int, K: int, M: int, target: int = _TARGET_WGS) -> int:
-    """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows each)."""
-    blocks = N // _ROWS_PER_WG
+    """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows x 64 A rows each)."""
+    blocks = N // _ROWS_PER_WG * (1 if M <= 64 else -(-M // SKINNY_TILE_M))
     s = 1
     while blocks * s < target and s < 16 and K % (_KCHUNK * s * 2) == 0:
         s *= 2

@@ -175,6 +175,8 @@ def _vote_board(st: ParallelState):
     if not all(ok):
         log.warning("shared-memory vote board unavailable (%s); lockstep votes over gloo", err)
         return None
+    if st.rank == 0:
+        board.unlink()  # every rank attached: nothing left in /dev/shm if the group is killed
     return board
 
 

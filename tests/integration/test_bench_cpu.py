@@ -3,12 +3,27 @@ from rank 0 with the BASELINE metric, whole-job value, and the DP parallelism / 
 of the launch; 2 ranks go through the torchrun child launch the driver itself uses."""
 import json
 import os
+import signal
 import subprocess
 import sys
 
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+def _run(cmd, cwd, env, timeout=300):
+    """bench.py in its own session: on a timeout the whole tree (torchrun, its ranks, load
+    generators) is killed, not just the launcher."""
+    p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        pytest.fail(f"bench.py timed out after {timeout} s\n{err[-3000:]}")
+    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
+
+
 ARGS = ["--model", "tiny-llama-gqa4", "--steps", "1", "--warmup", "1", "--concurrency", "4", "--prompt-len", "8",
         "--max-tokens", "4", "--no-graphs"]
 
@@ -18,9 +33,8 @@ ARGS = ["--model", "tiny-llama-gqa4", "--steps", "1", "--warmup", "1", "--concur
                                                  (3, "process", "gateway"), (2, "inproc", "single")])
 def test_bench_json_line(tmp_path, gpus, client, frontend):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--client", client,
-                        "--frontend", frontend] + ARGS, cwd=tmp_path,
-                       env=env, capture_output=True, text=True, timeout=300)
+    r = _run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--client", client,
+              "--frontend", frontend] + ARGS, tmp_path, env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -44,8 +58,7 @@ def test_bench_dp_attention_expert_all_to_all():
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     args = ["--model", "tiny-mixtral", "--ep", "2", "--steps", "1", "--warmup", "1", "--concurrency", "3",
             "--prompt-len", "8", "--max-tokens", "4", "--no-graphs"]
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"] + args, cwd=REPO,
-                       env=env, capture_output=True, text=True, timeout=300)
+    r = _run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"] + args, REPO, env)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["config"]["parallelism"] == "dp2_ep2_a2a" and out["config"]["global_batch"] == 6

@@ -307,3 +307,49 @@ def test_rowscale_half_blocks(M):
     b = gemm.linear_partial_rowscale(res, w, ws[4 * M * N:], rs, packed=wp, half=True)
     assert a.S == 4 and b.S == 2
     torch.testing.assert_close(a.view().sum(0), b.view().sum(0), atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.parametrize("M", [65, 128, 200, 512])
+def test_row_tiles_above_64(M):
+    """Decode batches above 64 rows: 128-row tiles of M per W tile (grid x row tiles, XCD-grouped),
+    for every mode the decode chain uses -- bf16 out (row-major and packed+NT: the LM head), fp32
+    split-K slabs, folded-norm QKV slabs (RowScale with per-row parts) and the SiLU gate_up."""
+    H, N, I = 4096, 6144, 1792
+    res = rnd(M, H)
+    w = rnd(N, H, scale=0.02)
+    exp = res.float() @ w.float().t()
+    torch.testing.assert_close(gemm.linear(res, w).float(), exp, atol=2e-2, rtol=2e-2)
+    wp = gemm.pack_weight(w)
+    torch.testing.assert_close(gemm.linear(res, w, packed=wp).float(), exp, atol=2e-2, rtol=2e-2)
+    S = gemm.choose_split(N, H, M)
+    assert S == max(1, 4 // (-(-M // 128)))  # 128-row tiles take the place of K splits
+    ws = torch.empty(4 * M * N, dtype=torch.float32, device="cuda")
+    p = gemm.linear_partial(res, w, ws, packed=wp)
+    torch.testing.assert_close(p.view().sum(0), exp, atol=1e-2, rtol=1e-2)
+    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    parts = gemm.residual_parts(None, res.clone(), torch.empty(4 * M, device="cuda"))
+    rs = gemm.RowScale(parts, 1e-5)
+    xin = ref.rms_norm(res, nw, 1e-5).float()
+    wfp = gemm.pack_weight(gemm.fold_norm(w, nw))
+    p = gemm.linear_partial_rowscale(res, w, ws, rs, packed=wfp)
+    torch.testing.assert_close(p.view().sum(0), xin @ w.float().t(), atol=3e-2, rtol=3e-2)
+    # 64 parts per row (more than the 128-row tile takes): 64-row tiles instead
+    p64 = gemm.linear_partial_rowscale(res, w, ws, gemm.RowScale(_sumsq_parts(res, 64), 1e-5), S=1, packed=wfp)
+    torch.testing.assert_close(p64.view().sum(0), xin @ w.float().t(), atol=3e-2, rtol=3e-2)
+    g, u = rnd(I, H, scale=0.05), rnd(I, H, scale=0.05)
+    wgu = gemm.interleave_gate_up(g, u)
+    y = gemm.linear_silu(res, wgu, packed=gemm.pack_weight(gemm.fold_norm(wgu, nw)), rowscale=rs)
+    rinv = torch.rsqrt(res.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    h = (res.float() @ gemm.fold_norm(wgu, nw).float().t()) * rinv
+    exp_folded = ref.silu_and_mul_interleaved(h.to(torch.bfloat16)).float()
+    assert (y.float() - exp_folded).abs().max().item() <= 0.01 * exp_folded.abs().max().item()
+
+
+def test_row_tiles_refuse_in_launch_reduction():
+    """The in-launch split-K modes keep M <= 64 (their per-n-block tickets are not per row tile)."""
+    M, H, K = 96, 1024, 512
+    x, w = rnd(M, K), rnd(H, K, scale=0.05)
+    ws = torch.empty(2 * M * H, dtype=torch.float32, device="cuda")
+    ctr = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    with pytest.raises(RuntimeError):
+        gemm.linear_add_residual(x, w, ws, ctr, rnd(M, H), torch.empty(H // 128 * M, device="cuda"), 2)
