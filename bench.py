@@ -297,6 +297,9 @@ def main(argv=None) -> int:
         local = AsyncLLM(engine)
         pool = dp_gateway(local, st, reuseport=True)
         tokens, elapsed, lats = asyncio.run(run_waves(args, engine, st, leaders_group, llm=pool, shared_port=True))
+        if os.environ.get("POLYKEY_BENCH_TIMING") == "1":  # requests each engine served (routing balance)
+            print(f"[gateway] rank {st.rank}: engine served {local.stats['requests']} requests, "
+                  f"{local.stats['steps']} steps", file=sys.stderr, flush=True)
     elif args.frontend == "single" and dp_front:
         from polykey_service_amd.engine.async_llm import AsyncLLM
         from polykey_service_amd.engine.remote import dp_gateway

@@ -48,7 +48,7 @@ struct GemmArgs {
   const int* row_offsets;    // grouped (MoE): rows of group e = [row_offsets[e], row_offsets[e+1]) of A /
   long long w_stride;        //   out / slabs, W of group e at W + e * w_stride; group = blockIdx.y
   int groups;                // number of groups (grid.y)
-  int max_group_rows;        // bound on any group's rows (<= 64): picks the M-tile count
+  int max_group_rows;        // bound on any group's rows (<= kMaxRows): picks the M tile / row tiles
   const int* a_rows;         // grouped: A row of group row i = a_rows[i] / a_row_div (MoE permute folded
   int a_row_div;             //   into the A staging: a_rows = expert-sorted slots, a_row_div = top-k)
   int row_scale;             // output row m scaled by rinv[m] from nrm_parts (RMSNorm folded: A is the
@@ -281,23 +281,21 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 #endif
   __shared__ int last_s;
   const int N = args.N, K = args.K, S = args.S;
-  int M = args.M;  // rows of this workgroup's group (all rows when not grouped)
-  int row0 = 0;
+  // rows of this workgroup's group: all rows, or (grouped) expert blockIdx.y's
+  int gbeg = 0, gend = args.M;
   const bf16_t* Wg = args.W;
   if (args.row_offsets != nullptr) {
-    row0 = args.row_offsets[blockIdx.y];
-    M = min(args.row_offsets[blockIdx.y + 1] - row0, 16 * MT);
-    if (M <= 0) return;  // no tokens routed to this expert: its weights are never read
+    gbeg = args.row_offsets[blockIdx.y];
+    gend = args.row_offsets[blockIdx.y + 1];
     Wg += static_cast<int64_t>(blockIdx.y) * args.w_stride;
   }
-  // Row tiles (M > 64, not grouped): every (n-block, split) tile runs once per 64-row tile of M.
-  // The RT workgroups of one W tile are given consecutive dispatch slots of ONE XCD (workgroups
-  // go round-robin over the 8 XCDs), so they stream the same W bytes at the same time through
-  // that XCD's L2 and HBM sees each weight byte about once.
-  int bx = blockIdx.x;
-  if (args.row_offsets == nullptr && args.row_tiles > 1) {
+  // Row tiles (a group of more than 64 rows): every (n-block, split) tile runs once per 16*MT-row
+  // tile.  The RT workgroups of one W tile are given consecutive dispatch slots of ONE XCD
+  // (workgroups go round-robin over the 8 XCDs), so they stream the same W bytes at the same
+  // time through that XCD's L2 and HBM sees each weight byte about once.
+  int bx = blockIdx.x, rt = 0;
+  if (args.row_tiles > 1) {
     const int RT = args.row_tiles, T = gridDim.x / RT;
-    int rt;
     if ((T & 7) == 0) {
       const int q = bx >> 3;
       rt = q % RT;
@@ -306,9 +304,10 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
       rt = bx % RT;
       bx /= RT;
     }
-    row0 = rt * 16 * MT;
-    M = min(args.M - row0, 16 * MT);
   }
+  const int row0 = gbeg + rt * 16 * MT;
+  const int M = min(gend - row0, 16 * MT);
+  if (M <= 0) return;  // no tokens routed to this expert (or this row tile): its weights are never read
   const bf16_t* __restrict__ A = args.a_rows != nullptr ? args.A : args.A + static_cast<int64_t>(row0) * args.lda;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
@@ -977,15 +976,16 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
   if (args.M <= 0) return 0;
   GemmArgs a = args;
   const bool grouped = a.row_offsets != nullptr;
-  if (grouped && (a.groups <= 0 || a.max_group_rows <= 0 || a.max_group_rows > 64 || (mode & 7) > kSiluMul ||
+  if (grouped && (a.groups <= 0 || a.max_group_rows <= 0 || a.max_group_rows > kMaxRows || (mode & 7) > kSiluMul ||
                   (mode & 32)))
     return -1;
-  // M > 64: row tiles of 128 (64 when the row scale has more than 16 parts per row) for the modes
-  // without an in-launch split-K reduction (its per-n-block tickets would be shared by the row
-  // tiles) and without the A-staging norm prologue
-  a.tile_rows = !grouped && a.M > 64 && !(a.row_scale && a.nrm_nparts > 16) ? 128 : 64;
-  a.row_tiles = grouped ? 1 : (a.M + a.tile_rows - 1) / a.tile_rows;
-  if (a.M > 64 && !grouped && (a.M > kMaxRows || (mode & 7) > kSiluMul || (mode & 32))) return -1;
+  // a group (dense: the whole M) above 64 rows: row tiles of 128 (64 when the row scale has more
+  // than 16 parts per row) for the modes without an in-launch split-K reduction (its per-n-block
+  // tickets would be shared by the row tiles) and without the A-staging norm prologue
+  const int rows = grouped ? a.max_group_rows : a.M;
+  a.tile_rows = rows > 64 && !(a.row_scale && a.nrm_nparts > 16) ? 128 : 64;
+  a.row_tiles = (rows + a.tile_rows - 1) / a.tile_rows;
+  if (rows > 64 && (rows > kMaxRows || (mode & 7) > kSiluMul || (mode & 32))) return -1;
   if (a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;
   const bool packed = (mode & 16) != 0;  // bit 4: W in block-packed layout
   const bool norm = (mode & 32) != 0;    // bit 5: RMSNorm prologue on A

@@ -197,18 +197,24 @@ class ReplicaPool:
     rank per GPU: :func:`~polykey_service_amd.engine.remote.dp_gateway`); the first replica must
     be local.  Duck-types :class:`AsyncLLM`."""
 
-    def __init__(self, replicas):
+    def __init__(self, replicas, loads=None, on_pick=None):
         self.replicas = list(replicas)
+        # per-replica load estimates (default: each replica's own load()) and routing hooks
+        self.loads = list(loads) if loads is not None else [r.load for r in self.replicas]
+        self.on_pick = list(on_pick) if on_pick is not None else [None] * len(self.replicas)
         self.tokenizer = self.replicas[0].tokenizer
         self.engine = self.replicas[0].engine
         self.on_fatal = None
         self.watchdog_s = 0.0
 
     def _pick(self):
-        return min(self.replicas, key=lambda r: r.load())
+        i = min(range(len(self.replicas)), key=lambda j: self.loads[j]())
+        if self.on_pick[i] is not None:
+            self.on_pick[i]()
+        return self.replicas[i]
 
     def load(self) -> int:
-        return sum(r.load() for r in self.replicas)
+        return sum(f() for f in self.loads)
 
     def generate(self, prompt_ids, params, request_id=None, final_only=False):
         return self._pick().generate(prompt_ids, params, request_id, final_only=final_only)

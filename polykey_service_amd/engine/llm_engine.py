@@ -88,6 +88,12 @@ class LLMEngine:
             if self.st.ep_a2a is None:
                 self.st.ep_a2a = ep_ipc.maybe_create(self.st, cfg.max_num_seqs * mcfg.experts_per_token,
                                                      mcfg.hidden_size)
+            if self.st.ep_a2a is not None and self.st.ep_a2a_prefill is None:
+                # prefill-sized steps: a second set of regions sized for the token budget (eager,
+                # host-free counts too: no per-layer read-back of the split sizes)
+                self.st.ep_a2a_prefill = ep_ipc.maybe_create(
+                    self.st, max(cfg.max_num_batched_tokens, cfg.max_num_seqs) * mcfg.experts_per_token,
+                    mcfg.hidden_size)
             cfg = dataclasses.replace(cfg, overlap=False,
                                       hip_graphs=cfg.hip_graphs and self.st.ep_a2a is not None)
             self.cfg = cfg
@@ -205,7 +211,8 @@ class LLMEngine:
         # (graph buckets pad decode rows, but only buckets within the IPC capacity are captured)
         a2a = self.st.ep_a2a
         ipc = a2a is not None and a2a.fits(max_tok * self.mcfg.experts_per_token)
-        self.st.ep_step_rows = max_tok if ipc else (1 << 30)
+        # every rank sees the same max: the same regions (decode-sized, prefill-sized or none) on all
+        self.st.ep_step_rows = max_tok
         self.runner.allow_graphs = ipc  # a replay holds the IPC path: only when every rank takes it
         if batch.empty:
             self.model.idle_forward()

@@ -335,8 +335,9 @@ class ModelRunner:
         for rc in (getattr(st, "rccl_tp", None), getattr(st, "rccl_ep", None)):
             if rc is not None:  # RCCL's asynchronous error word (non-blocking poll)
                 rc.check()
-        if getattr(st, "ep_a2a", None) is not None:
-            st.ep_a2a.check()
+        for a2a in (getattr(st, "ep_a2a", None), getattr(st, "ep_a2a_prefill", None)):
+            if a2a is not None:
+                a2a.check()
 
     def launch_continuation(self, batch: ScheduledBatch, prev) -> Optional[tuple]:
         """Decode step k+1 of ``batch.decodes`` enqueued while step k (``prev``) may still run:
@@ -477,8 +478,9 @@ class ModelRunner:
                 pass
         if st.custom_ar is not None:
             st.custom_ar.fail()
-        if getattr(st, "ep_a2a", None) is not None:
-            st.ep_a2a.fail()
+        for a2a in (getattr(st, "ep_a2a", None), getattr(st, "ep_a2a_prefill", None)):
+            if a2a is not None:
+                a2a.fail()
 
     def stop_workers(self) -> None:
         if self.channel is not None and self.model.st.tp_rank == 0:

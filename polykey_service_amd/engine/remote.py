@@ -188,10 +188,13 @@ class RemoteEngine:
     router (:class:`~polykey_service_amd.adapters.local_llm.ReplicaPool`) and the tools."""
 
     def __init__(self, addr: Tuple[str, int], tokenizer, name: str = "remote", connect_timeout: float = 120.0,
-                 token: Optional[str] = None, load_fn=None):
+                 token: Optional[str] = None, load_fn=None, load_add=None):
         self.tokenizer = tokenizer
         self.name = name
         self.load_fn = load_fn  # engine-wide load (shared-memory load board), else this handle's own
+        # routing a request bumps the board entry at once (the engine overwrites it with its true
+        # count every step): a burst at one acceptor spreads instead of herding on a stale minimum
+        self.load_add = load_add
         self.on_fatal = None
         self.watchdog_s = 0.0
         self.dead: Optional[BaseException] = None
@@ -276,6 +279,8 @@ class RemoteEngine:
         try:
             _send(self.sock, self._wlock, {"op": "add", "rid": rid, "prompt": list(prompt_ids),
                                            "params": _params_dict(params), "final": bool(final_only)})
+            if self.load_add is not None:
+                self.load_add(1)
             while True:
                 item = await q.get()
                 if isinstance(item, BaseException):
@@ -344,6 +349,11 @@ class LoadBoard:
 
     def get(self, rank: int) -> int:
         return int(self.arr[rank])
+
+    def add(self, rank: int, v: int) -> None:
+        """An acceptor's routing estimate (not atomic across processes: the owning engine's
+        next publish replaces it with the true count)."""
+        self.arr[rank] += v
 
     def unlink(self) -> None:
         """Owner, once every rank has attached: drop the /dev/shm name (mappings stay valid)."""
@@ -415,10 +425,15 @@ def dp_gateway(llm, st, group=None, reuseport: bool = False):
     th = threading.Thread(target=server.serve, args=(st.world_size - 1,), name="polykey-engine-server", daemon=True)
     th.start()
     remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0],
-                            load_fn=lambda b=board, r=r: b.get(r)) for r in range(st.world_size) if r != st.rank]
+                            load_fn=lambda b=board, r=r: b.get(r), load_add=lambda d, b=board, r=r: b.add(r, d))
+               for r in range(st.world_size) if r != st.rank]
     dist.barrier(group=group)  # every acceptor connected before any rank serves clients
     board.unlink()  # every rank attached the load board
-    pool = ReplicaPool([llm] + remotes)
+    # this rank's engine: its own exact count, or the board's when other acceptors have just
+    # routed requests to it that it has not drained yet
+    pool = ReplicaPool([llm] + remotes, loads=[lambda b=board, r=st.rank: max(llm.load(), b.get(r))]
+                       + [x.load for x in remotes],
+                       on_pick=[lambda b=board, r=st.rank: b.add(r, 1)] + [None] * len(remotes))
     pool.gateway_thread, pool.load_board = th, board
     return pool
 

@@ -92,6 +92,9 @@ def _lab(name: str, half: bool, S=None):
     return _LAB_SPLITS.get(name, (half, S))
 
 
+LM_HEAD_SKINNY_MAX_M = 128
+
+
 def ranks_per_device() -> int:
     """Local ranks sharing one GPU (1 on a real node; 8 in a one-GPU TP=8 rehearsal)."""
     local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
@@ -600,8 +603,11 @@ class LlamaForCausalLM(nn.Module):
         """hidden [B, H] → logits [B, vocab] (bf16; all-gathered across TP)."""
         # decode: the skinny kernel streams the block-packed vocab projection with non-temporal
         # loads (1 GB for Llama-3: 179 us vs hipBLASLt's 198-208 us, tools/gemm_lab.hip)
+        # above 128 rows hipBLASLt's MFMA GEMM is the faster one (tools/bench_gemm_rows.py, 8B:
+        # 284 vs 358 us at 256 rows, 492 vs 668 at 512; profiles/r3_decode_rows.txt)
         wp = getattr(self, "lm_head_p", None)
-        if wp is not None and gemm.skinny_ok(hidden, self.lm_head):
+        if wp is not None and gemm.skinny_ok(hidden, self.lm_head) and (
+                hidden.shape[0] <= LM_HEAD_SKINNY_MAX_M or self.lm_head.is_meta):
             logits = gemm.linear(hidden, self.lm_head, packed=wp)
         else:
             logits = F.linear(hidden, self.lm_head)

@@ -155,8 +155,8 @@ def grouped_linear(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_
                    S: int = 1, a_rows: Optional[torch.Tensor] = None, a_row_div: int = 1,
                    n_rows: Optional[int] = None) -> torch.Tensor:
     """Grouped decode GEMM (MoE experts): rows ``a[offsets[e]:offsets[e+1]]`` times ``w[e]^T``,
-    ``w`` [G, N, K] (``packed``: :func:`pack_weight` of ``w.view(G*N, K)``), every group <= 64
-    rows.  One launch; groups without rows read no weights.  ``silu``: interleaved gate/up →
+    ``w`` [G, N, K] (``packed``: :func:`pack_weight` of ``w.view(G*N, K)``), every group at most
+    ``max_rows`` rows (above 64: 128-row tiles).  One launch; groups without rows read no weights.  ``silu``: interleaved gate/up →
     [R, N/2] bf16.  Otherwise ``S`` > 1 returns fp32 split-K slabs [S, R, N] in ``ws``."""
     G, N, K = w.shape
     # a_rows: gather A rows (a_rows[i] // a_row_div) instead of reading group-contiguous rows —

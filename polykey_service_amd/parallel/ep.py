@@ -66,9 +66,9 @@ def ep_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch
     the IPC all-to-all when the step's largest token count fits its capacity (``st.ep_step_rows``
     from the lockstep vote), else the RCCL / gloo all-to-all with split lists on the host."""
     st = get_state()
-    a2a = st.ep_a2a
-    if a2a is not None and x.is_cuda and a2a.fits(st.ep_step_rows * k):
-        return _ep_moe_ipc(a2a, x, router_w, w13, w2, k, routing, w13_p, w2_p, defer_combine)
+    for a2a in (st.ep_a2a, st.ep_a2a_prefill):  # decode-sized regions first, then prefill-sized
+        if a2a is not None and x.is_cuda and a2a.fits(st.ep_step_rows * k):
+            return _ep_moe_ipc(a2a, x, router_w, w13, w2, k, routing, w13_p, w2_p, defer_combine)
     ep = st.ep_size
     E = router_w.shape[0]
     per = E // ep
@@ -126,7 +126,10 @@ def _ep_moe_ipc(a2a, x, router_w, w13, w2, k, routing, w13_p, w2_p, defer_combin
     a2a.dispatch(send_x.contiguous(), send_e, offsets)
     # every rank's rows are in this rank's receive regions (padding ids -1: no local expert)
     n = ep * a2a.C
-    y = _local_experts(a2a.recv_x, a2a.recv_e.view(-1, 1), w13, w2, w13_p, w2_p, rows=n, bound=a2a.C)
+    # any one local expert gets at most one row per token of every sender, and no sender has more
+    # than the step's largest token count (the lockstep vote's max, the graph bucket when captured)
+    bound = ep * min(st.ep_step_rows, a2a.C)
+    y = _local_experts(a2a.recv_x, a2a.recv_e.view(-1, 1), w13, w2, w13_p, w2_p, rows=n, bound=bound)
     back = a2a.return_(y.contiguous())[: T * k]  # this rank's rows, in the order they were sent
     pending = moe_ops.PendingCombine(back, inv, wts, T, k)
     if defer_combine and T > 0:

@@ -47,6 +47,7 @@ class ParallelState:
     rccl_ep: Optional[object] = None       # ... of the EP group (the TP one when EP runs inside TP)
     ep_a2a: Optional[object] = None        # IPC expert all-to-all (parallel/ep_ipc.py; DP attention + EP)
     ep_board: Optional[object] = None      # shared-memory lockstep vote (csrc/runtime/vote_board.cpp)
+    ep_a2a_prefill: Optional[object] = None  # IPC expert all-to-all sized for prefill steps (eager)
     ep_step_rows: int = 1 << 30            # largest token count of the current lockstep step (vote)
     backend: str = "none"
     device: torch.device = dataclasses.field(default_factory=lambda: torch.device("cpu"))
@@ -199,8 +200,9 @@ def destroy_parallel() -> None:
     st = get_state()
     if st.custom_ar is not None:
         st.custom_ar.close()
-    if st.ep_a2a is not None:
-        st.ep_a2a.close()
+    for a2a in (st.ep_a2a, st.ep_a2a_prefill):
+        if a2a is not None:
+            a2a.close()
     for c in {id(c): c for c in (st.rccl_tp, st.rccl_ep) if c is not None}.values():
         c.close()
     if dist.is_initialized():

@@ -80,6 +80,32 @@ def test_grouped_linear_skips_empty_groups_and_splits():
     torch.testing.assert_close(p[: 2 * R * N].view(2, R, N).sum(0), exp, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("bound", [128, 256, 512])
+def test_grouped_linear_row_tiles(bound):
+    """Expert groups above 64 rows (EP: every sender's tokens can pick one expert): 128-row tiles
+    per group, bf16 out, packed SiLU and split-K slabs; empty groups read nothing."""
+    G, N, K = 4, 512, 1024
+    sizes = [min(bound, s) for s in (130, 0, 64, 200)]
+    offs = [0]
+    for n in sizes:
+        offs.append(offs[-1] + n)
+    R = offs[-1]
+    a = torch.randn(R, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(G, N, K, device="cuda") * 0.05).to(torch.bfloat16)
+    offsets = torch.tensor(offs, dtype=torch.int32, device="cuda")
+    exp = torch.cat([a[offs[e]:offs[e + 1]].float() @ w[e].float().t() for e in range(G)])
+    y = gemm.grouped_linear(a, w, offsets, bound, silu=False)
+    torch.testing.assert_close(y.float(), exp, atol=2e-2, rtol=2e-2)
+    wp = gemm.pack_weight(w.view(-1, K)).view(w.shape)
+    ws = torch.empty(2 * R * N, dtype=torch.float32, device="cuda")
+    p = gemm.grouped_linear(a, w, offsets, bound, silu=False, packed=wp, ws=ws, S=2)
+    torch.testing.assert_close(p[: 2 * R * N].view(2, R, N).sum(0), exp, atol=2e-2, rtol=2e-2)
+    h = gemm.grouped_linear(a, w, offsets, bound, silu=True, packed=wp)
+    from polykey_service_amd.ops import reference as ref
+    torch.testing.assert_close(h.float(), ref.silu_and_mul_interleaved(exp.to(torch.bfloat16)).float(),
+                               atol=3e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("M,E,k", [(1, 8, 2), (64, 8, 2), (17, 64, 4)])
 def test_add_rmsnorm_with_routing(M, E, k):
     """Split-K residual add + RMSNorm that also routes each row == norm kernel + router GEMM

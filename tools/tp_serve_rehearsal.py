@@ -87,6 +87,8 @@ def main() -> int:
             except grpc.RpcError:
                 pass
             time.sleep(1.0)
+            if int(time.monotonic() - t0) % 30 == 0:  # heartbeat while the ranks build 80 layers
+                print(f"[serve] waiting for SERVING: {time.monotonic() - t0:.0f} s", flush=True)
         res["startup_s"] = round(time.monotonic() - t0, 1)
         # 1. OpenAI-compatible chat route (HTTP, non-streaming)
         body = json.dumps({"model": a.model, "messages": [{"role": "user", "content": "Say hello to the MI355X."}],
