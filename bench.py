@@ -280,7 +280,13 @@ def main(argv=None) -> int:
     st = init_parallel(tp=args.tp, ep=args.ep)
     max_len = args.prompt_len + args.max_tokens + 32
     max_len = (max_len + 511) // 512 * 512
-    ecfg = EngineConfig(model=args.model, seed=args.seed, max_num_seqs=max(args.concurrency, 1),
+    seqs = max(args.concurrency, 1)
+    if args.frontend != "replicas" and st.world_size > 1 and st.tp_size == 1 and not st.dp_attention:
+        # a routed front end balances only approximately: an engine that gets a few requests more
+        # than its share must still batch them all (a request over max_num_seqs would wait a
+        # whole wave) -- headroom up to the next graph bucket
+        seqs = seqs * 3 // 2
+    ecfg = EngineConfig(model=args.model, seed=args.seed, max_num_seqs=seqs,
                         max_num_batched_tokens=args.max_batched_tokens, max_model_len=max_len,
                         hip_graphs=not args.no_graphs, num_kv_blocks=args.num_kv_blocks,
                         gpu_mem_fraction=args.gpu_mem_fraction)

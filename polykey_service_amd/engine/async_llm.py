@@ -160,6 +160,8 @@ class AsyncLLM:
         self._stop = True
         self._wake.set()
         self._thread.join(timeout)
+        if self._watchdog is not threading.current_thread():
+            self._watchdog.join(2.0)  # sleeps <= 1 s between checks; not left running into exit
         try:
             self.engine.shutdown()
         except Exception:

@@ -341,6 +341,11 @@ class LoadBoard:
                 pass
         self.owner = create
         self.arr = np.ndarray((world,), dtype=np.int64, buffer=self.shm.buf)
+        try:
+            from .._native.loader import load_extension
+            self._atomic_add = load_extension("_pk_runtime").shm_add_i64
+        except Exception:  # noqa: BLE001 - extension not built: plain (racy) adds
+            self._atomic_add = None
         if create:
             self.arr[:] = 0
 
@@ -351,9 +356,12 @@ class LoadBoard:
         return int(self.arr[rank])
 
     def add(self, rank: int, v: int) -> None:
-        """An acceptor's routing estimate (not atomic across processes: the owning engine's
-        next publish replaces it with the true count)."""
-        self.arr[rank] += v
+        """An acceptor's routing estimate (an atomic add: the acceptors route concurrently; the
+        owning engine's next publish replaces it with the true count)."""
+        if self._atomic_add is not None:
+            self._atomic_add(self.shm.buf, rank, v)
+        else:
+            self.arr[rank] += v
 
     def unlink(self) -> None:
         """Owner, once every rank has attached: drop the /dev/shm name (mappings stay valid)."""

@@ -28,6 +28,7 @@ def served():
     th = threading.Thread(target=srv.serve, daemon=True)
     th.start()
     remote = RemoteEngine(("127.0.0.1", srv.port), llm.tokenizer, name="t")
+    remote.server = srv  # for tests that inspect the engine side
     yield llm, remote
     remote.shutdown()
     th.join(10)
@@ -143,9 +144,7 @@ def test_abort_of_a_final_only_request_drops_its_buffer(served):
     asyncio.run(go())
     import time as _t
     deadline = _t.monotonic() + 5
-    # the EngineServer behind the fixture is reachable through the remote's peer: find it via gc
-    import gc
-    servers = [o for o in gc.get_objects() if isinstance(o, EngineServer)]
+    servers = [remote.server]
     while _t.monotonic() < deadline and any("r-final" in s._final for s in servers):
         _t.sleep(0.05)
     assert not any("r-final" in s._final for s in servers)
