@@ -23,5 +23,18 @@ grep -h '^{"metric"' $OUT/rank0.log | cut -c1-200
 grep -h "\[wave\]\|\[gateway\]" $OUT/rank*.log | cut -c1-200
 python tools/busy_timeline.py $OUT/trace_r0 $OUT/trace_r1 $OUT/trace_r2 $OUT/trace_r3 --bin-ms 1000 --out $OUT/busy.md > /dev/null
 cat $OUT/busy.md
+python - <<'PY'
+import csv, glob
+for r in range(4):
+    f = glob.glob(f"gpurun_out/gw_prof/trace_r{r}/**/*kernel_trace.csv", recursive=True)[0]
+    rows = list(csv.DictReader(open(f)))
+    t0 = min(int(x["Start_Timestamp"]) for x in rows)
+    long = [x for x in rows if int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) > 20_000_000]
+    print(f"rank {r}: {len(rows)} kernels, {len(long)} longer than 20 ms")
+    for x in long[:12]:
+        s, e = int(x["Start_Timestamp"]), int(x["End_Timestamp"])
+        print(f"  t={(s - t0) / 1e9:8.3f}s dur={(e - s) / 1e6:9.1f}ms queue={x.get('Queue_Id', '?')} "
+              f"stream={x.get('Stream_Id', '?')} grid={x.get('Grid_Size', '?')} {x['Kernel_Name'][:110]}")
+PY
 find $OUT -name '*.csv' -delete
 exit $rc
