@@ -81,17 +81,6 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
     return comm.tp_all_reduce(_proj(x, w, ws, wp))
 
 
-# Lab-only A/B of the decode projections' split-K geometry (tools/gpu/decode_ab.sh):
-# POLYKEY_LAB_SPLITS="qkv=half:4,o=half:4,down=full:8" (full = 128-row n-blocks, half = 64-row;
-# then the split).  Unset: each projection's measured default.
-_LAB_SPLITS = {k: (v.split(":")[0] == "half", int(v.split(":")[1])) for k, v in
-               (e.split("=") for e in os.environ.get("POLYKEY_LAB_SPLITS", "").split(",") if e)}
-
-
-def _lab(name: str, half: bool, S=None):
-    return _LAB_SPLITS.get(name, (half, S))
-
-
 LM_HEAD_SKINNY_MAX_M = 128
 
 
@@ -450,14 +439,10 @@ class LlamaForCausalLM(nn.Module):
         last = len(self.layers) - 1
         if self.st.tp_size > 1:
             return self._forward_rowscale_tp(residual, parts, positions, md, kv_caches, ws, buf, buf2)
-        qh, qs = _lab("qkv", False)
-        oh, os_ = _lab("o", True)
-        dh, ds = _lab("down", False)
         for i, layer in enumerate(self.layers):
             at, mlp = layer.attn, layer.mlp
             kc, vc = kv_caches[i]
-            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf,
-                                             S=qs, half=qh)
+            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf)
             if md.num_prefill == 0:
                 a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
             else:
@@ -465,11 +450,10 @@ class LlamaForCausalLM(nn.Module):
                 a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
-            parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=oh, S=os_), residual,
-                                        buf2)
+            parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True), residual, buf2)
             h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf,
                                  rowscale=gemm.RowScale(parts, layer.eps))
-            d = gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p, half=dh, S=ds)
+            d = gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p)
             if i < last:
                 parts = gemm.residual_parts(d, residual, buf)
             else:
@@ -520,9 +504,6 @@ class LlamaForCausalLM(nn.Module):
             if w is not None:  # the split shrinks as row tiles grow: take the largest S * M
                 shapes.append(max(gemm.choose_split(w.shape[0], w.shape[1], M) * M
                                   for M in range(1, gemm.SKINNY_MAX_M + 1)) * w.shape[0])
-        if _LAB_SPLITS:  # lab splits may exceed the defaults
-            shapes.append(16 * gemm.SKINNY_TILE_M * max(w.shape[0] for w in (l0.attn.qkv, l0.attn.o, l0.mlp.down)
-                                                       if w is not None))
         return max(shapes + [1])
 
     def _mlp_weights(self, mlp) -> tuple:
