@@ -983,7 +983,8 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
   // than 16 parts per row) for the modes without an in-launch split-K reduction (its per-n-block
   // tickets would be shared by the row tiles) and without the A-staging norm prologue
   const int rows = grouped ? a.max_group_rows : a.M;
-  a.tile_rows = rows > 64 && !(a.row_scale && a.nrm_nparts > 16) ? 128 : 64;
+  // (bit 8: 64-row tiles regardless -- tools/bench_gemm_rows.py compares the two)
+  a.tile_rows = rows > 64 && !(a.row_scale && a.nrm_nparts > 16) && !(mode & 256) ? 128 : 64;
   a.row_tiles = (rows + a.tile_rows - 1) / a.tile_rows;
   if (rows > 64 && (rows > kMaxRows || (mode & 7) > kSiluMul || (mode & 32))) return -1;
   if (a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;

@@ -113,6 +113,7 @@ def _launch_ex(mode: int, x: torch.Tensor, w: torch.Tensor, packed: Optional[tor
 
 
 HALF_BIT = 128  # 64-row n-blocks (KR = 1): twice the n-blocks, half the split-K
+ROWS64_BIT = 256  # M > 64: 64-row tiles instead of 128 (A/B only: tools/bench_gemm_rows.py)
 
 
 def linear_add_residual(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, counters: torch.Tensor,

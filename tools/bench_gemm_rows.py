@@ -12,7 +12,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
-from polykey_service_amd.ops import gemm
+from polykey_service_amd.ops import gemm, native
 
 
 def timeit(fn, n, iters=30):
@@ -51,6 +51,13 @@ for name, N, K in SHAPES:
             for S in sorted({max(1, S0 // 2), S0, min(16, 2 * S0)}):
                 if K % (256 * S) == 0 and S * M * N <= ws.numel():
                     row[f"skinny_S{S}_us"] = timeit(lambda i: gemm.linear_partial(x, wl[i], ws, S, packed=pl[i]), n)
+        if M > 64:  # the same launch in 64-row tiles (W shared through the XCD L2) instead of 128
+            S0 = 1 if name in ("gate_up", "lm_head") else gemm.choose_split(N, K, M)
+            mode = {"gate_up": gemm.MODE_SILU, "lm_head": gemm.MODE_BF16}.get(name, gemm.MODE_PARTIAL)
+            o = out if name != "gate_up" else torch.empty(M, N // 2, dtype=torch.bfloat16, device="cuda")
+            row[f"skinny_rows64_S{S0}_us"] = timeit(lambda i: native.call(
+                "pk_skinny_gemm", o.data_ptr(), ws.data_ptr(), x.data_ptr(), pl[i].data_ptr(), M, N, K, K,
+                o.stride(0), S0, mode | gemm.PACKED_BIT | gemm.ROWS64_BIT, native.stream_ptr()), n)
         row["weight_tbs_best"] = round(nbytes / min(v for k, v in row.items() if k.endswith("_us")) / 1e6, 2)
         print(json.dumps(row), flush=True)
     del wl, pl
