@@ -75,6 +75,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 //                cache, v -> transposed V cache at the token's slot (slot < 0: not cached).
 enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4 };
 constexpr int kMaxRows = 1024;  // decode batch bound of the row-tiled modes
+constexpr int kPartCols = 512;  // columns per sum-of-squares part (residual_parts_kernel)
 
 
 __device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
@@ -675,35 +676,46 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
 
 // Residual update of the folded-RMSNorm decode chain: residual[m] += bf16(sum_s partial[s, m])
 // (partial == null: residual unchanged) and parts[blk, m] = sum of squares of the new residual
-// over columns [1024 blk, 1024 blk + 1024).  The consumer GEMM turns the parts into rinv[m]
+// over columns [512 blk, 512 blk + 512).  The consumer GEMM turns the parts into rinv[m]
 // (GemmArgs::row_scale) and streams the RMSNorm weight pre-multiplied into its W, so no
-// normalised copy of the residual is ever written.  grid (H / 1024, M): 4 x the workgroups of
-// the per-row norm kernel, each with one round trip of slab loads in flight.
+// normalised copy of the residual is ever written.  One wave per (512 columns, row): every lane
+// issues its 2 (S + 1) loads at once and the sum of squares is a cross-lane reduction -- no LDS,
+// no barrier (this kernel is latency-bound: 64 launches per 8B decode step).
 template <int SS>
-__global__ void __launch_bounds__(256) residual_parts_kernel(bf16_t* __restrict__ residual,
-                                                             const float* __restrict__ partial, int S, int M, int H,
-                                                             float* __restrict__ parts) {
-  __shared__ float red[16];
-  const int blk = blockIdx.x, m = blockIdx.y;
-  const int c = blk * 1024 + threadIdx.x * 4;
+__global__ void __launch_bounds__(64) residual_parts_kernel(bf16_t* __restrict__ residual,
+                                                            const float* __restrict__ partial, int S, int M, int H,
+                                                            float* __restrict__ parts) {
+  const int blk = blockIdx.x, m = blockIdx.y, lane = threadIdx.x;
+  const int c = blk * kPartCols + lane * 4;  // columns c..c+3 and c+256..c+259
   bf16_t* res = residual + static_cast<int64_t>(m) * H + c;
-  const uint2 rr = *reinterpret_cast<const uint2*>(res);
-  float v[4] = {bf2f(static_cast<bf16_t>(rr.x & 0xffff)), bf2f(static_cast<bf16_t>(rr.x >> 16)),
-                bf2f(static_cast<bf16_t>(rr.y & 0xffff)), bf2f(static_cast<bf16_t>(rr.y >> 16))};
+  const uint2 r0 = *reinterpret_cast<const uint2*>(res);
+  const uint2 r1 = *reinterpret_cast<const uint2*>(res + 256);
+  float v[8] = {bf2f(static_cast<bf16_t>(r0.x & 0xffff)), bf2f(static_cast<bf16_t>(r0.x >> 16)),
+                bf2f(static_cast<bf16_t>(r0.y & 0xffff)), bf2f(static_cast<bf16_t>(r0.y >> 16)),
+                bf2f(static_cast<bf16_t>(r1.x & 0xffff)), bf2f(static_cast<bf16_t>(r1.x >> 16)),
+                bf2f(static_cast<bf16_t>(r1.y & 0xffff)), bf2f(static_cast<bf16_t>(r1.y >> 16))};
   if (partial != nullptr) {
     // the projection output is rounded to bf16 first (as the unfused GEMM would store it)
-    const float4 a = slab_sum<SS>(partial + static_cast<int64_t>(m) * H + c, static_cast<int64_t>(M) * H, S);
-    v[0] = rbf(rbf(a.x) + v[0]);
-    v[1] = rbf(rbf(a.y) + v[1]);
-    v[2] = rbf(rbf(a.z) + v[2]);
-    v[3] = rbf(rbf(a.w) + v[3]);
-    uint2 o;
-    o.x = pack2(v[0], v[1]);
-    o.y = pack2(v[2], v[3]);
-    *reinterpret_cast<uint2*>(res) = o;
+    const float* src = partial + static_cast<int64_t>(m) * H + c;
+    const int64_t slab = static_cast<int64_t>(M) * H;
+    const float4 a = slab_sum<SS>(src, slab, S), b = slab_sum<SS>(src + 256, slab, S);
+    const float av[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = rbf(rbf(av[i]) + v[i]);
+    uint2 o0, o1;
+    o0.x = pack2(v[0], v[1]);
+    o0.y = pack2(v[2], v[3]);
+    o1.x = pack2(v[4], v[5]);
+    o1.y = pack2(v[6], v[7]);
+    *reinterpret_cast<uint2*>(res) = o0;
+    *reinterpret_cast<uint2*>(res + 256) = o1;
   }
-  const float ss = block_sum(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3], red);
-  if (threadIdx.x == 0) parts[static_cast<int64_t>(blk) * M + m] = ss;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss += v[i] * v[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+  if (lane == 0) parts[static_cast<int64_t>(blk) * M + m] = ss;
 }
 
 // residual = bf16(residual + bf16(sum_s partial[s])); x = rmsnorm(residual) * w.
@@ -1129,19 +1141,19 @@ static int add_rmsnorm_launch(void* x, void* residual, const void* partial, cons
   return PK_CHECK_LAUNCH();
 }
 
-// residual [M, H] += sum of the S fp32 slabs [S, M, H] (partial may be null), parts [H/1024, M].
+// residual [M, H] += sum of the S fp32 slabs [S, M, H] (partial may be null), parts [H/512, M].
 PK_EXPORT int pk_residual_parts(void* residual, const void* partial, int S, int M, int H, void* parts,
                                 hipStream_t stream) {
   if (M <= 0) return 0;
-  if (H % 1024 || (partial != nullptr && S < 1)) return -1;
-  const dim3 grid(H / 1024, M);
+  if (H % kPartCols || (partial != nullptr && S < 1)) return -1;
+  const dim3 grid(H / kPartCols, M);
   auto rs = static_cast<bf16_t*>(residual);
   auto ps = static_cast<const float*>(partial);
   auto qs = static_cast<float*>(parts);
   switch (partial == nullptr ? 0 : S) {
-    case 4: residual_parts_kernel<4><<<grid, 256, 0, stream>>>(rs, ps, S, M, H, qs); break;
-    case 8: residual_parts_kernel<8><<<grid, 256, 0, stream>>>(rs, ps, S, M, H, qs); break;
-    default: residual_parts_kernel<0><<<grid, 256, 0, stream>>>(rs, ps, S, M, H, qs); break;
+    case 4: residual_parts_kernel<4><<<grid, 64, 0, stream>>>(rs, ps, S, M, H, qs); break;
+    case 8: residual_parts_kernel<8><<<grid, 64, 0, stream>>>(rs, ps, S, M, H, qs); break;
+    default: residual_parts_kernel<0><<<grid, 64, 0, stream>>>(rs, ps, S, M, H, qs); break;
   }
   return PK_CHECK_LAUNCH();
 }

@@ -82,6 +82,7 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
 
 
 LM_HEAD_SKINNY_MAX_M = 128
+GATE_UP_SKINNY_MAX_M = 384
 
 
 def ranks_per_device() -> int:
@@ -341,7 +342,9 @@ class LlamaForCausalLM(nn.Module):
             return self._forward_sp(input_ids, positions, md, kv_caches)
         x = self.embed_tokens(input_ids)
         ws = self.workspace(x.shape[0])
-        if ws is not None and self._rowscale_ok(x):
+        # the folded chain serves decode batches up to DECODE_MAX_M rows; steps carrying prefill
+        # chunks above 64 rows keep the library GEMMs (hipBLASLt) of the general path
+        if ws is not None and (md.num_prefill == 0 or x.shape[0] <= gemm.SKINNY_MAX_M) and self._rowscale_ok(x):
             return self._forward_rowscale(x, positions, md, kv_caches, ws)
         residual = None
         for i, layer in enumerate(self.layers):
@@ -417,7 +420,7 @@ class LlamaForCausalLM(nn.Module):
                 return False
         return (l0.attn.qkv_pf is not None and getattr(l0.mlp, "gate_up_pf", None) is not None
                 and self.cfg.hidden_size % 1024 == 0 and gemm.norm_fusable(self.cfg.hidden_size)
-                and gemm.skinny_ok(x, l0.attn.qkv))
+                and gemm.skinny_ok(x, l0.attn.qkv, max_m=gemm.DECODE_MAX_M))
 
     def _forward_rowscale(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata,
                           kv_caches: List[Tuple[torch.Tensor, torch.Tensor]], ws: torch.Tensor) -> torch.Tensor:
@@ -431,7 +434,7 @@ class LlamaForCausalLM(nn.Module):
         rinv = rsqrt(mean(residual^2) + eps) is formed by each consumer from the parts."""
         T, H = x.shape
         if getattr(self, "_parts_buf", None) is None:
-            self._parts_buf = torch.zeros((H // 64) * gemm.SKINNY_MAX_M, dtype=torch.float32, device=self.device)
+            self._parts_buf = torch.zeros((H // 64) * gemm.DECODE_MAX_M, dtype=torch.float32, device=self.device)
             self._parts_buf2 = torch.zeros_like(self._parts_buf)
         buf, buf2 = self._parts_buf, self._parts_buf2
         residual = x
@@ -451,8 +454,14 @@ class LlamaForCausalLM(nn.Module):
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
             parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True), residual, buf2)
-            h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf,
-                                 rowscale=gemm.RowScale(parts, layer.eps))
+            if T > GATE_UP_SKINNY_MAX_M and not mlp.gate_up.is_meta:
+                # hipBLASLt's MFMA GEMM wins on the 235 MB gate_up above 384 rows (95 vs 149 us at
+                # 512, profiles/r3_decode_rows.txt) even with the norm and SiLU as separate kernels
+                x = gemm.norm_apply(residual, parts, layer.ln2, layer.eps)
+                h = gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
+            else:
+                h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf,
+                                     rowscale=gemm.RowScale(parts, layer.eps))
             d = gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p)
             if i < last:
                 parts = gemm.residual_parts(d, residual, buf)
@@ -491,7 +500,7 @@ class LlamaForCausalLM(nn.Module):
 
     def workspace(self, M: int) -> Optional[torch.Tensor]:
         """fp32 split-K slab buffer for decode-sized batches (fixed address: graph-safe)."""
-        if self.device.type != "cuda" or M > gemm.SKINNY_MAX_M:
+        if self.device.type != "cuda" or M > gemm.DECODE_MAX_M:
             return None
         if getattr(self, "_ws", None) is None:
             self._ws = torch.empty(self._workspace_elems(), dtype=torch.float32, device=self.device)
@@ -503,7 +512,7 @@ class LlamaForCausalLM(nn.Module):
         for w in (l0.attn.qkv, l0.attn.o) + self._mlp_weights(l0.mlp):
             if w is not None:  # the split shrinks as row tiles grow: take the largest S * M
                 shapes.append(max(gemm.choose_split(w.shape[0], w.shape[1], M) * M
-                                  for M in range(1, gemm.SKINNY_MAX_M + 1)) * w.shape[0])
+                                  for M in range(1, gemm.DECODE_MAX_M + 1)) * w.shape[0])
         return max(shapes + [1])
 
     def _mlp_weights(self, mlp) -> tuple:
@@ -587,9 +596,9 @@ class LlamaForCausalLM(nn.Module):
         # above 128 rows hipBLASLt's MFMA GEMM is the faster one (tools/bench_gemm_rows.py, 8B:
         # 284 vs 358 us at 256 rows, 492 vs 668 at 512; profiles/r3_decode_rows.txt)
         wp = getattr(self, "lm_head_p", None)
-        if wp is not None and gemm.skinny_ok(hidden, self.lm_head) and (
+        if wp is not None and gemm.skinny_ok(hidden, self.lm_head, max_m=gemm.DECODE_MAX_M) and (
                 hidden.shape[0] <= LM_HEAD_SKINNY_MAX_M or self.lm_head.is_meta):
-            logits = gemm.linear(hidden, self.lm_head, packed=wp)
+            logits = gemm.linear(hidden, self.lm_head, packed=wp, max_m=gemm.DECODE_MAX_M)
         else:
             logits = F.linear(hidden, self.lm_head)
         logits = comm.tp_all_gather_last(logits)

@@ -20,9 +20,12 @@ from . import native, reference
 
 import os
 
-# decode batches above 64 rows run the kernel in 64-row tiles whose workgroups share each W tile
-# through one XCD's L2 (csrc/kernels/gemm_skinny.hip "Row tiles")
-SKINNY_MAX_M = 512
+# automatic dispatch (linear / linear_silu on any caller, prefill chunks included) picks the
+# skinny kernel up to 64 rows; the decode chain (llama _forward_rowscale, LM head, EP expert
+# groups) uses it up to DECODE_MAX_M in row tiles whose workgroups share each W tile through one
+# XCD's L2 (csrc/kernels/gemm_skinny.hip "Row tiles", profiles/r3_decode_rows.txt)
+SKINNY_MAX_M = 64
+DECODE_MAX_M = 512
 SKINNY_TILE_M = 128  # rows per row tile above 64 (the kernel's MT = 8 variant)
 # measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
 _TARGET_WGS = 192
@@ -210,21 +213,26 @@ def deinterleave_gate_up(w: torch.Tensor, block: int = 16):
     return v[:, 0].reshape(I2 // 2, K), v[:, 1].reshape(I2 // 2, K)
 
 
-def choose_split(N: int, K: int, M: int, target: int = _TARGET_WGS) -> int:
-    """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows x 64 A rows each)."""
-    blocks = N // _ROWS_PER_WG * (1 if M <= 64 else -(-M // SKINNY_TILE_M))
+def choose_split(N: int, K: int, M: int, target: Optional[int] = None) -> int:
+    """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows x one row tile
+    each): 192 for one row tile, 384 when several row tiles share each W tile through the L2
+    (tools/bench_gemm_rows.py, profiles/r3_decode_rows.txt)."""
+    rt = 1 if M <= 64 else -(-M // SKINNY_TILE_M)
+    if target is None:
+        target = _TARGET_WGS if rt == 1 else 2 * _TARGET_WGS
+    blocks = N // _ROWS_PER_WG * rt
     s = 1
     while blocks * s < target and s < 16 and K % (_KCHUNK * s * 2) == 0:
         s *= 2
     return s
 
 
-def skinny_ok(x: torch.Tensor, w: torch.Tensor, force: bool = False) -> bool:
+def skinny_ok(x: torch.Tensor, w: torch.Tensor, force: bool = False, max_m: int = SKINNY_MAX_M) -> bool:
     if not (SKINNY_ENABLED or force) or not x.is_cuda or x.dtype != torch.bfloat16:
         return False
     M, K = x.shape
     N = w.shape[0]
-    return (0 < M <= SKINNY_MAX_M and N % _ROWS_PER_WG == 0 and K % _KCHUNK == 0 and x.stride(1) == 1
+    return (0 < M <= max_m and N % _ROWS_PER_WG == 0 and K % _KCHUNK == 0 and x.stride(1) == 1
             and x.stride(0) % 8 == 0)
 
 
@@ -263,9 +271,10 @@ def _wmode(packed: Optional[torch.Tensor]) -> int:
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
-           packed: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """bf16 out [M, N]; ``packed`` = :func:`pack_weight` (w) streamed instead of ``w`` when given."""
-    if not skinny_ok(x, w):
+           packed: Optional[torch.Tensor] = None, max_m: int = SKINNY_MAX_M) -> torch.Tensor:
+    """bf16 out [M, N]; ``packed`` = :func:`pack_weight` (w) streamed instead of ``w`` when given;
+    the skinny kernel up to ``max_m`` rows (decode callers: :data:`DECODE_MAX_M`)."""
+    if not skinny_ok(x, w, max_m=max_m):
         if w.is_meta:  # packed-only weights (LlamaForCausalLM.pack_decode_weights): prefill on them
             from . import gemm_prefill
             return gemm_prefill.linear(x, w, out=out, packed=packed)
@@ -305,7 +314,7 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
 
 def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[torch.Tensor] = None,
                 packed: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None,
-                rowscale: Optional[RowScale] = None) -> torch.Tensor:
+                rowscale: Optional[RowScale] = None, max_m: int = SKINNY_MAX_M) -> torch.Tensor:
     """silu(x @ Wg^T) * (x @ Wu^T) with interleaved gate/up rows → [M, I].  With ``norm``,
     ``x`` is the residual stream and the RMSNorm is applied in the kernel's prologue (S = 1);
     with ``rowscale`` the norm is folded (W pre-multiplied, rows scaled in the epilogue)."""
@@ -315,7 +324,7 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
         _launch_ex(MODE_SILU, x, w_gu_interleaved, packed, 1, out=out, norm=norm, rowscale=rowscale)
         return out
-    if not skinny_ok(x, w_gu_interleaved):
+    if not skinny_ok(x, w_gu_interleaved, max_m=max_m):
         if w_gu_interleaved.is_meta:  # packed-only weights: fused SiLU in the prefill GEMM epilogue
             from . import gemm_prefill
             return gemm_prefill.linear(x, w_gu_interleaved, packed=packed, silu=True)
@@ -357,19 +366,23 @@ def fold_norm(w: torch.Tensor, norm_weight: torch.Tensor) -> torch.Tensor:
     return (w.float() * norm_weight.float()[None, :]).to(w.dtype)
 
 
+PART_COLS = 512  # columns per sum-of-squares part written by residual_parts
+
+
 def residual_parts(p: Optional[Partial], residual: torch.Tensor, parts: torch.Tensor) -> torch.Tensor:
     """residual += sum of ``p``'s slabs (bf16, in place; ``p`` None: unchanged) and
-    parts [H/1024, M] = per-1024-column sums of squares of the new residual rows."""
+    parts [H/512, M] = per-512-column sums of squares of the new residual rows."""
     M, H = residual.shape
-    assert parts.numel() >= (H // 1024) * M and residual.is_contiguous()
+    n = H // PART_COLS
+    assert parts.numel() >= n * M and residual.is_contiguous()
     if not residual.is_cuda:
         if p is not None:
             residual.copy_((residual.float() + p.view().sum(0).to(torch.bfloat16).float()).to(residual.dtype))
-        parts.view(-1)[: (H // 1024) * M].copy_(residual.float().view(M, H // 1024, 1024).pow(2).sum(-1).t().reshape(-1))
-        return parts.view(-1)[: (H // 1024) * M].view(H // 1024, M)
+        parts.view(-1)[: n * M].copy_(residual.float().view(M, n, PART_COLS).pow(2).sum(-1).t().reshape(-1))
+        return parts.view(-1)[: n * M].view(n, M)
     native.call("pk_residual_parts", residual.data_ptr(), 0 if p is None else p.buf.data_ptr(), 0 if p is None else p.S,
                 M, H, parts.data_ptr(), native.stream_ptr())
-    return parts.view(-1)[: (H // 1024) * M].view(H // 1024, M)
+    return parts.view(-1)[: n * M].view(n, M)
 
 
 def reduce_partial(p: Partial, out: Optional[torch.Tensor] = None) -> torch.Tensor:

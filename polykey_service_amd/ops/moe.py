@@ -102,12 +102,12 @@ def unpermute(y: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, T: int, k: in
 def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, max_rows: int, silu: bool,
                  packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Rows of expert e = a[offsets[e]:offsets[e+1]] times w[e]^T (w: [E_local, N, K]).
-    Decode-sized groups (<= ``gemm.SKINNY_MAX_M`` rows; above 64 in 128-row tiles) run the
+    Decode-sized groups (<= ``gemm.DECODE_MAX_M`` rows; above 64 in 128-row tiles) run the
     weight-streaming decode GEMM of csrc/kernels/gemm_skinny.hip in grouped mode (``packed``:
     fragment-packed experts)."""
     E_local, N, K = w.shape
     n_out = N // 2 if silu else N
-    if (a.is_cuda and max_rows <= gemm.SKINNY_MAX_M and gemm.SKINNY_ENABLED and N % 128 == 0
+    if (a.is_cuda and max_rows <= gemm.DECODE_MAX_M and gemm.SKINNY_ENABLED and N % 128 == 0
             and K % 256 == 0):
         return gemm.grouped_linear(a, w, offsets, max_rows, silu, packed=packed)
     out = torch.empty((a.shape[0], n_out), dtype=a.dtype, device=a.device)

@@ -189,3 +189,32 @@ def test_packed_only_weights_match_row_major(monkeypatch):
     assert pk_model.packed_only and pk_model.layers[0].attn.qkv.is_meta and pk_model.layers[0].mlp.down.is_meta
     assert pk_model.layers[0].attn.qkv_p is not None and not getattr(ref_model, "packed_only", False)
     torch.testing.assert_close(logits["packed"], logits["rowmajor"], atol=5e-2, rtol=5e-2)
+
+
+def _decode_logits(gpu, prompts, graphs=False):
+    """Logits of the first decode step (one row per prompt, prompt order) and the prefill tokens."""
+    e = LLMEngine(EngineConfig(model="tiny-llama-gqa4", max_num_seqs=512, max_num_batched_tokens=4096,
+                               max_model_len=256, num_kv_blocks=1024, hip_graphs=graphs, device="cuda",
+                               prefix_caching=False), ParallelState(device=torch.device("cuda")), model=gpu)
+    e.runner.keep_logits = True
+    for p in prompts:
+        e.add_request(p, SamplingParams(max_tokens=2, ignore_eos=True))
+    e.step()
+    first = [s.output_ids[0] for s in sorted(e.scheduler.running, key=lambda s: s.seq_id)]
+    e.step()
+    return e.runner.last_logits.float().cpu().clone(), first
+
+
+@pytest.mark.parametrize("batch", [200, 450])
+def test_large_decode_batches_match_small(batch):
+    """Decode batches above 64 rows (128-row tiles of the skinny GEMM; above 384 rows gate_up on
+    hipBLASLt with the norm and SiLU as kernels of their own) give the same logits as the same
+    sequences decoded in a batch of 8 (the M <= 64 fused chain)."""
+    _, gpu = _models("tiny-llama-gqa4")
+    prompts = [[1] + [(7 * i + 3 * j) % 1000 + 3 for j in range(5)] for i in range(batch)]
+    big, fbig = _decode_logits(gpu, prompts)
+    small, fsmall = _decode_logits(gpu, prompts[:8])
+    scale = small.abs().max().item()
+    same = [i for i in range(8) if fbig[i] == fsmall[i]]
+    assert len(same) >= 6, (fbig[:8], fsmall)
+    torch.testing.assert_close(big[same], small[same], atol=0.02 * scale, rtol=0.05)

@@ -3,7 +3,8 @@
 8B projection shapes, M = 64 / 128 / 256 / 512, packed weights rotated over > 1 GiB of copies
 (cold, as in a decode step).  For the row-tiled kernel the split is the default
 (``gemm.choose_split``: row tiles replace K splits) and 2x / 0.5x of it.  One JSON line per
-(shape, M) -> decides ``gemm.SKINNY_MAX_M`` (profiles/r3_decode_rows.txt).
+(shape, M) -> the decode chain's limits (``gemm.DECODE_MAX_M``, LM head / gate_up switches;
+profiles/r3_decode_rows.txt).
 """
 import json
 import os
@@ -43,9 +44,11 @@ for name, N, K in SHAPES:
         row = {"shape": name, "N": N, "K": K, "M": M}
         row["hipblaslt_us"] = timeit(lambda i: torch.mm(x, wl[i].t(), out=out), n)
         if name == "gate_up":  # S = 1 with the SiLU epilogue (hipBLASLt: the GEMM alone)
-            row["skinny_us"] = timeit(lambda i: gemm.linear_silu(x, wl[i], ws, packed=pl[i]), n)
+            row["skinny_us"] = timeit(lambda i: gemm.linear_silu(x, wl[i], ws, packed=pl[i],
+                                                                 max_m=gemm.DECODE_MAX_M), n)
         elif name == "lm_head":
-            row["skinny_us"] = timeit(lambda i: gemm.linear(x, wl[i], out=out, packed=pl[i]), n)
+            row["skinny_us"] = timeit(lambda i: gemm.linear(x, wl[i], out=out, packed=pl[i],
+                                                            max_m=gemm.DECODE_MAX_M), n)
         else:
             S0 = gemm.choose_split(N, K, M)
             for S in sorted({max(1, S0 // 2), S0, min(16, 2 * S0)}):
