@@ -42,9 +42,9 @@ class EngineConfig:
     watermark: float = 0.01
     device: str = ""
     overlap: bool = False  # pipelined steps (see LLMEngine.step); AsyncLLM turns it on
-    # scheduler policy (engine/scheduler.py): prefill_first | decode_first; POLYKEY_SCHED_POLICY
-    sched_policy: str = dataclasses.field(default_factory=lambda: os.environ.get("POLYKEY_SCHED_POLICY",
-                                                                                 "prefill_first"))
+    # scheduler policy (engine/scheduler.py): prefill_first | decode_first (decode_first measured
+    # slower on the headline wave: profiles/r2_decode_ab.txt "scheduler policy")
+    sched_policy: str = "prefill_first"
     max_decode_stall: int = 4
     # > 0: keep only the first num_layers decoder layers of the preset (rehearsals of a large
     # model's per-rank shapes with fewer layers, tests); 0: the preset's depth

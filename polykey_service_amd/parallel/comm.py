@@ -50,7 +50,7 @@ def _comm_stream(device: torch.device) -> "torch.cuda.Stream":
     return s
 
 
-OVERLAP_MIN_ROWS = int(os.environ.get("POLYKEY_TP_OVERLAP_MIN_ROWS", "256"))
+OVERLAP_MIN_ROWS = 256
 
 
 def tp_row_parallel_overlapped(x: torch.Tensor, n_out: int, fn, chunks: int = 2,

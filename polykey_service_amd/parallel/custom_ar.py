@@ -64,8 +64,8 @@ class CustomAllReduce:
         self.blocks = blocks
         # grid of the fused decode collective (0: one workgroup per (row, 1024-column chunk), up
         # to 512).  Ranks sharing ONE GPU (rehearsals, tests) need every rank's grid resident at
-        # once -- POLYKEY_CUSTOM_AR_FUSED_BLOCKS caps it there.
-        self.fused_blocks = int(os.environ.get("POLYKEY_CUSTOM_AR_FUSED_BLOCKS", "0"))
+        # once: maybe_create caps it there.
+        self.fused_blocks = 0
         with torch.cuda.device(device):
             self.ctx = self.lib.pk_car_create(rank, world, max_bytes)
         if not self.ctx:
@@ -195,7 +195,7 @@ def maybe_create(st) -> Optional[CustomAllReduce]:
         car = CustomAllReduce(st.tp_cpu_group, st.tp_rank, st.tp_size, st.device)
         n_dev = max(torch.cuda.device_count(), 1)
         shared = int(os.environ.get("LOCAL_WORLD_SIZE", str(st.tp_size))) > n_dev
-        if shared and "POLYKEY_CUSTOM_AR_FUSED_BLOCKS" not in os.environ:
+        if shared:
             car.fused_blocks = 64  # ranks share a GPU: every rank's grid must be resident at once
         good = car.self_test()
         votes = [None] * st.tp_size

@@ -58,10 +58,12 @@ def _compare(got_logits, got_toks, ref_logits, ref_toks):
 
 def _worker(rank, port, model, out_path, sp=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
-                      LOCAL_RANK="0", POLYKEY_CUSTOM_AR="force", POLYKEY_TP_OVERLAP_MIN_ROWS="8",
+                      LOCAL_RANK="0", POLYKEY_CUSTOM_AR="force",
                       # sp: the 49-token prefill runs sequence-parallel with 2 comm-stream chunks
                       POLYKEY_SP_MIN_TOKENS="16" if sp else "100000")
+    from polykey_service_amd.parallel import comm
     from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    comm.OVERLAP_MIN_ROWS = 8  # the short prefills take the chunk-overlapped row-parallel path
     st = init_parallel(tp=2, device="cuda", backend="gloo")
     assert st.custom_ar is not None, "custom all-reduce did not come up"
     eng = _engine(model, st)
