@@ -269,34 +269,91 @@ constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows
 // MT = 8 (128 A rows, decode batches above 64): A is staged per 128-deep k-step instead of per
 // 256-deep chunk, so the double-buffered tile stays 68 KiB (two workgroups per CU) and the
 // register staging half as wide (no spills at 2 waves / SIMD).
-template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2>
-__global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args) {
+// LDS of one skinny-GEMM workgroup (passed in, so two roles of one fused launch share it)
+template <int MT>
+struct SkinnyLds {
+  static constexpr int kKA = MT > 4 ? 128 : kKC;  // k per staged A tile
+  bf16_t a[2][16 * MT][kKA + 8] __attribute__((aligned(16)));
+  float rinv[MT > 4 ? 16 * MT : 64];
+  int last;
+};
+
+// Dataflow hand-off between the two GEMMs of one fused launch (mlp_fused_kernel): a producer
+// workgroup publishes its finished output columns by a ticket on the consumer split-K slice that
+// reads them; a consumer workgroup issues its first weight loads, then waits for its slice's
+// tickets before staging A.  role 0: none.
+constexpr int kFlowPad = 64;  // words between two slices' counters (each on 256 B of its own)
+struct Flow {
+  int* ready;          // [slices] producer tickets (re-armed by the slice's last consumer)
+  int* done;           // [slices] consumers past the wait
+  int* err;            // sticky: a wait timed out (results invalid, the grid still drains)
+  int need;            // producer workgroups per slice
+  int consumers;       // consumer workgroups per slice
+  int cols_per_slice;  // producer output columns per slice (= the consumer's K / S)
+  int role;            // 1 producer, 2 consumer
+};
+
+// The hand-off needs no fence (guide, "Hand-offs measured with sc1 loads", first row): the
+// producer's output stores are write-through (sc1), every wave drains them (vmcnt(0)) before ONE
+// lane takes the ticket; the consumer's single polling lane matches, the workgroup joins it at a
+// barrier, and every load of the handed-off bytes is an sc1 load.  (Plain stores + release /
+// acquire fences -- an L2 write-back per producer and an L2 invalidate per consumer -- cost
+// 7-8 us per layer, tools/gpu/mlp_ab.sh.)
+__device__ __forceinline__ void flow_signal(const Flow& fl, int slice) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(fl.ready + kFlowPad * slice, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Consumer: one lane polls the slice's tickets (relaxed agent-scope loads + s_sleep, bounded:
+// a lost producer sets the sticky error word and the grid still drains) and the workgroup joins
+// it at a barrier.  The slice's last consumer re-arms both counters, so a graph replay starts
+// from zero without a memset.
+__device__ __forceinline__ void flow_wait(const Flow& fl, int slice) {
+  if (threadIdx.x == 0) {
+    int spins = 0;
+    while (__hip_atomic_load(fl.ready + kFlowPad * slice, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fl.need) {
+      __builtin_amdgcn_s_sleep(16);  // ~0.5 us between polls: pollers must not load the memory channel of the line
+      if (++spins > (1 << 20)) {
+        __hip_atomic_store(fl.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    if (__hip_atomic_fetch_add(fl.done + kFlowPad * slice, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        fl.consumers - 1) {
+      __hip_atomic_store(fl.ready + kFlowPad * slice, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(fl.done + kFlowPad * slice, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+}
+
+template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2, int FL = 0>
+__device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_in, const int by, const int gdx,
+                                            SkinnyLds<MT>& L, const Flow& fl) {
   constexpr int kR = KR;
-  constexpr int kKA = MT > 4 ? 128 : kKC;  // k per staged A tile
+  constexpr int kKA = SkinnyLds<MT>::kKA;  // k per staged A tile
   constexpr int kPPR = kKA / 8;             // 16-byte pieces per A row
-  __shared__ __attribute__((aligned(16))) bf16_t a_lds[2][16 * MT][kKA + 8];
-  __shared__ float rinv_s[MT > 4 ? 16 * MT : 64];
-#if PK_LAB_LDS_PAD
-  __shared__ char lab_pad[PK_LAB_LDS_PAD];  // timing only: force one workgroup per CU
-  if (args.M < 0) lab_pad[threadIdx.x] = 1;
-#endif
-  __shared__ int last_s;
+  auto& a_lds = L.a;
+  auto& rinv_s = L.rinv;
+  int& last_s = L.last;
   const int N = args.N, K = args.K, S = args.S;
-  // rows of this workgroup's group: all rows, or (grouped) expert blockIdx.y's
+  // rows of this workgroup's group: all rows, or (grouped) expert by's
   int gbeg = 0, gend = args.M;
   const bf16_t* Wg = args.W;
   if (args.row_offsets != nullptr) {
-    gbeg = args.row_offsets[blockIdx.y];
-    gend = args.row_offsets[blockIdx.y + 1];
-    Wg += static_cast<int64_t>(blockIdx.y) * args.w_stride;
+    gbeg = args.row_offsets[by];
+    gend = args.row_offsets[by + 1];
+    Wg += static_cast<int64_t>(by) * args.w_stride;
   }
   // Row tiles (a group of more than 64 rows): every (n-block, split) tile runs once per 16*MT-row
   // tile.  The RT workgroups of one W tile are given consecutive dispatch slots of ONE XCD
   // (workgroups go round-robin over the 8 XCDs), so they stream the same W bytes at the same
   // time through that XCD's L2 and HBM sees each weight byte about once.
-  int bx = blockIdx.x, rt = 0;
+  int bx = bx_in, rt = 0;
   if (args.row_tiles > 1) {
-    const int RT = args.row_tiles, T = gridDim.x / RT;
+    const int RT = args.row_tiles, T = gdx / RT;
     if ((T & 7) == 0) {
       const int q = bx >> 3;
       rt = q % RT;
@@ -365,7 +422,12 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) {
       const int col = ((tid + 256 * p) % kPPR) * 8;
-      stage[p] = *reinterpret_cast<const u32x4*>(arow[p] + kc + col);
+      if constexpr (FL == 2)  // the producers' output, handed off in-launch: sc1 loads
+        stage[p] = __builtin_amdgcn_raw_buffer_load_b128(
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(args.A), static_cast<short>(0), 0x7ffffff0, 0x00020000),
+            static_cast<int>((arow[p] + kc + col - args.A) * 2), 0, 16);
+      else
+        stage[p] = *reinterpret_cast<const u32x4*>(arow[p] + kc + col);
       if constexpr (NORM) stage_w[p] = *reinterpret_cast<const u32x4*>(args.nrm_w + kc + col);
     }
   };
@@ -484,9 +546,18 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
       }
     }
   } else {
-  load_a(ck(0));
-  load_w(wa, ck(0));
-  load_w(wb, ck(0) + 128);
+  if constexpr (FL == 2) {
+    // consumer: this workgroup's first two weight k-steps are requested before the wait, so
+    // they stream in while the producers finish; A (the producers' output) is read after it
+    load_w(wa, ck(0));
+    load_w(wb, ck(0) + 128);
+    flow_wait(fl, split);
+    load_a(ck(0));
+  } else {
+    load_a(ck(0));
+    load_w(wa, ck(0));
+    load_w(wb, ck(0) + 128);
+  }
   store_a(0);
   int buf = 0;
   for (int c = 0; c < nchunks; ++c) {
@@ -583,8 +654,17 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
       uint2 v;
       v.x = pack2(y[0], y[1]);
       v.y = pack2(y[2], y[3]);
-      *reinterpret_cast<uint2*>(o) = v;
+      if constexpr (FL == 1) {  // handed off in-launch: write-through (sc1) stores
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(args.out, static_cast<short>(0), 0x7ffffff0, 0x00020000);
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{v.x, v.y}, rsrc, static_cast<int>((o - args.out) * 2), 0, 16);
+      } else {
+        *reinterpret_cast<uint2*>(o) = v;
+      }
     }
+  }
+  if constexpr (MODE == kSiluMul) {
+    if constexpr (FL == 1) flow_signal(fl, (nb * 64 * kR / 2) / fl.cols_per_slice);
   }
   if constexpr (MODE == kAddResNorm || MODE == kQkvRope) {
     // ---- in-launch split-K reduction by the last split of this n-block to arrive
@@ -617,6 +697,36 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
       default: epilogue<MODE, 0, KR>(args, nb); break;
     }
   }
+}
+
+template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2>
+__global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args) {
+  __shared__ SkinnyLds<MT> lds;
+#if PK_LAB_LDS_PAD
+  __shared__ char lab_pad[PK_LAB_LDS_PAD];  // timing only: force one workgroup per CU
+  if (args.M < 0) lab_pad[threadIdx.x] = 1;
+#endif
+  skinny_tile<MT, MODE, PK, NORM, NT, RS, KR>(args, blockIdx.x, blockIdx.y, gridDim.x, lds, Flow{});
+}
+
+// Fused decode MLP (M <= 64): gate_up + SiLU (folded norm, non-temporal packed W) and the down
+// projection's split-K slabs in ONE launch of max(gate_up tiles, down tiles) workgroups, one per
+// CU: workgroup b runs gate_up tile b (if any), then down tile b (if any).  A down tile streams
+// its first weight k-steps, then waits until the gate_up tiles of its K slice have stored h, so
+// the down projection's launch boundary and weight ramp overlap the gate_up tail.  Every
+// workgroup is resident at once (one per CU) and a gate_up tile never waits: no deadlock.
+// (A/B, tools/gpu/mlp_ab.sh: down tiles as workgroups of their own, dispatched after the gate_up
+// ones, put two down tiles on some CUs and lost 7 us per layer.)
+template <int MT>
+__global__ void __launch_bounds__(256, 2) mlp_fused_kernel(const GemmArgs gu, const GemmArgs dn, const Flow fgu,
+                                                           const Flow fdn, int n_gu, int n_dn) {
+  __shared__ SkinnyLds<MT> lds;
+  const int b = blockIdx.x;
+  if (b < n_gu) {
+    skinny_tile<MT, kSiluMul, true, false, true, true, 2, 1>(gu, b, 0, n_gu, lds, fgu);
+    __syncthreads();  // the LDS tiles are reused by the down tile
+  }
+  if (b < n_dn) skinny_tile<MT, kPartial, true, false, false, false, 2, 2>(dn, b, 0, n_dn, lds, fdn);
 }
 
 // x[m] = bf16(bf16(residual[m] * rinv[m]) * w), rinv from the per-row sum-of-squares parts a
@@ -1066,6 +1176,38 @@ PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void
 // Full-featured entry: modes 0-4 (see Mode), bit 4 packed W, bit 5 RMSNorm prologue, bit 6 NT W.
 PK_EXPORT int pk_skinny_gemm_ex(const GemmArgs* args, int mode, hipStream_t stream) {
   return dispatch(*args, mode, stream);
+}
+
+// Fused decode MLP (mlp_fused_kernel): gu = gate_up + SiLU (packed, non-temporal, folded norm:
+// row_scale + nrm_parts), dn = down split-K slabs (packed) reading gu's output.  flow: a zeroed
+// int buffer of >= 128 * 64 + 1 words (64 tickets and 64 consumer counts, 64 words apart, then
+// the sticky error word),
+// left zeroed by every launch that completes.
+PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, hipStream_t stream) {
+  GemmArgs gu = *gu_in, dn = *dn_in;
+  if (gu.M <= 0) return 0;
+  if (gu.M > 64 || dn.M != gu.M || gu.N % 128 || gu.K % kKC || !gu.row_scale || gu.nrm_parts == nullptr ||
+      gu.nrm_nparts < 1 || gu.nrm_nparts > 64 || gu.out == nullptr || dn.K != gu.N / 2 || dn.N % 128 || dn.S < 1 ||
+      dn.S > 64 || dn.K % (kKC * dn.S) || (dn.K / dn.S) % 64 || dn.partial == nullptr || dn.A != gu.out ||
+      dn.lda % 8 || gu.lda % 8 || gu.row_offsets != nullptr || dn.row_offsets != nullptr || flow == nullptr)
+    return -1;
+  gu.S = 1;
+  gu.row_tiles = dn.row_tiles = 1;
+  gu.tile_rows = dn.tile_rows = 64;
+  gu.max_group_rows = dn.max_group_rows = 0;
+  int* done = flow + 64 * kFlowPad;
+  int* err = flow + 128 * kFlowPad;
+  Flow fgu{flow, done, err, 0, 0, dn.K / dn.S, 1};
+  Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / 128, dn.K / dn.S, 2};
+  const int n_gu = gu.N / 128, n_dn = (dn.N / 128) * dn.S;
+  const dim3 grid(n_gu > n_dn ? n_gu : n_dn);
+  switch ((gu.M + 15) / 16) {
+    case 1: mlp_fused_kernel<1><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+    case 2: mlp_fused_kernel<2><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+    case 3: mlp_fused_kernel<3><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+    default: mlp_fused_kernel<4><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+  }
+  return PK_CHECK_LAUNCH();
 }
 
 PK_EXPORT int pk_norm_apply(void* x, const void* residual, const void* parts, int nparts, const void* w, int M,

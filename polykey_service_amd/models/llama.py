@@ -454,6 +454,15 @@ class LlamaForCausalLM(nn.Module):
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
             parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True), residual, buf2)
+            if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p):
+                # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
+                d = gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, gemm.RowScale(parts, layer.eps), ws,
+                                   self._flow)
+                if i < last:
+                    parts = gemm.residual_parts(d, residual, buf)
+                else:
+                    x, _ = gemm.partial_add_rms_norm(d, residual, self.norm, self.cfg.rms_eps)
+                continue
             if T > GATE_UP_SKINNY_MAX_M and not mlp.gate_up.is_meta:
                 # hipBLASLt's MFMA GEMM wins on the 235 MB gate_up above 384 rows (95 vs 149 us at
                 # 512, profiles/r3_decode_rows.txt) even with the norm and SiLU as separate kernels
@@ -504,6 +513,8 @@ class LlamaForCausalLM(nn.Module):
             return None
         if getattr(self, "_ws", None) is None:
             self._ws = torch.empty(self._workspace_elems(), dtype=torch.float32, device=self.device)
+            # hand-off tickets of the fused decode MLP launch (gemm.mlp_fused), left zeroed by every launch
+            self._flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
         return self._ws
 
     def _workspace_elems(self) -> int:

@@ -34,6 +34,8 @@ _KCHUNK = 256
 # The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see
 # tools/bench_gemm.py and profiles/); POLYKEY_SKINNY_GEMM=0/1 forces it off/on.
 SKINNY_ENABLED = os.environ.get("POLYKEY_SKINNY_GEMM", "1") == "1"
+# decode MLP as one launch (gate_up -> down hand-off in-kernel, mlp_fused); 0: two launches
+MLP_FUSED = os.environ.get("POLYKEY_MLP_FUSED", "1") == "1"
 PACKED_BIT = 16
 
 
@@ -54,7 +56,7 @@ class GemmArgs(ctypes.Structure):
                 ("nkv", ctypes.c_int), ("bs", ctypes.c_int), ("row_offsets", ctypes.c_void_p),
                 ("w_stride", ctypes.c_longlong), ("groups", ctypes.c_int), ("max_group_rows", ctypes.c_int),
                 ("a_rows", ctypes.c_void_p), ("a_row_div", ctypes.c_int), ("row_scale", ctypes.c_int),
-                ("row_tiles", ctypes.c_int)]
+                ("row_tiles", ctypes.c_int), ("tile_rows", ctypes.c_int)]
 
 
 _ARGS_CHECKED = False
@@ -357,6 +359,46 @@ def linear_partial_rowscale(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, 
             S = max(1, S // 2)
     assert ws.numel() >= S * M * N, "split-K workspace too small"
     _launch_ex(MODE_PARTIAL | (HALF_BIT if half else 0), x, w, packed, S, ws=ws, rowscale=rowscale)
+    return Partial(ws, S, M, N)
+
+
+FLOW_WORDS = 128 * 64 + 1  # pk_mlp_fused hand-off buffer: 64 tickets + 64 consumer counts (256 B apart), error word
+
+
+def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_packed: Optional[torch.Tensor]) -> bool:
+    """Shapes the fused decode MLP launch (:func:`mlp_fused`) takes."""
+    if gate_up_packed is None or down_packed is None or not x.is_cuda or not MLP_FUSED:
+        return False
+    M, K = x.shape
+    N2, I = gate_up_packed.shape[0], down_packed.shape[1]
+    S = choose_split(down_packed.shape[0], I, M)
+    return (0 < M <= SKINNY_MAX_M and N2 == 2 * I and N2 % 128 == 0 and K % _KCHUNK == 0
+            and down_packed.shape[0] % 128 == 0 and I % (_KCHUNK * S) == 0 and (I // S) % 64 == 0 and S <= 64
+            and gate_up_packed.shape[1] == K)
+
+
+def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: RowScale,
+              ws: torch.Tensor, flow: torch.Tensor) -> Partial:
+    """Decode MLP in ONE launch (csrc/kernels/gemm_skinny.hip mlp_fused_kernel):
+    h = silu/mul of rinv * (x @ Wgu'^T) (folded norm, interleaved packed gate/up), then the down
+    projection's fp32 split-K slabs of h @ Wd^T in ``ws``.  Down workgroups stream their first
+    weight k-steps while gate_up finishes and wait on per-K-slice tickets in ``flow`` (int32,
+    >= :data:`FLOW_WORDS`, zeroed once; every launch leaves it zeroed).  Returns the slabs."""
+    M, K = x.shape
+    N2, I = gate_up_packed.shape[0], down_packed.shape[1]
+    N = down_packed.shape[0]
+    S = choose_split(N, I, M)
+    assert ws.numel() >= S * M * N and flow.numel() >= FLOW_WORDS and flow.dtype == torch.int32
+    h = torch.empty((M, I), dtype=x.dtype, device=x.device)
+    gu = GemmArgs()
+    gu.out, gu.A, gu.W = h.data_ptr(), x.data_ptr(), gate_up_packed.data_ptr()
+    gu.M, gu.N, gu.K, gu.lda, gu.ldo, gu.S = M, N2, K, x.stride(0), h.stride(0), 1
+    gu.row_scale, gu.nrm_parts, gu.nrm_nparts, gu.eps = 1, rowscale.parts.data_ptr(), rowscale.parts.shape[0], \
+        float(rowscale.eps)
+    dn = GemmArgs()
+    dn.partial, dn.A, dn.W = ws.data_ptr(), h.data_ptr(), down_packed.data_ptr()
+    dn.M, dn.N, dn.K, dn.lda, dn.ldo, dn.S = M, N, I, h.stride(0), N, S
+    native.call("pk_mlp_fused", ctypes.byref(gu), ctypes.byref(dn), flow.data_ptr(), native.stream_ptr())
     return Partial(ws, S, M, N)
 
 

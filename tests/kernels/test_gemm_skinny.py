@@ -309,6 +309,50 @@ def test_rowscale_half_blocks(M):
     torch.testing.assert_close(a.view().sum(0), b.view().sum(0), atol=2e-3, rtol=2e-3)
 
 
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("H,I", [(4096, 14336), (1024, 4096)])
+def test_mlp_fused_matches_two_launches(M, H, I):
+    """Fused decode MLP (gate_up + SiLU -> in-launch hand-off -> down slabs, one launch) is
+    bit-identical to the two launches it replaces, on repeated launches (the hand-off tickets
+    re-arm themselves), and never trips the wait timeout."""
+    res = rnd(M, H)
+    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wgu = gemm.interleave_gate_up(rnd(I, H, scale=0.05), rnd(I, H, scale=0.05))
+    gup = gemm.pack_weight(gemm.fold_norm(wgu, nw))
+    wd = rnd(H, I, scale=0.02)
+    dp = gemm.pack_weight(wd)
+    assert gemm.mlp_fused_ok(res, gup, dp)
+    parts = gemm.residual_parts(None, res.clone(), torch.empty(8 * 64, device="cuda"))
+    rs = gemm.RowScale(parts, 1e-5)
+    S = gemm.choose_split(H, I, M)
+    ws0 = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
+    h = gemm.linear_silu(res, wgu, packed=gup, rowscale=rs)
+    ref_slabs = gemm.linear_partial(h, wd, ws0, packed=dp).view().clone()
+    flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda")
+    ws = torch.empty_like(ws0)
+    for _ in range(4):
+        ws.fill_(float("nan"))
+        p = gemm.mlp_fused(res, gup, dp, rs, ws, flow)
+        assert p.S == S
+        torch.testing.assert_close(p.view(), ref_slabs, atol=0, rtol=0)
+    # against the fp32 reference of the whole MLP
+    rinv = torch.rsqrt(res.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    hx = ref.silu_and_mul_interleaved(((res.float() @ gemm.fold_norm(wgu, nw).float().t()) * rinv).to(torch.bfloat16))
+    exp = hx.float() @ wd.float().t()
+    torch.testing.assert_close(p.view().sum(0), exp, atol=3e-2, rtol=3e-2)
+    # new inputs every launch: a consumer reading a stale copy of the previous launch's h would show
+    for it in range(6):
+        r2 = rnd(M, H)
+        p2 = gemm.residual_parts(None, r2.clone(), torch.empty(8 * 64, device="cuda"))
+        rs2 = gemm.RowScale(p2, 1e-5)
+        h2 = gemm.linear_silu(r2, wgu, packed=gup, rowscale=rs2)
+        exp2 = gemm.linear_partial(h2, wd, ws0, packed=dp).view().clone()
+        got = gemm.mlp_fused(r2, gup, dp, rs2, ws, flow).view()
+        torch.testing.assert_close(got, exp2, atol=0, rtol=0)
+    torch.cuda.synchronize()
+    assert int(flow.abs().sum()) == 0, flow.tolist()
+
+
 @pytest.mark.parametrize("M", [65, 128, 200, 512])
 def test_row_tiles_above_64(M):
     """Decode batches above 64 rows: 128-row tiles of M per W tile (grid x row tiles, XCD-grouped),
