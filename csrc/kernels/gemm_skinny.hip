@@ -123,16 +123,27 @@ __device__ __forceinline__ float rbf(float x) { return bf2f(f2bf(x)); }
 // Sum of the SS fp32 slabs of element group (m, c..c+3) / (m, c+64..c+67); SS == 0: runtime S.
 // The loads of a batch of rows are all issued before any add, so one reducer thread has
 // RB * SS 16-byte loads in flight instead of paying the slab latency serially.
-template <int SS>
-__device__ __forceinline__ float4 slab_sum(const float* src, int64_t slab, int S) {
+// sc1 (coherent past the XCD L2) 16-byte load of p, inside the buffer that starts at base (< 2 GiB)
+__device__ __forceinline__ float4 ld4f_sc1(const float* base, const float* p) {
+  const auto r = __builtin_amdgcn_raw_buffer_load_b128(
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), static_cast<short>(0), 0x7ffffff0, 0x00020000),
+      static_cast<int>((p - base) * 4), 0, 16);
+  return __builtin_bit_cast(float4, r);
+}
+
+// SC1: the slabs were handed over in-launch by write-through stores: read them with sc1 loads
+// (no acquire fence, i.e. no L2 invalidate; guide "Hand-offs measured with sc1 loads")
+template <int SS, bool SC1 = false>
+__device__ __forceinline__ float4 slab_sum(const float* src, int64_t slab, int S, const float* base = nullptr) {
+  auto ld = [&](const float* p) { return SC1 ? ld4f_sc1(base, p) : ld4f(p); };
   if constexpr (SS == 0) {
-    float4 a = ld4f(src);
-    for (int s = 1; s < S; ++s) add4(a, ld4f(src + s * slab));
+    float4 a = ld(src);
+    for (int s = 1; s < S; ++s) add4(a, ld(src + s * slab));
     return a;
   } else {
     float4 v[SS];
 #pragma unroll
-    for (int s = 0; s < SS; ++s) v[s] = ld4f(src + s * slab);
+    for (int s = 0; s < SS; ++s) v[s] = ld(src + s * slab);
 #pragma unroll
     for (int s = 1; s < SS; ++s) add4(v[0], v[s]);
     return v[0];
@@ -155,7 +166,7 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
         const int m = min(m0 + RPP * i, M - 1);
-        a[i] = slab_sum<SS>(args.partial + static_cast<int64_t>(m) * N + c, slab, S);
+        a[i] = slab_sum<SS, true>(args.partial + static_cast<int64_t>(m) * N + c, slab, S, args.partial);
       }
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
@@ -680,7 +691,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
         last = t == S - 1;
         if (last) __hip_atomic_store(args.counters + nb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (last) {
+      if (last && !kSlabSc1) {  // write-through slabs are read back with sc1 loads: no acquire
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
