@@ -454,7 +454,7 @@ class LlamaForCausalLM(nn.Module):
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
             parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True), residual, buf2)
-            if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p):
+            if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p) and not self.st.shared_device:
                 # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
                 d = gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, gemm.RowScale(parts, layer.eps), ws,
                                    self._flow)

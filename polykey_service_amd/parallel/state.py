@@ -51,6 +51,10 @@ class ParallelState:
     ep_step_rows: int = 1 << 30            # largest token count of the current lockstep step (vote)
     backend: str = "none"
     device: torch.device = dataclasses.field(default_factory=lambda: torch.device("cpu"))
+    # several local ranks on one GPU (rehearsals): kernels whose workgroups wait on each other
+    # in-launch (gemm.mlp_fused) assume the whole grid is resident, which another process's
+    # waiting grid can prevent -- they are not used then
+    shared_device: bool = False
 
     @property
     def is_tp_leader(self) -> bool:
@@ -110,7 +114,8 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
                          "with tp=1 (DP attention + expert all-to-all)")
     st = ParallelState(world_size=world, rank=rank, local_rank=local, tp_size=tp, tp_rank=rank % tp,
                        dp_size=world // tp, dp_rank=rank // tp, ep_size=ep,
-                       ep_rank=rank if dp_attn else ((rank % tp) if ep > 1 else 0), device=dev)
+                       ep_rank=rank if dp_attn else ((rank % tp) if ep > 1 else 0), device=dev,
+                       shared_device=dev.type == "cuda" and int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > max(n_dev, 1))
     if world > 1:
         # POLYKEY_DIST_BACKEND overrides (gloo: several ranks on one GPU, which RCCL refuses)
         be = pick_backend(dev.type, n_dev, int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
