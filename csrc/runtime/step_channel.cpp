@@ -1,5 +1,6 @@
 // Step channel implementation + pybind11 face (see step_channel.h).
 #include "runtime/step_channel.h"
+#include "runtime/proc.h"
 
 #include <errno.h>
 #include <fcntl.h>
@@ -10,6 +11,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -52,9 +54,7 @@ class Backoff {
   uint64_t n_ = 0;
 };
 
-// A process exists (same node: every rank of a TP group shares the host).  EPERM means it
-// exists but belongs to another user.
-bool pid_alive(int32_t pid) { return pid <= 0 || kill(pid, 0) == 0 || errno != ESRCH; }
+
 }  // namespace
 
 StepChannelCore::StepChannelCore(const std::string& name, bool create, int nslots, int nconsumers,

@@ -10,6 +10,7 @@
 // liveness probe of the peers' pids, so a dead rank fails the vote instead of hanging it.
 // Fields are double-buffered by step parity: a rank can be at most one vote ahead (its next vote
 // waits for mine), so it never overwrites the parity I am still reading.
+#include "runtime/proc.h"
 #include <errno.h>
 #include <fcntl.h>
 #include <immintrin.h>
@@ -123,7 +124,7 @@ class VoteBoard {
           if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
             throw std::runtime_error("vote board: rank " + std::to_string(r) + " did not vote within the timeout");
           const int32_t pid = o.pid;
-          if (pid > 0 && kill(pid, 0) != 0 && errno == ESRCH)
+          if (pid > 0 && !pk::pid_alive(pid))
             throw std::runtime_error("vote board: rank " + std::to_string(r) + " died");
         }
         std::this_thread::sleep_for(std::chrono::microseconds(10));
