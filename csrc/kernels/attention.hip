@@ -23,192 +23,11 @@
 // workgroup that read the same K/V tile hit the CU's L1.
 // Decode splits long contexts into partitions of kPart keys (flash-decoding) and merges them
 // in a second kernel; sequences that fit one partition are finished in place.
-#include "common.h"
+#include "attn_decode.h"
 
 using namespace pk;
 
 namespace {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
-constexpr int kHD = 128;
-constexpr int kStep = 32;
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kNegBig = -1e30f;
-constexpr int kDecodeWaves = 4;  // waves per (seq, kv head, partition); 8 measured ~10 % slower at 384 keys
-int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
-
-__device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
-// K/V stream loads: plain (non-temporal measured slower: in-situ decode step 4.43 vs 4.45 ms,
-// tools/ab_decode.py)
-__device__ __forceinline__ bf16x8_t ldkv(const bf16_t* p) { return ld8(p); }
-
-__device__ __forceinline__ bf16x8_t zero8() {
-  u32x4 z = {0u, 0u, 0u, 0u};
-  return __builtin_bit_cast(bf16x8_t, z);
-}
-
-__device__ __forceinline__ bf16x8_t pack_p(const float* p) {
-  u32x4 v;
-  v[0] = pack2(p[0], p[1]);
-  v[1] = pack2(p[2], p[3]);
-  v[2] = pack2(p[4], p[5]);
-  v[3] = pack2(p[6], p[7]);
-  return __builtin_bit_cast(bf16x8_t, v);
-}
-
-// Reductions over the 4 lane groups of a column (lanes r, r+16, r+32, r+48) with the gfx950
-// VALU lane swaps (v_permlane16/32_swap: rows 1<->0 / 3<->2, then halves) instead of
-// ds_bpermute round trips through the LDS crossbar (__shfl_xor): max(x, swapped x) and
-// x + swapped x are already the pairwise results in every lane (prefill attention 1-4 % faster,
-// profiles/r2_prefill_attention.txt).
-__device__ __forceinline__ float col_max(float x) {
-  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
-}
-
-// Total exp-sum of the lane's column (reduce the 4 lane groups).
-__device__ __forceinline__ float col_sum(float l) {
-  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(l), __float_as_uint(l), false, false);
-  l = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
-  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-}
-
-struct WaveState {
-  float m;        // running max (base-2 scaled) of this lane's column
-  float l;        // partial exp-sum of this lane's 8 keys per step (summed over lane groups at the end)
-  f32x4 o[8];     // O^T: o[dt][i] = O[col = lane&15][d = 16*dt + 4*g + i]
-};
-
-// K/V fragments of one 32-key step (16 B per lane each): K as the A operand of S^T = K Q^T
-// (2 key tiles x 4 head-dim k-steps), V^T as the A operand of O^T += V^T P^T (8 d-tiles).
-struct KVFrag {
-  bf16x8_t k[2][4];
-  bf16x8_t v[8];
-};
-
-// bt[i - bt_base] = physical block of logical block i; `lim` bounds the tokens a load may touch
-// (past it the address is clamped, the data never used), so the block lookups stay inside the
-// caller's block-table window.  K comes from the fragment-native cache tile of step s (common.h
-// kcache_off: one contiguous KiB per load instruction); V likewise (common.h vcache_off): lane
-// (r, g) reads keys 8g..8g+7 of channel 16 dt + r, one contiguous KiB per d-tile (ldkv: plain loads).
-__device__ __forceinline__ void load_kv(KVFrag& f, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-                                        int64_t blk_stride, const int* __restrict__ bt, int bt_base, int bs, int s,
-                                        int lim) {
-  const int lane = threadIdx.x & 63;
-  const int r = lane & 15, g = lane >> 4;
-  const int ks = min(s, lim - 1) & ~31;  // the step's 32-key tile (clamped past the end)
-  const bf16_t* kt = kc + bt[ks / bs - bt_base] * blk_stride + (ks % bs) * kHD + 8 * lane;
-  PK_DEVICE_ASSERT(bt[ks / bs - bt_base] >= 0);
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) f.k[t][kk] = ldkv(kt + (t * 4 + kk) * 512);
-  int tok0 = s + 8 * g;
-  tok0 = min(tok0, ((lim - 1) >> 3) << 3);
-  const int blk = bt[tok0 / bs - bt_base];
-  const bf16_t* p = vc + blk * blk_stride + vcache_off(tok0 % bs, r);  // + 512 per 16-channel tile
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) f.v[dt] = ldkv(p + dt * 512);
-}
-
-__device__ __forceinline__ void attend_step(WaveState& st, const bf16x8_t (&qf)[4], const KVFrag& f, int s,
-                                            int n_valid, int col_limit, float scale2) {
-  const int g = (threadIdx.x & 63) >> 4;
-  // ---- S^T = K . Q^T
-  f32x4 acc[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.k[t][kk], qf[kk], acc[t], 0, 0, 0);
-  }
-  // ---- online softmax over this step's 32 keys (8 per lane)
-  float sv[8];
-  float mx = kNegBig;
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = s + 8 * g + 4 * t + i;
-      const bool ok = key < n_valid && key <= col_limit;
-      const float v = ok ? acc[t][i] * scale2 : -INFINITY;
-      sv[4 * t + i] = v;
-      mx = fmaxf(mx, v);
-    }
-  mx = col_max(mx);
-  const float m_new = fmaxf(st.m, mx);
-  const float alpha = exp2f(st.m - m_new);
-  st.m = m_new;
-  float p[8];
-  float psum = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    p[i] = exp2f(sv[i] - m_new);
-    psum += p[i];
-  }
-  st.l = st.l * alpha + psum;
-  const bf16x8_t pb = pack_p(p);
-  // ---- O^T += V^T . P^T
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) {
-    st.o[dt] *= alpha;
-    st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.v[dt], pb, st.o[dt], 0, 0, 0);
-  }
-}
-
-// Process keys [k_begin, k_end) in 32-key steps (k_begin multiple of 32), stride `k_stride`
-// between this wave's steps.  Keys >= n_valid or > col_limit are masked.  Software-pipelined
-// over two fragment sets: the next step's K/V loads are in flight while this step computes
-// (loads past the end are clamped to valid addresses and never consumed).
-__device__ __forceinline__ void attend(WaveState& st, const bf16x8_t (&qf)[4], const bf16_t* __restrict__ kc,
-                                       const bf16_t* __restrict__ vc, int64_t blk_stride, const int* __restrict__ bt,
-                                       int bt_base, int bs, int k_begin, int k_end, int k_stride, int n_valid,
-                                       int col_limit, float scale2, KVFrag& fa, bool fa_loaded = false) {
-  if (k_begin >= k_end) return;
-  const int lim = min(n_valid, k_end);
-  KVFrag fb;
-  if (!fa_loaded) load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, k_begin, lim);
-  for (int s = k_begin; s < k_end; s += 2 * k_stride) {
-    load_kv(fb, kc, vc, blk_stride, bt, bt_base, bs, s + k_stride, lim);
-    attend_step(st, qf, fa, s, n_valid, col_limit, scale2);
-    if (s + k_stride >= k_end) break;
-    load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, s + 2 * k_stride, lim);
-    attend_step(st, qf, fb, s + k_stride, n_valid, col_limit, scale2);
-  }
-}
-
-__device__ __forceinline__ void init_state(WaveState& st) {
-  st.m = kNegBig;
-  st.l = 0.f;
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-}
-
-__device__ __forceinline__ void load_q(bf16x8_t (&qf)[4], const bf16_t* q, bool valid) {
-  const int g = (threadIdx.x & 63) >> 4;
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) qf[kk] = valid ? ld8(q + 32 * g + 8 * kk) : zero8();
-}
-
-
-
-// ------------------------------------------------------------------------------ decode
-// grid (n_kv, n_seqs, min(n_parts, z)), block 64*NW (NW waves).  LDS: NW waves x 16 cols x 128 d fp32.
-// Decode attention fed straight from the QKV projection's split-K slabs (FROM_QKV): the
-// workgroup of (seq, kv head h) sums the S fp32 slabs of its G query heads and of k/v head h,
-// rounds to bf16 (the unfused GEMM output), applies RoPE, keeps q in LDS, and — the workgroup
-// that owns the partition holding the new token — writes k / v into the paged cache before
-// attending.  Replaces the separate QKV-reduce + RoPE + cache-write kernel of a decode layer.
-struct QkvIn {
-  const float* partial;    // [S, M, (n_q + 2 n_kv) * 128]
-  const int* positions;    // [M]
-  const float* cos_sin;    // [max_pos, 128] = cos[64] | sin[64]
-  const int* slots;        // [M], < 0: nothing cached
-  int S, M;
-};
 
 template <int kPart, int NW, bool FROM_QKV, int SS = 0>
 __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
@@ -216,272 +35,10 @@ __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
     float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int n_q, int n_kv, int bs,
     int max_blocks, int q_stride, int out_stride, int n_parts, float scale2, const QkvIn qi) {
-  __shared__ float o_lds[NW][16][kHD + 4];
-  __shared__ float ml_lds[NW][16][2];
-  __shared__ int last;
-  __shared__ int bt_s[kPart / 8 + 2];  // this partition's block-table window (LDS: lookups use lgkmcnt)
-  // FROM_QKV, new token folded in (see below): its rotated k, its v and its G scores
-  __shared__ __attribute__((aligned(16))) bf16_t kn_s[kHD];
-  __shared__ float vn_s[kHD];
-  __shared__ float sn_s[16];
-  static_assert(64 * NW >= 256, "the new-token scores use 16 lanes per query head, G <= 16");
-  const int h = blockIdx.x, seq = blockIdx.y;
-  // the first partition's block-table window, requested before anything else so its round
-  // trip overlaps the context / q preparation instead of following it (entries past the
-  // sequence's blocks are in-bounds of the row and never used)
-  const int pre_b0 = static_cast<int>(blockIdx.z) * (kPart / bs);
-  int bt_pre = 0;
-  if (static_cast<int>(threadIdx.x) <= kPart / bs && pre_b0 + static_cast<int>(threadIdx.x) < max_blocks)
-    bt_pre = block_tables[static_cast<int64_t>(seq) * max_blocks + pre_b0 + threadIdx.x];
-  const int ctx = context_lens[seq];
-  const int G = n_q / n_kv;
-  if (ctx <= 0) {
-    if (blockIdx.z == 0)  // a padded (graph) row -> zeros
-      for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW)
-        out[static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD] = 0;
-    return;
-  }
-  // n_parts comes from the launch's context bound; the clamp keeps a violated bound in-bounds
-  const int n_used = min((ctx + kPart - 1) / kPart, n_parts);
-  PK_DEVICE_ASSERT(ctx <= n_parts * kPart);
-  if (static_cast<int>(blockIdx.z) >= n_used) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
-  const bf16_t* kch = kc + static_cast<int64_t>(h) * bs * kHD;
-  const bf16_t* vch = vc + static_cast<int64_t>(h) * kHD * bs;
-  // (prefetching the first K/V step across the q preparation below was measured: it pushes
-  // the kernel to 256 VGPRs + AGPRs, one wave per SIMD, and is slower overall)
-  bf16x8_t qf[4];
-  // fold: the workgroup holding the new token (key ctx - 1) keeps its k / v in LDS, attends to
-  // keys [0, ctx - 1) from the cache and adds key ctx - 1 from LDS in the final combine; the
-  // cache write goes out at the end of the kernel.  Writing the row first and reading it back
-  // through the cache cost 4-5 us per launch at 384-512 keys (the scattered 2-byte V^T stores
-  // and the K tile stores land on lines the waves are about to stream).
-  bool fold = false;
-  int slot = -1;
-  if constexpr (FROM_QKV) {
-    __shared__ __attribute__((aligned(16))) bf16_t q_s[16][kHD];
-    const int N = (n_q + 2 * n_kv) * kHD;
-    const int64_t slab = static_cast<int64_t>(qi.M) * N;
-    const float* base = qi.partial + static_cast<int64_t>(seq) * N;
-    const float* cs = qi.cos_sin + static_cast<int64_t>(qi.positions[seq]) * kHD;
-    slot = qi.slots[seq];
-    const bool writer = slot >= 0 && static_cast<int>(blockIdx.z) == (n_used - 1) % static_cast<int>(gridDim.z);
-    fold = writer && qi.positions[seq] == ctx - 1;
-    const int n_items = G * 64 + (writer ? 128 : 0);
-    for (int it = threadIdx.x; it < n_items; it += 64 * NW) {
-      int col, j;
-      if (it < G * 64) {
-        j = it & 63;
-        col = (h * G + (it >> 6)) * kHD + j;
-      } else if (it < G * 64 + 64) {
-        j = it - G * 64;
-        col = (n_q + h) * kHD + j;
-      } else {
-        j = it - G * 64 - 64;
-        col = (n_q + n_kv + h) * kHD + j;
-      }
-      float a = 0.f, b = 0.f;
-      if constexpr (SS > 0) {  // all slab loads in flight before the first add
-        float va[SS], vb[SS];
-#pragma unroll
-        for (int sp = 0; sp < SS; ++sp) {
-          va[sp] = base[sp * slab + col];
-          vb[sp] = base[sp * slab + col + 64];
-        }
-#pragma unroll
-        for (int sp = 0; sp < SS; ++sp) {
-          a += va[sp];
-          b += vb[sp];
-        }
-      } else {
-        for (int sp = 0; sp < qi.S; ++sp) {
-          a += base[sp * slab + col];
-          b += base[sp * slab + col + 64];
-        }
-      }
-      if (it < G * 64 + 64) {  // q or k: round (the GEMM output), rotate (neox)
-        a = bf2f(f2bf(a));
-        b = bf2f(f2bf(b));
-        const float co = cs[j], si = cs[64 + j];
-        const bf16_t ra = f2bf(a * co - b * si), rb = f2bf(b * co + a * si);
-        if (it < G * 64) {
-          q_s[it >> 6][j] = ra;
-          q_s[it >> 6][j + 64] = rb;
-        } else if (fold) {
-          kn_s[j] = ra;
-          kn_s[j + 64] = rb;
-        } else {
-          bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * n_kv + h) * bs * kHD;
-          d[kcache_off(slot % bs, j)] = ra;
-          d[kcache_off(slot % bs, j + 64)] = rb;
-        }
-      } else if (fold) {
-        vn_s[j] = bf2f(f2bf(a));
-        vn_s[j + 64] = bf2f(f2bf(b));
-      } else {
-        bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs;
-        d[vcache_off(slot % bs, j)] = f2bf(a);
-        d[vcache_off(slot % bs, j + 64)] = f2bf(b);
-      }
-    }
-    if (!fold) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new k/v rows are in L2 before any wave reads them
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-      qf[kk] = r < G ? *reinterpret_cast<const bf16x8_t*>(&q_s[r][32 * g + 8 * kk]) : zero8();
-    if (fold) {  // scores of the new key, 16 lanes per query head (read after the combine's barrier)
-      const int c = threadIdx.x >> 4, part = threadIdx.x & 15;
-      float sdot = 0.f;
-      if (c < G)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sdot += bf2f(q_s[c][8 * part + e]) * bf2f(kn_s[8 * part + e]);
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) sdot += __shfl_xor(sdot, o, 64);
-      if (c < G && part == 0) sn_s[c] = sdot * scale2;
-    }
-  } else {
-    load_q(qf, q + static_cast<int64_t>(seq) * q_stride + (h * G + r) * kHD, r < G);
-  }
-
-  // the grid's z dimension is small (<= 4); a workgroup walks partitions z, z + gridDim.z, ...
-  // carrying its online-softmax state across them (the order of key blocks does not matter to
-  // the softmax), so it combines its waves and writes ONE partial at the end: no LDS combine /
-  // partial store between partitions and gridDim.z partials to merge instead of n_parts.
-  const int n_eff = min(n_used, static_cast<int>(gridDim.z));  // partials of this sequence
-  const int ctx_c = fold ? ctx - 1 : ctx;  // keys read from the cache
-  WaveState st;
-  init_state(st);
-  for (int part = blockIdx.z; part < n_used; part += gridDim.z) {
-    const int begin = part * kPart;
-    const int end = min(ctx_c, begin + kPart);
-    const int b0 = begin / bs, nblk = (end - 1) / bs - b0 + 1;
-    __syncthreads();  // the previous partition's block-table readers are done
-    if (part == static_cast<int>(blockIdx.z) && kPart % bs == 0) {  // nblk <= kPart / bs <= 64 * NW
-      if (static_cast<int>(threadIdx.x) < nblk) bt_s[threadIdx.x] = bt_pre;
-    } else
-      for (int i = threadIdx.x; i < nblk; i += 64 * NW)
-        bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
-    __syncthreads();
-    KVFrag fa;
-    if (end > begin)
-      attend(st, qf, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w, end, NW * kStep, ctx_c, ctx_c - 1, scale2,
-             fa);
-  }
-  const float lsum = col_sum(st.l);
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o_lds[w][r][16 * dt + 4 * g + i] = st.o[dt][i];
-  if (g == 0) {
-    ml_lds[w][r][0] = st.m;
-    ml_lds[w][r][1] = lsum;
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
-    const int c = idx / kHD, d = idx % kHD;
-    float M = kNegBig;
-#pragma unroll
-    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, ml_lds[ww][c][0]);
-    const float sn = fold ? sn_s[c] : kNegBig;
-    M = fmaxf(M, sn);
-    float O = 0.f, L = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < NW; ++ww) {
-      const float f = exp2f(ml_lds[ww][c][0] - M);
-      O += f * o_lds[ww][c][d];
-      L += f * ml_lds[ww][c][1];
-    }
-    if (fold) {  // key ctx - 1: P rounded to bf16 for the PV product as in attend_step
-      const float f = exp2f(sn - M);
-      O += bf2f(f2bf(f)) * vn_s[d];
-      L += f;
-    }
-    const int hq = h * G + c;
-    if (n_eff == 1) {
-      out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
-    } else {
-      const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + blockIdx.z;
-      part_o[pi * kHD + d] = O;
-      if (d == 0) {
-        part_ml[2 * pi] = M;
-        part_ml[2 * pi + 1] = L;
-      }
-    }
-  }
-  if (fold) {  // the new token's row into the paged cache, off the attention's critical path
-    const int t = threadIdx.x;
-    if (t < kHD) {
-      bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * n_kv + h) * bs * kHD;
-      d[kcache_off(slot % bs, t)] = kn_s[t];
-    } else if (t < 2 * kHD) {
-      bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs;
-      d[vcache_off(slot % bs, t - kHD)] = f2bf(vn_s[t - kHD]);
-    }
-  }
-  if (n_eff == 1 || counters == nullptr) return;
-  // ---- in-launch split-K merge: the last workgroup to arrive combines the partials
-  // (guide §5 "In-launch split-K reduction": plain slab stores, every wave drains, one agent
-  // release + ticket; the last arriver acquires, merges and re-arms the counter).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int* ctr = counters + seq * n_kv + h;
-    const int t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == n_eff - 1);
-    if (last) {
-      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
-    const int c = idx / kHD, d = idx % kHD;
-    const int hq = h * G + c;
-    const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
-    float M = kNegBig;
-    for (int p = 0; p < n_eff; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
-    float O = 0.f, L = 0.f;
-    for (int p = 0; p < n_eff; ++p) {
-      const float f = exp2f(part_ml[2 * (base + p)] - M);
-      O += f * part_o[(base + p) * kHD + d];
-      L += f * part_ml[2 * (base + p) + 1];
-    }
-    out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
-  }
-}
-
-// grid (n_q, n_seqs), block 128: merge the partitions of sequences that used more than one.
-template <int kPart>
-__global__ void __launch_bounds__(128) paged_decode_reduce_kernel(bf16_t* __restrict__ out,
-                                                                  const float* __restrict__ part_o,
-                                                                  const float* __restrict__ part_ml,
-                                                                  const int* __restrict__ context_lens, int n_q,
-                                                                  int out_stride, int n_parts, int z) {
-  const int hq = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
-  const int ctx = context_lens[seq];
-  const int n_used = min((ctx + kPart - 1) / kPart, z);  // one partial per partition workgroup
-  bf16_t* o = out + static_cast<int64_t>(seq) * out_stride + hq * kHD;
-  if (ctx <= 0) {
-    o[d] = 0;
-    return;
-  }
-  if (n_used <= 1) return;
-  const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
-  float M = kNegBig;
-  for (int p = 0; p < n_used; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
-  float O = 0.f, L = 0.f;
-  for (int p = 0; p < n_used; ++p) {
-    const float f = exp2f(part_ml[2 * (base + p)] - M);
-    O += f * part_o[(base + p) * kHD + d];
-    L += f * part_ml[2 * (base + p) + 1];
-  }
-  o[d] = f2bf(L > 0.f ? O / L : 0.f);
+  __shared__ DecodeLds<kPart, NW> lds;
+  decode_tile<kPart, NW, FROM_QKV, SS>(out, q, kc, vc, block_tables, context_lens, part_o, part_ml, counters, n_q, n_kv,
+                                       bs, max_blocks, q_stride, out_stride, n_parts, scale2, qi, blockIdx.x, blockIdx.y,
+                                       blockIdx.z, gridDim.z, lds, Flow{});
 }
 
 // ----------------------------------------------------------------------------- prefill
@@ -814,6 +371,8 @@ PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, 
   return decode_launch(out, nullptr, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, nullptr,
                        n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
 }
+
+int pk_get_decode_z() { return g_decode_z; }  // the fused QKV -> attention launch (decode_fused.hip)
 
 PK_EXPORT int pk_set_decode_z(int z) {
   if (z < 1) return -1;

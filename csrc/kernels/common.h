@@ -15,6 +15,7 @@ typedef uint16_t bf16_t;  // raw bits; converted explicitly
 typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (8 bf16)
 typedef __attribute__((ext_vector_type(4))) float f32x4;    // 16x16 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;  // 16-byte raw vector
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;  // MFMA bf16 operand (16x16x32)
 
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
@@ -31,6 +32,8 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   const f32x2_t v = {a, b};
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
+
+__device__ __forceinline__ bf16x8_t ld8(const bf16_t* p) { return *reinterpret_cast<const bf16x8_t*>(p); }
 
 __device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
 #pragma unroll

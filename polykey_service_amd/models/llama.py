@@ -445,12 +445,20 @@ class LlamaForCausalLM(nn.Module):
         for i, layer in enumerate(self.layers):
             at, mlp = layer.attn, layer.mlp
             kc, vc = kv_caches[i]
-            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf)
-            if md.num_prefill == 0:
-                a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
+            if (md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and T <= gemm.SKINNY_MAX_M and not self.st.shared_device
+                    and md.num_decode == T):
+                # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip)
+                a = gemm.qkv_attn_fused(residual, at.qkv_pf, gemm.RowScale(parts, layer.eps), ws, positions,
+                                        self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv, self._flow_qkv)
             else:
-                q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
-                a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
+                p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps),
+                                                 packed=at.qkv_pf)
+                if md.num_prefill == 0:
+                    a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq,
+                                                       at.nkv)
+                else:
+                    q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
+                    a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
             parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True), residual, buf2)
@@ -515,6 +523,7 @@ class LlamaForCausalLM(nn.Module):
             self._ws = torch.empty(self._workspace_elems(), dtype=torch.float32, device=self.device)
             # hand-off tickets of the fused decode MLP launch (gemm.mlp_fused), left zeroed by every launch
             self._flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
+            self._flow_qkv = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
         return self._ws
 
     def _workspace_elems(self) -> int:

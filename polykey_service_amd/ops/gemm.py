@@ -402,6 +402,37 @@ def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.
     return Partial(ws, S, M, N)
 
 
+QKV_ATTN_FUSED = os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1") == "1"
+
+
+def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: RowScale, ws: torch.Tensor,
+                   positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, md,
+                   scale: float, nq: int, nkv: int, flow: torch.Tensor) -> torch.Tensor:
+    """Decode layer front half in ONE launch (csrc/kernels/decode_fused.hip): the folded-norm
+    QKV projection's split-K slabs (``ws``), handed in-launch to the decode attention that
+    reduces them, applies RoPE, writes the new k / v to the paged cache and attends.  Same
+    result as :func:`linear_partial_rowscale` + ``attention.paged_decode_from_qkv``.  ``flow``:
+    int32 >= :data:`FLOW_WORDS`, zeroed once, left zeroed.  Returns [M, nq * 128] bf16."""
+    M, K = x.shape
+    N = qkv_packed.shape[0]
+    S = choose_split(N, K, M)
+    assert ws.numel() >= S * M * N and flow.numel() >= FLOW_WORDS and flow.dtype == torch.int32
+    assert md.num_prefill == 0 and md.num_decode == M and k_cache.shape[-1] == 128
+    out = torch.empty((M, nq * 128), dtype=torch.bfloat16, device=x.device)
+    a = GemmArgs()
+    a.partial, a.A, a.W = ws.data_ptr(), x.data_ptr(), qkv_packed.data_ptr()
+    a.M, a.N, a.K, a.lda, a.ldo, a.S = M, N, K, x.stride(0), N, S
+    a.row_scale, a.nrm_parts, a.nrm_nparts, a.eps = 1, rowscale.parts.data_ptr(), rowscale.parts.shape[0], \
+        float(rowscale.eps)
+    bt = md.decode_block_tables
+    native.call("pk_qkv_attn_fused", ctypes.byref(a), out.data_ptr(), positions.data_ptr(), cos_sin.data_ptr(),
+                md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), bt.data_ptr(),
+                md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,
+                native.ptr(md.decode_part_ml) or 0, nq, nkv, k_cache.shape[2], bt.stride(0), out.stride(0),
+                float(scale), int(md.decode_max_ctx), flow.data_ptr(), native.stream_ptr())
+    return out
+
+
 def fold_norm(w: torch.Tensor, norm_weight: torch.Tensor) -> torch.Tensor:
     """W' = W diag(norm_weight): the RMSNorm weight of the projection's input folded into its
     columns (bf16), for the row-scaled decode GEMM (:class:`RowScale`)."""

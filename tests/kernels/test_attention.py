@@ -213,3 +213,49 @@ def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S, pos_last):
     got = A.paged_decode_from_qkv(p, pos.to(d), cs, k2, v2, mk(), scale, nq, nkv)
     torch.testing.assert_close(got.float(), exp.float(), atol=2e-2, rtol=2e-2)
     assert torch.equal(k1, k2) and torch.equal(v1, v2)
+
+
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (16, 4, 32)])
+@pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [384] * 64, [512, 513, 1300, 0]])
+def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, ctxs):
+    """Fused QKV projection -> decode attention launch (csrc/kernels/decode_fused.hip): the QKV
+    tiles hand their write-through slabs to the attention tiles in-launch.  Attention output and
+    K / V cache bit-identical to linear_partial_rowscale + paged_decode_from_qkv, over repeated
+    launches with new inputs (stale slabs would show), tickets left zeroed."""
+    from polykey_service_amd.ops import gemm
+    d = "cuda"
+    B, H = len(ctxs), 1024
+    N = (nq + 2 * nkv) * HD
+    max_blocks = (max(ctxs) + bs - 1) // bs + 3
+    nb = sum((max(c, 1) + bs - 1) // bs for c in ctxs) + 4
+    bt = block_tables_for([max(c, 1) for c in ctxs], bs, nb, max_blocks, seed=3)
+    cl = torch.tensor(ctxs, dtype=torch.int32)
+    pos = (cl - 1).clamp(min=0)
+    slots = torch.tensor([int(bt[i, (c - 1) // bs]) * bs + (c - 1) % bs if c > 0 else -1 for i, c in enumerate(ctxs)],
+                         dtype=torch.int32)
+    cs = ref.rope_cos_sin_cache(4096, HD, 500000.0).to(d)
+    po, pml = A.decode_workspace(B, nq, max_blocks, bs, d)
+    mk = lambda: A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0,
+                                slot_mapping=slots.to(d), decode_block_tables=bt.to(d), decode_context_lens=cl.to(d),
+                                decode_part_o=po, decode_part_ml=pml)
+    scale = 1 / math.sqrt(HD)
+    w = (torch.randn(N, H, device=d) * 0.05).to(torch.bfloat16)
+    wp = gemm.pack_weight(w)
+    S = gemm.choose_split(N, H, B)
+    ws1 = torch.empty(S * B * N, dtype=torch.float32, device=d)
+    ws2 = torch.empty_like(ws1)
+    flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=d)
+    kc, vc = make_cache(nb, nkv, bs, seed=3)
+    k1, v1, k2, v2 = kc.to(d), vc.to(d), kc.to(d), vc.to(d)
+    for it in range(4):
+        res = (torch.randn(B, H, device=d)).to(torch.bfloat16)
+        parts = gemm.residual_parts(None, res.clone(), torch.empty(2 * 64, device=d))
+        rs = gemm.RowScale(parts, 1e-5)
+        p = gemm.linear_partial_rowscale(res, w, ws1, rs, S=S, packed=wp)
+        exp = A.paged_decode_from_qkv(p, pos.to(d), cs, k1, v1, mk(), scale, nq, nkv)
+        ws2.fill_(float("nan"))
+        got = gemm.qkv_attn_fused(res, wp, rs, ws2, pos.to(d), cs, k2, v2, mk(), scale, nq, nkv, flow)
+        torch.testing.assert_close(got, exp, atol=0, rtol=0)
+        assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    torch.cuda.synchronize()
+    assert int(flow.abs().sum()) == 0, flow.nonzero().tolist()
