@@ -215,7 +215,7 @@ def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S, pos_last):
     assert torch.equal(k1, k2) and torch.equal(v1, v2)
 
 
-@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (16, 4, 32)])
+@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (16, 4, 32), (64, 8, 32)])
 @pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [384] * 64, [512, 513, 1300, 0]])
 def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, ctxs):
     """Fused QKV projection -> decode attention launch (csrc/kernels/decode_fused.hip): the QKV
