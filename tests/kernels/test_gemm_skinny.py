@@ -322,7 +322,7 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     wd = rnd(H, I, scale=0.02)
     dp = gemm.pack_weight(wd)
     assert gemm.mlp_fused_ok(res, gup, dp)
-    parts = gemm.residual_parts(None, res.clone(), torch.empty(8 * 64, device="cuda"))
+    parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
     rs = gemm.RowScale(parts, 1e-5)
     S = gemm.choose_split(H, I, M)
     ws0 = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
@@ -339,11 +339,12 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     rinv = torch.rsqrt(res.float().pow(2).mean(-1, keepdim=True) + 1e-5)
     hx = ref.silu_and_mul_interleaved(((res.float() @ gemm.fold_norm(wgu, nw).float().t()) * rinv).to(torch.bfloat16))
     exp = hx.float() @ wd.float().t()
-    torch.testing.assert_close(p.view().sum(0), exp, atol=3e-2, rtol=3e-2)
+    # (fp32 reference: the bf16 h rounding differs; K = 28672 at the 70B shape -> a wider bound)
+    torch.testing.assert_close(p.view().sum(0), exp, atol=6e-2, rtol=3e-2)
     # new inputs every launch: a consumer reading a stale copy of the previous launch's h would show
     for it in range(6):
         r2 = rnd(M, H)
-        p2 = gemm.residual_parts(None, r2.clone(), torch.empty(8 * 64, device="cuda"))
+        p2 = gemm.residual_parts(None, r2.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
         rs2 = gemm.RowScale(p2, 1e-5)
         h2 = gemm.linear_silu(r2, wgu, packed=gup, rowscale=rs2)
         exp2 = gemm.linear_partial(h2, wd, ws0, packed=dp).view().clone()
