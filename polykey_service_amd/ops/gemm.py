@@ -362,6 +362,7 @@ def linear_partial_rowscale(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, 
     return Partial(ws, S, M, N)
 
 
+_SK_CUS = 256  # compute units of an MI355X
 FLOW_WORDS = 128 * 64 + 1  # pk_mlp_fused hand-off buffer: 64 tickets + 64 consumer counts (256 B apart), error word
 
 
@@ -372,9 +373,11 @@ def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_p
     M, K = x.shape
     N2, I = gate_up_packed.shape[0], down_packed.shape[1]
     S = choose_split(down_packed.shape[0], I, M)
+    # one workgroup per CU, each a gate_up tile then a down tile: above 256 tiles (70B on one GPU:
+    # 448 gate_up tiles) the fused launch measured 8 % slower end to end (profiles/r2_decode_ab.txt)
     return (0 < M <= SKINNY_MAX_M and N2 == 2 * I and N2 % 128 == 0 and K % _KCHUNK == 0
             and down_packed.shape[0] % 128 == 0 and I % (_KCHUNK * S) == 0 and (I // S) % 64 == 0 and S <= 64
-            and gate_up_packed.shape[1] == K)
+            and gate_up_packed.shape[1] == K and N2 // 128 <= _SK_CUS and (down_packed.shape[0] // 128) * S <= _SK_CUS)
 
 
 def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: RowScale,

@@ -321,7 +321,9 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     gup = gemm.pack_weight(gemm.fold_norm(wgu, nw))
     wd = rnd(H, I, scale=0.02)
     dp = gemm.pack_weight(wd)
-    assert gemm.mlp_fused_ok(res, gup, dp)
+    # the launch is correct at any grid; the engine takes it only up to one tile per CU (70B: 448
+    # gate_up tiles -> two launches, measured faster)
+    assert gemm.mlp_fused_ok(res, gup, dp) == (2 * I // 128 <= 256)
     parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
     rs = gemm.RowScale(parts, 1e-5)
     S = gemm.choose_split(H, I, M)
