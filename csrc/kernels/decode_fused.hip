@@ -85,7 +85,7 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
                     static_cast<float*>(part_o), static_cast<float*>(part_ml), n_q, n_kv, bs, max_blocks, out_stride,
                     n_parts, n_seqs, z, scale * 1.4426950408889634f, qi};
   int* done = flow + 64 * kFlowPad;
-  int* err = flow + 128 * kFlowPad;
+  int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
   const int G = n_q / n_kv;
   // producer: one ticket per (head, split) tile on its kv head; consumer: (G + 2) heads x S
   const Flow fq{flow, done, err, 0, 0, 0, 1, n_q, n_kv};

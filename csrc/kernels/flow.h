@@ -3,6 +3,11 @@
 #pragma once
 #include "common.h"
 
+// Host-mapped sticky word that a timed-out wait of any fused launch sets (pk_fused_err_word): the
+// engine reads it every step without a GPU sync (the custom all-reduce's error word, the same way).
+// Null: the flow buffer's own error slot.
+int* fused_err_word();
+
 namespace {
 
 // Dataflow hand-off between the two GEMMs of one fused launch (mlp_fused_kernel): a producer

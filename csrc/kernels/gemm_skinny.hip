@@ -19,6 +19,8 @@
 //     a workgroup consumes are contiguous, as 32 MFMA A-fragments of 1 KiB in lane order, so
 //     every wave load instruction reads 1 KiB and a workgroup sweeps one linear stream
 //     (tools/gemm_lab.hip: LM head 5.1 -> 5.9 TB/s with non-temporal loads).
+#include <cstring>
+
 #include "skinny_tile.h"
 
 using namespace pk;
@@ -522,7 +524,7 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   gu.tile_rows = dn.tile_rows = 64;
   gu.max_group_rows = dn.max_group_rows = 0;
   int* done = flow + 64 * kFlowPad;
-  int* err = flow + 128 * kFlowPad;
+  int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
   Flow fgu{flow, done, err, 0, 0, dn.K / dn.S, 1};
   Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / 128, dn.K / dn.S, 2};
   const int n_gu = gu.N / 128, n_dn = (dn.N / 128) * dn.S;
@@ -534,6 +536,21 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
     default: mlp_fused_kernel<4><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
   }
   return PK_CHECK_LAUNCH();
+}
+
+static int* g_fused_err = nullptr;
+int* fused_err_word() { return g_fused_err; }
+
+// The fused launches' sticky timeout word in host-mapped, coherent pinned memory (allocated once per
+// process): returns its address (the host reads it with a plain load; 0 = no wait ever timed out).
+PK_EXPORT void* pk_fused_err_word() {
+  if (g_fused_err == nullptr) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    std::memset(h, 0, 64);
+    g_fused_err = static_cast<int*>(h);
+  }
+  return g_fused_err;
 }
 
 PK_EXPORT int pk_norm_apply(void* x, const void* residual, const void* parts, int nparts, const void* w, int M,

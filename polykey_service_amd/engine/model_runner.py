@@ -34,6 +34,7 @@ import numpy as np
 import torch
 
 from ..ops import attention as attn_ops
+from ..ops import gemm
 from ..ops import native
 from ..ops import sampler as sampler_ops
 from .scheduler import ScheduledBatch
@@ -330,6 +331,7 @@ class ModelRunner:
         """Fail loudly once a custom all-reduce of this step (or an earlier one) timed out: the
         step's tokens were computed from incomplete sums (parallel/custom_ar.py)."""
         st = self.model.st
+        gemm.check_fused()
         if st.custom_ar is not None:
             st.custom_ar.check()
         for rc in (getattr(st, "rccl_tp", None), getattr(st, "rccl_ep", None)):

@@ -523,6 +523,7 @@ class LlamaForCausalLM(nn.Module):
             self._ws = torch.empty(self._workspace_elems(), dtype=torch.float32, device=self.device)
             # hand-off tickets of the fused decode MLP launch (gemm.mlp_fused), left zeroed by every launch
             self._flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
+            gemm.fused_err_word()  # before the first fused launch (engine polls gemm.check_fused)
             self._flow_qkv = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
         return self._ws
 

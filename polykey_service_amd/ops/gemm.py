@@ -366,6 +366,31 @@ _SK_CUS = 256  # compute units of an MI355X
 FLOW_WORDS = 128 * 64 + 1  # pk_mlp_fused hand-off buffer: 64 tickets + 64 consumer counts (256 B apart), error word
 
 
+_FUSED_ERR: Optional[int] = None
+
+
+def fused_err_word() -> int:
+    """Address of the fused launches' sticky timeout word (host-mapped pinned memory, allocated
+    once per process; every later fused launch reports into it)."""
+    global _FUSED_ERR
+    if _FUSED_ERR is None:
+        fn = native.lib().pk_fused_err_word
+        fn.restype, fn.argtypes = ctypes.c_void_p, []
+        _FUSED_ERR = fn()
+        if not _FUSED_ERR:
+            raise native.KernelError("pk_fused_err_word: hipHostMalloc failed")
+    return _FUSED_ERR
+
+
+def check_fused() -> None:
+    """Raise once any in-launch hand-off wait of a fused decode launch timed out: that launch's
+    outputs were computed from data that had not arrived (cannot happen while every workgroup of
+    the grid is resident; a GPU shared with other processes could break that).  A plain read of
+    host memory, no GPU sync: the engine calls it every step like the collectives' error words."""
+    if _FUSED_ERR is not None and ctypes.c_int.from_address(_FUSED_ERR).value != 0:
+        raise RuntimeError("a fused decode launch's in-kernel hand-off timed out (results invalid)")
+
+
 def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_packed: Optional[torch.Tensor]) -> bool:
     """Shapes the fused decode MLP launch (:func:`mlp_fused`) takes."""
     if gate_up_packed is None or down_packed is None or not x.is_cuda or not MLP_FUSED:

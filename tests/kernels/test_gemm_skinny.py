@@ -402,3 +402,30 @@ def test_row_tiles_refuse_in_launch_reduction():
     ctr = torch.zeros(1024, dtype=torch.int32, device="cuda")
     with pytest.raises(RuntimeError):
         gemm.linear_add_residual(x, w, ws, ctr, rnd(M, H), torch.empty(H // 128 * M, device="cuda"), 2)
+
+
+def test_fused_err_word_plumbing():
+    """The fused launches report a timed-out hand-off wait into one host-mapped sticky word that
+    the engine polls every step (gemm.check_fused): allocated once, zero after real launches,
+    and a set word fails the check loudly."""
+    import ctypes
+    addr = gemm.fused_err_word()
+    assert addr and gemm.fused_err_word() == addr
+    M, H, I = 64, 1024, 4096
+    res = rnd(M, H)
+    gup = gemm.pack_weight(gemm.interleave_gate_up(rnd(I, H, scale=0.05), rnd(I, H, scale=0.05)))
+    dp = gemm.pack_weight(rnd(H, I, scale=0.02))
+    parts = gemm.residual_parts(None, res.clone(), torch.empty(2 * 64, device="cuda"))
+    ws = torch.empty(gemm.choose_split(H, I, M) * M * H, dtype=torch.float32, device="cuda")
+    flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda")
+    gemm.mlp_fused(res, gup, dp, gemm.RowScale(parts, 1e-5), ws, flow)
+    torch.cuda.synchronize()
+    gemm.check_fused()
+    w = ctypes.c_int.from_address(addr)
+    w.value = 1
+    try:
+        with pytest.raises(RuntimeError, match="hand-off timed out"):
+            gemm.check_fused()
+    finally:
+        w.value = 0
+    gemm.check_fused()
