@@ -26,9 +26,11 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tag", default=os.environ.get("AB_TAG", ""))
+    ap.add_argument("--eager", action="store_true", help="no HIP graphs (PMC runs count per dispatch)")
     a = ap.parse_args()
     max_len = max(2048, (a.prompt + a.steps + 64 + 511) // 512 * 512)
-    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=a.batch, device="cuda:0", max_model_len=max_len))
+    eng = LLMEngine(EngineConfig(model=a.model, max_num_seqs=a.batch, device="cuda:0", max_model_len=max_len,
+                                 hip_graphs=not a.eager))
     g = torch.Generator().manual_seed(0)
     hi = min(30000, eng.mcfg.vocab_size - 1)
     prompts = [torch.randint(10, hi, (a.prompt,), generator=g).tolist() for _ in range(a.batch)]
