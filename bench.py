@@ -19,6 +19,13 @@ sides; elapsed = max over ranks; value = total output tokens of all replicas / e
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+With N > 1 (plain, or rank 0 of the driver's torchrun -- the other outer ranks exit without
+touching a GPU) the measurement runs in a fresh N-rank torchrun child whose JSON line is relayed;
+with ``--tp 1`` a second child then serves ``--tp-extra-model`` (default Llama-3-70B) at TP = N
+over the same gRPC load and its result is added under ``tp{N}_70b`` -- the 70B TP=8 half of the
+BASELINE metric on an 8-GPU node.  Each child has its own timeout: a TP failure is reported in
+that key and never loses the replica number.
 """
 from __future__ import annotations
 
@@ -65,15 +72,100 @@ def parse_args(argv=None):
                          "(gateway, engine/remote.py dp_gateway); or rank 0 alone as the front end (single)")
     ap.add_argument("--client", choices=["process", "inproc"], default="inproc",
                     help="load generator on the server's event loop (default) or in its own process")
+    ap.add_argument("--tp-extra-model", default="llama3-70b",
+                    help="N > 1 with --tp 1: after the replica run, measure this model at TP = N in a fresh "
+                         "torchrun child and report it under the extra key tp{N}_<model> (BASELINE.json: "
+                         "'Llama-3-8B TP=1 / 70B TP=8'); 'none' skips it")
+    ap.add_argument("--tp-extra-timeout", type=float, default=480.0,
+                    help="seconds the TP child may take (its failure or timeout never loses the main number)")
+    ap.add_argument("--child-timeout", type=float, default=1500.0, help="seconds the main measurement child may take")
+    ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)  # internal: the measuring torchrun job
     return ap.parse_args(argv)
 
 
-def relaunch_with_torchrun(args) -> int:
-    """`python bench.py --gpus N` without torchrun: start torchrun as a child (no exec)."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(29500 + random.randint(0, 999)),
-           os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd)
+# torchrun's per-worker variables: a nested launch must not inherit the outer job's rendezvous
+_LAUNCH_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+               "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_child(argv, n: int, timeout: float):
+    """One measurement as a fresh torchrun job of ``n`` ranks (a child process, never an exec;
+    its own session, so a timeout kills the whole tree and frees every GPU).  Returns
+    (rc, the child's JSON line as a dict or None, wall seconds)."""
+    import signal
+    env = {k: v for k, v in os.environ.items() if k not in _LAUNCH_ENV and not k.startswith("TORCHELASTIC_")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=timeout)
+        rc = p.returncode
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, _ = p.communicate()
+        rc = 124
+    line = None
+    for ln in out.splitlines():
+        if ln.startswith("{"):
+            try:
+                line = json.loads(ln)
+            except ValueError:
+                pass
+        else:
+            print(ln, file=sys.stderr)
+    return rc, line, time.perf_counter() - t0
+
+
+def _strip(argv, names):
+    """argv without the options in ``names`` (and their values)."""
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        k = a.split("=", 1)[0]
+        if k in names:
+            skip = "=" not in a
+            continue
+        out.append(a)
+    return out
+
+
+def orchestrate(args, argv) -> int:
+    """``--gpus N`` (N > 1), plain or under the driver's torchrun (rank 0 only: the other outer
+    ranks exit without touching a GPU).  The measurement runs as a fresh N-rank torchrun child
+    whose JSON line is relayed; with ``--tp 1`` a second child then measures ``--tp-extra-model``
+    at TP = N (70B TP=8 on an 8-GPU node) under the extra key ``tp{N}_<model>``.  Each child has
+    its own timeout, so a TP failure can never erase the replica number."""
+    rc, main_line, _ = run_child(argv + ["--child"], args.gpus, args.child_timeout)
+    if main_line is None:
+        print(f"bench: measurement child failed (rc {rc})", file=sys.stderr)
+        return rc or 1
+    extra = args.tp_extra_model
+    if args.tp == 1 and args.ep == 1 and extra and extra != "none":
+        key = f"tp{args.gpus}_" + {"llama3-70b": "70b", "llama3-8b": "8b"}.get(extra, extra)
+        targv = _strip(argv, {"--model", "--tp", "--ep", "--frontend", "--tp-extra-model"}) + [
+            "--model", extra, "--tp", str(args.gpus), "--tp-extra-model", "none", "--child"]
+        trc, tl, wall = run_child(targv, args.gpus, args.tp_extra_timeout)
+        if tl is not None:
+            main_line[key] = {k: tl.get(k) for k in ("value", "unit", "p50_e2e_latency_ms", "ms_per_step", "steps",
+                                                     "warmup", "scaling")}
+            main_line[key].update(model=tl["config"]["model"], parallelism=tl["config"]["parallelism"],
+                                  global_batch=tl["config"]["global_batch"], init_s=tl["config"].get("init_s"),
+                                  wall_s=round(wall, 1))
+        else:
+            main_line[key] = {"error": f"TP child rc {trc}" + (" (timeout)" if trc == 124 else ""),
+                              "wall_s": round(wall, 1)}
+    print(json.dumps(main_line), flush=True)
+    return 0
 
 
 async def _abarrier(group) -> None:
@@ -266,10 +358,12 @@ async def _drive_external(args, engine, st, leaders_group, port, srv, llm, conc,
 
 
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 and world == 1:
-        return relaunch_with_torchrun(args)
+    if args.gpus > 1 and not args.child:
+        if int(os.environ.get("RANK", "0")) != 0:
+            return 0  # under the driver's torchrun: rank 0 runs the measurement children
+        return orchestrate(args, argv)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import torch
     import torch.distributed as dist
@@ -292,6 +386,10 @@ def main(argv=None) -> int:
                         gpu_mem_fraction=args.gpu_mem_fraction)
     t_init = time.perf_counter()
     engine = LLMEngine(ecfg, st)
+    if engine.device.type == "cuda":
+        torch.cuda.synchronize(engine.device)  # weight init / packing / graph capture run asynchronously
+    if dist.is_initialized():
+        dist.barrier()
     init_s = time.perf_counter() - t_init
     leaders = list(range(0, st.world_size, st.tp_size))
     leaders_group = dist.new_group(leaders) if dist.is_initialized() else None

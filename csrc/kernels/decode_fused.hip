@@ -69,7 +69,8 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   if (n_seqs <= 0) return 0;
   if (n_seqs > 64 || g.N != (n_q + 2 * n_kv) * kHD || g.N % 128 || g.S < 1 || g.K % (kKC * g.S) || !g.row_scale ||
       g.nrm_parts == nullptr || g.nrm_nparts < 1 || g.nrm_nparts > 64 || g.partial == nullptr || g.lda % 8 ||
-      g.row_offsets != nullptr || n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0 || flow == nullptr)
+      g.row_offsets != nullptr || n_kv > 64 || n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0 ||
+      flow == nullptr)  // n_kv <= 64: one ticket slot per kv head below the done counters
     return -1;
   if (max_ctx <= 0 || max_ctx > max_blocks * bs) max_ctx = max_blocks * bs;
   const int n_parts = (max_ctx + kFusedPart - 1) / kFusedPart;

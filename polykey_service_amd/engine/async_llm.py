@@ -49,6 +49,9 @@ class AsyncLLM:
         self._stop = False
         self.dead: Optional[BaseException] = None
         self.last_step_time = time.monotonic()
+        # monotonic start of the step in flight (None between steps): the watchdog only judges a
+        # step that has started and not returned, never an idle gap before a new request
+        self.step_started: Optional[float] = None
         self.watchdog_s = watchdog_s
         self.stats = {"steps": 0, "requests": 0, "output_tokens": 0, "step_time_s": 0.0, "arrival_waits": 0}
         # Arrival coalescing: an idle engine that receives a request keeps collecting arrivals
@@ -170,9 +173,14 @@ class AsyncLLM:
     async def aclose(self) -> None:
         await asyncio.get_running_loop().run_in_executor(None, self.shutdown)
 
+    def stalled_for(self) -> float:
+        """Seconds the step in flight has been running (0 between steps)."""
+        t0 = self.step_started
+        return 0.0 if t0 is None else time.monotonic() - t0
+
     def _watch(self) -> None:
-        """Step watchdog: a step stuck for ``watchdog_s`` while work is pending
-        (a collective hung on a dead peer, a wedged GPU) kills the engine: its communicators
+        """Step watchdog: a step in flight for ``watchdog_s`` (a collective hung
+        on a dead peer, a wedged GPU) kills the engine: its communicators
         are aborted (the hung RCCL call returns, IPC collectives stop waiting), every stream
         gets the error and ``on_fatal`` fires -- the server goes NOT_SERVING and exits non-zero
         for its supervisor to restart the group.  Disabled while ``watchdog_s`` is 0."""
@@ -181,7 +189,7 @@ class AsyncLLM:
             w = self.watchdog_s
             if not w or self.dead is not None or self._stop:
                 continue
-            if self.engine.has_unfinished() and time.monotonic() - self.last_step_time > w:
+            if self.stalled_for() > w:
                 err = TimeoutError(f"engine step stalled for more than {w:.0f} s (hung collective or GPU)")
                 self.dead = err
                 try:
@@ -206,8 +214,8 @@ class AsyncLLM:
     def healthy(self) -> bool:
         if self.dead is not None:
             return False
-        if self.watchdog_s and self.engine.has_unfinished():
-            return time.monotonic() - self.last_step_time < self.watchdog_s
+        if self.watchdog_s:
+            return self.stalled_for() < self.watchdog_s
         return True
 
     # ---------------------------------------------------------------- engine side
@@ -304,7 +312,9 @@ class AsyncLLM:
                 if not eng.lockstep and self.arrival_window_s > 0 and eng.idle_with_waiting():
                     self._coalesce_arrivals()
                 t0 = time.perf_counter()
+                self.step_started = time.monotonic()
                 outs = eng.step()
+                self.step_started = None
                 if prof is not None:
                     prof.step()
                 dt = time.perf_counter() - t0

@@ -286,7 +286,12 @@ class ModelRunner:
             h["cu_rel"][:n - nd + 1] = rel
             max_q = int(np.max(np.diff(rel)))
         elif self.graphs and self.allow_graphs:
-            g = self._graph_bucket(nd) or 0
+            st = self.model.st
+            # DP attention + EP: every rank replays the bucket of the group's largest token count
+            # (the lockstep vote's max): a graph's grouped expert GEMMs tile the rows any expert
+            # can receive from the bucket it was captured at, so a rank with fewer sequences than
+            # its peers must not replay a smaller one
+            g = self._graph_bucket(max(nd, st.ep_step_rows) if st.dp_attention else nd) or 0
             if g:
                 self._pad_decode(nd, g)
         short = self._short(g, nd)

@@ -85,13 +85,6 @@ LM_HEAD_SKINNY_MAX_M = 128
 GATE_UP_SKINNY_MAX_M = 384
 
 
-def ranks_per_device() -> int:
-    """Local ranks sharing one GPU (1 on a real node; 8 in a one-GPU TP=8 rehearsal)."""
-    local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-    n_dev = max(torch.cuda.device_count(), 1) if torch.cuda.is_available() else 1
-    return max(1, (local + n_dev - 1) // n_dev)
-
-
 def pack_folded(owner, name: str, norm_w: torch.Tensor, packed_only: bool) -> torch.Tensor:
     """Block-packed copy of ``owner.<name>`` with ``norm_w`` folded into its columns; with
     ``packed_only`` the row-major weight becomes a meta placeholder (freed before the next)."""
@@ -558,7 +551,7 @@ class LlamaForCausalLM(nn.Module):
         head_bytes = self.lm_head.numel() * self.lm_head.element_size()
         packed_only = mode == "packed"
         if mode == "auto":
-            total = torch.cuda.get_device_properties(self.device).total_memory / ranks_per_device()
+            total = torch.cuda.get_device_properties(self.device).total_memory / max(1, self.st.ranks_per_device)
             proj = sum(w.numel() * w.element_size() for w in self.layers.parameters())
             if 2 * proj + 2 * head_bytes > 0.75 * total:
                 packed_only = True

@@ -362,7 +362,17 @@ def linear_partial_rowscale(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, 
     return Partial(ws, S, M, N)
 
 
-_SK_CUS = 256  # compute units of an MI355X
+_CUS: dict = {}
+
+
+def device_cus(dev: torch.device) -> int:
+    """Compute units of ``dev`` (256 on an MI355X), queried once per device."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _CUS:
+        _CUS[i] = torch.cuda.get_device_properties(i).multi_processor_count
+    return _CUS[i]
+
+
 FLOW_WORDS = 128 * 64 + 1  # pk_mlp_fused hand-off buffer: 64 tickets + 64 consumer counts (256 B apart), error word
 
 
@@ -402,7 +412,8 @@ def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_p
     # 448 gate_up tiles) the fused launch measured 8 % slower end to end (profiles/r2_decode_ab.txt)
     return (0 < M <= SKINNY_MAX_M and N2 == 2 * I and N2 % 128 == 0 and K % _KCHUNK == 0
             and down_packed.shape[0] % 128 == 0 and I % (_KCHUNK * S) == 0 and (I // S) % 64 == 0 and S <= 64
-            and gate_up_packed.shape[1] == K and N2 // 128 <= _SK_CUS and (down_packed.shape[0] // 128) * S <= _SK_CUS)
+            and gate_up_packed.shape[1] == K and N2 // 128 <= device_cus(x.device)
+            and (down_packed.shape[0] // 128) * S <= device_cus(x.device))
 
 
 def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: RowScale,

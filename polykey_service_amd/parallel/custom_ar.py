@@ -66,19 +66,31 @@ class CustomAllReduce:
         # to 512).  Ranks sharing ONE GPU (rehearsals, tests) need every rank's grid resident at
         # once: maybe_create caps it there.
         self.fused_blocks = 0
-        with torch.cuda.device(device):
-            self.ctx = self.lib.pk_car_create(rank, world, max_bytes)
-        if not self.ctx:
-            raise RuntimeError("pk_car_create failed (uncached IPC buffer allocation)")
-        if timeout_s is None:
-            timeout_s = float(os.environ.get("POLYKEY_CUSTOM_AR_TIMEOUT_S", "30"))
-        self.set_timeout(timeout_s)
+        self.ctx = None
         hsz = self.lib.pk_car_ipc_handle_size()
-        mine = ctypes.create_string_buffer(hsz)
-        if self.lib.pk_car_get_handle(self.ctx, mine) != 0:
-            raise RuntimeError("hipIpcGetMemHandle failed")
+        # the local half (allocation, IPC handle) never skips the handle exchange: a rank that
+        # failed still reaches the all-gather (with None), so no peer blocks in it, and every rank
+        # then raises together
+        mine, err = None, None
+        try:
+            with torch.cuda.device(device):
+                self.ctx = self.lib.pk_car_create(rank, world, max_bytes)
+            if not self.ctx:
+                raise RuntimeError("pk_car_create failed (uncached IPC buffer allocation)")
+            if timeout_s is None:
+                timeout_s = float(os.environ.get("POLYKEY_CUSTOM_AR_TIMEOUT_S", "30"))
+            self.set_timeout(timeout_s)
+            buf = ctypes.create_string_buffer(hsz)
+            if self.lib.pk_car_get_handle(self.ctx, buf) != 0:
+                raise RuntimeError("hipIpcGetMemHandle failed")
+            mine = bytes(buf.raw)
+        except Exception as e:  # noqa: BLE001 - re-raised after the exchange
+            err = e
         allh = [None] * world
-        dist.all_gather_object(allh, bytes(mine.raw), group=cpu_group)
+        dist.all_gather_object(allh, mine, group=cpu_group)
+        if err is not None or any(h is None for h in allh):
+            self.close()
+            raise err if err is not None else RuntimeError("a TP peer could not create its IPC buffers")
         blob = ctypes.create_string_buffer(b"".join(allh), hsz * world)
         with torch.cuda.device(device):
             rc = self.lib.pk_car_open(self.ctx, blob)
@@ -191,19 +203,34 @@ def maybe_create(st) -> Optional[CustomAllReduce]:
         return None
     if st.tp_size > 8 or int(os.environ.get("LOCAL_WORLD_SIZE", str(st.world_size))) < st.tp_size:
         return None
+    # every rank reaches the same collectives whatever fails where: the constructor's handle
+    # exchange, an open vote, the self-test vote (all ranks keep the IPC path or none does)
+    car, err = None, None
     try:
         car = CustomAllReduce(st.tp_cpu_group, st.tp_rank, st.tp_size, st.device)
-        n_dev = max(torch.cuda.device_count(), 1)
-        shared = int(os.environ.get("LOCAL_WORLD_SIZE", str(st.tp_size))) > n_dev
-        if shared:
-            car.fused_blocks = 64  # ranks share a GPU: every rank's grid must be resident at once
-        good = car.self_test()
-        votes = [None] * st.tp_size
-        dist.all_gather_object(votes, good, group=st.tp_cpu_group)
-        if all(votes):
-            return car
-        log.warning("custom all-reduce self-test failed on some rank; using RCCL")
-        car.close()
     except Exception as e:  # noqa: BLE001 - any failure → RCCL path
-        log.warning("custom all-reduce unavailable (%s); using RCCL", e)
+        err = e
+    if not _all_ranks(car is not None, st.tp_cpu_group, st.tp_size):
+        log.warning("custom all-reduce unavailable (%s); using RCCL", err or "failed on a peer")
+        if car is not None:
+            car.close()
+        return None
+    if st.shared_device:
+        car.fused_blocks = 64  # ranks share a GPU: every rank's grid must be resident at once
+    good = False
+    try:
+        good = car.self_test()
+    except Exception as e:  # noqa: BLE001
+        log.warning("custom all-reduce self-test raised (%s)", e)
+    if _all_ranks(good, st.tp_cpu_group, st.tp_size):
+        return car
+    log.warning("custom all-reduce self-test failed on some rank; using RCCL")
+    car.close()
     return None
+
+
+def _all_ranks(ok: bool, cpu_group, world: int) -> bool:
+    """All-or-none vote over the group's gloo control group."""
+    votes = [None] * world
+    dist.all_gather_object(votes, bool(ok), group=cpu_group)
+    return all(votes)

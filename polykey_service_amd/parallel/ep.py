@@ -127,7 +127,8 @@ def _ep_moe_ipc(a2a, x, router_w, w13, w2, k, routing, w13_p, w2_p, defer_combin
     # every rank's rows are in this rank's receive regions (padding ids -1: no local expert)
     n = ep * a2a.C
     # any one local expert gets at most one row per token of every sender, and no sender has more
-    # than the step's largest token count (the lockstep vote's max, the graph bucket when captured)
+    # than the step's largest token count (the lockstep vote's max; a captured graph's bucket, and
+    # every rank replays the bucket of the vote's max: ModelRunner.launch)
     bound = ep * min(st.ep_step_rows, a2a.C)
     y = _local_experts(a2a.recv_x, a2a.recv_e.view(-1, 1), w13, w2, w13_p, w2_p, rows=n, bound=bound)
     back = a2a.return_(y.contiguous())[: T * k]  # this rank's rows, in the order they were sent

@@ -58,18 +58,29 @@ class EpAllToAll:
         self.lib = _lib()
         self.rank, self.world, self.device = rank, world, device
         self.C, self.H = capacity, hidden
-        with torch.cuda.device(device):
-            self.ctx = self.lib.pk_ep_create(rank, world, capacity, hidden)
-        if not self.ctx:
-            raise RuntimeError("pk_ep_create failed")
-        t = timeout_s if timeout_s is not None else float(os.environ.get("POLYKEY_CUSTOM_AR_TIMEOUT_S", "30"))
-        self.lib.pk_ep_set_timeout_ms(self.ctx, max(1, int(t * 1000)))
+        self.ctx = None
         hsz = self.lib.pk_ep_ipc_handle_size()
-        mine = ctypes.create_string_buffer(hsz)
-        if self.lib.pk_ep_get_handle(self.ctx, mine) != 0:
-            raise RuntimeError("hipIpcGetMemHandle failed")
+        # a rank whose local setup failed still joins the handle exchange (with None): no peer
+        # blocks in it, and every rank raises together
+        mine, err = None, None
+        try:
+            with torch.cuda.device(device):
+                self.ctx = self.lib.pk_ep_create(rank, world, capacity, hidden)
+            if not self.ctx:
+                raise RuntimeError("pk_ep_create failed")
+            t = timeout_s if timeout_s is not None else float(os.environ.get("POLYKEY_CUSTOM_AR_TIMEOUT_S", "30"))
+            self.lib.pk_ep_set_timeout_ms(self.ctx, max(1, int(t * 1000)))
+            buf = ctypes.create_string_buffer(hsz)
+            if self.lib.pk_ep_get_handle(self.ctx, buf) != 0:
+                raise RuntimeError("hipIpcGetMemHandle failed")
+            mine = bytes(buf.raw)
+        except Exception as e:  # noqa: BLE001 - re-raised after the exchange
+            err = e
         allh = [None] * world
-        dist.all_gather_object(allh, bytes(mine.raw), group=cpu_group)
+        dist.all_gather_object(allh, mine, group=cpu_group)
+        if err is not None or any(h is None for h in allh):
+            self.close()
+            raise err if err is not None else RuntimeError("an EP peer could not create its IPC regions")
         blob = ctypes.create_string_buffer(b"".join(allh), hsz * world)
         with torch.cuda.device(device):
             rc = self.lib.pk_ep_open(self.ctx, blob)
@@ -142,8 +153,17 @@ def maybe_create(st, capacity: int, hidden: int) -> Optional[EpAllToAll]:
         return None
     if st.ep_size > 8 or int(os.environ.get("LOCAL_WORLD_SIZE", str(st.world_size))) < st.ep_size:
         return None
+    a2a, err = None, None
     try:
-        return EpAllToAll(st.ep_cpu_group, st.ep_rank, st.ep_size, st.device, capacity, hidden)
+        a2a = EpAllToAll(st.ep_cpu_group, st.ep_rank, st.ep_size, st.device, capacity, hidden)
     except Exception as e:  # noqa: BLE001 - RCCL all-to-all stays
-        log.warning("IPC expert all-to-all unavailable (%s); using RCCL", e)
-        return None
+        err = e
+    # all ranks on the IPC path or none: a subset on IPC would spin on flags the others never set
+    votes = [None] * st.ep_size
+    dist.all_gather_object(votes, a2a is not None, group=st.ep_cpu_group)
+    if all(votes):
+        return a2a
+    log.warning("IPC expert all-to-all unavailable (%s); using RCCL", err or "failed on a peer")
+    if a2a is not None:
+        a2a.close()
+    return None

@@ -55,6 +55,11 @@ class ParallelState:
     # in-launch (gemm.mlp_fused) assume the whole grid is resident, which another process's
     # waiting grid can prevent -- they are not used then
     shared_device: bool = False
+    # ranks of this job on this rank's physical GPU (counted by device identity, not inferred
+    # from LOCAL_WORLD_SIZE vs the visible-device count: a rank per GPU that sees only its own
+    # device through HIP_VISIBLE_DEVICES is not sharing)
+    ranks_per_device: int = 1
+    world_cpu_group: Optional[object] = None  # gloo over every rank (start-up exchanges)
 
     @property
     def is_tp_leader(self) -> bool:
@@ -114,8 +119,7 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
                          "with tp=1 (DP attention + expert all-to-all)")
     st = ParallelState(world_size=world, rank=rank, local_rank=local, tp_size=tp, tp_rank=rank % tp,
                        dp_size=world // tp, dp_rank=rank // tp, ep_size=ep,
-                       ep_rank=rank if dp_attn else ((rank % tp) if ep > 1 else 0), device=dev,
-                       shared_device=dev.type == "cuda" and int(os.environ.get("LOCAL_WORLD_SIZE", "1")) > max(n_dev, 1))
+                       ep_rank=rank if dp_attn else ((rank % tp) if ep > 1 else 0), device=dev)
     if world > 1:
         # POLYKEY_DIST_BACKEND overrides (gloo: several ranks on one GPU, which RCCL refuses)
         be = pick_backend(dev.type, n_dev, int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
@@ -130,6 +134,9 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
                 kw["device_id"] = dev
             dist.init_process_group(**kw)
         st.backend = be
+        st.world_cpu_group = dist.group.WORLD if be == "gloo" else dist.new_group(list(range(world)), backend="gloo")
+        st.ranks_per_device = _ranks_on_my_device(st)
+        st.shared_device = dev.type == "cuda" and st.ranks_per_device > 1
         for r in range(world // tp):
             ranks = list(range(r * tp, (r + 1) * tp))
             g = dist.new_group(ranks) if tp < world else dist.group.WORLD
@@ -151,6 +158,24 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
             _create_rccl(st)
     set_state(st)
     return st
+
+
+def device_identity(dev: torch.device) -> str:
+    """Host + PCI address + UUID of a GPU (what two processes compare to tell whether they share
+    one physical device); the host alone for CPU ranks (never 'sharing')."""
+    import socket
+    host = socket.gethostname()
+    if dev.type != "cuda":
+        return f"{host}/cpu/{os.getpid()}"
+    p = torch.cuda.get_device_properties(dev)
+    return f"{host}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}/{p.uuid}"
+
+
+def _ranks_on_my_device(st: ParallelState) -> int:
+    ids = [None] * st.world_size
+    dist.all_gather_object(ids, device_identity(st.device), group=st.world_cpu_group)
+    mine = ids[st.rank]
+    return sum(1 for i in ids if i == mine)
 
 
 def _vote_board(st: ParallelState):

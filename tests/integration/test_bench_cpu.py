@@ -63,3 +63,31 @@ def test_bench_dp_attention_expert_all_to_all():
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["config"]["parallelism"] == "dp2_ep2_a2a" and out["config"]["global_batch"] == 6
     assert out["value"] == pytest.approx(3 * 4 * 2 / (out["ms_per_step"] / 1000.0), rel=0.02)
+
+
+def test_bench_world8_reports_tp_child():
+    """The 8-GPU driver launch (torchrun, 8 ranks running bench.py --gpus 8) on the CPU: rank 0
+    relays the replica measurement of a fresh 8-rank child and adds the TP=8 child's result under
+    tp8_<model> (a 70B-shaped tiny model: 8 kv heads, GQA 8, ragged vocab); a TP child that fails
+    leaves the replica number intact."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+            "--master-addr", "127.0.0.1", "--master-port", "0", os.path.join(REPO, "bench.py"), "--gpus", "8",
+            "--model", "tiny-llama-g8", "--steps", "1", "--warmup", "1", "--concurrency", "2", "--prompt-len", "8",
+            "--max-tokens", "3", "--no-graphs"]
+    r = _run(base + ["--tp-extra-model", "tiny-llama-g8"], REPO, env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 16
+    assert out["value"] == pytest.approx(2 * 3 * 8 / (out["ms_per_step"] / 1000.0), rel=0.02)
+    tp = out["tp8_tiny-llama-g8"]
+    assert "error" not in tp, tp
+    assert tp["parallelism"] == "tp8" and tp["global_batch"] == 2 and tp["scaling"] == "strong"
+    assert tp["value"] == pytest.approx(2 * 3 / (tp["ms_per_step"] / 1000.0), rel=0.02)
+    # a TP child that cannot run (unknown model) is reported in its key, the main number stays
+    r = _run(base + ["--tp-extra-model", "no-such-model", "--tp-extra-timeout", "120"], REPO, env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["value"] > 0 and "error" in out["tp8_no-such-model"]

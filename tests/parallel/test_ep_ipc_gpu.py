@@ -16,6 +16,11 @@ pytestmark = pytest.mark.gpu
 MODEL = "tiny-mixtral-e8"
 PROMPTS = {0: [[1, 5, 6, 7, 8, 9], [1, 2]], 1: [[1] + list(range(20, 60))], 3: [[1, 3, 3, 7], [1, 9]]}
 MAX_TOKENS = {0: 12, 1: 7, 3: 9}
+# skewed load: rank 0 decodes ONE sequence while its peer decodes 24, so every expert
+# on rank 0 receives more than 16 rows from the peer per step -- rank 0 must replay the graph of
+# the group's largest batch (a bucket-1 graph tiles one 16-row block per expert)
+SKEW_PROMPTS = {0: [[1, 4, 4, 2]], 1: [[1, 7 + i, 11 + 3 * i] for i in range(24)]}
+SKEW_MAX_TOKENS = {0: 10, 1: 8}
 
 
 def _port():
@@ -26,21 +31,26 @@ def _port():
     return p
 
 
-def _engine(st, graphs):
+def _engine(st, graphs, max_seqs=8):
     from polykey_service_amd.engine import EngineConfig, LLMEngine
-    return LLMEngine(EngineConfig(model=MODEL, max_num_seqs=8, max_num_batched_tokens=128, max_model_len=256,
+    return LLMEngine(EngineConfig(model=MODEL, max_num_seqs=max_seqs, max_num_batched_tokens=128, max_model_len=256,
                                   hip_graphs=graphs, device="cuda:0", prefix_caching=False), st)
 
 
-def _worker(rank, world, port, out_path):
+def _scenario(skew):
+    return (SKEW_PROMPTS, SKEW_MAX_TOKENS, 32) if skew else (PROMPTS, MAX_TOKENS, 8)
+
+
+def _worker(rank, world, port, out_path, skew=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(world), GPU_MAX_HW_QUEUES="1")
     from polykey_service_amd.engine import SamplingParams
     from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    prompts, max_tokens, max_seqs = _scenario(skew)
     st = init_parallel(tp=1, ep=world, device="cuda", backend="gloo")
-    eng = _engine(st, graphs=True)
-    seqs = [eng.add_request(p, SamplingParams(max_tokens=MAX_TOKENS[rank], ignore_eos=True))
-            for p in PROMPTS.get(rank, [])]
+    eng = _engine(st, graphs=True, max_seqs=max_seqs)
+    seqs = [eng.add_request(p, SamplingParams(max_tokens=max_tokens[rank], ignore_eos=True))
+            for p in prompts.get(rank, [])]
     while eng.any_unfinished():
         eng.step()
     torch.save({"tokens": [s.output_ids for s in seqs], "ipc": st.ep_a2a is not None,
@@ -50,11 +60,11 @@ def _worker(rank, world, port, out_path):
     destroy_parallel()
 
 
-def _reference(prompts, max_tokens):
+def _reference(prompts, max_tokens, max_seqs=8):
     """Greedy tokens and every step's logits of a single-rank engine (eager) on ``prompts``."""
     from polykey_service_amd.engine import SamplingParams
     from polykey_service_amd.parallel.state import ParallelState
-    eng = _engine(ParallelState(device=torch.device("cuda:0")), graphs=False)
+    eng = _engine(ParallelState(device=torch.device("cuda:0")), graphs=False, max_seqs=max_seqs)
     eng.runner.keep_logits = True
     seqs = [eng.add_request(p, SamplingParams(max_tokens=max_tokens, ignore_eos=True)) for p in prompts]
     steps = []
@@ -77,17 +87,18 @@ def _follows(got, ref_toks, seqs, steps, tie=0.1):
             break  # a legitimate near-tie flip: the sequences part here
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_dp_attention_ipc_expert_all_to_all_graphs(tmp_path, world):
+@pytest.mark.parametrize("world,skew", [(2, False), (8, False), (2, True)])
+def test_dp_attention_ipc_expert_all_to_all_graphs(tmp_path, world, skew):
     out = str(tmp_path / "epipc")
-    mp.start_processes(_worker, args=(world, _port(), out), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _port(), out, skew), nprocs=world, join=True, start_method="spawn")
+    all_prompts, max_tokens, max_seqs = _scenario(skew)
     for r in range(world):
         d = torch.load(f"{out}.{r}", weights_only=True)
         assert d["ipc"] and d["board"] and d["err"] == 0, d
-        prompts = PROMPTS.get(r, [])
+        prompts = all_prompts.get(r, [])
         if not prompts:
             assert d["tokens"] == [] and d["idle"] > 0  # served only the other ranks' rows
             continue
         assert d["graph_steps"] > 0, d  # decode steps replayed graphs holding the IPC all-to-all
-        ref_toks, seqs, steps = _reference(prompts, MAX_TOKENS[r])
+        ref_toks, seqs, steps = _reference(prompts, max_tokens[r], max_seqs)
         _follows(d["tokens"], ref_toks, seqs, steps)
