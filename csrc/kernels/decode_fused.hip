@@ -89,8 +89,8 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
   const int G = n_q / n_kv;
   // producer: one ticket per (head, split) tile on its kv head; consumer: (G + 2) heads x S
-  const Flow fq{flow, done, err, 0, 0, 0, 1, n_q, n_kv};
-  const Flow fa{flow, done, err, (G + 2) * g.S, n_seqs * z, 0, 2, n_q, n_kv};
+  const Flow fq{flow, done, err, 0, 0, 0, 1, n_q, n_kv, fused_spin_limit()};
+  const Flow fa{flow, done, err, (G + 2) * g.S, n_seqs * z, 0, 2, n_q, n_kv, fused_spin_limit()};
   const int n_qkv = (g.N / 128) * g.S;
   const int n_attn = n_kv * n_seqs * z;
   const dim3 grid(n_attn > n_qkv ? n_attn : n_qkv);

@@ -7,6 +7,9 @@
 // engine reads it every step without a GPU sync (the custom all-reduce's error word, the same way).
 // Null: the flow buffer's own error slot.
 int* fused_err_word();
+// Polls a consumer makes before it gives up on its tickets (pk_set_fused_spin_limit; tests shrink
+// it to force a hand-off timeout and exercise the engine's fallback to the two-launch path).
+int fused_spin_limit();
 
 namespace {
 
@@ -25,6 +28,7 @@ struct Flow {
   int role;            // 1 producer, 2 consumer
   int nq, nkv;         // > 0: producer n-blocks are the heads of a fused q | k | v projection, and
                        //   slice = the kv head a head belongs to (GQA group of q, or k / v head)
+  int spin_limit = 1 << 20;  // polls before a wait gives up (~0.5 s; fused_spin_limit()); < 0: test hook
 };
 
 // slice of producer n-block nb: a QKV head's kv head, or nb's output columns / cols_per_slice
@@ -63,9 +67,11 @@ __device__ __forceinline__ void flow_signal(const Flow& fl, int slice) {
 __device__ __forceinline__ void flow_wait(const Flow& fl, int slice) {
   if (threadIdx.x == 0) {
     int spins = 0;
+    if (fl.spin_limit < 0)  // test hook (pk_set_fused_spin_limit(-1)): report a lost hand-off
+      __hip_atomic_store(fl.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     while (__hip_atomic_load(fl.ready + kFlowPad * slice, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fl.need) {
       __builtin_amdgcn_s_sleep(16);  // ~0.5 us between polls: pollers must not load the memory channel of the line
-      if (++spins > (1 << 20)) {
+      if (++spins > fl.spin_limit) {
         __hip_atomic_store(fl.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }

@@ -525,8 +525,8 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   gu.max_group_rows = dn.max_group_rows = 0;
   int* done = flow + 64 * kFlowPad;
   int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
-  Flow fgu{flow, done, err, 0, 0, dn.K / dn.S, 1};
-  Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / 128, dn.K / dn.S, 2};
+  Flow fgu{flow, done, err, 0, 0, dn.K / dn.S, 1, 0, 0, fused_spin_limit()};
+  Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / 128, dn.K / dn.S, 2, 0, 0, fused_spin_limit()};
   const int n_gu = gu.N / 128, n_dn = (dn.N / 128) * dn.S;
   const dim3 grid(n_gu > n_dn ? n_gu : n_dn);
   switch ((gu.M + 15) / 16) {
@@ -540,6 +540,18 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
 
 static int* g_fused_err = nullptr;
 int* fused_err_word() { return g_fused_err; }
+static int g_fused_spin_limit = 1 << 20;
+int fused_spin_limit() { return g_fused_spin_limit; }
+
+// Polls a fused launch's consumer makes before it declares its hand-off lost (default 2^20, ~0.5 s;
+// n == 0 restores it).  n < 0 is a test hook: every wait reports a lost hand-off (the results are
+// still computed correctly), so tests can drive the engine's fallback deterministically.
+PK_EXPORT void pk_set_fused_spin_limit(int n) { g_fused_spin_limit = n != 0 ? n : (1 << 20); }
+
+// Re-arm the sticky word after the engine has fallen back to the two-launch path.
+PK_EXPORT void pk_clear_fused_err() {
+  if (g_fused_err != nullptr) __atomic_store_n(g_fused_err, 0, __ATOMIC_SEQ_CST);
+}
 
 // The fused launches' sticky timeout word in host-mapped, coherent pinned memory (allocated once per
 // process): returns its address (the host reads it with a plain load; 0 = no wait ever timed out).

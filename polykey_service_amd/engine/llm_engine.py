@@ -182,9 +182,9 @@ class LLMEngine:
         if self._inflight is not None:
             batch, sampling, handle = self._inflight
             nxt = self._continuation(batch, handle)
-            done = self._complete(batch, sampling, handle)
+            done, redone = self._complete_or_redo(batch, sampling, handle)
             self._inflight = None
-            if nxt is not None:
+            if nxt is not None and not redone:  # a redone step's continuation ran on its bad tokens
                 self._inflight = (batch, batch.decodes, nxt)
                 self.continuation_steps += 1
                 return self._outputs(done)
@@ -193,9 +193,24 @@ class LLMEngine:
             sampling = batch.sampling_seqs()
             self._inflight = (batch, sampling, self.runner.launch(batch))
             if not self.overlap:
-                done = self._complete(*self._inflight)
+                done, _ = self._complete_or_redo(*self._inflight)
                 self._inflight = None
         return self._outputs(done) if done else []
+
+    def _complete_or_redo(self, batch, sampling, handle):
+        """``_complete`` of a launched step; if a fused decode launch of it lost its in-launch
+        hand-off (FusedHandoffError: co-tenant on the GPU), the runner falls back to the
+        two-launch path and the step is launched again -- the sequences' state is untouched until
+        a step completes and the re-run rewrites the same KV slots.  A TP / lockstep group cannot
+        re-run one rank alone: there the error stays fatal.  Returns (done, redone)."""
+        from ..ops.gemm import FusedHandoffError
+        try:
+            return self._complete(batch, sampling, handle), False
+        except FusedHandoffError:
+            if self.st.tp_size > 1 or self.lockstep:
+                raise
+            self.runner.fallback_unfused()  # drains the GPU: an in-flight continuation is finished
+            return self._complete(batch, sampling, self.runner.launch(batch)), True
 
     def _step_lockstep(self) -> List[RequestOutput]:
         """DP attention + EP step: one lockstep vote (shared memory on one node) per step decides

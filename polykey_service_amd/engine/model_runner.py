@@ -472,6 +472,30 @@ class ModelRunner:
                 self._prev_toks = toks
             self.stats["steps"] += 1
 
+    def fallback_unfused(self) -> None:
+        """A fused decode launch lost an in-launch hand-off (another process on this GPU kept part
+        of its grid from being resident): wait for the GPU, re-arm the sticky word, switch this
+        process to the two-launch path for good (WARN) and re-capture the decode graphs that held
+        the fused kernels.  The caller re-runs the step (LLMEngine._complete_or_redo)."""
+        import logging
+        logging.getLogger(__name__).warning(
+            "fused decode launch hand-off timed out (GPU shared with another process?): the failed step is "
+            "re-run and every later step takes the two-launch path")
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        gemm.disable_fused()
+        gemm.clear_fused_error()
+        self.stats["fused_fallbacks"] = self.stats.get("fused_fallbacks", 0) + 1
+        if self.graphs:
+            sizes = sorted(self.graphs)
+            self.graphs.clear()
+            self.graph_out.clear()
+            self.short_graphs.clear()
+            self.short_graph_out.clear()
+            self._graph_logits.clear()
+            self.graph_pool = None
+            self.capture_graphs(sizes)
+
     def abort_comms(self) -> None:
         """Watchdog / failure path: tear down this rank's RCCL communicators (a collective hung on
         a dead peer returns) and mark the IPC collectives failed (every later call skips its

@@ -438,9 +438,9 @@ class LlamaForCausalLM(nn.Module):
         for i, layer in enumerate(self.layers):
             at, mlp = layer.attn, layer.mlp
             kc, vc = kv_caches[i]
-            if (md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and T <= gemm.SKINNY_MAX_M and not self.st.shared_device
-                    and md.num_decode == T):
-                # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip)
+            if md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and T <= gemm.SKINNY_MAX_M and md.num_decode == T:
+                # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip);
+                # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
                 a = gemm.qkv_attn_fused(residual, at.qkv_pf, gemm.RowScale(parts, layer.eps), ws, positions,
                                         self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv, self._flow_qkv)
             else:

@@ -392,13 +392,41 @@ def fused_err_word() -> int:
     return _FUSED_ERR
 
 
+class FusedHandoffError(RuntimeError):
+    """An in-launch hand-off of a fused decode launch timed out: its outputs are invalid."""
+
+
 def check_fused() -> None:
-    """Raise once any in-launch hand-off wait of a fused decode launch timed out: that launch's
-    outputs were computed from data that had not arrived (cannot happen while every workgroup of
-    the grid is resident; a GPU shared with other processes could break that).  A plain read of
-    host memory, no GPU sync: the engine calls it every step like the collectives' error words."""
+    """Raise :class:`FusedHandoffError` once any in-launch hand-off wait of a fused decode launch
+    timed out: that launch's outputs were computed from data that had not arrived (cannot happen
+    while every workgroup of the grid is resident; another process on the same GPU could break
+    that).  A plain read of host memory, no GPU sync: the engine calls it every step like the
+    collectives' error words, and falls back to the two-launch path (LLMEngine)."""
     if _FUSED_ERR is not None and ctypes.c_int.from_address(_FUSED_ERR).value != 0:
-        raise RuntimeError("a fused decode launch's in-kernel hand-off timed out (results invalid)")
+        raise FusedHandoffError("a fused decode launch's in-kernel hand-off timed out (results invalid)")
+
+
+def clear_fused_error() -> None:
+    """Re-arm the sticky word (after the caller has stopped using the fused launches)."""
+    if _FUSED_ERR is not None:
+        fn = native.lib().pk_clear_fused_err
+        fn.restype, fn.argtypes = None, []
+        fn()
+
+
+def disable_fused() -> None:
+    """Every later decode step takes the two-launch path (QKV | attention, gate_up | down)."""
+    global MLP_FUSED, QKV_ATTN_FUSED
+    MLP_FUSED = False
+    QKV_ATTN_FUSED = False
+
+
+def set_fused_spin_limit(n: int) -> None:
+    """Tests: polls a fused consumer makes before declaring its hand-off lost (0: default; < 0:
+    every wait reports a lost hand-off, to drive the engine's fallback deterministically)."""
+    fn = native.lib().pk_set_fused_spin_limit
+    fn.restype, fn.argtypes = None, [ctypes.c_int]
+    fn(int(n))
 
 
 def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_packed: Optional[torch.Tensor]) -> bool:

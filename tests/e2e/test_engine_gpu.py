@@ -218,3 +218,42 @@ def test_large_decode_batches_match_small(batch):
     same = [i for i in range(8) if fbig[i] == fsmall[i]]
     assert len(same) >= 6, (fbig[:8], fsmall)
     torch.testing.assert_close(big[same], small[same], atol=0.02 * scale, rtol=0.05)
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_fused_handoff_timeout_falls_back_to_two_launches(overlap):
+    """Co-tenancy safety of the fused decode launches: a lost in-launch hand-off (forced here by
+    the spin-limit test hook, which makes every consumer wait report a timeout) does not kill the
+    engine.  The failed step is re-run on the two-launch path, the decode graphs are re-captured
+    without the fused kernels, the fallback is counted once, and every token equals the engine
+    that never used the fused launches."""
+    from polykey_service_amd.ops import gemm
+    _, gpu = _models("tiny-llama-gqa4")
+    prompts = [[1] + list(range(5, 5 + n)) for n in (3, 17, 40)]
+    sp = SamplingParams(max_tokens=12, ignore_eos=True)
+    saved = (gemm.MLP_FUSED, gemm.QKV_ATTN_FUSED)
+
+    def engine():
+        return LLMEngine(EngineConfig(model="tiny-llama-gqa4", max_num_seqs=8, max_num_batched_tokens=256,
+                                      max_model_len=512, hip_graphs=True, device="cuda", overlap=overlap),
+                         ParallelState(device=torch.device("cuda")), model=gpu)
+    try:
+        gemm.disable_fused()
+        ref = engine().generate(prompts, sp)  # the two-launch chain throughout
+        gemm.MLP_FUSED, gemm.QKV_ATTN_FUSED = saved
+        assert gemm.MLP_FUSED and gemm.QKV_ATTN_FUSED
+        gemm.set_fused_spin_limit(-1)
+        e = engine()  # graph capture itself runs the fused kernels: the word is set from the start
+        seqs = [e.add_request(p, sp) for p in prompts]
+        while e.has_unfinished():
+            e.step()
+        gemm.set_fused_spin_limit(0)
+        assert e.runner.stats.get("fused_fallbacks") == 1, e.runner.stats
+        assert not gemm.MLP_FUSED and not gemm.QKV_ATTN_FUSED
+        gemm.check_fused()  # re-armed
+        assert e.runner.stats["graph_steps"] > 0  # re-captured graphs served the rest
+        assert [s.output_ids for s in seqs] == ref
+    finally:
+        gemm.set_fused_spin_limit(0)
+        gemm.clear_fused_error()
+        gemm.MLP_FUSED, gemm.QKV_ATTN_FUSED = saved
