@@ -94,6 +94,9 @@ class LLMEngine:
                 self.st.ep_a2a_prefill = ep_ipc.maybe_create(
                     self.st, max(cfg.max_num_batched_tokens, cfg.max_num_seqs) * mcfg.experts_per_token,
                     mcfg.hidden_size)
+            if self.st.ep_a2a is not None and os.environ.get("POLYKEY_PREFLIGHT", "1") != "0":
+                from ..parallel import preflight  # dispatch / return checked once; a failure -> RCCL path
+                preflight.run(self.st, paths=("ep_ipc",))
             cfg = dataclasses.replace(cfg, overlap=False,
                                       hip_graphs=cfg.hip_graphs and self.st.ep_a2a is not None)
             self.cfg = cfg

@@ -1,0 +1,207 @@
+"""Multi-GPU preflight (SURVEY.md §5.8 "comm backend"): before the first
+step, every device collective the engine will use is run once on a few KB of rank-seeded data and
+checked against the exact result, which every rank computes locally from the same seeds:
+
+* the direct RCCL communicators (``parallel/rccl.py``): all-reduce, all-gather, reduce-scatter
+  (TP / SP), all-to-allv (expert dispatch);
+* the IPC collectives of ``csrc/comm/custom_allreduce.hip`` beyond its own start-up all-reduce
+  self-test: the one-shot all-gather (LM-head logits) and the fused decode collective
+  (``reduce_residual``: partial sum + xGMI peer sum + residual add + norm parts);
+* the IPC expert all-to-all (``csrc/comm/ep_alltoall.hip``): dispatch and return.
+
+The verdict of each check is agreed over the group's gloo control group (all ranks keep a path
+or none does, so no rank ever waits in a collective its peers abandoned) and a failed path is
+disabled -- the engine falls back to the next one (RCCL direct -> torch.distributed, IPC ->
+RCCL) exactly as if it had never been created.  One JSON line per rank that saw a failure (and
+always on rank 0) records the peer-access matrix, every check and every fallback, so the first
+one-rank-per-GPU run on a new node is diagnosable from its log alone.
+"""
+from __future__ import annotations
+
+import json
+import sys
+import time
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .state import ParallelState
+
+
+def _pattern(rank: int, n: int, dtype=torch.bfloat16, device="cpu", salt: int = 0) -> torch.Tensor:
+    """Small integers (exact in bf16 and in any summation order) that differ per rank."""
+    i = torch.arange(n, dtype=torch.int64)
+    return (((i * (rank + 3) + 7 * rank + salt) % 13) - 6).to(dtype).to(device)
+
+
+def _close(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return a.shape == b.shape and bool(torch.equal(a.float().cpu(), b.float().cpu()))
+
+
+def _sync(dev: torch.device) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+# ----------------------------------------------------------------------------------- checks
+def check_rccl(rc, rank: int, world: int, dev: torch.device) -> Dict[str, bool]:
+    """all_reduce / all_gather / reduce_scatter / all_to_allv of a direct communicator."""
+    out = {}
+    n = 1024 * world
+    x = _pattern(rank, n, device=dev)
+    want = sum(_pattern(r, n) for r in range(world))
+    y = rc.all_reduce(x.clone())
+    _sync(dev)
+    out["all_reduce"] = _close(y, want)
+    g = rc.all_gather(_pattern(rank, 256, device=dev, salt=1))
+    _sync(dev)
+    out["all_gather"] = _close(g, torch.cat([_pattern(r, 256, salt=1) for r in range(world)]))
+    rs = rc.reduce_scatter(_pattern(rank, n, device=dev, salt=2))
+    _sync(dev)
+    full = sum(_pattern(r, n, salt=2) for r in range(world))
+    out["reduce_scatter"] = _close(rs, full.view(world, -1)[rank])
+    # all-to-allv with uneven splits: rank r sends (r + j) % 3 + 1 rows of width 8 to rank j
+    sends = [(rank + j) % 3 + 1 for j in range(world)]
+    recvs = [(j + rank) % 3 + 1 for j in range(world)]
+    rows = torch.cat([_pattern(rank, sends[j] * 8, device=dev, salt=10 + j).view(-1, 8) for j in range(world)])
+    a2a = rc.all_to_allv(rows, recvs, sends)
+    _sync(dev)
+    out["all_to_allv"] = _close(a2a, torch.cat([_pattern(j, recvs[j] * 8, salt=10 + rank).view(-1, 8)
+                                                for j in range(world)]))
+    return out
+
+
+def check_custom_ar(car, rank: int, world: int, dev: torch.device) -> Dict[str, bool]:
+    """The IPC all-gather and the fused decode collective (reduce_residual) of custom_ar."""
+    out = {}
+    x = _pattern(rank, 4 * 64, device=dev, salt=3).view(4, 64)
+    if car.supports_gather(x):
+        g = car.all_gather_last(x)
+        _sync(dev)
+        out["all_gather_1shot"] = _close(g, torch.cat([_pattern(r, 256, salt=3).view(4, 64) for r in range(world)], -1))
+    M, N = 2, 1024
+    if car.supports_reduce_residual(M, N):
+        part = _pattern(rank, M * N, device=dev, salt=4).view(M, N)
+        res0 = _pattern(0, M * N, salt=5).view(M, N)
+        residual = res0.to(dev).clone()
+        parts = torch.zeros((N // 1024) * M, dtype=torch.float32, device=dev)
+        p = car.reduce_residual(part.contiguous(), residual, parts)
+        _sync(dev)
+        want = res0.float() + sum(_pattern(r, M * N, salt=4).view(M, N).float() for r in range(world))
+        out["reduce_residual"] = _close(residual, want.to(torch.bfloat16)) and bool(
+            torch.allclose(p.float().cpu(), want.pow(2).sum(-1).view(1, M), rtol=1e-5))
+    return out
+
+
+def check_ep_ipc(a2a, rank: int, world: int, dev: torch.device) -> Dict[str, bool]:
+    """Dispatch + return of the IPC expert all-to-all: rank r sends (r + j) % 2 + 1 rows to rank j
+    (expert id j + 10 * row), the owners return each row doubled."""
+    H = a2a.H
+    sends = [(rank + j) % 2 + 1 for j in range(world)]
+    if sum(sends) > a2a.C:
+        return {}
+    rows = torch.cat([_pattern(rank, sends[j] * H, device=dev, salt=20 + j).view(-1, H) for j in range(world)])
+    ids = torch.cat([torch.arange(sends[j], dtype=torch.int32) * 10 + j for j in range(world)]).to(dev)
+    offs = torch.tensor([0] + list(torch.tensor(sends).cumsum(0)), dtype=torch.int32, device=dev)
+    a2a.dispatch(rows.contiguous(), ids, offs)
+    _sync(dev)
+    ok = True
+    for j in range(world):  # region j of this rank holds rank j's rows for this rank
+        n = (j + rank) % 2 + 1
+        got = a2a.recv_x[j * a2a.C: j * a2a.C + n]
+        ok &= _close(got, _pattern(j, n * H, salt=20 + rank).view(-1, H))
+        ok &= bool(torch.equal(a2a.recv_e[j * a2a.C: j * a2a.C + n].cpu(),
+                               torch.arange(n, dtype=torch.int32) * 10 + rank))
+    y = (a2a.recv_x.float() * 2).to(torch.bfloat16).contiguous()
+    back = a2a.return_(y)
+    _sync(dev)
+    ok2 = _close(back[: rows.shape[0]], (rows.float() * 2).to(torch.bfloat16))
+    return {"dispatch": bool(ok), "return": bool(ok2)}
+
+
+# ------------------------------------------------------------------------------------- run
+def _agree(ok: bool, group, world: int) -> bool:
+    votes = [None] * world
+    dist.all_gather_object(votes, bool(ok), group=group)
+    return all(votes)
+
+
+def _safe(fn: Callable[[], Dict[str, bool]]) -> Tuple[Dict[str, bool], Optional[str]]:
+    try:
+        return fn(), None
+    except Exception as e:  # noqa: BLE001 - a raising path fails its check
+        return {}, f"{type(e).__name__}: {e}"
+
+
+def peer_access(st: ParallelState) -> Optional[List[List[int]]]:
+    """Row r: can rank r's device read each rank's device (hipDeviceCanAccessPeer)?  None when
+    the ranks do not all see each other's devices (per-rank visibility) or run on the CPU."""
+    if st.device.type != "cuda" or st.world_cpu_group is None:
+        return None
+    devs = [None] * st.world_size
+    dist.all_gather_object(devs, st.device.index, group=st.world_cpu_group)
+    n = torch.cuda.device_count()
+    if any(d is None or d >= n for d in devs):
+        row = None
+    else:
+        me = st.device.index
+        row = [1 if d == me else int(torch.cuda.can_device_access_peer(me, d)) for d in devs]
+    rows = [None] * st.world_size
+    dist.all_gather_object(rows, row, group=st.world_cpu_group)
+    return None if any(r is None for r in rows) else rows
+
+
+def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit: Callable[[str], None] = None) -> dict:
+    """Check every created device-collective path in ``paths`` ("rccl", "custom_ar", "ep_ipc"),
+    disable the failed ones on every rank, return (and emit) the report."""
+    t0 = time.perf_counter()
+    report = {"event": "multi_gpu_preflight", "rank": st.rank, "world": st.world_size, "backend": st.backend,
+              "ranks_per_device": st.ranks_per_device, "checks": {}, "disabled": []}
+    if "rccl" in paths or "custom_ar" in paths:
+        report["peer_access"] = peer_access(st)
+    dev = st.device
+
+    def verdict(name, res, err, group, world, disable):
+        ok = bool(res) and all(res.values()) and err is None
+        agreed = _agree(ok, group, world)
+        report["checks"][name] = {"ok": ok, "group_ok": agreed, **({"error": err} if err else {}),
+                                  **{k: v for k, v in res.items()}}
+        if not agreed:
+            disable()
+            report["disabled"].append(name)
+
+    if "rccl" in paths and st.rccl_tp is not None and st.tp_size > 1:
+        res, err = _safe(lambda: check_rccl(st.rccl_tp, st.tp_rank, st.tp_size, dev))
+
+        def off_tp():
+            if st.rccl_ep is st.rccl_tp:
+                st.rccl_ep = None
+            st.rccl_tp = None
+        verdict("rccl_tp", res, err, st.tp_cpu_group, st.tp_size, off_tp)
+    if "rccl" in paths and st.rccl_ep is not None and st.rccl_ep is not st.rccl_tp and st.ep_size > 1:
+        res, err = _safe(lambda: check_rccl(st.rccl_ep, st.ep_rank, st.ep_size, dev))
+        verdict("rccl_ep", res, err, st.ep_cpu_group, st.ep_size, lambda: setattr(st, "rccl_ep", None))
+    if "custom_ar" in paths and st.custom_ar is not None:
+        car = st.custom_ar
+        res, err = _safe(lambda: check_custom_ar(car, st.tp_rank, st.tp_size, dev))
+
+        def off_car():
+            car.close()
+            st.custom_ar = None
+        verdict("custom_ar", res, err, st.tp_cpu_group, st.tp_size, off_car)
+    if "ep_ipc" in paths and st.ep_a2a is not None:
+        a2a = st.ep_a2a
+        res, err = _safe(lambda: check_ep_ipc(a2a, st.ep_rank, st.ep_size, dev))
+
+        def off_ep():
+            for x in (st.ep_a2a, st.ep_a2a_prefill):
+                if x is not None:
+                    x.close()
+            st.ep_a2a = st.ep_a2a_prefill = None
+        verdict("ep_ipc", res, err, st.ep_cpu_group, st.ep_size, off_ep)
+    report["seconds"] = round(time.perf_counter() - t0, 3)
+    if st.rank == 0 or report["disabled"] or any(not c["ok"] for c in report["checks"].values()):
+        line = json.dumps(report)
+        (emit or (lambda s: print(s, file=sys.stderr, flush=True)))(line)
+    return report

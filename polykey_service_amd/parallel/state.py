@@ -156,6 +156,12 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
             st.custom_ar = maybe_create(st)
         if be == "nccl" and os.environ.get("POLYKEY_RCCL_DIRECT", "1") == "1":
             _create_rccl(st)
+        # every device collective path checked once on a few KB before the first step; a failed
+        # one is disabled on all ranks (parallel/preflight.py).  POLYKEY_PREFLIGHT=0 skips it.
+        if os.environ.get("POLYKEY_PREFLIGHT", "1") != "0" and (st.rccl_tp is not None or st.rccl_ep is not None
+                                                                 or st.custom_ar is not None):
+            from . import preflight
+            preflight.run(st)
     set_state(st)
     return st
 
