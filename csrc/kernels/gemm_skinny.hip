@@ -45,13 +45,16 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 // workgroup is resident at once (one per CU) and a gate_up tile never waits: no deadlock.
 // (A/B, tools/gpu/mlp_ab.sh: down tiles as workgroups of their own, dispatched after the gate_up
 // ones, put two down tiles on some CUs and lost 7 us per layer.)
-template <int MT>
+// SPLIT: gate_up split over K (gu.S > 1; kSiluSplit: write-through slabs, the last split of an
+// n-block sums them, applies SiLU and publishes h) -- for shapes whose gate_up n-blocks alone
+// cannot fill the chip (70B TP=8: 56).
+template <int MT, bool SPLIT>
 __global__ void __launch_bounds__(256, 2) mlp_fused_kernel(const GemmArgs gu, const GemmArgs dn, const Flow fgu,
                                                            const Flow fdn, int n_gu, int n_dn) {
   __shared__ SkinnyLds<MT> lds;
   const int b = blockIdx.x;
   if (b < n_gu) {
-    skinny_tile<MT, kSiluMul, true, false, true, true, 2, 1>(gu, b, 0, n_gu, lds, fgu);
+    skinny_tile<MT, SPLIT ? kSiluSplit : kSiluMul, true, false, true, true, 2, 1>(gu, b, 0, n_gu, lds, fgu);
     __syncthreads();  // the LDS tiles are reused by the down tile
   }
   if (b < n_dn) skinny_tile<MT, kPartial, true, false, false, false, 2, 2>(dn, b, 0, n_dn, lds, fdn);
@@ -507,19 +510,24 @@ PK_EXPORT int pk_skinny_gemm_ex(const GemmArgs* args, int mode, hipStream_t stre
 }
 
 // Fused decode MLP (mlp_fused_kernel): gu = gate_up + SiLU (packed, non-temporal, folded norm:
-// row_scale + nrm_parts), dn = down split-K slabs (packed) reading gu's output.  flow: a zeroed
-// int buffer of >= 128 * 64 + 1 words (64 tickets and 64 consumer counts, 64 words apart, then
-// the sticky error word),
-// left zeroed by every launch that completes.
+// row_scale + nrm_parts; gu.S > 1: split over K with fp32 slabs in gu.partial), dn = down split-K
+// slabs (packed) reading gu's output.  flow: a zeroed int buffer of >= kFlowWords words (64
+// tickets and 64 consumer counts, 64 words apart, the sticky error word, then the gate_up split
+// counters), left zeroed by every launch that completes.
+constexpr int kFlowCounters = 128 * kFlowPad + 64;  // gate_up n-block counters (kSiluSplit)
+constexpr int kFlowWords = kFlowCounters + 1024;
+
 PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, hipStream_t stream) {
   GemmArgs gu = *gu_in, dn = *dn_in;
   if (gu.M <= 0) return 0;
-  if (gu.M > 64 || dn.M != gu.M || gu.N % 128 || gu.K % kKC || !gu.row_scale || gu.nrm_parts == nullptr ||
-      gu.nrm_nparts < 1 || gu.nrm_nparts > 64 || gu.out == nullptr || dn.K != gu.N / 2 || dn.N % 128 || dn.S < 1 ||
-      dn.S > 64 || dn.K % (kKC * dn.S) || (dn.K / dn.S) % 64 || dn.partial == nullptr || dn.A != gu.out ||
-      dn.lda % 8 || gu.lda % 8 || gu.row_offsets != nullptr || dn.row_offsets != nullptr || flow == nullptr)
+  if (gu.M > 64 || dn.M != gu.M || gu.N % 128 || gu.S < 1 || gu.K % (kKC * gu.S) || !gu.row_scale ||
+      gu.nrm_parts == nullptr || gu.nrm_nparts < 1 || gu.nrm_nparts > 64 || gu.out == nullptr || dn.K != gu.N / 2 ||
+      dn.N % 128 || dn.S < 1 || dn.S > 64 || dn.K % (kKC * dn.S) || (dn.K / dn.S) % 64 || dn.partial == nullptr ||
+      dn.A != gu.out || dn.lda % 8 || gu.lda % 8 || gu.row_offsets != nullptr || dn.row_offsets != nullptr ||
+      flow == nullptr || (gu.S > 1 && (gu.partial == nullptr || gu.N / 128 > kFlowWords - kFlowCounters)))
     return -1;
-  gu.S = 1;
+  const bool split = gu.S > 1;
+  gu.counters = split ? flow + kFlowCounters : nullptr;
   gu.row_tiles = dn.row_tiles = 1;
   gu.tile_rows = dn.tile_rows = 64;
   gu.max_group_rows = dn.max_group_rows = 0;
@@ -527,16 +535,25 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
   Flow fgu{flow, done, err, 0, 0, dn.K / dn.S, 1, 0, 0, fused_spin_limit()};
   Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / 128, dn.K / dn.S, 2, 0, 0, fused_spin_limit()};
-  const int n_gu = gu.N / 128, n_dn = (dn.N / 128) * dn.S;
+  const int n_gu = (gu.N / 128) * gu.S, n_dn = (dn.N / 128) * dn.S;
   const dim3 grid(n_gu > n_dn ? n_gu : n_dn);
-  switch ((gu.M + 15) / 16) {
-    case 1: mlp_fused_kernel<1><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-    case 2: mlp_fused_kernel<2><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-    case 3: mlp_fused_kernel<3><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-    default: mlp_fused_kernel<4><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-  }
+  auto go = [&](auto sp) {
+    constexpr bool SP = decltype(sp)::value;
+    switch ((gu.M + 15) / 16) {
+      case 1: mlp_fused_kernel<1, SP><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      case 2: mlp_fused_kernel<2, SP><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      case 3: mlp_fused_kernel<3, SP><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      default: mlp_fused_kernel<4, SP><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+    }
+  };
+  if (split)
+    go(std::true_type{});
+  else
+    go(std::false_type{});
   return PK_CHECK_LAUNCH();
 }
+
+PK_EXPORT int pk_flow_words() { return kFlowWords; }
 
 static int* g_fused_err = nullptr;
 int* fused_err_word() { return g_fused_err; }

@@ -55,7 +55,10 @@ namespace {
 //                of the new residual, consumed by the next GEMM's RMSNorm prologue;
 //   kQkvRope:    128-column n-block = one head: RoPE (neox) for q / k heads, q -> out, k -> K
 //                cache, v -> transposed V cache at the token's slot (slot < 0: not cached).
-enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4 };
+//   kSiluSplit:  interleaved gate / up split over K (the fused MLP's gate_up when N / 128 tiles
+//                alone cannot fill the chip, e.g. 70B TP=8: 56 n-blocks): silu(gate) * up of the
+//                summed slabs -> h, stored write-through for the in-launch hand-off.
+enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4, kSiluSplit = 5 };
 constexpr int kMaxRows = 1024;  // decode batch bound of the row-tiled modes
 constexpr int kPartCols = 512;  // columns per sum-of-squares part (residual_parts_kernel)
 
@@ -138,7 +141,39 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
   constexpr int NCOL = 64 * KR;  // columns of an n-block
   const int nbase = nb * NCOL;
   constexpr int RB = (SS == 0 || SS >= 16) ? 1 : (SS == 8 ? 2 : 4);  // rows per thread per batch
-  if constexpr (MODE == kAddResNorm) {
+  if constexpr (MODE == kSiluSplit) {
+    // 128 slab columns = 4 waves x (16 gate | 16 up) -> 64 h columns; 16 threads per row, each
+    // 4 gate columns and their 4 up columns (16 further), the same arithmetic as kSiluMul's
+    // single-pass epilogue on the summed slabs
+    static_assert(KR == 2, "gate / up pairs need 32-row wave tiles");
+    const int q = tid & 15, wv = q >> 2, j = (q & 3) * 4;
+    const int gc = nbase + wv * 32 + j;
+    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(args.out, static_cast<short>(0), 0x7ffffff0, 0x00020000);
+    for (int m0 = tid >> 4; m0 < M; m0 += 16 * RB) {
+      float4 g[RB], u[RB];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int m = min(m0 + 16 * i, M - 1);
+        const float* src = args.partial + static_cast<int64_t>(m) * N + gc;
+        g[i] = slab_sum<SS, true>(src, slab, S, args.partial);
+        u[i] = slab_sum<SS, true>(src + 16, slab, S, args.partial);
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int m = m0 + 16 * i;
+        if (m >= M) break;
+        const float gv[4] = {g[i].x, g[i].y, g[i].z, g[i].w}, uv[4] = {u[i].x, u[i].y, u[i].z, u[i].w};
+        float y[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = rbf(silu(rbf(gv[e]))) * rbf(uv[e]);
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        const bf16_t* o = args.out + static_cast<int64_t>(m) * args.ldo + nb * 64 + wv * 16 + j;
+        // handed off in-launch to the down tiles: write-through (sc1) stores
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack2(y[0], y[1]), pack2(y[2], y[3])}, orsrc,
+                                              static_cast<int>((o - args.out) * 2), 0, 16);
+      }
+    }
+  } else if constexpr (MODE == kAddResNorm) {
     // TPR threads per row (4 columns each), RPP rows per pass of the workgroup
     constexpr int TPR = NCOL / 4, RPP = 256 / TPR;
     const int c = nbase + (tid % TPR) * 4;
@@ -538,11 +573,11 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   }
 
   // C^T tile: rows = W rows (n), cols = m:  acc[t][mt][i] = C[m = 16*mt + r][n = n0 + 16*t + 4*g + i]
-  constexpr bool kSlab = MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope;
+  constexpr bool kSlab = MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit;
   // the in-launch residual update hands its slabs over write-through (measured faster than plain
   // stores + release: tools/gemm_lab.hip o_res / down_res); the plain split-K slabs are read by
   // the next kernel and stay plain (write-through made those slower)
-  constexpr bool kSlabSc1 = MODE == kAddResNorm || PK_SLAB_SC1 || (MODE == kPartial && FL == 1);
+  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kSiluSplit || PK_SLAB_SC1 || (MODE == kPartial && FL == 1);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = 16 * mt + r;
@@ -606,7 +641,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   }
   if constexpr ((MODE == kSiluMul || MODE == kPartial) && FL == 1)  // output columns of n-block nb
     flow_signal(fl, flow_slice(fl, nb, MODE == kSiluMul ? 64 * kR / 2 : 64 * kR));
-  if constexpr (MODE == kAddResNorm || MODE == kQkvRope) {
+  if constexpr (MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit) {
     // ---- in-launch split-K reduction by the last split of this n-block to arrive
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -636,6 +671,8 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       case 16: epilogue<MODE, 16, KR>(args, nb); break;
       default: epilogue<MODE, 0, KR>(args, nb); break;
     }
+    if constexpr (MODE == kSiluSplit && FL == 1)  // h columns of n-block nb are out: one ticket
+      flow_signal(fl, flow_slice(fl, nb, 64));
   }
 }
 

@@ -117,6 +117,12 @@ class LlamaAttention(nn.Module):
         self.qkv_p = None  # block-packed decode copies (LlamaForCausalLM.pack_decode_weights)
         self.o_p = None
         self.qkv_pf = None  # block-packed with ln1 folded in (FOLD_NORM)
+        # fault injection for the TP correctness tests (LlamaForCausalLM, POLYKEY_FAULT_DROP_PARTIAL):
+        # this rank's o-projection input is zeroed, i.e. its partial never reaches the collective
+        self.fault_drop = False
+
+    def drop(self, a: torch.Tensor) -> torch.Tensor:
+        return a.zero_() if self.fault_drop else a
 
     def forward(self, x: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
                 kv: Tuple[torch.Tensor, torch.Tensor], ws: Optional[torch.Tensor] = None):
@@ -132,15 +138,15 @@ class LlamaAttention(nn.Module):
                 # and writes the new k / v into the paged cache
                 a = attn_ops.paged_decode_from_qkv(p, positions, cos_sin, k_cache, v_cache, md, self.scale,
                                                    self.nq, self.nkv)
-                return _proj_out(a, self.o, ws, self.o_p, half=True)
+                return _proj_out(self.drop(a), self.o, ws, self.o_p, half=True)
             # split-K QKV whose epilogue kernel also applies RoPE and writes the KV cache
             q = gemm.qkv_reduce_rope_cache(p, positions, cos_sin, k_cache, v_cache, md.slot_mapping, self.nq,
                                            self.nkv)
         else:
-            return _proj_out(self.attend(gemm.linear(x, self.qkv, packed=self.qkv_p), positions, md, cos_sin, kv),
-                             self.o, ws, self.o_p)
+            return _proj_out(self.drop(self.attend(gemm.linear(x, self.qkv, packed=self.qkv_p), positions, md,
+                                                   cos_sin, kv)), self.o, ws, self.o_p)
         a = attn_ops.paged_attention(q, k_cache, v_cache, md, self.scale)
-        return _proj_out(a, self.o, ws, self.o_p, half=True)
+        return _proj_out(self.drop(a), self.o, ws, self.o_p, half=True)
 
     def attend(self, qkv: torch.Tensor, positions: torch.Tensor, md: attn_ops.AttnMetadata, cos_sin: torch.Tensor,
                kv: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
@@ -196,6 +202,13 @@ class LlamaForCausalLM(nn.Module):
             self.vocab_local = (self.vocab_local + 127) // 128 * 128
         self.vocab_start = self.st.tp_rank * self.vocab_local
         self.layers = nn.ModuleList([LlamaLayer(cfg, self.st, self._make_mlp(i)) for i in range(cfg.num_layers)])
+        # POLYKEY_FAULT_DROP_PARTIAL=<layer>,<tp rank>: a deliberately wrong TP model (that rank's
+        # attention partial of that layer is dropped) -- the TP=8 correctness test must fail on it
+        fault = os.environ.get("POLYKEY_FAULT_DROP_PARTIAL")
+        if fault:
+            li, rk = (int(v) for v in fault.split(","))
+            if rk == self.st.tp_rank and 0 <= li < cfg.num_layers:
+                self.layers[li].attn.fault_drop = True
         self.embed = None
         self.norm = None
         self.lm_head = None
@@ -383,7 +396,7 @@ class LlamaForCausalLM(nn.Module):
             at = layer.attn
             qkv = comm.sp_all_gather(h, lay, comm.RowsFn(
                 lambda r, o, w=at.qkv, wp=at.qkv_p: gemm.linear(r, w, out=o, packed=wp), at.qkv.shape[0]))
-            a = at.attend(qkv, positions, md, self.cos_sin, kv_caches[i])
+            a = at.drop(at.attend(qkv, positions, md, self.cos_sin, kv_caches[i]))
             del qkv
             o = comm.sp_reduce_scatter(a, lay, comm.RowsFn(
                 lambda r, out, w=at.o, wp=at.o_p: gemm.linear(r, w, out=out, packed=wp), at.o.shape[0]))
@@ -436,76 +449,74 @@ class LlamaForCausalLM(nn.Module):
         if self.st.tp_size > 1:
             return self._forward_rowscale_tp(residual, parts, positions, md, kv_caches, ws, buf, buf2)
         for i, layer in enumerate(self.layers):
-            at, mlp = layer.attn, layer.mlp
-            kc, vc = kv_caches[i]
-            if md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and T <= gemm.SKINNY_MAX_M and md.num_decode == T:
-                # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip);
-                # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
-                a = gemm.qkv_attn_fused(residual, at.qkv_pf, gemm.RowScale(parts, layer.eps), ws, positions,
-                                        self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv, self._flow_qkv)
-            else:
-                p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps),
-                                                 packed=at.qkv_pf)
-                if md.num_prefill == 0:
-                    a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq,
-                                                       at.nkv)
-                else:
-                    q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
-                    a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
+            a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws)
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
-            parts = gemm.residual_parts(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True), residual, buf2)
-            if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p) and not self.st.shared_device:
-                # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
-                d = gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, gemm.RowScale(parts, layer.eps), ws,
-                                   self._flow)
-                if i < last:
-                    parts = gemm.residual_parts(d, residual, buf)
-                else:
-                    x, _ = gemm.partial_add_rms_norm(d, residual, self.norm, self.cfg.rms_eps)
-                continue
-            if T > GATE_UP_SKINNY_MAX_M and not mlp.gate_up.is_meta:
-                # hipBLASLt's MFMA GEMM wins on the 235 MB gate_up above 384 rows (95 vs 149 us at
-                # 512, profiles/r3_decode_rows.txt) even with the norm and SiLU as separate kernels
-                x = gemm.norm_apply(residual, parts, layer.ln2, layer.eps)
-                h = gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
-            else:
-                h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf,
-                                     rowscale=gemm.RowScale(parts, layer.eps))
-            d = gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p)
+            parts = gemm.residual_parts(gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p, half=True),
+                                        residual, buf2)
+            d = self._decode_mlp(layer, residual, parts, ws)
             if i < last:
                 parts = gemm.residual_parts(d, residual, buf)
             else:
                 x, _ = gemm.partial_add_rms_norm(d, residual, self.norm, self.cfg.rms_eps)
         return x
 
+    def _decode_attn(self, layer, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
+                     md: attn_ops.AttnMetadata, kv: Tuple[torch.Tensor, torch.Tensor], ws: torch.Tensor) -> torch.Tensor:
+        """Folded-norm QKV projection + RoPE + KV write + attention of one layer -> [T, nq * 128]."""
+        at = layer.attn
+        kc, vc = kv
+        T = residual.shape[0]
+        rs = gemm.RowScale(parts, layer.eps)
+        if md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and T <= gemm.SKINNY_MAX_M and md.num_decode == T:
+            # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip);
+            # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
+            return gemm.qkv_attn_fused(residual, at.qkv_pf, rs, ws, positions, self.cos_sin, kc, vc, md, at.scale,
+                                       at.nq, at.nkv, self._flow_qkv)
+        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, packed=at.qkv_pf)
+        if md.num_prefill == 0:
+            return attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
+        q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
+        return attn_ops.paged_attention(q, kc, vc, md, at.scale)
+
+    def _decode_mlp(self, layer, residual: torch.Tensor, parts: torch.Tensor, ws: torch.Tensor) -> gemm.Partial:
+        """Folded-norm gate_up + SiLU and the down projection of one layer -> down's split-K slabs."""
+        mlp = layer.mlp
+        rs = gemm.RowScale(parts, layer.eps)
+        if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p) and not self.st.shared_device:
+            # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
+            return gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, rs, ws, self._flow, ws_gu=self._ws_gu)
+        if residual.shape[0] > GATE_UP_SKINNY_MAX_M and not mlp.gate_up.is_meta:
+            # hipBLASLt's MFMA GEMM wins on the 235 MB gate_up above 384 rows (95 vs 149 us at
+            # 512, profiles/r3_decode_rows.txt) even with the norm and SiLU as separate kernels
+            x = gemm.norm_apply(residual, parts, layer.ln2, layer.eps)
+            h = gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
+        else:  # split over K like the fused launch's gate_up when its n-blocks cannot fill the chip
+            h = gemm.linear_silu(residual, mlp.gate_up, ws=self._ws_gu, packed=mlp.gate_up_pf, rowscale=rs)
+        return gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p)
+
     def _forward_rowscale_tp(self, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
                              md: attn_ops.AttnMetadata, kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
                              ws: torch.Tensor, buf: torch.Tensor, buf2: torch.Tensor) -> torch.Tensor:
-        """TP decode step of the folded-norm chain: per layer four launches plus attention,
+        """TP decode step of the folded-norm chain, per layer (the TP=1 chain's launches with the
+        residual updates replaced by the fused collective):
 
-            qkv   = rinv1 * (residual @ (Wqkv_local diag ln1)^T)   split-K slabs -> attention
-            o     = split-K slabs of attn @ Wo_local^T  -> fused collective: slab sum, xGMI
-                    peer sum, residual += , norm parts (parallel/custom_ar.py reduce_residual)
-            h     = silu / mul of rinv2 * (residual @ (Wgu_local diag ln2)^T)
-            down  = split-K slabs -> fused collective
+            a     = qkv_attn_fused: rinv1 * (residual @ (Wqkv_local diag ln1)^T) split-K slabs
+                    handed in-launch to the decode attention (RoPE, KV write)
+            o     = split-K slabs of a @ Wo_local^T  -> fused collective: slab sum, xGMI peer
+                    sum, residual += , norm parts (parallel/custom_ar.py reduce_residual)
+            d     = mlp_fused: silu / mul of rinv2 * (residual @ (Wgu_local diag ln2)^T) (split
+                    over K: 56 n-blocks at 70B TP=8) handed in-launch to the down slabs
+                  -> fused collective
 
-        so each row-parallel projection costs its GEMM and ONE collective launch (SURVEY.md
-        §2.3: 2 x 80 all-reduces per 70B TP=8 step)."""
+        five launches per layer; each row-parallel projection costs its GEMM and ONE collective
+        launch (2 x 80 all-reduces per 70B TP=8 step)."""
         car = self.st.custom_ar
         for i, layer in enumerate(self.layers):
-            at, mlp = layer.attn, layer.mlp
-            kc, vc = kv_caches[i]
-            p = gemm.linear_partial_rowscale(residual, at.qkv, ws, gemm.RowScale(parts, layer.eps), packed=at.qkv_pf)
-            if md.num_prefill == 0:
-                a = attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
-            else:
-                q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
-                a = attn_ops.paged_attention(q, kc, vc, md, at.scale)
-            parts = car.reduce_residual(gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True),
+            a = layer.attn.drop(self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws))
+            parts = car.reduce_residual(gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p, half=True),
                                         residual, buf2)
-            h = gemm.linear_silu(residual, mlp.gate_up, packed=mlp.gate_up_pf, rowscale=gemm.RowScale(parts, layer.eps))
-            parts = car.reduce_residual(gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p), residual, buf)
+            parts = car.reduce_residual(self._decode_mlp(layer, residual, parts, ws), residual, buf)
         return gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
 
     def workspace(self, M: int) -> Optional[torch.Tensor]:
@@ -518,7 +529,18 @@ class LlamaForCausalLM(nn.Module):
             self._flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
             gemm.fused_err_word()  # before the first fused launch (engine polls gemm.check_fused)
             self._flow_qkv = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
+            # slabs of a gate_up split over K (gemm.gate_up_split > 1: the 70B TP=8 shard)
+            n = self._gate_up_split_elems()
+            self._ws_gu = torch.empty(n, dtype=torch.float32, device=self.device) if n else None
         return self._ws
+
+    def _gate_up_split_elems(self) -> int:
+        gu = getattr(self.layers[0].mlp, "gate_up", None)
+        if gu is None or gu.dim() != 2:
+            return 0
+        N2, K = gu.shape
+        n = max(gemm.gate_up_split(N2, K, M) * M * N2 for M in range(1, gemm.SKINNY_MAX_M + 1))
+        return n if n > gemm.SKINNY_MAX_M * N2 else 0
 
     def _workspace_elems(self) -> int:
         shapes = []

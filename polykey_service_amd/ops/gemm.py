@@ -324,6 +324,14 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         M, K = x.shape
         N = w_gu_interleaved.shape[0]
         out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
+        Sg = gate_up_split(N, K, M) if rowscale is not None and M <= SKINNY_MAX_M else 1
+        if Sg > 1 and ws is not None and ws.numel() >= Sg * M * N:
+            # split over K like the fused MLP's gate_up (bit-identical: the same slabs, summed in
+            # split order, the same SiLU arithmetic)
+            p = linear_partial_rowscale(x, w_gu_interleaved, ws, rowscale, S=Sg, packed=packed)
+            native.call("pk_splitk_reduce", out.data_ptr(), p.buf.data_ptr(), Sg, M, N, out.stride(0), 1,
+                        native.stream_ptr())
+            return out
         _launch_ex(MODE_SILU, x, w_gu_interleaved, packed, 1, out=out, norm=norm, rowscale=rowscale)
         return out
     if not skinny_ok(x, w_gu_interleaved, max_m=max_m):
@@ -373,7 +381,9 @@ def device_cus(dev: torch.device) -> int:
     return _CUS[i]
 
 
-FLOW_WORDS = 128 * 64 + 1  # pk_mlp_fused hand-off buffer: 64 tickets + 64 consumer counts (256 B apart), error word
+# fused-launch hand-off buffer (csrc/kernels/gemm_skinny.hip kFlowWords): 64 tickets + 64 consumer
+# counts (256 B apart), the error word, then the split gate_up's per-n-block counters
+FLOW_WORDS = 128 * 64 + 64 + 1024
 
 
 _FUSED_ERR: Optional[int] = None
@@ -429,6 +439,12 @@ def set_fused_spin_limit(n: int) -> None:
     fn(int(n))
 
 
+def gate_up_split(N2: int, K: int, M: int) -> int:
+    """K split of a decode gate_up projection (1: the single-pass SiLU epilogue).  Its n-blocks
+    alone fill the chip for 8B (224) but not for the 70B TP=8 shard (56: split 4)."""
+    return choose_split(N2, K, M)
+
+
 def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_packed: Optional[torch.Tensor]) -> bool:
     """Shapes the fused decode MLP launch (:func:`mlp_fused`) takes."""
     if gate_up_packed is None or down_packed is None or not x.is_cuda or not MLP_FUSED:
@@ -436,30 +452,36 @@ def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_p
     M, K = x.shape
     N2, I = gate_up_packed.shape[0], down_packed.shape[1]
     S = choose_split(down_packed.shape[0], I, M)
+    Sg = gate_up_split(N2, K, M)
     # one workgroup per CU, each a gate_up tile then a down tile: above 256 tiles (70B on one GPU:
     # 448 gate_up tiles) the fused launch measured 8 % slower end to end (profiles/r2_decode_ab.txt)
-    return (0 < M <= SKINNY_MAX_M and N2 == 2 * I and N2 % 128 == 0 and K % _KCHUNK == 0
+    return (0 < M <= SKINNY_MAX_M and N2 == 2 * I and N2 % 128 == 0 and K % (_KCHUNK * Sg) == 0
             and down_packed.shape[0] % 128 == 0 and I % (_KCHUNK * S) == 0 and (I // S) % 64 == 0 and S <= 64
-            and gate_up_packed.shape[1] == K and N2 // 128 <= device_cus(x.device)
+            and gate_up_packed.shape[1] == K and (N2 // 128) * Sg <= device_cus(x.device)
             and (down_packed.shape[0] // 128) * S <= device_cus(x.device))
 
 
 def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: RowScale,
-              ws: torch.Tensor, flow: torch.Tensor) -> Partial:
+              ws: torch.Tensor, flow: torch.Tensor, ws_gu: Optional[torch.Tensor] = None) -> Partial:
     """Decode MLP in ONE launch (csrc/kernels/gemm_skinny.hip mlp_fused_kernel):
     h = silu/mul of rinv * (x @ Wgu'^T) (folded norm, interleaved packed gate/up), then the down
     projection's fp32 split-K slabs of h @ Wd^T in ``ws``.  Down workgroups stream their first
     weight k-steps while gate_up finishes and wait on per-K-slice tickets in ``flow`` (int32,
-    >= :data:`FLOW_WORDS`, zeroed once; every launch leaves it zeroed).  Returns the slabs."""
+    >= :data:`FLOW_WORDS`, zeroed once; every launch leaves it zeroed).  When gate_up is split
+    over K (:func:`gate_up_split` > 1) its slabs go to ``ws_gu`` and the last split of each
+    n-block applies SiLU.  Returns the down slabs."""
     M, K = x.shape
     N2, I = gate_up_packed.shape[0], down_packed.shape[1]
     N = down_packed.shape[0]
     S = choose_split(N, I, M)
+    Sg = gate_up_split(N2, K, M)
     assert ws.numel() >= S * M * N and flow.numel() >= FLOW_WORDS and flow.dtype == torch.int32
+    assert Sg == 1 or (ws_gu is not None and ws_gu.numel() >= Sg * M * N2), "split gate_up needs its slab workspace"
     h = torch.empty((M, I), dtype=x.dtype, device=x.device)
     gu = GemmArgs()
     gu.out, gu.A, gu.W = h.data_ptr(), x.data_ptr(), gate_up_packed.data_ptr()
-    gu.M, gu.N, gu.K, gu.lda, gu.ldo, gu.S = M, N2, K, x.stride(0), h.stride(0), 1
+    gu.M, gu.N, gu.K, gu.lda, gu.ldo, gu.S = M, N2, K, x.stride(0), h.stride(0), Sg
+    gu.partial = ws_gu.data_ptr() if Sg > 1 else None
     gu.row_scale, gu.nrm_parts, gu.nrm_nparts, gu.eps = 1, rowscale.parts.data_ptr(), rowscale.parts.shape[0], \
         float(rowscale.eps)
     dn = GemmArgs()

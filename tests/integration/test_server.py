@@ -3,6 +3,7 @@ import asyncio
 import io
 import json
 import threading
+import time
 
 import grpc
 import pytest
@@ -186,3 +187,51 @@ def test_graceful_shutdown_lets_in_flight_streams_finish():
                 proto.ExecuteToolRequest(tool_name="example_tool"), timeout=2)
         msgs = [r["msg"] for r in s.records()]
     assert msgs.index("server shutting down") < msgs.index("server stopped")
+
+
+def test_keepalive_10s_pings_on_a_live_connection_get_no_goaway():
+    """SURVEY §2.5 #10 / §4.2, live: a dev_client-style channel pinging every 10 s
+    (keepalive_time 10 s, permit without calls: /root/reference/cmd/dev_client/main.go:182-186)
+    stays on ONE connection for > 30 s against our server.  Control: the same client against a
+    server with grpc's default enforcement (no ping-interval setting, 2 ping strikes) is sent
+    GOAWAY too_many_pings in that time -- so the check can see the failure it guards against."""
+    import grpc
+
+    from polykey_service_amd.server import app
+
+    client_opts = [("grpc.keepalive_time_ms", 10_000), ("grpc.keepalive_timeout_ms", 5_000),
+                   ("grpc.keepalive_permit_without_calls", 1), ("grpc.http2.max_pings_without_data", 0)]
+    default_enforcement = [o for o in app.SERVER_OPTIONS if o[0] not in (
+        "grpc.http2.min_recv_ping_interval_without_data_ms", "grpc.http2.max_ping_strikes")]
+
+    def watch(addr):
+        ch = grpc.insecure_channel(addr, options=client_opts)
+        states = []
+        ch.subscribe(lambda s: states.append(s), try_to_connect=True)
+        grpc.channel_ready_future(ch).result(timeout=10)
+        call = ch.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                              response_deserializer=proto.ExecuteToolResponse.FromString)
+        assert call(proto.ExecuteToolRequest(tool_name="example_tool"), timeout=10).status.code == 200
+        return ch, states, call
+
+    saved = app.SERVER_OPTIONS
+    with ServerThread() as ours:
+        try:
+            app.SERVER_OPTIONS = default_enforcement
+            control = ServerThread().__enter__()
+        finally:
+            app.SERVER_OPTIONS = saved
+        chans = []
+        try:
+            ch1, st1, call1 = watch(ours.addr)
+            ch2, st2, _ = watch(control.addr)
+            chans += [ch1, ch2]
+            time.sleep(36)  # three or more 10 s pings with no data in between
+            after_ready = lambda st: st[st.index(grpc.ChannelConnectivity.READY) + 1:]
+            assert after_ready(st1) == [], st1  # never left READY: no GOAWAY, no reconnect
+            assert call1(proto.ExecuteToolRequest(tool_name="example_tool"), timeout=10).status.code == 200
+            assert any(s != grpc.ChannelConnectivity.READY for s in after_ready(st2)), st2  # control was cut
+        finally:
+            for ch in chans:
+                ch.close()
+            control.__exit__(None, None, None)

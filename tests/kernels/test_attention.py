@@ -215,16 +215,17 @@ def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S, pos_last):
     assert torch.equal(k1, k2) and torch.equal(v1, v2)
 
 
-@pytest.mark.parametrize("nq,nkv,bs", [(32, 8, 32), (16, 4, 32), (64, 8, 32)])
+@pytest.mark.parametrize("nq,nkv,bs,H", [(32, 8, 32, 1024), (16, 4, 32, 1024), (64, 8, 32, 1024),
+                                         (32, 8, 32, 4096), (8, 1, 32, 8192)])
 @pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [384] * 64, [512, 513, 1300, 0]])
-def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, ctxs):
+def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, H, ctxs):
     """Fused QKV projection -> decode attention launch (csrc/kernels/decode_fused.hip): the QKV
     tiles hand their write-through slabs to the attention tiles in-launch.  Attention output and
     K / V cache bit-identical to linear_partial_rowscale + paged_decode_from_qkv, over repeated
     launches with new inputs (stale slabs would show), tickets left zeroed."""
     from polykey_service_amd.ops import gemm
     d = "cuda"
-    B, H = len(ctxs), 1024
+    B = len(ctxs)  # H: 8B width (32 q / 8 kv heads) and the 70B TP=8 shard (8 q / 1 kv head, H 8192)
     N = (nq + 2 * nkv) * HD
     max_blocks = (max(ctxs) + bs - 1) // bs + 3
     nb = sum((max(c, 1) + bs - 1) // bs for c in ctxs) + 4
@@ -249,7 +250,7 @@ def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, ctxs):
     k1, v1, k2, v2 = kc.to(d), vc.to(d), kc.to(d), vc.to(d)
     for it in range(4):
         res = (torch.randn(B, H, device=d)).to(torch.bfloat16)
-        parts = gemm.residual_parts(None, res.clone(), torch.empty(2 * 64, device=d))
+        parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 64, device=d))
         rs = gemm.RowScale(parts, 1e-5)
         p = gemm.linear_partial_rowscale(res, w, ws1, rs, S=S, packed=wp)
         exp = A.paged_decode_from_qkv(p, pos.to(d), cs, k1, v1, mk(), scale, nq, nkv)

@@ -310,11 +310,13 @@ def test_rowscale_half_blocks(M):
 
 
 @pytest.mark.parametrize("M", [1, 17, 64])
-@pytest.mark.parametrize("H,I", [(4096, 14336), (1024, 4096), (8192, 28672)])
+@pytest.mark.parametrize("H,I", [(4096, 14336), (1024, 4096), (8192, 28672), (8192, 3584)])
 def test_mlp_fused_matches_two_launches(M, H, I):
     """Fused decode MLP (gate_up + SiLU -> in-launch hand-off -> down slabs, one launch) is
     bit-identical to the two launches it replaces, on repeated launches (the hand-off tickets
-    re-arm themselves), and never trips the wait timeout."""
+    re-arm themselves), and never trips the wait timeout.  (8192, 3584) is the 70B TP=8 shard:
+    its 56 gate_up n-blocks are split over K (the last split of each n-block applies SiLU and
+    hands h over), the two-launch reference splits the same way."""
     res = rnd(M, H)
     nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
     wgu = gemm.interleave_gate_up(rnd(I, H, scale=0.05), rnd(I, H, scale=0.05))
@@ -323,18 +325,20 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     dp = gemm.pack_weight(wd)
     # the launch is correct at any grid; the engine takes it only up to one tile per CU (70B: 448
     # gate_up tiles -> two launches, measured faster)
-    assert gemm.mlp_fused_ok(res, gup, dp) == (2 * I // 128 <= 256)
+    Sg = gemm.gate_up_split(2 * I, H, M)
+    assert (Sg > 1) == (2 * I // 128 < 192) and gemm.mlp_fused_ok(res, gup, dp) == (2 * I // 128 * Sg <= 256)
+    ws_gu = torch.empty(Sg * M * 2 * I, dtype=torch.float32, device="cuda")
     parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
     rs = gemm.RowScale(parts, 1e-5)
     S = gemm.choose_split(H, I, M)
     ws0 = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
-    h = gemm.linear_silu(res, wgu, packed=gup, rowscale=rs)
+    h = gemm.linear_silu(res, wgu, ws=ws_gu, packed=gup, rowscale=rs)
     ref_slabs = gemm.linear_partial(h, wd, ws0, packed=dp).view().clone()
     flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda")
     ws = torch.empty_like(ws0)
     for _ in range(4):
         ws.fill_(float("nan"))
-        p = gemm.mlp_fused(res, gup, dp, rs, ws, flow)
+        p = gemm.mlp_fused(res, gup, dp, rs, ws, flow, ws_gu=ws_gu)
         assert p.S == S
         torch.testing.assert_close(p.view(), ref_slabs, atol=0, rtol=0)
     # against the fp32 reference of the whole MLP
@@ -348,9 +352,9 @@ def test_mlp_fused_matches_two_launches(M, H, I):
         r2 = rnd(M, H)
         p2 = gemm.residual_parts(None, r2.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
         rs2 = gemm.RowScale(p2, 1e-5)
-        h2 = gemm.linear_silu(r2, wgu, packed=gup, rowscale=rs2)
+        h2 = gemm.linear_silu(r2, wgu, ws=ws_gu, packed=gup, rowscale=rs2)
         exp2 = gemm.linear_partial(h2, wd, ws0, packed=dp).view().clone()
-        got = gemm.mlp_fused(r2, gup, dp, rs2, ws, flow).view()
+        got = gemm.mlp_fused(r2, gup, dp, rs2, ws, flow, ws_gu=ws_gu).view()
         torch.testing.assert_close(got, exp2, atol=0, rtol=0)
     torch.cuda.synchronize()
     assert int(flow.abs().sum()) == 0, flow.tolist()
