@@ -30,10 +30,6 @@ namespace {
 template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2>
 __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args) {
   __shared__ SkinnyLds<MT> lds;
-#if PK_LAB_LDS_PAD
-  __shared__ char lab_pad[PK_LAB_LDS_PAD];  // timing only: force one workgroup per CU
-  if (args.M < 0) lab_pad[threadIdx.x] = 1;
-#endif
   skinny_tile<MT, MODE, PK, NORM, NT, RS, KR>(args, blockIdx.x, blockIdx.y, gridDim.x, lds, Flow{});
 }
 

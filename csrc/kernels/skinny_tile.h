@@ -64,30 +64,6 @@ constexpr int kPartCols = 512;  // columns per sum-of-squares part (residual_par
 
 
 
-// Experiment knobs for tools/gemm_lab.hip (all 0 in the library build; the NO_* ones give
-// wrong results and exist only to attribute time).
-#ifndef PK_W_DEPTH
-#define PK_W_DEPTH 2         // k-steps of W in flight per wave (register ring; 4 measured slower)
-#endif
-#ifndef PK_SLAB_NT
-#define PK_SLAB_NT 0         // non-temporal stores for the fp32 split-K slabs
-#endif
-#ifndef PK_SLAB_SC1
-#define PK_SLAB_SC1 0        // write-through (sc1) buffer stores for the fp32 split-K slabs
-#endif
-#ifndef PK_LAB_LDS_PAD
-#define PK_LAB_LDS_PAD 0     // extra LDS per workgroup (forces one workgroup per CU)
-#endif
-#ifndef PK_LAB_NO_MFMA
-#define PK_LAB_NO_MFMA 0     // no MFMA / LDS reads: the bare W stream
-#endif
-#ifndef PK_LAB_NO_ASTAGE
-#define PK_LAB_NO_ASTAGE 0   // stage A once, no per-chunk barrier
-#endif
-#ifndef PK_LAB_NO_SLAB
-#define PK_LAB_NO_SLAB 0     // skip the fp32 split-K slab stores (timing only)
-#endif
-
 // Weight loads.  NT: non-temporal (no Infinity-Cache allocation) -- measured faster for the
 // large, read-once streams (gate_up 235 MB: -6 %, LM head 1 GB: -10 %) and slower for the
 // small ones, which profit from whatever the Infinity Cache still holds.
@@ -442,13 +418,6 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
                        : ldw<NT>(wp[t] + k + 32 * s);
   };
   auto mma_step = [&](const bf16x8_t (&wf)[kR][4], int buf, int kk) {
-    if constexpr (PK_LAB_NO_MFMA) {  // timing only: consume W with one VALU op per register
-#pragma unroll
-      for (int t = 0; t < kR; ++t)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc[t][s & (MT - 1)][0] += __builtin_bit_cast(f32x4, wf[t][s])[0];
-      return;
-    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       bf16x8_t af[MT];
@@ -494,33 +463,6 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       store_a(buf ^ 1);
       buf ^= 1;
     }
-  } else if constexpr (PK_W_DEPTH > 2) {
-    // W register ring PK_W_DEPTH k-steps deep (step j = half j&1 of chunk j>>1)
-    constexpr int WD = PK_W_DEPTH;
-    bf16x8_t wr[WD][kR][4];
-    const int nsteps = 2 * nchunks;
-    auto ks = [&](int j) { return ck(j >> 1) + (j & 1) * 128; };
-    load_a(ck(0));
-#pragma unroll
-    for (int u = 0; u < WD; ++u) load_w(wr[u], ks(u));
-    store_a(0);
-    int buf = 0;
-    for (int j0 = 0; j0 < nsteps; j0 += WD) {
-#pragma unroll
-      for (int u = 0; u < WD; ++u) {
-        const int j = j0 + u;
-        if ((u & 1) == 0) {
-          load_a(ck((j >> 1) + 1));
-          __syncthreads();
-        }
-        if (j < nsteps) mma_step(wr[u], buf, (u & 1) * 128);
-        load_w(wr[u], ks(j + WD));
-        if (u & 1) {
-          store_a(buf ^ 1);
-          buf ^= 1;
-        }
-      }
-    }
   } else {
   if constexpr (FL == 2) {
     // consumer: this workgroup's first two weight k-steps are requested before the wait, so
@@ -538,14 +480,6 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   int buf = 0;
   for (int c = 0; c < nchunks; ++c) {
     const int kn = ck(c + 1);
-    if constexpr (PK_LAB_NO_ASTAGE) {
-      if (c == 0) __syncthreads();
-      mma_step(wa, 0, 0);
-      load_w(wa, kn);
-      mma_step(wb, 0, 128);
-      load_w(wb, kn + 128);
-      continue;
-    }
     load_a(kn);
     __syncthreads();  // chunk c visible in a_lds[buf]; every wave is done with a_lds[buf^1]
     mma_step(wa, buf, 0);
@@ -577,7 +511,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   // the in-launch residual update hands its slabs over write-through (measured faster than plain
   // stores + release: tools/gemm_lab.hip o_res / down_res); the plain split-K slabs are read by
   // the next kernel and stay plain (write-through made those slower)
-  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kSiluSplit || PK_SLAB_SC1 || (MODE == kPartial && FL == 1);
+  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kSiluSplit || (MODE == kPartial && FL == 1);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = 16 * mt + r;
@@ -588,11 +522,6 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       for (int t = 0; t < kR; ++t) acc[t][mt] *= sc;
     }
     if constexpr (kSlab) {
-      if (PK_LAB_NO_SLAB && args.M > 0) {  // timing only: keep acc live, store nothing
-#pragma unroll
-        for (int t = 0; t < kR; ++t) asm volatile("" ::"v"(acc[t][mt]));
-        continue;
-      }
       float* p = args.partial + (static_cast<int64_t>(split) * args.M + row0 + m) * N + n0 + 4 * g;
       if constexpr (kSlabSc1) {
         // write-through (sc1) stores: the slab lines leave the XCD L2 clean, so the split-K
@@ -605,13 +534,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t][mt]), rsrc, boff + 64 * t, 0, 16);
       } else {
 #pragma unroll
-        for (int t = 0; t < kR; ++t) {
-          const f32x4 v = acc[t][mt];
-          if constexpr (PK_SLAB_NT)  // streaming store: no dirty L2 lines left for the launch-end write-back
-            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p + 16 * t));
-          else
-            *reinterpret_cast<f32x4*>(p + 16 * t) = v;
-        }
+        for (int t = 0; t < kR; ++t) *reinterpret_cast<f32x4*>(p + 16 * t) = acc[t][mt];
       }
     } else if constexpr (MODE == kBF16) {
       bf16_t* o = args.out + static_cast<int64_t>(row0 + m) * args.ldo + n0 + 4 * g;

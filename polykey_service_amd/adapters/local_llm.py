@@ -250,6 +250,96 @@ class ReplicaPool:
             await r.aclose()
 
 
+class ModelSet:
+    """Several served models behind one front end (``ServerConfig.serve_models``): duck-types the
+    backend face the server watches -- healthy only while every model's engines are, one fatal
+    handler and watchdog for all of them, closed together."""
+
+    def __init__(self, llms: Dict[str, object]):
+        self.llms = dict(llms)
+        self.on_fatal = None
+        self.watchdog_s = 0.0
+
+    def __setattr__(self, k, v):
+        object.__setattr__(self, k, v)
+        if k in ("on_fatal", "watchdog_s") and "llms" in self.__dict__:
+            for llm in self.llms.values():
+                setattr(llm, k, v)
+
+    def healthy(self) -> bool:
+        return all(llm.healthy() for llm in self.llms.values())
+
+    def load(self) -> int:
+        return sum(llm.load() for llm in self.llms.values())
+
+    def shutdown(self, timeout: float = 10.0) -> None:
+        for llm in self.llms.values():
+            llm.shutdown(timeout)
+
+    async def aclose(self) -> None:
+        for llm in self.llms.values():
+            await llm.aclose()
+
+
+def parse_serve_models(spec: str) -> List[tuple]:
+    """``"llama3-8b@0-3,mixtral-8x7b@4,tiny"`` -> [("llama3-8b", [0, 1, 2, 3]), ("mixtral-8x7b", [4]),
+    ("tiny", [])] (no ``@``: the next free device)."""
+    out = []
+    for item in (x.strip() for x in spec.split(",")):
+        if not item:
+            continue
+        name, _, dev = item.partition("@")
+        if not name:
+            raise ValueError(f"serve_models entry {item!r} has no model name")
+        if not dev:
+            devs: List[int] = []
+        elif "-" in dev:
+            a, b = (int(v) for v in dev.split("-"))
+            if b < a:
+                raise ValueError(f"serve_models entry {item!r}: empty device range")
+            devs = list(range(a, b + 1))
+        else:
+            devs = [int(dev)]
+        out.append((name, devs))
+    names = [n for n, _ in out]
+    if len(set(names)) != len(names):
+        raise ValueError(f"serve_models names a model twice: {spec!r}")
+    return out
+
+
+def attach_models(router, cfg, logger) -> ModelSet:
+    """Build every model of ``cfg.serve_models`` (one process; each model's engines on their own
+    devices, one engine thread each) and register its tools; the first listed is the default for
+    ``llm.chat`` / ``llm.generate`` without a model."""
+    import dataclasses as _dc
+
+    import torch
+
+    from ..engine.async_llm import AsyncLLM
+    from ..engine.llm_engine import EngineConfig, LLMEngine
+    from ..parallel.state import ParallelState
+    entries = parse_serve_models(cfg.serve_models)
+    n_dev = torch.cuda.device_count() if torch.cuda.is_available() and cfg.device != "cpu" else 0
+    taken = {d for _, devs in entries for d in devs}
+    free = iter([d for d in range(max(n_dev, 1)) if d not in taken])
+    llms = {}
+    for name, devs in entries:
+        if not devs:
+            devs = [next(free, 0)]
+        engines = []
+        for d in devs:
+            if n_dev and d >= n_dev:
+                raise ValueError(f"model {name!r} asks for GPU {d}; this node has {n_dev}")
+            dev = torch.device(f"cuda:{d}") if n_dev else torch.device("cpu")
+            ecfg = _dc.replace(EngineConfig.from_server_config(_dc.replace(cfg, model=name)), device=str(dev))
+            engines.append(LLMEngine(ecfg, ParallelState(device=dev)))
+        llm = AsyncLLM(engines[0]) if len(engines) == 1 else ReplicaPool([AsyncLLM(e) for e in engines])
+        attach_local_llm(router, _dc.replace(cfg, model=name), logger, engine=engines[0], llm=llm)
+        llms[name] = llm
+    router.llm = ModelSet(llms)
+    return router.llm
+
+
 def attach_local_llm(router, cfg, logger, engine=None, llm=None):
     """Build (or reuse) the engine for ``cfg.model`` and register its tools (``llm``: an already
     built AsyncLLM / ReplicaPool over ``engine``)."""

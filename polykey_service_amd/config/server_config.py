@@ -24,6 +24,10 @@ class ServerConfig:
     environment: str = "development"
     backend: str = "mock"          # mock | local
     model: str = "llama3-8b"
+    # several models behind this one front end, each on its own GPU(s) of the node:
+    # "<model>[@<gpu>|@<first>-<last>][,...]", e.g. "llama3-8b@0-3,mixtral-8x7b@4" (a device range
+    # = replicas of that model); "llm.chat:<model>" / OpenAI "model" pick one.  "" -> ``model``
+    serve_models: str = ""
     model_path: str = ""           # directory of safetensors shards; "" → random init
     tokenizer: str = ""            # tokenizer.json path; "" → byte-level tokenizer
     dtype: str = "bfloat16"
@@ -57,6 +61,7 @@ _ENV = {
     "environment": "POLYKEY_ENV",
     "backend": "POLYKEY_BACKEND",
     "model": "POLYKEY_MODEL",
+    "serve_models": "POLYKEY_SERVE_MODELS",
     "model_path": "POLYKEY_MODEL_PATH",
     "tokenizer": "POLYKEY_TOKENIZER",
     "dtype": "POLYKEY_DTYPE",

@@ -1,19 +1,30 @@
 """Llama-3 family decoder (8B / 70B; also the attention half of Mixtral), TP-aware.
 
-Per layer on one rank (TP degree ``tp``; shapes for 8B TP1 / 70B TP8 in SURVEY.md §2.3):
+Prefill (and decode batches above the fused kernels' limits), per layer on one rank (TP degree
+``tp``; shapes for 8B TP1 / 70B TP8 in SURVEY.md §2.3):
 
     x, res = fused_add_rmsnorm(x, res)                       HIP  (csrc/kernels/norm_act.hip)
-    qkv    = x @ Wqkv^T          column-parallel by heads     hipBLASLt
-    rope_and_cache(qkv)          rotate q,k in place, write paged K / V^T cache   HIP
-    a      = paged_attention(q)  decode split-K / varlen causal prefill          HIP (MFMA)
-    o      = a @ Wo^T            row-parallel → all-reduce (RCCL over xGMI)
+    qkv    = x @ Wqkv^T          column-parallel by heads     hipBLASLt, or the hand-written MFMA GEMM
+                                                              on block-packed weights (gemm_prefill.hip)
+    rope_and_cache(qkv)          rotate q,k in place, write the paged K / V cache (fragment-native
+                                 32-token tiles, common.h kcache_off / vcache_off)   HIP
+    a      = paged_attention(q)  varlen causal prefill over the cached prefix (MFMA) HIP
+    o      = a @ Wo^T            row-parallel -> all-reduce (RCCL over xGMI; chunk-overlapped, or
+                                 reduce-scatter / all-gather around the norms: sequence parallel)
     x, res = fused_add_rmsnorm(o, res)                       HIP
-    h      = silu_and_mul(x @ Wgu^T)                         hipBLASLt + HIP
-    x      = h @ Wdown^T         row-parallel → all-reduce
+    h      = silu_and_mul(x @ Wgu^T)                         hipBLASLt / MFMA GEMM + HIP
+    x      = h @ Wdown^T         row-parallel -> all-reduce
 
-Fused projections (q|k|v, gate|up) halve the GEMM launches of a decode step; the residual
-stream stays bf16 and is updated in place by the fused norm.  Vocab-parallel embedding and
-LM head for TP>1 (logits all-gathered for sampling).
+Decode (M <= 64 rows; ``_forward_rowscale``): the RMSNorm weights are folded into the block-packed
+QKV / gate_up weights and every projection is the hand-written weight-streaming GEMM
+(gemm_skinny.hip / skinny_tile.h), per layer
+
+    qkv_attn_fused   QKV split-K slabs handed in-launch to the decode attention (RoPE, KV write)
+    o-proj slabs  -> residual update + norm parts (TP: the fused xGMI collective, custom_ar)
+    mlp_fused        gate_up + SiLU handed in-launch to the down projection's slabs
+                  -> residual update + norm parts (TP: the fused collective)
+
+Vocab-parallel embedding and LM head for TP>1 (logits all-gathered for sampling).
 """
 from __future__ import annotations
 

@@ -176,7 +176,10 @@ def build_service(cfg, logger: slog.Logger):
     from ..adapters.security.secret_store import SecretStore
 
     router = ToolRouter(secret_store=SecretStore.from_env())
-    if cfg.backend == "local":
+    if cfg.backend == "local" and getattr(cfg, "serve_models", ""):
+        from ..adapters.local_llm import attach_models  # several models, one front end
+        attach_models(router, cfg, logger)
+    elif cfg.backend == "local":
         from ..adapters.local_llm import attach_local_llm
         attach_local_llm(router, cfg, logger)
     elif cfg.backend != "mock":

@@ -206,3 +206,41 @@ def test_torch_profiler_toggle(tmp_path, monkeypatch):
     llm.shutdown()
     assert len(toks) == 60 and last.finished
     assert any(p.name.endswith(".json") or p.name.endswith(".json.gz") for p in tmp_path.iterdir())
+
+
+def test_serve_models_routes_one_front_end_to_several_engines():
+    """``serve_models`` (POLYKEY_SERVE_MODELS): one gRPC front end, two models, each on its own
+    engine (its own device on a GPU node); ``<family>:<model>`` routes to each, the first listed
+    is the default, health follows every engine, an unknown model is NOT_FOUND."""
+    from polykey_service_amd.adapters.local_llm import ModelSet, parse_serve_models
+    from polykey_service_amd.server.app import build_service
+
+    assert parse_serve_models("llama3-8b@0-3,mixtral-8x7b@4,x") == [
+        ("llama3-8b", [0, 1, 2, 3]), ("mixtral-8x7b", [4]), ("x", [])]
+    with pytest.raises(ValueError):
+        parse_serve_models("a@0,a@1")
+    cfg = ServerConfig(backend="local", serve_models="tiny-llama,tiny-mixtral", device="cpu", max_num_seqs=8,
+                       max_num_batched_tokens=128, max_model_len=512, hip_graphs=False)
+    router = build_service(cfg, slog.Logger(open("/dev/null", "w")))
+    try:
+        assert isinstance(router.llm, ModelSet) and sorted(router.llm.llms) == ["tiny-llama", "tiny-mixtral"]
+        assert router.models("llm.chat") == ["tiny-llama", "tiny-mixtral"] and router.llm.healthy()
+        engines = {n: getattr(l, "engine", None) for n, l in router.llm.llms.items()}
+        assert engines["tiny-llama"] is not engines["tiny-mixtral"]
+        with ServerThread(router) as s, grpc.insecure_channel(s.addr) as ch:
+            call = ch.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
+                                  response_deserializer=proto.ExecuteToolResponse.FromString)
+            for tool, want in (("llm.generate:tiny-llama", "tiny-llama"), ("llm.generate:tiny-mixtral", "tiny-mixtral"),
+                               ("llm.generate", "tiny-llama")):
+                r = call(req(tool, prompt_token_ids=[1, 5, 6], max_tokens=3, ignore_eos=True, **{"return": "struct"}),
+                         timeout=60)
+                d = proto.struct_to_dict(r.struct_output)
+                assert d["model"] == want and d["usage"]["completion_tokens"] == 3.0, (tool, d)
+            r = call(req("llm.chat:tiny-mixtral", messages=[{"role": "user", "content": "hi"}], max_tokens=2,
+                         ignore_eos=True), timeout=60)
+            assert r.status.code == 200
+            with pytest.raises(grpc.RpcError) as ei:
+                call(req("llm.generate:no-such-model", prompt="x", max_tokens=1), timeout=10)
+            assert ei.value.code() == grpc.StatusCode.NOT_FOUND
+    finally:
+        router.llm.shutdown()

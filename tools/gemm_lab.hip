@@ -1,10 +1,12 @@
 // Decode-GEMM lab: times the library's skinny GEMM (csrc/kernels/gemm_skinny.hip, included
 // verbatim) on the Llama-3-8B decode shapes at M = 64 with cold weights (copies rotated over
-// > 1 GiB, so nothing is served from the 256 MiB Infinity Cache).  Built several times with
-// different PK_LAB_* knobs to attribute where the kernel loses against the HBM read ceiling
-// (tools/hbm_read.hip).  Prints one line per shape: us per call and TB/s of weight bytes.
+// > 1 GiB, so nothing is served from the 256 MiB Infinity Cache).  Prints one line per shape: us
+// per call and TB/s of weight bytes, against the HBM read ceiling (tools/hbm_read.hip).  (The
+// round-1/2 attribution knobs -- W register-ring depth, no-MFMA / no-A-staging / no-slab builds,
+// slab store policies -- were retired from the library header in round 4; their results are in
+// profiles/r1b_gemm_lab.txt and profiles/r2_decode_ab.txt.)
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc [-DPK_W_DEPTH=4 | -DPK_LAB_NO_MFMA=1 ...] tools/gemm_lab.hip -o tools/gemm_lab
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc tools/gemm_lab.hip -o tools/gemm_lab
 #include "../csrc/kernels/gemm_skinny.hip"
 
 #include <cstdio>
