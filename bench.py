@@ -66,16 +66,17 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     # measured on 1x MI355X (profiles/r2_bench_client_ab.txt): unary 12,879 tok/s with the clients on
     # the server's event loop vs 12,299 from a separate load-generator process (streaming: 12,787)
-    ap.add_argument("--frontend", choices=["replicas", "gateway", "single"], default="replicas",
-                    help="N > 1, tp 1: every rank serves its own gRPC endpoint (replicas); ONE gRPC address served "
-                         "by an acceptor in every rank (SO_REUSEPORT), each routing to the least-loaded engine "
-                         "(gateway, engine/remote.py dp_gateway); or rank 0 alone as the front end (single)")
+    ap.add_argument("--frontend", choices=["replicas", "single"], default="replicas",
+                    help="N > 1, tp 1: every rank serves its own gRPC endpoint (replicas, the DP design); or rank 0 "
+                         "alone as the front end, routing to every rank's engine process (single, "
+                         "engine/remote.py dp_gateway)")
     ap.add_argument("--client", choices=["process", "inproc"], default="inproc",
                     help="load generator on the server's event loop (default) or in its own process")
-    ap.add_argument("--tp-extra-model", default="llama3-70b",
+    ap.add_argument("--tp-extra-model", default="auto",
                     help="N > 1 with --tp 1: after the replica run, measure this model at TP = N in a fresh "
                          "torchrun child and report it under the extra key tp{N}_<model> (BASELINE.json: "
-                         "'Llama-3-8B TP=1 / 70B TP=8'); 'none' skips it")
+                         "'Llama-3-8B TP=1 / 70B TP=8'); auto: llama3-70b when --model is llama3-8b (the "
+                         "BASELINE pair), else none; 'none' skips it")
     ap.add_argument("--tp-extra-timeout", type=float, default=480.0,
                     help="seconds the TP child may take (its failure or timeout never loses the main number)")
     ap.add_argument("--child-timeout", type=float, default=1500.0, help="seconds the main measurement child may take")
@@ -150,6 +151,8 @@ def orchestrate(args, argv) -> int:
         print(f"bench: measurement child failed (rc {rc})", file=sys.stderr)
         return rc or 1
     extra = args.tp_extra_model
+    if extra == "auto":
+        extra = "llama3-70b" if args.model == "llama3-8b" else "none"
     if args.tp == 1 and args.ep == 1 and extra and extra != "none":
         key = f"tp{args.gpus}_" + {"llama3-70b": "70b", "llama3-8b": "8b"}.get(extra, extra)
         targv = _strip(argv, {"--model", "--tp", "--ep", "--frontend", "--tp-extra-model"}) + [
@@ -169,14 +172,12 @@ def orchestrate(args, argv) -> int:
 
 
 async def _abarrier(group) -> None:
-    """A barrier that keeps this rank's event loop running: with the SO_REUSEPORT gateway the
-    rank's acceptor serves other ranks' clients too, and blocking its loop in a collective
-    while their requests are in flight through it would deadlock the wave."""
+    """A barrier that keeps this rank's event loop (and its gRPC server) running."""
     import torch.distributed as dist
     await asyncio.get_running_loop().run_in_executor(None, lambda: dist.barrier(group=group))
 
 
-async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, shared_port=0):
+async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
     import grpc
     import torch
     import torch.distributed as dist
@@ -192,30 +193,15 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, sha
     router = ToolRouter()
     cfg = ServerConfig(model=args.model, backend="local")
     attach_local_llm(router, cfg, logger, engine=engine, llm=llm)
-    conc = args.concurrency * n_replicas  # gateway: one front end for every replica's clients
-    if shared_port:
-        # SO_REUSEPORT gateway: rank 0's server takes a port from the kernel and holds it before the
-        # other ranks join it (a port picked, closed and re-bound later could be handed to another
-        # process meanwhile, whose reuseport listeners would then share our connections)
-        holder = [None]
-        if st.rank == 0:
-            srv = PolykeyServer(router, logger, f"127.0.0.1:{args.port_base or 0}")
-            holder[0] = await srv.start()
-        dist.broadcast_object_list(holder, src=0)
-        if st.rank != 0:
-            srv = PolykeyServer(router, logger, f"127.0.0.1:{holder[0]}")
-            await srv.start()
-        port = holder[0]
-        dist.barrier()  # every acceptor is listening before any client connects
-    else:
-        port = args.port_base + st.rank if args.port_base > 0 else 0
-        srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
-        port = await srv.start()
+    conc = args.concurrency * n_replicas  # single front end: every replica's clients
+    port = args.port_base + st.rank if args.port_base > 0 else 0
+    srv = PolykeyServer(router, logger, f"127.0.0.1:{port}")
+    port = await srv.start()
     if args.client == "process":
         try:
             return await _drive_external(args, engine, st, leaders_group if n_replicas == 1 else None, port, srv,
                                          llm=router.llm, conc=args.concurrency * n_replicas,
-                                         stop_after=engine.lockstep or n_replicas > 1 or bool(shared_port))
+                                         stop_after=engine.lockstep or n_replicas > 1)
         finally:
             await srv.server.stop(0)
     channel = grpc.aio.insecure_channel(f"127.0.0.1:{port}", options=[
@@ -229,7 +215,7 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, sha
     rng = random.Random(args.seed * 1000 + st.rank)
     tool = f"llm.generate:{args.model}"
     llm = router.llm
-    # gateway: the other ranks sit in their engine servers, so rank 0 times the waves alone
+    # single front end: the other ranks sit in their engine servers, so rank 0 times the waves alone
     sync_ranks = dist.is_initialized() and n_replicas == 1
 
     timing = os.environ.get("POLYKEY_BENCH_TIMING") == "1"
@@ -300,10 +286,9 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1, sha
     elapsed = time.perf_counter() - t0
     await channel.close()
     await srv.server.stop(0)
-    if engine.lockstep or n_replicas > 1 or shared_port:
+    if engine.lockstep or n_replicas > 1:
         # DP attention + EP: leave the lockstep loop together with the other ranks; single front
-        # end: stop the other ranks' engine servers (they are waiting on it); SO_REUSEPORT gateway:
-        # every rank's waves are done (the barrier above) before any engine stops
+        # end: stop the other ranks' engine servers (they are waiting on it)
         await asyncio.get_running_loop().run_in_executor(None, llm.shutdown)
     return tokens, elapsed, lats
 
@@ -352,7 +337,7 @@ async def _drive_external(args, engine, st, leaders_group, port, srv, llm, conc,
                 await asyncio.wait_for(proc.wait(), 30)
             except asyncio.TimeoutError:
                 proc.kill()
-    if stop_after:  # DP attention + EP lockstep / gateway engine servers: stop with the other ranks
+    if stop_after:  # DP attention + EP lockstep / single-front-end engine servers: stop with the other ranks
         await asyncio.get_running_loop().run_in_executor(None, llm.shutdown)
     return res["tokens"], elapsed, res["lats"]
 
@@ -394,17 +379,7 @@ def main(argv=None) -> int:
     leaders = list(range(0, st.world_size, st.tp_size))
     leaders_group = dist.new_group(leaders) if dist.is_initialized() else None
     dp_front = st.world_size > 1 and st.tp_size == 1 and not engine.lockstep
-    gateway = args.frontend == "gateway" and dp_front
-    if gateway:  # one gRPC address, an acceptor per rank (SO_REUSEPORT), least-loaded routing
-        from polykey_service_amd.engine.async_llm import AsyncLLM
-        from polykey_service_amd.engine.remote import dp_gateway
-        local = AsyncLLM(engine)
-        pool = dp_gateway(local, st, reuseport=True)
-        tokens, elapsed, lats = asyncio.run(run_waves(args, engine, st, leaders_group, llm=pool, shared_port=True))
-        if os.environ.get("POLYKEY_BENCH_TIMING") == "1":  # requests each engine served (routing balance)
-            print(f"[gateway] rank {st.rank}: engine served {local.stats['requests']} requests, "
-                  f"{local.stats['steps']} steps", file=sys.stderr, flush=True)
-    elif args.frontend == "single" and dp_front:
+    if args.frontend == "single" and dp_front:
         from polykey_service_amd.engine.async_llm import AsyncLLM
         from polykey_service_amd.engine.remote import dp_gateway
         local = AsyncLLM(engine)
@@ -456,8 +431,7 @@ def main(argv=None) -> int:
                 "parallelism": (f"tp{st.tp_size}" + (f"_dp{st.dp_size}" if st.dp_size > 1 else "")
                                 + (f"_ep{st.ep_size}" if st.ep_size > 1 else "")) if st.tp_size > 1
                 else f"dp{st.world_size}" + (f"_ep{st.ep_size}_a2a" if st.ep_size > 1 else "")
-                + ("_gateway" if gateway else "") + ("_single_frontend" if args.frontend == "single" and dp_front
-                                                          else ""),
+                + ("_single_frontend" if args.frontend == "single" and dp_front else ""),
                 "concurrency_per_replica": args.concurrency,
                 "rpc": f"ExecuteTool ({args.mode})",
                 "clients": "load-generator process" if args.client == "process" else "server event loop",

@@ -166,15 +166,4 @@ void bind_vote_board(py::module_& m) {
           py::arg("busy"), py::arg("stopping") = false, py::arg("ntok") = 0, py::arg("timeout_ms") = 600000)
       .def_property_readonly("nranks", &pk::VoteBoard::nranks)
       .def_property_readonly("step", &pk::VoteBoard::step);
-  // Atomic add / store on an int64 slot of a shared-memory buffer (the DP gateway's load board:
-  // several acceptor processes bump an engine's count while that engine publishes its own).
-  m.def(
-      "shm_add_i64",
-      [](py::buffer b, int64_t index, int64_t v) {
-        py::buffer_info info = b.request(true);
-        if (index < 0 || (index + 1) * 8 > info.size * info.itemsize) throw std::out_of_range("shm_add_i64 index");
-        auto* p = static_cast<int64_t*>(info.ptr) + index;
-        return __atomic_add_fetch(p, v, __ATOMIC_ACQ_REL);
-      },
-      py::arg("buffer"), py::arg("index"), py::arg("value"));
 }

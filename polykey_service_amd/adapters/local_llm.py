@@ -197,24 +197,18 @@ class ReplicaPool:
     rank per GPU: :func:`~polykey_service_amd.engine.remote.dp_gateway`); the first replica must
     be local.  Duck-types :class:`AsyncLLM`."""
 
-    def __init__(self, replicas, loads=None, on_pick=None):
+    def __init__(self, replicas):
         self.replicas = list(replicas)
-        # per-replica load estimates (default: each replica's own load()) and routing hooks
-        self.loads = list(loads) if loads is not None else [r.load for r in self.replicas]
-        self.on_pick = list(on_pick) if on_pick is not None else [None] * len(self.replicas)
         self.tokenizer = self.replicas[0].tokenizer
         self.engine = self.replicas[0].engine
         self.on_fatal = None
         self.watchdog_s = 0.0
 
     def _pick(self):
-        i = min(range(len(self.replicas)), key=lambda j: self.loads[j]())
-        if self.on_pick[i] is not None:
-            self.on_pick[i]()
-        return self.replicas[i]
+        return min(self.replicas, key=lambda r: r.load())
 
     def load(self) -> int:
-        return sum(f() for f in self.loads)
+        return sum(r.load() for r in self.replicas)
 
     def generate(self, prompt_ids, params, request_id=None, final_only=False):
         return self._pick().generate(prompt_ids, params, request_id, final_only=final_only)
@@ -232,18 +226,10 @@ class ReplicaPool:
                 setattr(r, k, v)
 
     def shutdown(self, timeout: float = 10.0) -> None:
-        # remote handles first (their "stop" frames release the other ranks' engine servers), then
-        # -- SO_REUSEPORT gateway -- wait until every other acceptor has released this rank's
-        # engine before stopping it
+        # remote handles first: their "stop" frames release the other ranks' engine servers
         for r in self.replicas[1:]:
             r.shutdown(timeout)
-        th = self.__dict__.get("gateway_thread")
-        if th is not None:
-            th.join(timeout)
         self.replicas[0].shutdown(timeout)
-        board = self.__dict__.get("load_board")
-        if board is not None:
-            board.close()
 
     async def aclose(self) -> None:
         for r in self.replicas:

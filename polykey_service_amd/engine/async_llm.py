@@ -68,9 +68,6 @@ class AsyncLLM:
         # decode steps (the GPU idles meanwhile); a short interval hands the GIL over promptly.
         sys.setswitchinterval(0.002)
         self._fatal_sent = False
-        # SO_REUSEPORT gateway (engine/remote.py dp_gateway): this engine's load, published for the
-        # other ranks' acceptors after every step and every batch of submissions
-        self.load_pub: Optional[Callable[[int], None]] = None
         self._thread = threading.Thread(target=self._run, name="polykey-engine", daemon=True)
         self._thread.start()
         self._watchdog = threading.Thread(target=self._watch, name="polykey-watchdog", daemon=True)
@@ -223,8 +220,6 @@ class AsyncLLM:
         with self._lock:
             cmds = list(self._cmds)
             self._cmds.clear()
-        if cmds and self.load_pub is not None:
-            self.load_pub(self.engine.scheduler.num_unfinished() + len(cmds))
         for kind, arg in cmds:
             if kind == "add":
                 rid, prompt, params = arg
@@ -323,8 +318,6 @@ class AsyncLLM:
                     self.metrics.observe_step(eng, dt, outs)
                 self.stats["steps"] += 1
                 self.last_step_time = time.monotonic()
-                if self.load_pub is not None:
-                    self.load_pub(self.load())
                 if outs:
                     self.stats["output_tokens"] += sum(len(o.new_token_ids) for o in outs)
                     self._deliver([(o.request_id, o) for o in outs])

@@ -67,9 +67,9 @@ def _params_dict(p: SamplingParams) -> dict:
 class EngineServer:
     """Serves one :class:`~polykey_service_amd.engine.async_llm.AsyncLLM` to front ends.
 
-    ``serve(n)`` blocks: it accepts ``n`` authenticated front-end connections (the single
-    gateway: 1; the SO_REUSEPORT gateway: every other rank's acceptor), feeds their commands to
-    the engine, and returns once every one of them has sent "stop" or closed; outputs go back
+    ``serve(n)`` blocks: it accepts ``n`` authenticated front-end connections (the rank-0 front
+    end: 1), feeds their commands to the engine, and returns once every one of them has sent
+    "stop" or closed; outputs go back
     from the engine thread through :meth:`AsyncLLM.set_external_sink`, each to the connection
     that submitted the request."""
 
@@ -188,13 +188,9 @@ class RemoteEngine:
     router (:class:`~polykey_service_amd.adapters.local_llm.ReplicaPool`) and the tools."""
 
     def __init__(self, addr: Tuple[str, int], tokenizer, name: str = "remote", connect_timeout: float = 120.0,
-                 token: Optional[str] = None, load_fn=None, load_add=None):
+                 token: Optional[str] = None):
         self.tokenizer = tokenizer
         self.name = name
-        self.load_fn = load_fn  # engine-wide load (shared-memory load board), else this handle's own
-        # routing a request bumps the board entry at once (the engine overwrites it with its true
-        # count every step): a burst at one acceptor spreads instead of herding on a stale minimum
-        self.load_add = load_add
         self.on_fatal = None
         self.watchdog_s = 0.0
         self.dead: Optional[BaseException] = None
@@ -219,7 +215,7 @@ class RemoteEngine:
         self._reader.start()
 
     def load(self) -> int:
-        return self.load_fn() if self.load_fn is not None else len(self._streams)
+        return len(self._streams)
 
     def healthy(self) -> bool:
         return self.dead is None
@@ -279,8 +275,6 @@ class RemoteEngine:
         try:
             _send(self.sock, self._wlock, {"op": "add", "rid": rid, "prompt": list(prompt_ids),
                                            "params": _params_dict(params), "final": bool(final_only)})
-            if self.load_add is not None:
-                self.load_add(1)
             while True:
                 item = await q.get()
                 if isinstance(item, BaseException):
@@ -326,75 +320,19 @@ class RemoteEngine:
         await asyncio.get_running_loop().run_in_executor(None, self.shutdown)
 
 
-class LoadBoard:
-    """Per-rank unfinished-request counts in POSIX shared memory: every front end of the
-    SO_REUSEPORT gateway routes by the engines' true loads, whoever submitted the requests."""
+def dp_gateway(llm, st, group=None):
+    """Wire the DP ranks (tp = 1, one engine per rank) to ONE gRPC front end on rank 0.
 
-    def __init__(self, name: str, create: bool, world: int):
-        import numpy as np
-        from multiprocessing import resource_tracker, shared_memory
-        self.shm = shared_memory.SharedMemory(name=name, create=create, size=8 * world)
-        if not create:  # the creator owns (and unlinks) the segment
-            try:
-                resource_tracker.unregister(self.shm._name, "shared_memory")
-            except Exception:  # noqa: BLE001
-                pass
-        self.owner = create
-        self.arr = np.ndarray((world,), dtype=np.int64, buffer=self.shm.buf)
-        try:
-            from .._native.loader import load_extension
-            self._atomic_add = load_extension("_pk_runtime").shm_add_i64
-        except Exception:  # noqa: BLE001 - extension not built: plain (racy) adds
-            self._atomic_add = None
-        if create:
-            self.arr[:] = 0
-
-    def set(self, rank: int, v: int) -> None:
-        self.arr[rank] = v
-
-    def get(self, rank: int) -> int:
-        return int(self.arr[rank])
-
-    def add(self, rank: int, v: int) -> None:
-        """An acceptor's routing estimate (an atomic add: the acceptors route concurrently; the
-        owning engine's next publish replaces it with the true count)."""
-        if self._atomic_add is not None:
-            self._atomic_add(self.shm.buf, rank, v)
-        else:
-            self.arr[rank] += v
-
-    def unlink(self) -> None:
-        """Owner, once every rank has attached: drop the /dev/shm name (mappings stay valid)."""
-        if self.owner:
-            self.owner = False
-            try:
-                self.shm.unlink()
-            except FileNotFoundError:
-                pass
-
-    def close(self) -> None:
-        self.arr = None
-        self.shm.close()
-        self.unlink()
-
-
-def dp_gateway(llm, st, group=None, reuseport: bool = False):
-    """Wire the DP ranks (tp = 1, one engine per rank) to the gRPC front end.
-
-    Collective over ``group`` (default: the world).
-
-    ``reuseport=False`` (one front end): every rank but 0 serves its ``llm`` to rank 0 and blocks
-    until the front end stops it (returns None); rank 0 returns a
+    Collective over ``group`` (default: the world): every rank but 0 serves its ``llm`` to rank 0
+    and blocks until the front end stops it (returns None); rank 0 returns a
     :class:`~polykey_service_amd.adapters.local_llm.ReplicaPool` over its own ``llm`` and a
-    :class:`RemoteEngine` per other rank.
+    :class:`RemoteEngine` per other rank (least-loaded routing).
 
-    ``reuseport=True`` (one front-end ADDRESS, N acceptor processes): every rank returns a
-    ReplicaPool over its own engine and every other rank's, serves its engine to the other ranks'
-    acceptors from a background thread, and publishes its load on a shared-memory board; each
-    rank then binds the SAME gRPC port (SO_REUSEPORT, grpc's default on Linux), the kernel spreads
-    client connections over the acceptors and each routes a request to the least-loaded engine --
-    request parsing and response building scale with the ranks instead of funnelling through one
-    Python process (profiles/r2_gateway_ab.txt)."""
+    (Round 4 retired the SO_REUSEPORT variant -- one address, an acceptor per rank over a
+    shared-memory load board: it cost 1.8-2.4 % against per-rank endpoints when it ran clean and
+    stalled intermittently on the shared-GPU rehearsal, profiles/r3_gateway_ab.txt.  Per-rank
+    endpoints (bench.py's replicas, one gRPC server per GPU behind any TCP load balancer) are the
+    DP design; this single front end serves deployments that need one address.)"""
     import os
     import secrets
 
@@ -409,41 +347,15 @@ def dp_gateway(llm, st, group=None, reuseport: bool = False):
     # rank 0 draws the shared token; every engine server accepts only a front end that presents it
     tok = [secrets.token_hex(16) if st.rank == 0 else None]
     dist.broadcast_object_list(tok, src=0, group=group)
-    if not reuseport:
-        server = EngineServer(llm, host=bind, token=tok[0]) if st.rank != 0 else None
-        addrs: List = [None] * st.world_size
-        dist.all_gather_object(addrs, (advertise, server.port) if server is not None else None, group=group)
-        if server is not None:
-            server.serve()
-            return None
-        remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0])
-                   for r in range(1, st.world_size)]
-        return ReplicaPool([llm] + remotes)
-    if not single_node:
-        raise ValueError("the SO_REUSEPORT gateway shares one address: its ranks must share a node")
-    server = EngineServer(llm, host=bind, token=tok[0])
-    addrs = [None] * st.world_size
-    dist.all_gather_object(addrs, (advertise, server.port), group=group)
-    name = [f"pk_load_{os.getpid()}_{secrets.token_hex(4)}" if st.rank == 0 else None]
-    board = LoadBoard(name[0], True, st.world_size) if st.rank == 0 else None
-    dist.broadcast_object_list(name, src=0, group=group)
-    if board is None:
-        board = LoadBoard(name[0], False, st.world_size)
-    llm.load_pub = lambda v, b=board, r=st.rank: b.set(r, v)
-    th = threading.Thread(target=server.serve, args=(st.world_size - 1,), name="polykey-engine-server", daemon=True)
-    th.start()
-    remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0],
-                            load_fn=lambda b=board, r=r: b.get(r), load_add=lambda d, b=board, r=r: b.add(r, d))
-               for r in range(st.world_size) if r != st.rank]
-    dist.barrier(group=group)  # every acceptor connected before any rank serves clients
-    board.unlink()  # every rank attached the load board
-    # this rank's engine: its own exact count, or the board's when other acceptors have just
-    # routed requests to it that it has not drained yet
-    pool = ReplicaPool([llm] + remotes, loads=[lambda b=board, r=st.rank: max(llm.load(), b.get(r))]
-                       + [x.load for x in remotes],
-                       on_pick=[lambda b=board, r=st.rank: b.add(r, 1)] + [None] * len(remotes))
-    pool.gateway_thread, pool.load_board = th, board
-    return pool
+    server = EngineServer(llm, host=bind, token=tok[0]) if st.rank != 0 else None
+    addrs: List = [None] * st.world_size
+    dist.all_gather_object(addrs, (advertise, server.port) if server is not None else None, group=group)
+    if server is not None:
+        server.serve()
+        return None
+    remotes = [RemoteEngine(tuple(addrs[r]), llm.tokenizer, name=f"rank{r}", token=tok[0])
+               for r in range(1, st.world_size)]
+    return ReplicaPool([llm] + remotes)
 
 
 def _fanout(batch) -> None:

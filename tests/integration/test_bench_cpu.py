@@ -29,8 +29,8 @@ ARGS = ["--model", "tiny-llama-gqa4", "--steps", "1", "--warmup", "1", "--concur
 
 
 @pytest.mark.parametrize("gpus,client,frontend", [(1, "process", "replicas"), (2, "process", "replicas"),
-                                                 (1, "inproc", "replicas"), (2, "inproc", "gateway"),
-                                                 (3, "process", "gateway"), (2, "inproc", "single")])
+                                                 (1, "inproc", "replicas"), (3, "inproc", "single"),
+                                                 (2, "inproc", "single")])
 def test_bench_json_line(tmp_path, gpus, client, frontend):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     r = _run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--client", client,
@@ -43,7 +43,8 @@ def test_bench_json_line(tmp_path, gpus, client, frontend):
     assert out["n_gpus"] == gpus and out["steps"] == 1 and out["warmup"] == 1
     assert out["value"] > 0 and out["ms_per_step"] > 0 and out["higher_is_better"] is True
     assert out["scaling"] == "weak" and out["dtype"] == "bf16"
-    gw = {"gateway": "_gateway", "single": "_single_frontend"}.get(frontend, "") if gpus > 1 else ""
+    gw = {"single": "_single_frontend"}.get(frontend, "") if gpus > 1 else ""
+    assert not any(k.startswith("tp") for k in out)  # no TP child for a model other than Llama-3-8B
     assert out["config"]["parallelism"] == f"dp{gpus}{gw}" and out["config"]["global_batch"] == 4 * gpus
     assert out["config"]["clients"] == ("load-generator process" if client == "process" else "server event loop")
     # unique random prompts: the prefix cache serves nothing, so no prefill work is skipped

@@ -148,29 +148,3 @@ def test_abort_of_a_final_only_request_drops_its_buffer(served):
     while _t.monotonic() < deadline and any("r-final" in s._final for s in servers):
         _t.sleep(0.05)
     assert not any("r-final" in s._final for s in servers)
-
-
-def test_gateway_burst_spreads_over_engines():
-    """A burst at one acceptor of the SO_REUSEPORT gateway: routing bumps the shared load board
-    at once, so 64 back-to-back picks spread 16 / 16 / 16 / 16 instead of herding on whichever
-    engine looked least loaded before the burst (profiles/r3_gateway_ab.txt)."""
-    import os
-    import secrets
-
-    from polykey_service_amd.adapters.local_llm import ReplicaPool
-    from polykey_service_amd.engine.remote import LoadBoard
-
-    class _R:
-        tokenizer = engine = None
-
-    board = LoadBoard(f"pk_test_{os.getpid()}_{secrets.token_hex(4)}", True, 4)
-    try:
-        reps = [_R() for _ in range(4)]
-        pool = ReplicaPool(reps, loads=[lambda i=i: board.get(i) for i in range(4)],
-                           on_pick=[lambda i=i: board.add(i, 1) for i in range(4)])
-        picks = [reps.index(pool._pick()) for _ in range(64)]
-        assert sorted(picks.count(i) for i in range(4)) == [16, 16, 16, 16]
-        board.set(2, 0)  # an engine's publish replaces the estimate with its true count
-        assert reps.index(pool._pick()) == 2
-    finally:
-        board.close()
