@@ -422,7 +422,8 @@ def test_fused_err_word_plumbing():
     parts = gemm.residual_parts(None, res.clone(), torch.empty(2 * 64, device="cuda"))
     ws = torch.empty(gemm.choose_split(H, I, M) * M * H, dtype=torch.float32, device="cuda")
     flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda")
-    gemm.mlp_fused(res, gup, dp, gemm.RowScale(parts, 1e-5), ws, flow)
+    ws_gu = torch.empty(gemm.gate_up_split(2 * I, H, M) * M * 2 * I, dtype=torch.float32, device="cuda")
+    gemm.mlp_fused(res, gup, dp, gemm.RowScale(parts, 1e-5), ws, flow, ws_gu=ws_gu)
     torch.cuda.synchronize()
     gemm.check_fused()
     w = ctypes.c_int.from_address(addr)

@@ -4,7 +4,8 @@ LM-head shards on the packed decode GEMM, W=8 one-shot / fused IPC collectives, 
 pipelined continuations, the shared-memory step channel; 4 of the 80 layers (the full depth runs
 in tools/tp_rehearsal.py).  The graphed engine must emit exactly the eager engine's tokens, and
 its prefill logits must match a TP=1 engine on the same seed to within 3x the TP=1 engine's own
-rounding noise at this depth (the same prefill in one step vs in two halves, per prompt).  A
+rounding noise at this depth (the same prefill in one step vs in two halves, the largest over the
+comparison prompts).  A
 deliberately wrong model -- one rank's attention partial dropped in one layer -- must fail that
 check."""
 import json
@@ -41,7 +42,7 @@ def test_llama3_70b_tp8_shapes_on_one_gpu(tmp_path):
     assert res["graph_equals_eager"], res
     assert res["ref_first_token_rows_not_near_tie"] == [], res
     # bf16 partials are rounded per rank before the sum: logits agree to the TP=1 noise, not bits
-    assert min(res["ref_noise_row_mean_abs_diff"]) > 0, res  # the calibration measured something
+    assert res["ref_noise_band"] > 0, res  # the calibration measured something
     assert res["ref_rows_outside_noise"] == [], res
 
 
@@ -50,4 +51,4 @@ def test_llama3_70b_tp8_dropped_partial_is_caught(tmp_path):
     every comparison prompt's logits must leave the noise band."""
     env = dict(os.environ, POLYKEY_FAULT_DROP_PARTIAL="1,3")
     res = _rehearse(str(tmp_path / "tp8f"), ["--check-only"], env=env)
-    assert len(res["ref_rows_outside_noise"]) == 4, res
+    assert res["ref_noise_band"] > 0 and len(res["ref_rows_outside_noise"]) == 4, res

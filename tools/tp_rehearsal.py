@@ -222,11 +222,14 @@ def role_rank(a) -> int:
                    ref_logits_scale=round(float(rl.abs().mean()), 4),
                    ref_tokens_equal_all=eager == ref["tokens"])
         if "noise_mean" in ref:
-            # per comparison prompt: TP = N vs TP = 1 within NOISE_FACTOR x the TP = 1 noise
+            # every comparison prompt: TP = N vs TP = 1 within NOISE_FACTOR x the TP = 1 noise at this
+            # depth (the largest over the prompts: a prompt whose two TP = 1 computations happen to
+            # be bit-identical -- row-independent decode GEMMs for <= 64-token steps -- says nothing
+            # about the scale of a valid reordering)
             nm = ref["noise_mean"]
-            res.update(ref_noise_row_mean_abs_diff=nm,
-                       ref_rows_outside_noise=[r for r, (d, n) in enumerate(zip(row_mean, nm))
-                                               if d > NOISE_FACTOR * n + 1e-4])
+            band = NOISE_FACTOR * max(nm)
+            res.update(ref_noise_row_mean_abs_diff=nm, ref_noise_band=round(band, 5),
+                       ref_rows_outside_noise=[r for r, d in enumerate(row_mean) if d > band])
     if a.check_only:
         eng.runner.stop_workers()
         print(json.dumps(res), flush=True)
