@@ -305,8 +305,53 @@ constexpr int kDecodePart = 512;  // keys per decode partition (ops/attention.py
 
 }  // namespace
 
-// Workspace for decode: part_o [n_seqs, n_q, n_parts, 128] fp32, part_ml [n_seqs, n_q, n_parts, 2] fp32.
-PK_EXPORT int pk_decode_num_parts(int max_context) { return (max_context + kDecodePart - 1) / kDecodePart; }
+// Workspace for decode: part_o [n_seqs, n_q, n_parts, 128] fp32, part_ml [n_seqs, n_q, n_parts, 2] fp32,
+// n_parts counted in the smallest partition (kDecodePartSmall, ops/attention.py _PART_MIN).
+PK_EXPORT int pk_decode_num_parts(int max_context) { return (max_context + kDecodePartSmall - 1) / kDecodePartSmall; }
+
+// Keys per partition of a launch: 512, or 128 when (seq, kv head) pairs x partitions would leave
+// most CUs idle -- the 70B TP=8 shard has ONE kv head per rank, so 64 sequences are 64 workgroups
+// at 512 keys (22.5 us for 12.6 MB of K/V, profiles/r4_solo_70b_tp8_unfused_kstats.md) and 256 at
+// 128 (4 partials per sequence, merged after).
+int decode_part(int n_seqs, int n_kv, int max_ctx) {
+  const int big = (max_ctx + kDecodePart - 1) / kDecodePart;
+  const int z = big < g_decode_z ? big : g_decode_z;
+  return n_seqs * n_kv * z < kDecodeFill ? kDecodePartSmall : kDecodePart;
+}
+
+template <int P>
+static int decode_launch_p(void* out, const void* q, const QkvIn& qi, const void* k_cache, const void* v_cache,
+                           const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
+                           void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
+                           int out_stride, float scale, int max_ctx, hipStream_t stream) {
+  const int n_parts = (max_ctx + P - 1) / P;
+  if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
+  // z is capped: a short context leaves the extra z-workgroups idle, and graph capture fixes
+  // the grid for max_model_len, so a z of n_parts would launch mostly-empty workgroups
+  dim3 grid(n_kv, n_seqs, n_parts < g_decode_z ? n_parts : g_decode_z);
+#define PK_DECODE_ARGS                                                                                            \
+  static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<bf16_t*>(const_cast<void*>(k_cache)),   \
+      static_cast<bf16_t*>(const_cast<void*>(v_cache)), static_cast<const int*>(block_tables),                  \
+      static_cast<const int*>(context_lens), static_cast<float*>(part_o), static_cast<float*>(part_ml),          \
+      static_cast<int*>(counters), n_q, n_kv, bs, max_blocks, q_stride, out_stride, n_parts, scale * kLog2e, qi
+  if (qi.partial != nullptr) {
+    switch (qi.S) {
+      case 2: paged_decode_kernel<P, kDecodeWaves, true, 2><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+      case 4: paged_decode_kernel<P, kDecodeWaves, true, 4><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+      case 8: paged_decode_kernel<P, kDecodeWaves, true, 8><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+      default: paged_decode_kernel<P, kDecodeWaves, true, 0><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+    }
+  } else
+    paged_decode_kernel<P, kDecodeWaves, false><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS);
+#undef PK_DECODE_ARGS
+  int rc = PK_CHECK_LAUNCH();
+  if (rc || counters != nullptr || n_parts == 1) return rc;
+  dim3 g2(n_q, n_seqs);
+  paged_decode_reduce_kernel<P><<<g2, 128, 0, stream>>>(
+      static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
+      static_cast<const int*>(context_lens), n_q, out_stride, n_parts, static_cast<int>(grid.z));
+  return PK_CHECK_LAUNCH();
+}
 
 // counters: [n_seqs, n_kv] int32, zero-initialised once (the merging workgroup re-arms its
 // counter); with counters == null the partitions are merged by a second kernel instead.
@@ -319,33 +364,13 @@ static int decode_launch(void* out, const void* q, const QkvIn& qi, const void* 
   // max_ctx bounds the contexts of this launch (<= 0: the block-table capacity).  A launch
   // known to stay within one partition needs no partition grid and no merge kernel.
   if (max_ctx <= 0 || max_ctx > max_blocks * bs) max_ctx = max_blocks * bs;
-  const int n_parts = (max_ctx + kDecodePart - 1) / kDecodePart;
-  if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
-  // z is capped: a short context leaves the extra z-workgroups idle, and graph capture fixes
-  // the grid for max_model_len, so a z of n_parts would launch mostly-empty workgroups
-  dim3 grid(n_kv, n_seqs, n_parts < g_decode_z ? n_parts : g_decode_z);
-#define PK_DECODE_ARGS                                                                                            \
-  static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<bf16_t*>(const_cast<void*>(k_cache)),   \
-      static_cast<bf16_t*>(const_cast<void*>(v_cache)), static_cast<const int*>(block_tables),                  \
-      static_cast<const int*>(context_lens), static_cast<float*>(part_o), static_cast<float*>(part_ml),          \
-      static_cast<int*>(counters), n_q, n_kv, bs, max_blocks, q_stride, out_stride, n_parts, scale * kLog2e, qi
-  if (qi.partial != nullptr) {
-    switch (qi.S) {
-      case 2: paged_decode_kernel<kDecodePart, kDecodeWaves, true, 2><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
-      case 4: paged_decode_kernel<kDecodePart, kDecodeWaves, true, 4><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
-      case 8: paged_decode_kernel<kDecodePart, kDecodeWaves, true, 8><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
-      default: paged_decode_kernel<kDecodePart, kDecodeWaves, true, 0><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
-    }
-  } else
-    paged_decode_kernel<kDecodePart, kDecodeWaves, false><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS);
-#undef PK_DECODE_ARGS
-  int rc = PK_CHECK_LAUNCH();
-  if (rc || counters != nullptr || n_parts == 1) return rc;
-  dim3 g2(n_q, n_seqs);
-  paged_decode_reduce_kernel<kDecodePart><<<g2, 128, 0, stream>>>(
-      static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
-      static_cast<const int*>(context_lens), n_q, out_stride, n_parts, static_cast<int>(grid.z));
-  return PK_CHECK_LAUNCH();
+  if (decode_part(n_seqs, n_kv, max_ctx) == kDecodePartSmall)
+    return decode_launch_p<kDecodePartSmall>(out, q, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml,
+                                             counters, n_seqs, n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale,
+                                             max_ctx, stream);
+  return decode_launch_p<kDecodePart>(out, q, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml,
+                                      counters, n_seqs, n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale, max_ctx,
+                                      stream);
 }
 
 // max_blocks: block-table row stride; max_ctx: bound on every context of this launch (<= 0: no bound)

@@ -13,11 +13,10 @@
 
 using namespace pk;
 
-int pk_get_decode_z();  // attention.hip
+int pk_get_decode_z();                          // attention.hip
+int decode_part(int n_seqs, int n_kv, int max_ctx);  // attention.hip: keys per partition (512 or 128)
 
 namespace {
-
-constexpr int kFusedPart = 512;  // attention.hip kDecodePart
 
 struct AttnArgs {
   bf16_t* out;
@@ -32,16 +31,16 @@ struct AttnArgs {
   QkvIn qi;
 };
 
-template <int MT>
+template <int MT, int P>
 union FusedLds {
   SkinnyLds<MT> g;
-  DecodeLds<kFusedPart, kDecodeWaves> a;
+  DecodeLds<P, kDecodeWaves> a;
 };
 
-template <int MT, int SS>
+template <int MT, int SS, int P>
 __global__ void __launch_bounds__(256, 2) qkv_attn_fused_kernel(const GemmArgs qkv, const AttnArgs aa,
                                                                 const Flow fq, const Flow fa, int n_qkv, int n_attn) {
-  __shared__ FusedLds<MT> lds;
+  __shared__ FusedLds<MT, P> lds;
   const int b = blockIdx.x;
   if (b < n_qkv) {
     skinny_tile<MT, kPartial, true, false, false, true, 2, 1>(qkv, b, 0, n_qkv, lds.g, fq);
@@ -49,7 +48,7 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_fused_kernel(const GemmArgs q
   }
   if (b >= n_attn) return;  // small batches: more QKV tiles than attention tiles
   const int x = b % aa.n_kv, y = (b / aa.n_kv) % aa.n_seqs, z = b / (aa.n_kv * aa.n_seqs);
-  decode_tile<kFusedPart, kDecodeWaves, true, SS, 2>(
+  decode_tile<P, kDecodeWaves, true, SS, 2>(
       aa.out, nullptr, aa.kc, aa.vc, aa.block_tables, aa.context_lens, aa.part_o, aa.part_ml, nullptr, aa.n_q, aa.n_kv,
       aa.bs, aa.max_blocks, 0, aa.out_stride, aa.n_parts, aa.scale2, aa.qi, x, y, z, aa.z, lds.a, fa);
 }
@@ -73,7 +72,8 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
       flow == nullptr)  // n_kv <= 64: one ticket slot per kv head below the done counters
     return -1;
   if (max_ctx <= 0 || max_ctx > max_blocks * bs) max_ctx = max_blocks * bs;
-  const int n_parts = (max_ctx + kFusedPart - 1) / kFusedPart;
+  const int P = decode_part(n_seqs, n_kv, max_ctx);  // 128-key partitions when the pairs alone cannot fill the chip
+  const int n_parts = (max_ctx + P - 1) / P;
   if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
   const int z = n_parts < pk_get_decode_z() ? n_parts : pk_get_decode_z();
   g.row_tiles = 1;
@@ -95,7 +95,12 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   const int n_attn = n_kv * n_seqs * z;
   const dim3 grid(n_attn > n_qkv ? n_attn : n_qkv);
   auto go = [&](auto mt, auto ss) {
-    qkv_attn_fused_kernel<decltype(mt)::value, decltype(ss)::value><<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv, n_attn);
+    if (P == kDecodePartSmall)
+      qkv_attn_fused_kernel<decltype(mt)::value, decltype(ss)::value, kDecodePartSmall>
+          <<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv, n_attn);
+    else
+      qkv_attn_fused_kernel<decltype(mt)::value, decltype(ss)::value, 512><<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv,
+                                                                                                    n_attn);
   };
   auto go_mt = [&](auto ss) {
     switch ((n_seqs + 15) / 16) {
@@ -111,8 +116,13 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
     go_mt(std::integral_constant<int, 0>{});
   int rc = PK_CHECK_LAUNCH();
   if (rc || n_parts == 1) return rc;
-  paged_decode_reduce_kernel<kFusedPart><<<dim3(n_q, n_seqs), 128, 0, stream>>>(
-      static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
-      static_cast<const int*>(context_lens), n_q, out_stride, n_parts, z);
+  if (P == kDecodePartSmall)
+    paged_decode_reduce_kernel<kDecodePartSmall><<<dim3(n_q, n_seqs), 128, 0, stream>>>(
+        static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
+        static_cast<const int*>(context_lens), n_q, out_stride, n_parts, z);
+  else
+    paged_decode_reduce_kernel<512><<<dim3(n_q, n_seqs), 128, 0, stream>>>(
+        static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
+        static_cast<const int*>(context_lens), n_q, out_stride, n_parts, z);
   return PK_CHECK_LAUNCH();
 }

@@ -44,7 +44,9 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 // SPLIT: gate_up split over K (gu.S > 1; kSiluSplit: write-through slabs, the last split of an
 // n-block sums them, applies SiLU and publishes h) -- for shapes whose gate_up n-blocks alone
 // cannot fill the chip (70B TP=8: 56).
-template <int MT, bool SPLIT>
+// DKR: the down projection's n-block height (2: 128 rows; 1: 64 rows -- twice the tiles at the
+// same split when 128-row tiles would leave CUs idle: 8B 32 x 4, 70B TP=8 64 x 2 -> 256).
+template <int MT, bool SPLIT, int DKR>
 __global__ void __launch_bounds__(256, 2) mlp_fused_kernel(const GemmArgs gu, const GemmArgs dn, const Flow fgu,
                                                            const Flow fdn, int n_gu, int n_dn) {
   __shared__ SkinnyLds<MT> lds;
@@ -53,7 +55,7 @@ __global__ void __launch_bounds__(256, 2) mlp_fused_kernel(const GemmArgs gu, co
     skinny_tile<MT, SPLIT ? kSiluSplit : kSiluMul, true, false, true, true, 2, 1>(gu, b, 0, n_gu, lds, fgu);
     __syncthreads();  // the LDS tiles are reused by the down tile
   }
-  if (b < n_dn) skinny_tile<MT, kPartial, true, false, false, false, 2, 2>(dn, b, 0, n_dn, lds, fdn);
+  if (b < n_dn) skinny_tile<MT, kPartial, true, false, false, false, DKR, 2>(dn, b, 0, n_dn, lds, fdn);
 }
 
 // x[m] = bf16(bf16(residual[m] * rinv[m]) * w), rinv from the per-row sum-of-squares parts a
@@ -513,6 +515,10 @@ PK_EXPORT int pk_skinny_gemm_ex(const GemmArgs* args, int mode, hipStream_t stre
 constexpr int kFlowCounters = 128 * kFlowPad + 64;  // gate_up n-block counters (kSiluSplit)
 constexpr int kFlowWords = kFlowCounters + 1024;
 
+// n-block height of the fused MLP's down tiles (ops/gemm.py down_kr must agree): 64 rows when
+// 128-row tiles at split S would be fewer than 192 workgroups
+static int down_kr(int N, int S) { return (N / 128) * S < 192 ? 1 : 2; }
+
 PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, hipStream_t stream) {
   GemmArgs gu = *gu_in, dn = *dn_in;
   if (gu.M <= 0) return 0;
@@ -529,23 +535,27 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   gu.max_group_rows = dn.max_group_rows = 0;
   int* done = flow + 64 * kFlowPad;
   int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
+  const int dkr = down_kr(dn.N, dn.S);
   Flow fgu{flow, done, err, 0, 0, dn.K / dn.S, 1, 0, 0, fused_spin_limit()};
-  Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / 128, dn.K / dn.S, 2, 0, 0, fused_spin_limit()};
-  const int n_gu = (gu.N / 128) * gu.S, n_dn = (dn.N / 128) * dn.S;
+  Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / (64 * dkr), dn.K / dn.S, 2, 0, 0, fused_spin_limit()};
+  const int n_gu = (gu.N / 128) * gu.S, n_dn = (dn.N / (64 * dkr)) * dn.S;
   const dim3 grid(n_gu > n_dn ? n_gu : n_dn);
-  auto go = [&](auto sp) {
+  auto go = [&](auto sp, auto kr) {
     constexpr bool SP = decltype(sp)::value;
+    constexpr int KR = decltype(kr)::value;
     switch ((gu.M + 15) / 16) {
-      case 1: mlp_fused_kernel<1, SP><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      case 2: mlp_fused_kernel<2, SP><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      case 3: mlp_fused_kernel<3, SP><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      default: mlp_fused_kernel<4, SP><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      case 1: mlp_fused_kernel<1, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      case 2: mlp_fused_kernel<2, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      case 3: mlp_fused_kernel<3, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      default: mlp_fused_kernel<4, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
     }
   };
+  using K1 = std::integral_constant<int, 1>;
+  using K2 = std::integral_constant<int, 2>;
   if (split)
-    go(std::true_type{});
+    dkr == 1 ? go(std::true_type{}, K1{}) : go(std::true_type{}, K2{});
   else
-    go(std::false_type{});
+    dkr == 1 ? go(std::false_type{}, K1{}) : go(std::false_type{}, K2{});
   return PK_CHECK_LAUNCH();
 }
 

@@ -504,7 +504,7 @@ class LlamaForCausalLM(nn.Module):
             h = gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
         else:  # split over K like the fused launch's gate_up when its n-blocks cannot fill the chip
             h = gemm.linear_silu(residual, mlp.gate_up, ws=self._ws_gu, packed=mlp.gate_up_pf, rowscale=rs)
-        return gemm.linear_partial(h, mlp.down, ws, packed=mlp.down_p)
+        return gemm.linear_down(h, mlp.down, ws, mlp.down_p)  # tiled as the fused launch tiles it
 
     def _forward_rowscale_tp(self, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
                              md: attn_ops.AttnMetadata, kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],

@@ -40,11 +40,13 @@ class AttnMetadata:
 
 
 _PART = 512  # must match kDecodePart in csrc/kernels/attention.hip
+_PART_MIN = 128  # kDecodePartSmall: launches whose (seq, kv head) pairs cannot fill the chip
 
 
 def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, device, n_kv: int = 0) -> tuple:
-    """Partition slabs (+ arrival counters when ``n_kv``) for split-K decode attention."""
-    n_parts = (max_blocks * block_size + _PART - 1) // _PART
+    """Partition slabs (+ arrival counters when ``n_kv``) for split-K decode attention, sized for
+    the smallest partition a launch may pick (the slab stride is the launch's partition count)."""
+    n_parts = (max_blocks * block_size + _PART_MIN - 1) // _PART_MIN
     if n_parts <= 1:
         return (None, None, None) if n_kv else (None, None)
     o = torch.empty((n_seqs, n_q, n_parts, 128), dtype=torch.float32, device=device)

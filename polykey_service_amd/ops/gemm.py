@@ -439,6 +439,28 @@ def set_fused_spin_limit(n: int) -> None:
     fn(int(n))
 
 
+def down_kr(N: int, K: int, M: int) -> int:
+    """n-block height of a decode down projection's tiles (in 64 rows; csrc gemm_skinny.hip
+    down_kr): 1 when 128-row tiles at its split would be fewer than 192 workgroups (8B: 32 x 4,
+    70B TP=8: 64 x 2 -> 256 tiles of 64 rows), else 2.  The fused MLP and the two-launch chain
+    use the same, so their slabs are bit-identical."""
+    return 1 if (N // _ROWS_PER_WG) * choose_split(N, K, M) < _TARGET_WGS else 2
+
+
+def linear_down(h: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, packed: Optional[torch.Tensor]) -> Partial:
+    """The decode down projection as the fused MLP launch tiles it (split :func:`choose_split`,
+    n-blocks of :func:`down_kr` x 64 rows) -> fp32 slabs."""
+    M, K = h.shape
+    N = w.shape[0]
+    S = choose_split(N, K, M)
+    if packed is not None and down_kr(N, K, M) == 1 and M <= SKINNY_MAX_M:
+        assert ws.numel() >= S * M * N, "split-K workspace too small"
+        native.call("pk_skinny_gemm", 0, ws.data_ptr(), h.data_ptr(), packed.data_ptr(), M, N, K, h.stride(0), N, S,
+                    1 | PACKED_BIT | HALF_BIT, native.stream_ptr())
+        return Partial(ws, S, M, N)
+    return linear_partial(h, w, ws, S, packed=packed)
+
+
 def gate_up_split(N2: int, K: int, M: int) -> int:
     """K split of a decode gate_up projection (1: the single-pass SiLU epilogue).  Its n-blocks
     alone fill the chip for 8B (224) but not for the 70B TP=8 shard (56: split 4)."""
@@ -458,7 +480,7 @@ def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_p
     return (0 < M <= SKINNY_MAX_M and N2 == 2 * I and N2 % 128 == 0 and K % (_KCHUNK * Sg) == 0
             and down_packed.shape[0] % 128 == 0 and I % (_KCHUNK * S) == 0 and (I // S) % 64 == 0 and S <= 64
             and gate_up_packed.shape[1] == K and (N2 // 128) * Sg <= device_cus(x.device)
-            and (down_packed.shape[0] // 128) * S <= device_cus(x.device))
+            and (down_packed.shape[0] // (64 * down_kr(down_packed.shape[0], I, M))) * S <= device_cus(x.device))
 
 
 def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: RowScale,

@@ -333,7 +333,7 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     S = gemm.choose_split(H, I, M)
     ws0 = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
     h = gemm.linear_silu(res, wgu, ws=ws_gu, packed=gup, rowscale=rs)
-    ref_slabs = gemm.linear_partial(h, wd, ws0, packed=dp).view().clone()
+    ref_slabs = gemm.linear_down(h, wd, ws0, dp).view().clone()
     flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda")
     ws = torch.empty_like(ws0)
     for _ in range(4):
@@ -353,7 +353,7 @@ def test_mlp_fused_matches_two_launches(M, H, I):
         p2 = gemm.residual_parts(None, r2.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
         rs2 = gemm.RowScale(p2, 1e-5)
         h2 = gemm.linear_silu(r2, wgu, ws=ws_gu, packed=gup, rowscale=rs2)
-        exp2 = gemm.linear_partial(h2, wd, ws0, packed=dp).view().clone()
+        exp2 = gemm.linear_down(h2, wd, ws0, dp).view().clone()
         got = gemm.mlp_fused(r2, gup, dp, rs2, ws, flow, ws_gu=ws_gu).view()
         torch.testing.assert_close(got, exp2, atol=0, rtol=0)
     torch.cuda.synchronize()
