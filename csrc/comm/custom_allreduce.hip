@@ -431,6 +431,125 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
   end_call(my_sig, e);
 }
 
+// Two-shot form of the fused collective (reduce_residual_2shot): for W >= 4 the one-shot form
+// has every rank read every peer's whole [M, N] partial over xGMI -- (W - 1) x the message per
+// rank, 7 MB at 70B TP=8 / 64 rows, serialised on the 7 links -- while here each rank reads only
+// ~2 (W - 1) / W of it:
+//   0. stage: the local split-K sum of every column (bf16 partial -> in_slot), as one-shot;
+//   1. reduce-scatter: the owner of each 256-column chunk (chunk c -> rank c % W) sums that chunk
+//      of the W partials in rank order, adds it into its residual, and publishes the new residual
+//      chunk and its row sums of squares in its result slot;
+//   2. all-gather: every rank copies the other owners' new residual chunks and parts.
+// Work item (row r, chunk group j) = chunks j W .. j W + W - 1 (one per owner); workgroup b takes
+// items b, b + nb, ... and synchronises only with the workgroups b of its peers (flag / flag2), so
+// the parts are per 256-column chunk: [N / 256, M].  Arithmetic per element as the one-shot
+// (fp32 rank-order sum of bf16 partials, bf16 round, bf16 residual add); every rank ends with the
+// owner's bits.
+constexpr int kRrChunk = 256;
+
+template <int W>
+__global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPtrs* __restrict__ peers, int rank,
+                                                                     size_t data_bytes, const float* __restrict__ slabs,
+                                                                     int S, const uint4* __restrict__ partial,
+                                                                     uint16_t* __restrict__ residual,
+                                                                     float* __restrict__ parts, int M, int N,
+                                                                     const Fail fail) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
+  __shared__ uint32_t e_s, err_s;
+  if (threadIdx.x == 0) {
+    e_s = my_sig->epoch[b] + 1;
+    err_s = my_sig->error;
+  }
+  __syncthreads();
+  if (err_s) return;
+  const uint32_t e = e_s;
+  const size_t in_slot = kSigBytes + (e & 1u) * data_bytes;
+  const size_t res_slot = kSigBytes + (2 + (e & 1u)) * data_bytes;
+  const int nchunk = N / kRrChunk, ngroups = nchunk / W;
+  const int items = M * ngroups;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  const int64_t parts_off = static_cast<int64_t>(M) * N * 2;  // byte offset of the parts in a result slot
+  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + in_slot);
+  const int t = threadIdx.x;
+  // 0. stage the local partial of every chunk of my items (W chunks x 256 columns = 32 W uint4)
+  for (int it = b; it < items; it += nb) {
+    const int r = it / ngroups, j = it - r * ngroups;
+    for (int u = t; u < 32 * W; u += 128) {
+      const int c = j * W + u / 32;
+      const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + (u % 32) * 8;  // element offset
+      uint4 pk;
+      if (S > 0) {
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int sidx = 0; sidx < S; ++sidx) {
+          const float4 p0 = *reinterpret_cast<const float4*>(slabs + sidx * slab + off);
+          const float4 p1 = *reinterpret_cast<const float4*>(slabs + sidx * slab + off + 4);
+          a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w;
+          a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
+        }
+        pk = make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7]));
+      } else {
+        pk = partial[off >> 3];
+      }
+      mine[off >> 3] = pk;
+    }
+  }
+  publish<W>(peers, rank, b, e, false);
+  if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
+  // 1. my chunk of each item: rank-order sum over xGMI, residual add, sums of squares
+  uint4* res_mine = reinterpret_cast<uint4*>(peers->base[rank] + res_slot);
+  float* parts_mine = reinterpret_cast<float*>(peers->base[rank] + res_slot + parts_off);
+  for (int it = b; it < items; it += nb) {
+    const int r = it / ngroups, j = it - r * ngroups;
+    const int c = j * W + rank;
+    if (t < 32) {  // one wave: 32 lanes x 8 columns
+      const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + t * 8;
+      uint4 v[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) v[q] = reinterpret_cast<const uint4*>(peers->base[q] + in_slot)[off >> 3];
+      const uint4 rr = *reinterpret_cast<const uint4*>(residual + off);
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) acc8(acc, v[q]);
+      float res[8];
+      unpack8f(rr, res);
+      float ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        res[q] = rbf(rbf(acc[q]) + res[q]);
+        ss += res[q] * res[q];
+      }
+      const uint4 out = make_uint4(pack2(res[0], res[1]), pack2(res[2], res[3]), pack2(res[4], res[5]),
+                                   pack2(res[6], res[7]));
+      *reinterpret_cast<uint4*>(residual + off) = out;
+      res_mine[off >> 3] = out;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 32);
+      if (t == 0) {
+        parts[static_cast<int64_t>(c) * M + r] = ss;
+        parts_mine[static_cast<int64_t>(c) * M + r] = ss;
+      }
+    }
+  }
+  publish<W>(peers, rank, b, e, true);
+  if (!wait_all<W>(my_sig->flag2, b, e, my_sig, fail)) return;
+  // 2. the other owners' chunks: new residual and parts
+  for (int it = b; it < items; it += nb) {
+    const int r = it / ngroups, j = it - r * ngroups;
+    for (int u = t; u < 32 * W; u += 128) {
+      const int q = u / 32;
+      if (q == rank) continue;
+      const int c = j * W + q;
+      const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + (u % 32) * 8;
+      *reinterpret_cast<uint4*>(residual + off) = reinterpret_cast<const uint4*>(peers->base[q] + res_slot)[off >> 3];
+      if (u % 32 == 0)
+        parts[static_cast<int64_t>(c) * M + r] =
+            reinterpret_cast<const float*>(peers->base[q] + res_slot + parts_off)[static_cast<int64_t>(c) * M + r];
+    }
+  }
+  end_call(my_sig, e);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------- host API
@@ -645,6 +764,16 @@ PK_EXPORT int pk_car_allgather(void* ctx, const void* inp, void* out, long long 
 // slabs: fp32 [S, M, N] (S >= 1), or S == 0 and `partial` a bf16 [M, N] partial.
 // N % 1024 == 0, M * N * 2 <= data_bytes; blocks <= 0: one workgroup per (row, chunk) item up to
 // 512 workgroups.
+// The two-shot form (reduce_residual_2shot_kernel) where it moves fewer bytes over xGMI: W >= 4
+// and whole 256-column chunk groups per owner.  Its parts are per 256 columns ([N / 256, M]).
+PK_EXPORT int pk_car_reduce_residual_nparts(void* ctx, int M, int N) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr) return -1;
+  const bool two = c->world >= 4 && N % (kRrChunk * c->world) == 0 &&
+                   static_cast<size_t>(M) * N * 2 + static_cast<size_t>(N / kRrChunk) * M * 4 <= c->data_bytes;
+  return two ? N / kRrChunk : N / 1024;
+}
+
 PK_EXPORT int pk_car_reduce_residual(void* ctx, const void* slabs, int S, const void* partial, void* residual,
                                      void* parts, int M, int N, int blocks, hipStream_t stream) {
   Ctx* c = static_cast<Ctx*>(ctx);
@@ -654,14 +783,34 @@ PK_EXPORT int pk_car_reduce_residual(void* ctx, const void* slabs, int S, const 
       residual == nullptr || parts == nullptr)
     return -2;
   if (static_cast<size_t>(M) * N * 2 > c->data_bytes) return -2;
-  const int items = M * (N / 1024);
-  if (blocks <= 0) blocks = std::min(items, 512);
-  blocks = std::max(1, std::min({blocks, items, kMaxBlocks}));
   const Fail fail{c->d_err, c->timeout_ticks};
   const float* sl = static_cast<const float*>(slabs);
   const uint4* pt = static_cast<const uint4*>(partial);
   uint16_t* rs = static_cast<uint16_t*>(residual);
   float* ps = static_cast<float*>(parts);
+  if (pk_car_reduce_residual_nparts(ctx, M, N) == N / kRrChunk) {
+    const int items = M * (N / kRrChunk / c->world);
+    int nb = blocks <= 0 ? std::min(items, 512) : blocks;
+    nb = std::max(1, std::min({nb, items, kMaxBlocks}));
+    switch (c->world) {
+#define PK_CRR2_CASE(WW)                                                                                       \
+  case WW:                                                                                                   \
+    reduce_residual_2shot_kernel<WW><<<nb, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, sl, S, pt, rs, ps, \
+                                                             M, N, fail);                                     \
+    break;
+      PK_CRR2_CASE(4)
+      PK_CRR2_CASE(5)
+      PK_CRR2_CASE(6)
+      PK_CRR2_CASE(7)
+      PK_CRR2_CASE(8)
+#undef PK_CRR2_CASE
+      default: return -3;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -4;
+  }
+  const int items = M * (N / 1024);
+  if (blocks <= 0) blocks = std::min(items, 512);
+  blocks = std::max(1, std::min({blocks, items, kMaxBlocks}));
   switch (c->world) {
 #define PK_CRR_CASE(WW)                                                                                          \
   case WW:                                                                                                     \

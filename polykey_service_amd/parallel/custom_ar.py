@@ -41,6 +41,7 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_allreduce_bf16_algo.argtypes = [_P, _P, _P, _LL, _I, _I, _P]
         lib.pk_car_allgather.argtypes = [_P, _P, _P, _LL, _LL, _I, _P]
         lib.pk_car_reduce_residual.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _P]
+        lib.pk_car_reduce_residual_nparts.argtypes = [_P, _I, _I]
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_clear_error.argtypes = [_P]
         lib.pk_car_set_error.argtypes = [_P]
@@ -137,12 +138,15 @@ class CustomAllReduce:
         """Fused TP collective of a row-parallel decode projection, one launch: this rank's
         split-K slabs (a :class:`~polykey_service_amd.ops.gemm.Partial`) or bf16 partial [M, N]
         are reduced locally, summed over the group through the IPC slots (rank order), added
-        into ``residual`` in place, and ``parts`` receives the per-1024-column sums of squares of
-        the new residual ([N / 1024, M] view returned) for the next folded-norm projection."""
+        into ``residual`` in place, and ``parts`` receives per-column-chunk sums of squares of
+        the new residual ([nparts, M] view returned) for the next folded-norm projection.  With
+        4+ ranks the collective is two-shot (reduce-scatter to the owner of each 256-column
+        chunk, then all-gather: ~2 (W-1)/W of the message over xGMI per rank instead of
+        (W-1)x; parts per 256 columns), else one-shot (parts per 1024 columns)."""
         M, N = residual.shape
         if not (residual.is_contiguous() and residual.dtype == torch.bfloat16 and self.supports_reduce_residual(M, N)):
             raise ValueError(f"reduce_residual: unsupported residual {tuple(residual.shape)} {residual.dtype}")
-        nparts = N // 1024
+        nparts = self.lib.pk_car_reduce_residual_nparts(self.ctx, M, N)
         assert parts.numel() >= nparts * M and parts.dtype == torch.float32
         if isinstance(pending, torch.Tensor):
             assert pending.shape == (M, N) and pending.is_contiguous() and pending.dtype == torch.bfloat16

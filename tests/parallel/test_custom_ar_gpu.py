@@ -94,8 +94,9 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e) + " " + traceback.format_exc()[-1500:]))
 
 
-def _rr_reference(slabs_all, partials_all, res, S):
-    """Sequential fp32 reference of pk_car_reduce_residual (same summation order)."""
+def _rr_reference(slabs_all, partials_all, res, S, nparts=None):
+    """Sequential fp32 reference of pk_car_reduce_residual (same summation order); parts per
+    N / nparts columns (1024: one-shot; 256: the two-shot form at 4+ ranks)."""
     world = len(partials_all)
     parts_bf = []
     for j in range(world):
@@ -111,7 +112,8 @@ def _rr_reference(slabs_all, partials_all, res, S):
         acc = acc + parts_bf[j]
     new = (acc.to(torch.bfloat16).float() + res.float()).to(torch.bfloat16)
     M, N = res.shape
-    sq = new.float().view(M, N // 1024, 1024).pow(2).sum(-1).t().contiguous()
+    nparts = nparts or N // 1024
+    sq = new.float().view(M, nparts, N // nparts).pow(2).sum(-1).t().contiguous()
     return new, sq
 
 
@@ -132,12 +134,15 @@ def _fused_phase(car, rank, world, dev):
             dist.all_gather(all_slabs, slabs)
         else:
             dist.all_gather(all_part, partial)
-        want, want_sq = _rr_reference(all_slabs, all_part, res, S)
         from polykey_service_amd.ops.gemm import Partial
         r_dev = res.to(dev)
-        parts = torch.zeros(8 * 64, dtype=torch.float32, device=dev)
+        parts = torch.zeros((N // 256) * M, dtype=torch.float32, device=dev)
         pend = Partial(slabs.to(dev).reshape(-1), S, M, N) if S else partial.to(dev)
         out_parts = car.reduce_residual(pend, r_dev, parts)
+        # two-shot (4+ ranks, 256-column chunk groups per owner) or one-shot
+        two = world >= 4 and N % (256 * world) == 0
+        assert out_parts.shape[0] == (N // 256 if two else N // 1024), (world, N, tuple(out_parts.shape))
+        want, want_sq = _rr_reference(all_slabs, all_part, res, S, out_parts.shape[0])
         torch.cuda.synchronize()
         gotr = r_dev.cpu()
         if not torch.equal(gotr, want):
@@ -159,7 +164,7 @@ def _fused_phase(car, rank, world, dev):
     res0 = torch.randn(M, N, generator=g).to(torch.bfloat16)
     part_in = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
     r_dev = res0.to(dev)
-    parts = torch.zeros(4 * M, dtype=torch.float32, device=dev)
+    parts = torch.zeros((N // 256) * M, dtype=torch.float32, device=dev)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -180,7 +185,7 @@ def _fused_phase(car, rank, world, dev):
     assert car.error() == 0
 
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_custom_allreduce_ranks_share_one_gpu(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
