@@ -66,7 +66,8 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   GemmArgs g = *qkv_in;
   const int n_seqs = g.M;
   if (n_seqs <= 0) return 0;
-  if (n_seqs > 64 || g.N != (n_q + 2 * n_kv) * kHD || g.N % 128 || g.S < 1 || g.K % (kKC * g.S) || !g.row_scale ||
+  // up to 128 rows (one row tile; 128 rows take the MT = 8 tile, whose row scale reads <= 16 parts)
+  if (n_seqs > 128 || (n_seqs > 64 && g.nrm_nparts > 16) || g.N != (n_q + 2 * n_kv) * kHD || g.N % 128 || g.S < 1 || g.K % (kKC * g.S) || !g.row_scale ||
       g.nrm_parts == nullptr || g.nrm_nparts < 1 || g.nrm_nparts > 64 || g.partial == nullptr || g.lda % 8 ||
       g.row_offsets != nullptr || n_kv > 64 || n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0 ||
       flow == nullptr)  // n_kv <= 64: one ticket slot per kv head below the done counters
@@ -77,7 +78,7 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
   const int z = n_parts < pk_get_decode_z() ? n_parts : pk_get_decode_z();
   g.row_tiles = 1;
-  g.tile_rows = 64;
+  g.tile_rows = n_seqs > 64 ? 128 : 64;
   g.max_group_rows = 0;
   const QkvIn qi{static_cast<const float*>(g.partial), static_cast<const int*>(positions),
                  static_cast<const float*>(cos_sin), static_cast<const int*>(slots), g.S, g.M};
@@ -107,7 +108,8 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
       case 1: go(std::integral_constant<int, 1>{}, ss); break;
       case 2: go(std::integral_constant<int, 2>{}, ss); break;
       case 3: go(std::integral_constant<int, 3>{}, ss); break;
-      default: go(std::integral_constant<int, 4>{}, ss); break;
+      case 4: go(std::integral_constant<int, 4>{}, ss); break;
+      default: go(std::integral_constant<int, 8>{}, ss); break;  // 65-128 rows: one 128-row tile
     }
   };
   if (g.S == 4)

@@ -522,7 +522,8 @@ static int down_kr(int N, int S) { return (N / 128) * S < 192 ? 1 : 2; }
 PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, hipStream_t stream) {
   GemmArgs gu = *gu_in, dn = *dn_in;
   if (gu.M <= 0) return 0;
-  if (gu.M > 64 || dn.M != gu.M || gu.N % 128 || gu.S < 1 || gu.K % (kKC * gu.S) || !gu.row_scale ||
+  // up to 128 rows (one row tile; MT = 8 above 64 rows, whose row scale reads <= 16 parts)
+  if (gu.M > 128 || (gu.M > 64 && gu.nrm_nparts > 16) || dn.M != gu.M || gu.N % 128 || gu.S < 1 || gu.K % (kKC * gu.S) || !gu.row_scale ||
       gu.nrm_parts == nullptr || gu.nrm_nparts < 1 || gu.nrm_nparts > 64 || gu.out == nullptr || dn.K != gu.N / 2 ||
       dn.N % 128 || dn.S < 1 || dn.S > 64 || dn.K % (kKC * dn.S) || (dn.K / dn.S) % 64 || dn.partial == nullptr ||
       dn.A != gu.out || dn.lda % 8 || gu.lda % 8 || gu.row_offsets != nullptr || dn.row_offsets != nullptr ||
@@ -531,7 +532,7 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   const bool split = gu.S > 1;
   gu.counters = split ? flow + kFlowCounters : nullptr;
   gu.row_tiles = dn.row_tiles = 1;
-  gu.tile_rows = dn.tile_rows = 64;
+  gu.tile_rows = dn.tile_rows = gu.M > 64 ? 128 : 64;
   gu.max_group_rows = dn.max_group_rows = 0;
   int* done = flow + 64 * kFlowPad;
   int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
@@ -547,7 +548,8 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
       case 1: mlp_fused_kernel<1, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
       case 2: mlp_fused_kernel<2, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
       case 3: mlp_fused_kernel<3, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      default: mlp_fused_kernel<4, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      case 4: mlp_fused_kernel<4, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      default: mlp_fused_kernel<8, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
     }
   };
   using K1 = std::integral_constant<int, 1>;

@@ -444,9 +444,16 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
     const int nsteps = 2 * nchunks;  // even
     const int rot2 = 2 * rot;
     auto ks = [&](int j) { return k0 + ((min(j, nsteps - 1) + rot2) % nsteps) * 128; };
-    load_a(ks(0));
-    load_w(wa, ks(0));
-    load_w(wb, ks(1));
+    if constexpr (FL == 2) {  // consumer of an in-launch hand-off: weights first, A after the wait
+      load_w(wa, ks(0));
+      load_w(wb, ks(1));
+      flow_wait(fl, split);
+      load_a(ks(0));
+    } else {
+      load_a(ks(0));
+      load_w(wa, ks(0));
+      load_w(wb, ks(1));
+    }
     store_a(0);
     int buf = 0;
     for (int j = 0; j < nsteps; j += 2) {

@@ -479,7 +479,7 @@ class LlamaForCausalLM(nn.Module):
         kc, vc = kv
         T = residual.shape[0]
         rs = gemm.RowScale(parts, layer.eps)
-        if md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and T <= gemm.SKINNY_MAX_M and md.num_decode == T:
+        if md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and gemm.fused_rows_ok(T, parts.shape[0]) and md.num_decode == T:
             # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip);
             # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
             return gemm.qkv_attn_fused(residual, at.qkv_pf, rs, ws, positions, self.cos_sin, kc, vc, md, at.scale,
@@ -494,7 +494,7 @@ class LlamaForCausalLM(nn.Module):
         """Folded-norm gate_up + SiLU and the down projection of one layer -> down's split-K slabs."""
         mlp = layer.mlp
         rs = gemm.RowScale(parts, layer.eps)
-        if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p) and not self.st.shared_device:
+        if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, parts.shape[0]) and not self.st.shared_device:
             # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
             return gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, rs, ws, self._flow, ws_gu=self._ws_gu)
         if residual.shape[0] > GATE_UP_SKINNY_MAX_M and not mlp.gate_up.is_meta:
@@ -550,8 +550,8 @@ class LlamaForCausalLM(nn.Module):
         if gu is None or gu.dim() != 2:
             return 0
         N2, K = gu.shape
-        n = max(gemm.gate_up_split(N2, K, M) * M * N2 for M in range(1, gemm.SKINNY_MAX_M + 1))
-        return n if n > gemm.SKINNY_MAX_M * N2 else 0
+        splits = [(gemm.gate_up_split(N2, K, M), M) for M in range(1, gemm.FUSED_MAX_M + 1)]
+        return max(sg * M * N2 for sg, M in splits) if any(sg > 1 for sg, _ in splits) else 0
 
     def _workspace_elems(self) -> int:
         shapes = []

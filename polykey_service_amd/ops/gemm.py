@@ -26,6 +26,10 @@ import os
 # XCD's L2 (csrc/kernels/gemm_skinny.hip "Row tiles", profiles/r3_decode_rows.txt)
 SKINNY_MAX_M = 64
 DECODE_MAX_M = 512
+# the fused decode launches (qkv_attn_fused, mlp_fused) take up to one 128-row tile; above 64 rows
+# its row scale reads at most 16 norm parts (the TP=1 chain's residual_parts: H / 512)
+FUSED_MAX_M = 128
+FUSED_MT8_MAX_PARTS = 16
 SKINNY_TILE_M = 128  # rows per row tile above 64 (the kernel's MT = 8 variant)
 # measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
 _TARGET_WGS = 192
@@ -324,7 +328,7 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         M, K = x.shape
         N = w_gu_interleaved.shape[0]
         out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
-        Sg = gate_up_split(N, K, M) if rowscale is not None and M <= SKINNY_MAX_M else 1
+        Sg = gate_up_split(N, K, M) if rowscale is not None and M <= FUSED_MAX_M else 1
         if Sg > 1 and ws is not None and ws.numel() >= Sg * M * N:
             # split over K like the fused MLP's gate_up (bit-identical: the same slabs, summed in
             # split order, the same SiLU arithmetic)
@@ -453,7 +457,7 @@ def linear_down(h: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, packed: Opti
     M, K = h.shape
     N = w.shape[0]
     S = choose_split(N, K, M)
-    if packed is not None and down_kr(N, K, M) == 1 and M <= SKINNY_MAX_M:
+    if packed is not None and down_kr(N, K, M) == 1 and M <= FUSED_MAX_M:
         assert ws.numel() >= S * M * N, "split-K workspace too small"
         native.call("pk_skinny_gemm", 0, ws.data_ptr(), h.data_ptr(), packed.data_ptr(), M, N, K, h.stride(0), N, S,
                     1 | PACKED_BIT | HALF_BIT, native.stream_ptr())
@@ -467,17 +471,27 @@ def gate_up_split(N2: int, K: int, M: int) -> int:
     return choose_split(N2, K, M)
 
 
-def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_packed: Optional[torch.Tensor]) -> bool:
-    """Shapes the fused decode MLP launch (:func:`mlp_fused`) takes."""
+def fused_rows_ok(M: int, nparts: int) -> bool:
+    """Row counts the fused decode launches take: one tile of up to 64 rows, or of 128 rows when
+    the row scale has at most :data:`FUSED_MT8_MAX_PARTS` norm parts."""
+    return 0 < M <= SKINNY_MAX_M or (M <= FUSED_MAX_M and nparts <= FUSED_MT8_MAX_PARTS)
+
+
+def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_packed: Optional[torch.Tensor],
+                 nparts: int = 0) -> bool:
+    """Shapes the fused decode MLP launch (:func:`mlp_fused`) takes (``nparts``: norm parts of
+    its row scale)."""
     if gate_up_packed is None or down_packed is None or not x.is_cuda or not MLP_FUSED:
         return False
     M, K = x.shape
+    if not fused_rows_ok(M, nparts):
+        return False
     N2, I = gate_up_packed.shape[0], down_packed.shape[1]
     S = choose_split(down_packed.shape[0], I, M)
     Sg = gate_up_split(N2, K, M)
     # one workgroup per CU, each a gate_up tile then a down tile: above 256 tiles (70B on one GPU:
     # 448 gate_up tiles) the fused launch measured 8 % slower end to end (profiles/r2_decode_ab.txt)
-    return (0 < M <= SKINNY_MAX_M and N2 == 2 * I and N2 % 128 == 0 and K % (_KCHUNK * Sg) == 0
+    return (N2 == 2 * I and N2 % 128 == 0 and K % (_KCHUNK * Sg) == 0
             and down_packed.shape[0] % 128 == 0 and I % (_KCHUNK * S) == 0 and (I // S) % 64 == 0 and S <= 64
             and gate_up_packed.shape[1] == K and (N2 // 128) * Sg <= device_cus(x.device)
             and (down_packed.shape[0] // (64 * down_kr(down_packed.shape[0], I, M))) * S <= device_cus(x.device))

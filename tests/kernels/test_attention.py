@@ -217,7 +217,7 @@ def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S, pos_last):
 
 @pytest.mark.parametrize("nq,nkv,bs,H", [(32, 8, 32, 1024), (16, 4, 32, 1024), (64, 8, 32, 1024),
                                          (32, 8, 32, 4096), (8, 1, 32, 8192)])
-@pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [384] * 64, [512, 513, 1300, 0]])
+@pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [384] * 64, [512, 513, 1300, 0], [40 + 3 * i for i in range(100)]])
 def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, H, ctxs):
     """Fused QKV projection -> decode attention launch (csrc/kernels/decode_fused.hip): the QKV
     tiles hand their write-through slabs to the attention tiles in-launch.  Attention output and
@@ -250,7 +250,7 @@ def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, H, ctxs):
     k1, v1, k2, v2 = kc.to(d), vc.to(d), kc.to(d), vc.to(d)
     for it in range(4):
         res = (torch.randn(B, H, device=d)).to(torch.bfloat16)
-        parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 64, device=d))
+        parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * B, device=d))
         rs = gemm.RowScale(parts, 1e-5)
         p = gemm.linear_partial_rowscale(res, w, ws1, rs, S=S, packed=wp)
         exp = A.paged_decode_from_qkv(p, pos.to(d), cs, k1, v1, mk(), scale, nq, nkv)

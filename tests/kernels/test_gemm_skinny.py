@@ -309,7 +309,7 @@ def test_rowscale_half_blocks(M):
     torch.testing.assert_close(a.view().sum(0), b.view().sum(0), atol=2e-3, rtol=2e-3)
 
 
-@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("M", [1, 17, 64, 100, 128])
 @pytest.mark.parametrize("H,I", [(4096, 14336), (1024, 4096), (8192, 28672), (8192, 3584)])
 def test_mlp_fused_matches_two_launches(M, H, I):
     """Fused decode MLP (gate_up + SiLU -> in-launch hand-off -> down slabs, one launch) is
@@ -326,9 +326,10 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     # the launch is correct at any grid; the engine takes it only up to one tile per CU (70B: 448
     # gate_up tiles -> two launches, measured faster)
     Sg = gemm.gate_up_split(2 * I, H, M)
-    assert (Sg > 1) == (2 * I // 128 < 192) and gemm.mlp_fused_ok(res, gup, dp) == (2 * I // 128 * Sg <= 256)
+    nparts = H // gemm.PART_COLS
+    assert (Sg > 1) == (2 * I // 128 < 192) and gemm.mlp_fused_ok(res, gup, dp, nparts) == (2 * I // 128 * Sg <= 256)
     ws_gu = torch.empty(Sg * M * 2 * I, dtype=torch.float32, device="cuda")
-    parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
+    parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 128, device="cuda"))
     rs = gemm.RowScale(parts, 1e-5)
     S = gemm.choose_split(H, I, M)
     ws0 = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
@@ -350,7 +351,7 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     # new inputs every launch: a consumer reading a stale copy of the previous launch's h would show
     for it in range(6):
         r2 = rnd(M, H)
-        p2 = gemm.residual_parts(None, r2.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
+        p2 = gemm.residual_parts(None, r2.clone(), torch.empty((H // gemm.PART_COLS) * 128, device="cuda"))
         rs2 = gemm.RowScale(p2, 1e-5)
         h2 = gemm.linear_silu(r2, wgu, ws=ws_gu, packed=gup, rowscale=rs2)
         exp2 = gemm.linear_down(h2, wd, ws0, dp).view().clone()
