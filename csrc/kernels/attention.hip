@@ -339,6 +339,7 @@ static int decode_launch_p(void* out, const void* q, const QkvIn& qi, const void
       case 2: paged_decode_kernel<P, kDecodeWaves, true, 2><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       case 4: paged_decode_kernel<P, kDecodeWaves, true, 4><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       case 8: paged_decode_kernel<P, kDecodeWaves, true, 8><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+      case 16: paged_decode_kernel<P, kDecodeWaves, true, 16><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       default: paged_decode_kernel<P, kDecodeWaves, true, 0><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
     }
   } else

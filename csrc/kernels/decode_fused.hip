@@ -112,10 +112,14 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
       default: go(std::integral_constant<int, 8>{}, ss); break;  // 65-128 rows: one 128-row tile
     }
   };
-  if (g.S == 4)
-    go_mt(std::integral_constant<int, 4>{});
-  else
-    go_mt(std::integral_constant<int, 0>{});
+  // the attention prologue sums the S slabs of its q / k / v columns: a compile-time S issues all
+  // of them at once (a runtime loop serialised 16 sc1 round trips per column at 70B TP=8: S = 16)
+  switch (g.S) {
+    case 4: go_mt(std::integral_constant<int, 4>{}); break;
+    case 8: go_mt(std::integral_constant<int, 8>{}); break;
+    case 16: go_mt(std::integral_constant<int, 16>{}); break;
+    default: go_mt(std::integral_constant<int, 0>{}); break;
+  }
   int rc = PK_CHECK_LAUNCH();
   if (rc || n_parts == 1) return rc;
   if (P == kDecodePartSmall)

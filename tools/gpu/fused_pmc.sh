@@ -10,7 +10,7 @@ run() {  # $1 tag, rest: counters
   local tag=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d /tmp/pmc_$tag -- \
     python3 $R/tools/ab_decode.py --eager --steps 8 --reps 1 > /tmp/pmc_$tag.log 2>&1 || { tail -20 /tmp/pmc_$tag.log; return 1; }
-  python3 $R/tools/pmc_summary.py /tmp/pmc_$tag $R/gpurun_out/r3_fused_pmc_$tag.md > /dev/null || return 1
-  head -16 $R/gpurun_out/r3_fused_pmc_$tag.md
+  python3 $R/tools/pmc_summary.py /tmp/pmc_$tag $R/gpurun_out/r4_fused_pmc_$tag.md > /dev/null || return 1
+  head -16 $R/gpurun_out/r4_fused_pmc_$tag.md
 }
 run a FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_MFMA && run b WRITE_SIZE GRBM_GUI_ACTIVE SQ_BUSY_CYCLES

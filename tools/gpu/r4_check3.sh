@@ -1,9 +1,10 @@
 #!/bin/bash
-# kernels + e2e GPU tests, per-rank decode step (tp_solo) fused / unfused, headline bench
+# kernels + e2e + collective GPU tests, per-rank decode step (tp_solo) fused / unfused, headline bench
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/kernels tests/e2e \
-  tests/parallel/test_tp_chain_gpu.py > gpurun_out/r4c3_tests.log 2>&1 || { tail -40 gpurun_out/r4c3_tests.log; exit 1; }
+timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/kernels tests/e2e \
+  tests/parallel/test_tp_chain_gpu.py tests/parallel/test_custom_ar_gpu.py tests/parallel/test_tp8_shapes_gpu.py \
+  > gpurun_out/r4c3_tests.log 2>&1 || { tail -40 gpurun_out/r4c3_tests.log; exit 1; }
 tail -1 gpurun_out/r4c3_tests.log
 rm -f gpurun_out/solo3.jsonl
 for cfg in "llama3-8b 1" "llama3-70b 8"; do
