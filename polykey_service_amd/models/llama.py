@@ -479,7 +479,8 @@ class LlamaForCausalLM(nn.Module):
         kc, vc = kv
         T = residual.shape[0]
         rs = gemm.RowScale(parts, layer.eps)
-        if md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and gemm.fused_rows_ok(T, parts.shape[0]) and md.num_decode == T:
+        if (md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and at.nkv >= gemm.QKV_ATTN_MIN_KV
+                and gemm.fused_rows_ok(T, parts.shape[0]) and md.num_decode == T):
             # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip);
             # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
             return gemm.qkv_attn_fused(residual, at.qkv_pf, rs, ws, positions, self.cos_sin, kc, vc, md, at.scale,

@@ -40,6 +40,14 @@ _KCHUNK = 256
 SKINNY_ENABLED = os.environ.get("POLYKEY_SKINNY_GEMM", "1") == "1"
 # decode MLP as one launch (gate_up -> down hand-off in-kernel, mlp_fused); 0: two launches
 MLP_FUSED = os.environ.get("POLYKEY_MLP_FUSED", "1") == "1"
+# ... also when its gate_up must be split over K (kSiluSplit: the 70B TP=8 shard's 56 n-blocks):
+# measured 1.4 us / layer slower than the two launches there (profiles/r4_tp_solo.md), so off
+MLP_FUSED_SPLIT = os.environ.get("POLYKEY_MLP_FUSED_SPLIT", "0") == "1"
+# the QKV -> attention launch wins where each kv head's attention tiles wait on a slice of the QKV
+# tiles (8B: 8 kv heads); with one or two kv heads per rank (70B TP=8 / TP=4) every attention tile
+# waits for the whole projection and the launch measured slower (26.6 vs ~20 us per layer at
+# 70B TP=8, profiles/r4_tp_solo.md)
+QKV_ATTN_MIN_KV = 4
 PACKED_BIT = 16
 
 
@@ -489,6 +497,8 @@ def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_p
     N2, I = gate_up_packed.shape[0], down_packed.shape[1]
     S = choose_split(down_packed.shape[0], I, M)
     Sg = gate_up_split(N2, K, M)
+    if Sg > 1 and not MLP_FUSED_SPLIT:
+        return False
     # one workgroup per CU, each a gate_up tile then a down tile: above 256 tiles (70B on one GPU:
     # 448 gate_up tiles) the fused launch measured 8 % slower end to end (profiles/r2_decode_ab.txt)
     return (N2 == 2 * I and N2 % 128 == 0 and K % (_KCHUNK * Sg) == 0

@@ -1,7 +1,9 @@
 """The TP decode chain at the 70B TP=8 per-rank shapes (H 8192, 8 q / 1 kv heads, gate_up 7168 x
 8192 split over K, down 8192 x 3584), one rank on one GPU with the collectives reduced to their
 local half (tools/tp_solo.py SoloAR): the fused launches (QKV -> attention, gate_up -> down) give
-hidden states and KV caches bit-identical to the two-launch chain, and the step really ran them."""
+hidden states and KV caches bit-identical to the two-launch chain, and the step really ran them.
+(Serving keeps them off at this shape -- measured slower, profiles/r4_tp_solo.md -- the test
+turns them on.)"""
 import pytest
 import torch
 
@@ -67,6 +69,10 @@ def test_tp8_shard_fused_chain_bit_identical_to_two_launches(monkeypatch):
             return real_qkv(*a, **k)
         monkeypatch.setattr(gemm, "mlp_fused", mlp)
         monkeypatch.setattr(gemm, "qkv_attn_fused", qkv)
+        # the serving policy keeps both off at this shape (measured slower, gemm.MLP_FUSED_SPLIT /
+        # QKV_ATTN_MIN_KV); the launches must still be exact where they are allowed
+        monkeypatch.setattr(gemm, "MLP_FUSED_SPLIT", True)
+        monkeypatch.setattr(gemm, "QKV_ATTN_MIN_KV", 1)
         outs = []
         for fused in (False, True):
             gemm.MLP_FUSED = gemm.QKV_ATTN_FUSED = fused
