@@ -9,8 +9,9 @@ ep = world) and owns experts ``[r*E/ep, (r+1)*E/ep)``.  Per MoE layer (SURVEY.md
 2. order the ``T_local * k`` (token, slot) pairs by owning rank with the expert-align
    counting sort keyed by destination rank, gather the rows into that order (the MoE permute
    kernel) -- the send buffer is contiguous per destination;
-3. exchange per-destination counts (one int64 all-to-all; the only host read-back), then the
-   token rows and their expert ids (two variable-size all-to-alls over RCCL / xGMI);
+3. exchange the rows and their expert ids: on one node through fixed-capacity IPC regions with
+   device-side counts (:mod:`.ep_ipc`, graph-capturable), otherwise per-destination counts
+   (one int64 all-to-all and a host read-back) and two variable-size all-to-alls over RCCL;
 4. the received rows run through this rank's experts (align / grouped GEMM with the SiLU
    epilogue / grouped GEMM, k = 1) and are put back into arrival order;
 5. the results travel back with the inverse all-to-all, landing in the same per-destination
@@ -64,7 +65,12 @@ def ep_moe(x: torch.Tensor, router_w: torch.Tensor, w13: torch.Tensor, w2: torch
 
     The step's path is uniform over the EP group (every rank must issue the same collectives):
     the IPC all-to-all when the step's largest token count fits its capacity (``st.ep_step_rows``
-    from the lockstep vote), else the RCCL / gloo all-to-all with split lists on the host."""
+    from the lockstep vote), else the RCCL / gloo all-to-all with split lists on the host.  On
+    one node the IPC regions cover every step -- the decode set sized for ``max_num_seqs`` x k
+    rows per peer, the prefill set for the whole ``max_num_batched_tokens`` x k token budget
+    (llm_engine.py; ~1.2 GB of receive + return regions per rank for Mixtral at 8192 tokens,
+    EP = 8) -- so the per-layer count read-back below runs only where those regions do not
+    exist: across nodes, on CPU / gloo, or after the multi-GPU preflight disabled the IPC path."""
     st = get_state()
     for a2a in (st.ep_a2a, st.ep_a2a_prefill):  # decode-sized regions first, then prefill-sized
         if a2a is not None and x.is_cuda and a2a.fits(st.ep_step_rows * k):
