@@ -69,10 +69,10 @@ __global__ void __launch_bounds__(512) paged_prefill_kernel(
   load_q(qf, q + static_cast<int64_t>(q0 + (valid ? qi : 0)) * q_stride + hq * kHD, valid);
   WaveState st;
   init_state(st);
-  KVFrag fa;
+  KVFrag fa, fb;
   attend(st, qf, kc + static_cast<int64_t>(h) * bs * kHD, vc + static_cast<int64_t>(h) * kHD * bs,
          static_cast<int64_t>(n_kv) * bs * kHD, block_tables + static_cast<int64_t>(seq) * max_blocks, 0, bs, 0,
-         k_end, kStep, ctx, valid ? qpos : -1, scale2, fa);
+         k_end, kStep, ctx, valid ? qpos : -1, scale2, fa, fb);
   const float lsum = col_sum(st.l);
   if (!valid) return;
   const float inv = lsum > 0.f ? 1.f / lsum : 0.f;

@@ -142,15 +142,26 @@ __device__ __forceinline__ void attend_step(WaveState& st, const bf16x8_t (&qf)[
 // between this wave's steps.  Keys >= n_valid or > col_limit are masked.  Software-pipelined
 // over two fragment sets: the next step's K/V loads are in flight while this step computes
 // (loads past the end are clamped to valid addresses and never consumed).
+// PRE = 1 / 2: the caller already loaded the first step / two steps (fa: k_begin, fb: k_begin +
+// k_stride, with the same clamp `lim`), e.g. while it waited for an in-launch hand-off.
+template <int PRE = 0>
 __device__ __forceinline__ void attend(WaveState& st, const bf16x8_t (&qf)[4], const bf16_t* __restrict__ kc,
                                        const bf16_t* __restrict__ vc, int64_t blk_stride, const int* __restrict__ bt,
                                        int bt_base, int bs, int k_begin, int k_end, int k_stride, int n_valid,
-                                       int col_limit, float scale2, KVFrag& fa, bool fa_loaded = false) {
+                                       int col_limit, float scale2, KVFrag& fa, KVFrag& fb) {
   if (k_begin >= k_end) return;
   const int lim = min(n_valid, k_end);
-  KVFrag fb;
-  if (!fa_loaded) load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, k_begin, lim);
-  for (int s = k_begin; s < k_end; s += 2 * k_stride) {
+  int s = k_begin;
+  if constexpr (PRE == 2) {  // first iteration peeled: its fb is already in flight
+    attend_step(st, qf, fa, s, n_valid, col_limit, scale2);
+    if (s + k_stride >= k_end) return;
+    load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, s + 2 * k_stride, lim);
+    attend_step(st, qf, fb, s + k_stride, n_valid, col_limit, scale2);
+    s += 2 * k_stride;
+  } else if constexpr (PRE == 0) {
+    load_kv(fa, kc, vc, blk_stride, bt, bt_base, bs, k_begin, lim);
+  }
+  for (; s < k_end; s += 2 * k_stride) {
     load_kv(fb, kc, vc, blk_stride, bt, bt_base, bs, s + k_stride, lim);
     attend_step(st, qf, fa, s, n_valid, col_limit, scale2);
     if (s + k_stride >= k_end) break;
@@ -206,7 +217,9 @@ struct DecodeLds {
 // One decode-attention workgroup (seq = by, kv head = bx, partition = bz of gdz).  FL & 2: the
 // QKV slabs are handed over in-launch (decode_fused.hip): wait on kv head bx's tickets in fin
 // before reading them, and read them with sc1 loads.
-template <int kPart, int NW, bool FROM_QKV, int SS = 0, int FL = 0>
+// PRE = 1 / 2 (fused launch): the first partition's first one / two K/V steps per wave are
+// requested before the hand-off wait, so they stream in while the QKV tiles finish.
+template <int kPart, int NW, bool FROM_QKV, int SS = 0, int FL = 0, int PRE = 0>
 __device__ __forceinline__ void decode_tile(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, bf16_t* __restrict__ kc,
     bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
@@ -230,6 +243,33 @@ __device__ __forceinline__ void decode_tile(
   if (static_cast<int>(threadIdx.x) <= kPart / bs && pre_b0 + static_cast<int>(threadIdx.x) < max_blocks)
     bt_pre = block_tables[static_cast<int64_t>(seq) * max_blocks + pre_b0 + threadIdx.x];
   const int ctx = context_lens[seq];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
+  const bf16_t* kch = kc + static_cast<int64_t>(h) * bs * kHD;
+  const bf16_t* vch = vc + static_cast<int64_t>(h) * kHD * bs;
+  KVFrag fa, fb;
+  bool prefetched = false;
+  if constexpr (PRE > 0) {
+    static_assert(FROM_QKV && kPart % 32 == 0, "prefetch: fused launches, whole 32-key blocks");
+    // the same partition range / fold decision as below (positions and slots are launch inputs,
+    // not produced by the QKV tiles)
+    const int n_used0 = min((ctx + kPart - 1) / kPart, n_parts);
+    if (ctx > 0 && static_cast<int>(bz) < n_used0) {
+      const bool writer0 = qi.slots[seq] >= 0 && static_cast<int>(bz) == (n_used0 - 1) % static_cast<int>(gdz);
+      const bool fold0 = writer0 && qi.positions[seq] == ctx - 1;
+      const int ctx_c0 = fold0 ? ctx - 1 : ctx;
+      const int begin = bz * kPart, end = min(ctx_c0, begin + kPart);
+      // (a writer that does not fold stores the new row into the cache before attending: no prefetch)
+      prefetched = kPart % bs == 0 && end > begin && (fold0 || !writer0);
+      if (prefetched && static_cast<int>(threadIdx.x) < (end - 1) / bs - begin / bs + 1) bt_s[threadIdx.x] = bt_pre;
+      __syncthreads();  // uniform: ctx, bz and the fold decision are per workgroup
+      if (prefetched) {
+        const int lim = min(ctx_c0, end), k0 = begin + kStep * w;
+        load_kv(fa, kch, vch, blk_stride, bt_s, begin / bs, bs, k0, lim);
+        if constexpr (PRE == 2) load_kv(fb, kch, vch, blk_stride, bt_s, begin / bs, bs, k0 + NW * kStep, lim);
+      }
+    }
+  }
   if constexpr ((FL & 2) != 0) flow_wait(fin, h);  // this kv head's QKV tiles (every workgroup: re-arm count)
   const int G = n_q / n_kv;
   if (ctx <= 0) {
@@ -242,11 +282,7 @@ __device__ __forceinline__ void decode_tile(
   const int n_used = min((ctx + kPart - 1) / kPart, n_parts);
   PK_DEVICE_ASSERT(ctx <= n_parts * kPart);
   if (static_cast<int>(bz) >= n_used) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
-  const bf16_t* kch = kc + static_cast<int64_t>(h) * bs * kHD;
-  const bf16_t* vch = vc + static_cast<int64_t>(h) * kHD * bs;
   // (prefetching the first K/V step across the q preparation below was measured: it pushes
   // the kernel to 256 VGPRs + AGPRs, one wave per SIMD, and is slower overall)
   bf16x8_t qf[4];
@@ -364,17 +400,29 @@ __device__ __forceinline__ void decode_tile(
     const int begin = part * kPart;
     const int end = min(ctx_c, begin + kPart);
     const int b0 = begin / bs, nblk = (end - 1) / bs - b0 + 1;
-    __syncthreads();  // the previous partition's block-table readers are done
-    if (part == static_cast<int>(bz) && kPart % bs == 0) {  // nblk <= kPart / bs <= 64 * NW
-      if (static_cast<int>(threadIdx.x) < nblk) bt_s[threadIdx.x] = bt_pre;
-    } else
-      for (int i = threadIdx.x; i < nblk; i += 64 * NW)
-        bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
-    __syncthreads();
-    KVFrag fa;
-    if (end > begin)
-      attend(st, qf, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w, end, NW * kStep, ctx_c, ctx_c - 1, scale2,
-             fa);
+    const bool pre = PRE > 0 && part == static_cast<int>(bz) && prefetched;  // window + steps loaded
+    if (!pre) {
+      __syncthreads();  // the previous partition's block-table readers are done
+      if (part == static_cast<int>(bz) && kPart % bs == 0) {  // nblk <= kPart / bs <= 64 * NW
+        if (static_cast<int>(threadIdx.x) < nblk) bt_s[threadIdx.x] = bt_pre;
+      } else
+        for (int i = threadIdx.x; i < nblk; i += 64 * NW)
+          bt_s[i] = block_tables[static_cast<int64_t>(seq) * max_blocks + b0 + i];
+      __syncthreads();
+    }
+    if (end > begin) {
+      // ONE attend instantiation per kernel (a second, inlined next to it, made hipcc spill ~60
+      // registers): with the prefetch, partitions that were not prefetched load their first step here
+      if constexpr (PRE > 0) {
+        if (!pre) {
+          load_kv(fa, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w, min(ctx_c, end));
+          if constexpr (PRE == 2)
+            load_kv(fb, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w + NW * kStep, min(ctx_c, end));
+        }
+      }
+      attend<PRE>(st, qf, kch, vch, blk_stride, bt_s, b0, bs, begin + kStep * w, end, NW * kStep, ctx_c, ctx_c - 1,
+                  scale2, fa, fb);
+    }
   }
   const float lsum = col_sum(st.l);
 #pragma unroll

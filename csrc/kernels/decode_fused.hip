@@ -7,7 +7,10 @@
 // and reads the slabs with sc1 loads.  No fence anywhere (guide, "Hand-offs measured with sc1
 // loads", first row).  The attention tiles' block-table and context loads, their launch and the
 // QKV -> attention kernel boundary overlap the QKV tail.  Deadlock-free: the QKV tiles are the
-// lowest workgroup indices, dispatched first, and never wait.
+// lowest workgroup indices, dispatched first, and never wait.  Every attention tile requests the
+// first two K/V steps of each wave before its hand-off wait (decode_tile PRE = 2): 37.5-38 vs
+// 39.5-40 us per 8B layer (tools/qa_stamps.py, profiles/r4_qa_fused_stamps.txt -- the QKV phase
+// stretches from ~16 to ~22 us while the attention after the hand-off shrinks from ~20 to ~13 us).
 #include "skinny_tile.h"
 #include "attn_decode.h"
 
@@ -48,7 +51,7 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_fused_kernel(const GemmArgs q
   }
   if (b >= n_attn) return;  // small batches: more QKV tiles than attention tiles
   const int x = b % aa.n_kv, y = (b / aa.n_kv) % aa.n_seqs, z = b / (aa.n_kv * aa.n_seqs);
-  decode_tile<P, kDecodeWaves, true, SS, 2>(
+  decode_tile<P, kDecodeWaves, true, SS, 2, 2>(
       aa.out, nullptr, aa.kc, aa.vc, aa.block_tables, aa.context_lens, aa.part_o, aa.part_ml, nullptr, aa.n_q, aa.n_kv,
       aa.bs, aa.max_blocks, 0, aa.out_stride, aa.n_parts, aa.scale2, aa.qi, x, y, z, aa.z, lds.a, fa);
 }
@@ -96,12 +99,11 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   const int n_attn = n_kv * n_seqs * z;
   const dim3 grid(n_attn > n_qkv ? n_attn : n_qkv);
   auto go = [&](auto mt, auto ss) {
+    constexpr int MT = decltype(mt)::value, SS = decltype(ss)::value;
     if (P == kDecodePartSmall)
-      qkv_attn_fused_kernel<decltype(mt)::value, decltype(ss)::value, kDecodePartSmall>
-          <<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv, n_attn);
+      qkv_attn_fused_kernel<MT, SS, kDecodePartSmall><<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv, n_attn);
     else
-      qkv_attn_fused_kernel<decltype(mt)::value, decltype(ss)::value, 512><<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv,
-                                                                                                    n_attn);
+      qkv_attn_fused_kernel<MT, SS, 512><<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv, n_attn);
   };
   auto go_mt = [&](auto ss) {
     switch ((n_seqs + 15) / 16) {

@@ -462,7 +462,9 @@ class LlamaForCausalLM(nn.Module):
         for i, layer in enumerate(self.layers):
             a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws)
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
-            # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read)
+            # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read); the residual
+            # update by the last split of each n-block inside the O launch measured 1 % slower
+            # (profiles/r4_o_inlaunch_ab.jsonl)
             parts = gemm.residual_parts(gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p, half=True),
                                         residual, buf2)
             d = self._decode_mlp(layer, residual, parts, ws)

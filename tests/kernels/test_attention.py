@@ -218,7 +218,8 @@ def test_decode_from_qkv_slabs(nq, nkv, bs, ctxs, S, pos_last):
 @pytest.mark.parametrize("nq,nkv,bs,H", [(32, 8, 32, 1024), (16, 4, 32, 1024), (64, 8, 32, 1024),
                                          (32, 8, 32, 4096), (8, 1, 32, 8192)])
 @pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [384] * 64, [512, 513, 1300, 0], [40 + 3 * i for i in range(100)]])
-def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, H, ctxs):
+@pytest.mark.parametrize("pos_last", [True, False])
+def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, H, ctxs, pos_last):
     """Fused QKV projection -> decode attention launch (csrc/kernels/decode_fused.hip): the QKV
     tiles hand their write-through slabs to the attention tiles in-launch.  Attention output and
     K / V cache bit-identical to linear_partial_rowscale + paged_decode_from_qkv, over repeated
@@ -231,7 +232,9 @@ def test_qkv_attn_fused_matches_two_launches(nq, nkv, bs, H, ctxs):
     nb = sum((max(c, 1) + bs - 1) // bs for c in ctxs) + 4
     bt = block_tables_for([max(c, 1) for c in ctxs], bs, nb, max_blocks, seed=3)
     cl = torch.tensor(ctxs, dtype=torch.int32)
-    pos = (cl - 1).clamp(min=0)
+    # pos_last False: the new token is not the last key (the writer stores it before attending,
+    # no K/V prefetch for that workgroup)
+    pos = (cl - 1).clamp(min=0) if pos_last else (cl // 2).clamp(min=0)
     slots = torch.tensor([int(bt[i, (c - 1) // bs]) * bs + (c - 1) % bs if c > 0 else -1 for i, c in enumerate(ctxs)],
                          dtype=torch.int32)
     cs = ref.rope_cos_sin_cache(4096, HD, 500000.0).to(d)

@@ -13,4 +13,4 @@ run() {  # $1 tag, rest: counters
   python3 $R/tools/pmc_summary.py /tmp/pmc_$tag $R/gpurun_out/r4_fused_pmc_$tag.md > /dev/null || return 1
   head -16 $R/gpurun_out/r4_fused_pmc_$tag.md
 }
-run a FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_MFMA && run b WRITE_SIZE GRBM_GUI_ACTIVE SQ_BUSY_CYCLES
+run a FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES && run b WRITE_SIZE GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES
