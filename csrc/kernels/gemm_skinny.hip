@@ -520,6 +520,19 @@ constexpr int kFlowWords = kFlowCounters + 1024;
 // 128-row tiles at split S would be fewer than 192 workgroups
 static int down_kr(int N, int S) { return (N / 128) * S < 192 ? 1 : 2; }
 
+// compute units of the current device (queried once)
+static int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      cus = n;
+    else
+      cus = 256;
+  }
+  return cus;
+}
+
 static int g_mlp_down_nt = 0;
 PK_EXPORT void pk_set_mlp_down_nt(int on) { g_mlp_down_nt = on; }
 
@@ -545,6 +558,8 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / (64 * dkr), dn.K / dn.S, 2, 0, 0, fused_spin_limit()};
   const int n_gu = (gu.N / 128) * gu.S, n_dn = (dn.N / (64 * dkr)) * dn.S;
   const dim3 grid(n_gu > n_dn ? n_gu : n_dn);
+  // the LDS weight prefetch leaves room for one workgroup per CU: only when the grid fits the chip
+  const bool lds_one_per_cu_ok = static_cast<int>(grid.x) <= device_cus();
   auto go = [&](auto sp, auto kr) {
     constexpr bool SP = decltype(sp)::value;
     constexpr int KR = decltype(kr)::value;
@@ -553,8 +568,13 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
       case 2: mlp_fused_kernel<2, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
       case 3: mlp_fused_kernel<3, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
       case 4:
-        if (g_mlp_down_nt == 3 && !SP && KR == 2)  // A/B: 2 more down k-steps prefetched into LDS
-          mlp_fused_kernel<4, SP, KR, false, 2, KR == 2 ? 2 : 0><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
+        if (g_mlp_down_nt >= 3 && !SP && KR == 2 && lds_one_per_cu_ok) {  // A/B: LDS prefetch (4: + NT down)
+          if (g_mlp_down_nt == 4)
+            mlp_fused_kernel<4, SP, KR, true, 2, KR == 2 ? 2 : 0><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
+          else
+            mlp_fused_kernel<4, SP, KR, false, 2, KR == 2 ? 2 : 0><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
+        } else if (g_mlp_down_nt == 4 && !SP)
+          mlp_fused_kernel<4, SP, KR, true><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
         else if (g_mlp_down_nt == 2 && !SP)  // A/B: plain (L2) loads of h -- NOT coherent, timing only
           mlp_fused_kernel<4, SP, KR, false, 3><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
         else if (g_mlp_down_nt && !SP)  // A/B: non-temporal down weights

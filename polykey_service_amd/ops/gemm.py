@@ -542,7 +542,7 @@ QKV_ATTN_FUSED = os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1") == "1"
 
 def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: RowScale, ws: torch.Tensor,
                    positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, md,
-                   scale: float, nq: int, nkv: int, flow: torch.Tensor) -> torch.Tensor:
+                   scale: float, nq: int, nkv: int, flow: torch.Tensor, S: Optional[int] = None) -> torch.Tensor:
     """Decode layer front half in ONE launch (csrc/kernels/decode_fused.hip): the folded-norm
     QKV projection's split-K slabs (``ws``), handed in-launch to the decode attention that
     reduces them, applies RoPE, writes the new k / v to the paged cache and attends.  Same
@@ -550,7 +550,7 @@ def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: RowScale
     int32 >= :data:`FLOW_WORDS`, zeroed once, left zeroed.  Returns [M, nq * 128] bf16."""
     M, K = x.shape
     N = qkv_packed.shape[0]
-    S = choose_split(N, K, M)
+    S = S or choose_split(N, K, M)
     assert ws.numel() >= S * M * N and flow.numel() >= FLOW_WORDS and flow.dtype == torch.int32
     assert md.num_prefill == 0 and md.num_decode == M and k_cache.shape[-1] == 128
     out = torch.empty((M, nq * 128), dtype=torch.bfloat16, device=x.device)

@@ -221,7 +221,7 @@ def test_large_decode_batches_match_small(batch):
 
 
 @pytest.mark.parametrize("overlap", [False, True])
-def test_fused_handoff_timeout_falls_back_to_two_launches(overlap):
+def test_fused_handoff_timeout_falls_back_to_two_launches(overlap, monkeypatch):
     """Co-tenancy safety of the fused decode launches: a lost in-launch hand-off (forced here by
     the spin-limit test hook, which makes every consumer wait report a timeout) does not kill the
     engine.  The failed step is re-run on the two-launch path, the decode graphs are re-captured
@@ -229,6 +229,10 @@ def test_fused_handoff_timeout_falls_back_to_two_launches(overlap):
     that never used the fused launches."""
     from polykey_service_amd.ops import gemm
     _, gpu = _models("tiny-llama-gqa4")
+    # the serving policy takes neither fused launch for this model (2 kv heads; a gate_up that is
+    # split over K): enable both so the hand-off and its fallback are exercised
+    monkeypatch.setattr(gemm, "QKV_ATTN_MIN_KV", 1)
+    monkeypatch.setattr(gemm, "MLP_FUSED_SPLIT", True)
     prompts = [[1] + list(range(5, 5 + n)) for n in (3, 17, 40)]
     sp = SamplingParams(max_tokens=12, ignore_eos=True)
     saved = (gemm.MLP_FUSED, gemm.QKV_ATTN_FUSED)

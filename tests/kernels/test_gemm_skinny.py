@@ -311,7 +311,7 @@ def test_rowscale_half_blocks(M):
 
 @pytest.mark.parametrize("M", [1, 17, 64, 100, 128])
 @pytest.mark.parametrize("H,I", [(4096, 14336), (1024, 4096), (8192, 28672), (8192, 3584)])
-@pytest.mark.parametrize("variant", [0, 1, 3])
+@pytest.mark.parametrize("variant", [0, 1, 3, 4])
 def test_mlp_fused_matches_two_launches(M, H, I, variant):
     """Fused decode MLP (gate_up + SiLU -> in-launch hand-off -> down slabs, one launch) is
     bit-identical to the two launches it replaces, on repeated launches (the hand-off tickets

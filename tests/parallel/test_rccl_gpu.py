@@ -63,7 +63,9 @@ def test_all_reduce_in_a_hip_graph(comm):
         comm.all_reduce(x, out=out)  # warm-up outside capture
     torch.cuda.current_stream().wait_stream(s)
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    # captured like the engine captures its decode graphs: under inference mode (the CUDA
+    # generator's graph-capture state is then an inference tensor for every later capture)
+    with torch.inference_mode(), torch.cuda.graph(graph):
         comm.all_reduce(x, out=out)
     x.fill_(3.0)
     graph.replay()

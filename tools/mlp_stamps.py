@@ -85,7 +85,7 @@ def main() -> None:
 
     row = {"S_down": S, "down_kr": dkr, "n_gu": n_gu, "n_dn": n_dn}
     lk = native.lib()
-    runs = {v: [] for v in (0, 1, 3)}  # 0 production, 1 non-temporal down W, 3 LDS prefetch of 2 down k-steps
+    runs = {v: [] for v in (0, 1, 3, 4)}  # 0 production, 1 NT down W, 3 LDS prefetch of 2 down k-steps, 4 both
     for rep in range(6):
         for v in runs:
             lk.pk_set_mlp_down_nt(v)
