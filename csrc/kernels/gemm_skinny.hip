@@ -46,17 +46,17 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 // cannot fill the chip (70B TP=8: 56).
 // DKR: the down projection's n-block height (2: 128 rows; 1: 64 rows -- twice the tiles at the
 // same split when 128-row tiles would leave CUs idle: 8B 32 x 4, 70B TP=8 64 x 2 -> 256).
-template <int MT, bool SPLIT, int DKR, bool DNT = false, int DFL = 2, int DPF = 0>
+// DNT: non-temporal down weights (A/B builds: tools/lab/build_variant.py)
+template <int MT, bool SPLIT, int DKR, bool DNT = false>
 __global__ void __launch_bounds__(256, 2) mlp_fused_kernel(const GemmArgs gu, const GemmArgs dn, const Flow fgu,
                                                            const Flow fdn, int n_gu, int n_dn) {
   __shared__ SkinnyLds<MT> lds;
-  __shared__ bf16_t dpf[DPF > 0 ? DPF * 16384 : 1] __attribute__((aligned(16)));  // DPF x 32 KiB
   const int b = blockIdx.x;
   if (b < n_gu) {
     skinny_tile<MT, SPLIT ? kSiluSplit : kSiluMul, true, false, true, true, 2, 1>(gu, b, 0, n_gu, lds, fgu);
     __syncthreads();  // the LDS tiles are reused by the down tile
   }
-  if (b < n_dn) skinny_tile<MT, kPartial, true, false, DNT, false, DKR, DFL, DPF>(dn, b, 0, n_dn, lds, fdn, dpf);
+  if (b < n_dn) skinny_tile<MT, kPartial, true, false, DNT, false, DKR, 2>(dn, b, 0, n_dn, lds, fdn);
 }
 
 // x[m] = bf16(bf16(residual[m] * rinv[m]) * w), rinv from the per-row sum-of-squares parts a
@@ -520,22 +520,6 @@ constexpr int kFlowWords = kFlowCounters + 1024;
 // 128-row tiles at split S would be fewer than 192 workgroups
 static int down_kr(int N, int S) { return (N / 128) * S < 192 ? 1 : 2; }
 
-// compute units of the current device (queried once)
-static int device_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      cus = n;
-    else
-      cus = 256;
-  }
-  return cus;
-}
-
-static int g_mlp_down_nt = 0;
-PK_EXPORT void pk_set_mlp_down_nt(int on) { g_mlp_down_nt = on; }
-
 PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, hipStream_t stream) {
   GemmArgs gu = *gu_in, dn = *dn_in;
   if (gu.M <= 0) return 0;
@@ -558,8 +542,6 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / (64 * dkr), dn.K / dn.S, 2, 0, 0, fused_spin_limit()};
   const int n_gu = (gu.N / 128) * gu.S, n_dn = (dn.N / (64 * dkr)) * dn.S;
   const dim3 grid(n_gu > n_dn ? n_gu : n_dn);
-  // the LDS weight prefetch leaves room for one workgroup per CU: only when the grid fits the chip
-  const bool lds_one_per_cu_ok = static_cast<int>(grid.x) <= device_cus();
   auto go = [&](auto sp, auto kr) {
     constexpr bool SP = decltype(sp)::value;
     constexpr int KR = decltype(kr)::value;
@@ -567,21 +549,7 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
       case 1: mlp_fused_kernel<1, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
       case 2: mlp_fused_kernel<2, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
       case 3: mlp_fused_kernel<3, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      case 4:
-        if (g_mlp_down_nt >= 3 && !SP && KR == 2 && lds_one_per_cu_ok) {  // A/B: LDS prefetch (4: + NT down)
-          if (g_mlp_down_nt == 4)
-            mlp_fused_kernel<4, SP, KR, true, 2, KR == 2 ? 2 : 0><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
-          else
-            mlp_fused_kernel<4, SP, KR, false, 2, KR == 2 ? 2 : 0><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
-        } else if (g_mlp_down_nt == 4 && !SP)
-          mlp_fused_kernel<4, SP, KR, true><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
-        else if (g_mlp_down_nt == 2 && !SP)  // A/B: plain (L2) loads of h -- NOT coherent, timing only
-          mlp_fused_kernel<4, SP, KR, false, 3><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
-        else if (g_mlp_down_nt && !SP)  // A/B: non-temporal down weights
-          mlp_fused_kernel<4, SP, KR, true><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
-        else
-          mlp_fused_kernel<4, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn);
-        break;
+      case 4: mlp_fused_kernel<4, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
       default: mlp_fused_kernel<8, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
     }
   };

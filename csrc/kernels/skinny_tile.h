@@ -75,9 +75,6 @@ __device__ __forceinline__ bf16x8_t ldw(const bf16_t* p) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
-// 16-byte LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds + 16 l (lds wave-uniform)
-__device__ __forceinline__ void lds_dma16(const bf16_t* g, bf16_t* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
-
 __device__ __forceinline__ float4 ld4f(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void add4(float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; }
 __device__ __forceinline__ float rbf(float x) { return bf2f(f2bf(x)); }
@@ -284,12 +281,9 @@ struct SkinnyLds {
   int last;
 };
 
-// DPF = 2 (hand-off consumer, packed W, MT <= 4): the tile's 3rd and 4th weight k-steps go to `pf`
-// (2 x 32 KiB of LDS, KR = 2) by LDS-DMA before the hand-off wait, on top of the two k-steps in
-// registers, so 4 of its k-steps stream in while the producers finish.
-template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2, int FL = 0, int DPF = 0>
+template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2, int FL = 0>
 __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_in, const int by, const int gdx,
-                                            SkinnyLds<MT>& L, const Flow& fl, bf16_t* pf = nullptr) {
+                                            SkinnyLds<MT>& L, const Flow& fl) {
   constexpr int kR = KR;
   constexpr int kKA = SkinnyLds<MT>::kKA;  // k per staged A tile
   constexpr int kPPR = kKA / 8;             // 16-byte pieces per A row
@@ -380,7 +374,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) {
       const int col = ((tid + 256 * p) % kPPR) * 8;
-      if constexpr (FL == 2)  // the producers' output, handed off in-launch: sc1 loads (FL 3: plain)
+      if constexpr (FL == 2)  // the producers' output, handed off in-launch: sc1 loads
         stage[p] = __builtin_amdgcn_raw_buffer_load_b128(
             __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(args.A), static_cast<short>(0), 0x7ffffff0, 0x00020000),
             static_cast<int>((arow[p] + kc + col - args.A) * 2), 0, 16);
@@ -450,7 +444,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
     const int nsteps = 2 * nchunks;  // even
     const int rot2 = 2 * rot;
     auto ks = [&](int j) { return k0 + ((min(j, nsteps - 1) + rot2) % nsteps) * 128; };
-    if constexpr (FL >= 2) {  // consumer of an in-launch hand-off: weights first, A after the wait
+    if constexpr (FL == 2) {  // consumer of an in-launch hand-off: weights first, A after the wait
       load_w(wa, ks(0));
       load_w(wb, ks(1));
       flow_wait(fl, split);
@@ -477,22 +471,9 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       buf ^= 1;
     }
   } else {
-  static_assert(DPF == 0 || (DPF == 2 && FL >= 2 && PK && KR == 2), "LDS weight prefetch: packed consumer tiles");
-  // LDS slot of (k-step j, wave w, tile t, fragment s): the WG's 32 KiB packed block of a k-step, in order
-  auto pf_at = [&](int j, int t, int sf) { return pf + (((j * 4 + w) * kR + t) * 4 + sf) * 512; };
-  if constexpr (FL >= 2) {
+  if constexpr (FL == 2) {
     // consumer: this workgroup's first two weight k-steps are requested before the wait, so
     // they stream in while the producers finish; A (the producers' output) is read after it
-    if constexpr (DPF == 2) {
-      const int k1 = ck(1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int t = 0; t < kR; ++t)
-#pragma unroll
-          for (int sf = 0; sf < 4; ++sf)
-            lds_dma16(wp[t] + static_cast<int64_t>((k1 + 128 * j) >> 7) * (32 * 512) + sf * 512, pf_at(j, t, sf));
-    }
     load_w(wa, ck(0));
     load_w(wb, ck(0) + 128);
     flow_wait(fl, split);
@@ -502,27 +483,9 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
     load_w(wa, ck(0));
     load_w(wb, ck(0) + 128);
   }
-  store_a(0);  // (its vmcnt wait also retires this wave's LDS-DMA pieces, issued before)
+  store_a(0);
   int buf = 0;
-  int c0 = 0;
-  if constexpr (DPF == 2) {  // chunk 0 peeled: chunk 1's weights come from the LDS prefetch
-    auto lds_w = [&](bf16x8_t (&dst)[kR][4], int j) {
-#pragma unroll
-      for (int t = 0; t < kR; ++t)
-#pragma unroll
-        for (int sf = 0; sf < 4; ++sf) dst[t][sf] = *reinterpret_cast<const bf16x8_t*>(pf_at(j, t, sf) + 8 * lane);
-    };
-    load_a(ck(1));
-    __syncthreads();  // chunk 0 and every wave's LDS-DMA pieces visible
-    mma_step(wa, buf, 0);
-    lds_w(wa, 0);
-    mma_step(wb, buf, 128);
-    lds_w(wb, 1);
-    store_a(buf ^ 1);
-    buf ^= 1;
-    c0 = 1;
-  }
-  for (int c = c0; c < nchunks; ++c) {
+  for (int c = 0; c < nchunks; ++c) {
     const int kn = ck(c + 1);
     load_a(kn);
     __syncthreads();  // chunk c visible in a_lds[buf]; every wave is done with a_lds[buf^1]

@@ -93,7 +93,7 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
 
 
 LM_HEAD_SKINNY_MAX_M = 128
-GATE_UP_SKINNY_MAX_M = 384
+GATE_UP_SKINNY_MAX_M = int(os.environ.get("POLYKEY_AB_GATE_UP_MAX_M", "384"))  # A/B only
 
 
 def pack_folded(owner, name: str, norm_w: torch.Tensor, packed_only: bool) -> torch.Tensor:

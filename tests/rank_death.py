@@ -61,7 +61,18 @@ def health(ch) -> int:
 
 
 def run_kill(tmp, model: str, gpu: bool, victim: int, bound_s: float):
-    """Returns (survivor exit code, seconds from kill to exit, health statuses seen after the kill)."""
+    """Returns (survivor exit code, seconds from kill to exit, health statuses seen after the kill).
+    A group whose gRPC port was taken between the free-port probe and the bind (an ephemeral port
+    handed to another socket meanwhile) is started once more on new ports."""
+    for attempt in range(2):
+        try:
+            return _run_kill(tmp, model, gpu, victim, bound_s)
+        except AssertionError as e:
+            if attempt or "Failed to bind to address" not in str(e):
+                raise
+
+
+def _run_kill(tmp, model: str, gpu: bool, victim: int, bound_s: float):
     procs, addr = start_group(tmp, model, gpu)
     try:
         ch = grpc.insecure_channel(addr)

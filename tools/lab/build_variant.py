@@ -1,0 +1,60 @@
+"""Build an A/B variant of libpk_kernels from a patched COPY of csrc/kernels (the production sources
+stay free of lab switches).  A variant is a list of (file, old, new) text replacements; the result
+lands in tools/lab/libpk_kernels_<variant>.so and is loaded instead of the in-tree library with
+POLYKEY_LIB_LIBPK_KERNELS=<path> (polykey_service_amd/_native/loader.py).
+
+    python tools/lab/build_variant.py pre0 mlp_nt
+"""
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+from polykey_service_amd._native.build import HIP_FLAGS, HIPCC  # noqa: E402
+
+VARIANTS = {
+    # the fused QKV -> attention launch without the K/V prefetch before the hand-off wait
+    "pre0": [("decode_fused.hip", "decode_tile<P, kDecodeWaves, true, SS, 2, 2>(",
+              "decode_tile<P, kDecodeWaves, true, SS, 2, 0>(")],
+    # the fused MLP's down tiles with non-temporal weight loads
+    "mlp_nt": [("gemm_skinny.hip", "case 4: mlp_fused_kernel<4, SP, KR><<<", "case 4: mlp_fused_kernel<4, SP, KR, !SP><<<")],
+    # measured and removed this round (variant builds of the sources of that time): "mlp_v0" (no NT /
+    # LDS prefetch in the down tiles: 4.063 vs 4.063 ms per graph-captured 8B step), "o_ring2" (the
+    # o-projection without whole-slice weight registers: 3.997 vs 4.063 ms) -- profiles/r4_variant_ab.jsonl
+}
+
+
+def build(name: str) -> str:
+    src = os.path.join(REPO, "csrc", "kernels")
+    work = tempfile.mkdtemp(prefix=f"pkvar_{name}_")
+    kdir = os.path.join(work, "kernels")
+    shutil.copytree(src, kdir)
+    for fname, old, new in VARIANTS[name]:
+        p = os.path.join(kdir, fname)
+        text = open(p).read()
+        if old not in text:
+            raise SystemExit(f"variant {name}: pattern not found in {fname}: {old!r}")
+        open(p, "w").write(text.replace(old, new))
+    objs = []
+
+    def one(s):
+        o = os.path.join(work, os.path.basename(s) + ".o")
+        subprocess.run([HIPCC, "-x", "hip", *HIP_FLAGS, "-I" + work, "-c", s, "-o", o], check=True)
+        return o
+
+    with cf.ThreadPoolExecutor(max_workers=8) as ex:
+        objs = list(ex.map(one, sorted(glob.glob(os.path.join(kdir, "*.hip")))))
+    out = os.path.join(REPO, "tools", "lab", f"libpk_kernels_{name}.so")
+    subprocess.run([HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", *objs, "-o", out], check=True)
+    shutil.rmtree(work, ignore_errors=True)
+    return out
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or list(VARIANTS):
+        print(build(n), flush=True)

@@ -84,16 +84,8 @@ def main() -> None:
         return round(e0.elapsed_time(e1) * 1000 / n, 2)
 
     row = {"S_down": S, "down_kr": dkr, "n_gu": n_gu, "n_dn": n_dn}
-    lk = native.lib()
-    runs = {v: [] for v in (0, 1, 3, 4)}  # 0 production, 1 NT down W, 3 LDS prefetch of 2 down k-steps, 4 both
-    for rep in range(6):
-        for v in runs:
-            lk.pk_set_mlp_down_nt(v)
-            runs[v].append(timeit(fused, 60))
-    lk.pk_set_mlp_down_nt(0)
-    for v, t in runs.items():
-        row[f"fused_v{v}_median_us"] = round(sorted(t)[len(t) // 2], 2)
-        row[f"fused_v{v}_min_us"] = min(t)
+    for rep in range(3):
+        row[f"fused_us_{rep}"] = timeit(fused, 60)
     for name, fn in (("stamped_us", stamped), ("gate_up_us", gate_up_only),
                      ("down_us", down_only)):
         try:
