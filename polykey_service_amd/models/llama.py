@@ -93,7 +93,9 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
 
 
 LM_HEAD_SKINNY_MAX_M = 128
-GATE_UP_SKINNY_MAX_M = int(os.environ.get("POLYKEY_AB_GATE_UP_MAX_M", "384"))  # A/B only
+# above this many decode rows gate_up runs on hipBLASLt (+ the norm / SiLU kernels): 256 clients
+# 19,030-19,728 -> 20,177-20,218 tok/s with 192 instead of 384 (profiles/r4_gate_up_rows_ab.jsonl)
+GATE_UP_SKINNY_MAX_M = 192
 
 
 def pack_folded(owner, name: str, norm_w: torch.Tensor, packed_only: bool) -> torch.Tensor:
@@ -501,8 +503,9 @@ class LlamaForCausalLM(nn.Module):
             # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
             return gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, rs, ws, self._flow, ws_gu=self._ws_gu)
         if residual.shape[0] > GATE_UP_SKINNY_MAX_M and not mlp.gate_up.is_meta:
-            # hipBLASLt's MFMA GEMM wins on the 235 MB gate_up above 384 rows (95 vs 149 us at
-            # 512, profiles/r3_decode_rows.txt) even with the norm and SiLU as separate kernels
+            # hipBLASLt's MFMA GEMM wins on the 235 MB gate_up above 192 rows (67 vs 85 us at 256,
+            # 97 vs 155 at 512: profiles/r4_wide_decode_probe.jsonl) even with the norm and SiLU as
+            # separate kernels
             x = gemm.norm_apply(residual, parts, layer.ln2, layer.eps)
             h = gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
         else:  # split over K like the fused launch's gate_up when its n-blocks cannot fill the chip
