@@ -283,8 +283,9 @@ __device__ __forceinline__ void decode_tile(
   PK_DEVICE_ASSERT(ctx <= n_parts * kPart);
   if (static_cast<int>(bz) >= n_used) return;
   const int r = lane & 15, g = lane >> 4;
-  // (prefetching the first K/V step across the q preparation below was measured: it pushes
-  // the kernel to 256 VGPRs + AGPRs, one wave per SIMD, and is slower overall)
+  // (in the standalone kernel, prefetching the first K/V step across the q preparation below
+  // was measured slower: 256 VGPRs + AGPRs, one wave per SIMD; the fused launch does prefetch
+  // (PRE), before its hand-off wait, where the registers are otherwise idle)
   bf16x8_t qf[4];
   // fold: the workgroup holding the new token (key ctx - 1) keeps its k / v in LDS, attends to
   // keys [0, ctx - 1) from the cache and adds key ctx - 1 from LDS in the final combine; the
