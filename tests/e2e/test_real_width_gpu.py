@@ -19,18 +19,20 @@ from polykey_service_amd.parallel.state import ParallelState
 pytestmark = pytest.mark.gpu
 
 PROMPTS = [[128000] + list(range(1000, 1000 + n)) for n in (5, 37, 70)]
+# the headline decode shape: 64 sequences (the fused launches' 4 x 16-row tile), and 40 (3 tiles)
+MANY = {n: [[128000] + [(97 * i + 13 * j) % 20000 + 500 for j in range(3 + i % 13)] for i in range(n)] for n in (40, 64)}
 
 
-def _engine(model, dev, cfg):
-    e = LLMEngine(EngineConfig(model="llama3-8b", num_layers=cfg.num_layers, max_num_seqs=8,
-                               max_num_batched_tokens=256, max_model_len=1024, num_kv_blocks=64, hip_graphs=False,
+def _engine(model, dev, cfg, n=8):
+    e = LLMEngine(EngineConfig(model="llama3-8b", num_layers=cfg.num_layers, max_num_seqs=max(8, n),
+                               max_num_batched_tokens=2048, max_model_len=1024, num_kv_blocks=256, hip_graphs=False,
                                device=dev, prefix_caching=False), ParallelState(device=torch.device(dev)), model=model)
     e.runner.keep_logits = True
     return e
 
 
-def _two_steps(e):
-    for p in PROMPTS:
+def _two_steps(e, prompts=PROMPTS):
+    for p in prompts:
         e.add_request(p, SamplingParams(max_tokens=2, ignore_eos=True))
     e.step()
     prefill = e.runner.last_logits.float().cpu().clone()
@@ -41,7 +43,9 @@ def _two_steps(e):
     return prefill, first, decode
 
 
-def test_llama3_8b_width_prefill_and_fused_decode_match_cpu_reference():
+@pytest.mark.parametrize("n", [3, 40, 64])
+def test_llama3_8b_width_prefill_and_fused_decode_match_cpu_reference(n):
+    prompts = PROMPTS if n == 3 else MANY[n]
     cfg = dataclasses.replace(get_config("llama3-8b"), num_layers=2)
     cpu = build_model(cfg, ParallelState(), torch.bfloat16, torch.device("cpu")).init_random(11)
     with torch.no_grad():
@@ -50,12 +54,12 @@ def test_llama3_8b_width_prefill_and_fused_decode_match_cpu_reference():
             layer.ln2.copy_(torch.linspace(1.5, 0.5, layer.ln2.numel()).to(layer.ln2.dtype))
     gpu = copy.deepcopy(cpu).to("cuda")
     gpu.device = torch.device("cuda")
-    ge = _engine(gpu, "cuda", cfg)
+    ge = _engine(gpu, "cuda", cfg, len(prompts))
     assert gpu.layers[0].attn.qkv_pf is not None and gpu.lm_head_p is not None, "fused decode chain not packed"
-    x = torch.zeros((len(PROMPTS), cfg.hidden_size), dtype=torch.bfloat16, device="cuda")
+    x = torch.zeros((len(prompts), cfg.hidden_size), dtype=torch.bfloat16, device="cuda")
     assert gpu._rowscale_ok(x), "decode would not take the folded-norm fused chain"
-    gp, gfirst, gd = _two_steps(ge)
-    cp, cfirst, cd = _two_steps(_engine(cpu, "cpu", cfg))
+    gp, gfirst, gd = _two_steps(ge, prompts)
+    cp, cfirst, cd = _two_steps(_engine(cpu, "cpu", cfg, len(prompts)), prompts)
     scale = cp.abs().max().item()
     # prefill: bf16 GEMMs / attention vs the fp32-accumulating reference
     torch.testing.assert_close(gp, cp, atol=0.02 * scale, rtol=0.05)
