@@ -23,6 +23,8 @@ VARIANTS = {
               "decode_tile<P, kDecodeWaves, true, SS, 2, 0>(")],
     # the fused MLP's down tiles with non-temporal weight loads
     "mlp_nt": [("gemm_skinny.hip", "case 4: mlp_fused_kernel<4, SP, KR><<<", "case 4: mlp_fused_kernel<4, SP, KR, !SP><<<")],
+    # the fused launches' hand-off pollers sleeping 4 instead of 16 (x 64 cycles) between polls
+    "sleep4": [("flow.h", "__builtin_amdgcn_s_sleep(16);", "__builtin_amdgcn_s_sleep(4);")],
     # measured and removed this round (variant builds of the sources of that time): "mlp_v0" (no NT /
     # LDS prefetch in the down tiles: 4.063 vs 4.063 ms per graph-captured 8B step), "o_ring2" (the
     # o-projection without whole-slice weight registers: 3.997 vs 4.063 ms) -- profiles/r4_variant_ab.jsonl

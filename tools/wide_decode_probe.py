@@ -1,16 +1,15 @@
 """Decode GEMMs at 256 / 512 rows (Llama-3-8B shapes, cold weights rotated over 4 copies):
-hipBLASLt (F.linear) vs the hand-written MFMA prefill GEMM (256 x 256 tiles, block-packed W,
-csrc/kernels/gemm_prefill.hip) vs the row-tiled skinny decode GEMM.  One JSON line per shape."""
+hipBLASLt (torch.mm) vs the skinny decode GEMM with 128-row tiles vs 256-row tiles (gemm.WIDE_TILES,
+MT = 16), each at the split the decode chain uses (gate_up: the folded-norm SiLU launch, S = 1).
+One JSON line per shape and row count."""
 import json
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
 
 from polykey_service_amd.ops import gemm  # noqa: E402
-from polykey_service_amd.ops import gemm_prefill  # noqa: E402
 
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
 L = 4
@@ -32,29 +31,34 @@ def timeit(fn, n=30):
 def main():
     d = "cuda"
     for name, (N, K) in SHAPES.items():
-        ws = [(torch.randn(N, K, device=d) * 0.02).to(torch.bfloat16) for _ in range(L)]
-        wp = [gemm.pack_weight(w) for w in ws]
+        ws_ = [(torch.randn(N, K, device=d) * 0.02).to(torch.bfloat16) for _ in range(L)]
+        wp = [gemm.pack_weight(w) for w in ws_]
         for M in (256, 512):
             x = torch.randn(M, K, device=d).to(torch.bfloat16)
             out = torch.empty(M, N, dtype=torch.bfloat16, device=d)
-            flops = 2.0 * M * N * K
+            slab = torch.empty(16 * M * N, dtype=torch.float32, device=d)
+            parts = gemm.residual_parts(None, x.clone(), torch.empty((K // gemm.PART_COLS) * M, device=d))
+            rs = gemm.RowScale(parts.view(-1, M), 1e-5)
             row = {"shape": name, "M": M, "N": N, "K": K}
-            row["hipblaslt_us"] = timeit(lambda i: torch.mm(x, ws[i % L].t(), out=out))
-            try:
-                row["prefill_mfma_us"] = timeit(lambda i: gemm_prefill.linear(x, ws[i % L], out=out,
-                                                                               packed=wp[i % L]))
-            except Exception as e:  # noqa: BLE001 - a probe: report and go on
-                row["prefill_mfma_us"] = f"error: {e}"
-            try:
-                row["skinny_us"] = timeit(lambda i: gemm.linear(x, ws[i % L], packed=wp[i % L],
-                                                                max_m=gemm.DECODE_MAX_M))
-            except Exception as e:  # noqa: BLE001
-                row["skinny_us"] = f"error: {e}"
-            for k in ("hipblaslt_us", "prefill_mfma_us", "skinny_us"):
+            row["hipblaslt_us"] = timeit(lambda i: torch.mm(x, ws_[i % L].t(), out=out))
+            for wide in (False, True):
+                gemm.WIDE_TILES = wide
+                tag = "wide" if wide else "rows128"
+                if name == "gate_up":
+                    fn = lambda i: gemm.linear_silu(x, ws_[i % L], packed=wp[i % L], rowscale=rs)  # noqa: E731
+                else:
+                    fn = lambda i: gemm.linear_partial(x, ws_[i % L], slab, packed=wp[i % L])  # noqa: E731
+                try:
+                    row[f"{tag}_us"] = timeit(fn)
+                except Exception as e:  # noqa: BLE001 - a probe: report and go on
+                    row[f"{tag}_us"] = f"error: {e}"
+            gemm.WIDE_TILES = False
+            flops = 2.0 * M * N * K
+            for k in ("hipblaslt_us", "rows128_us", "wide_us"):
                 if isinstance(row[k], float):
                     row[k.replace("_us", "_tfs")] = round(flops / row[k] / 1e6, 1)
             print(json.dumps(row), flush=True)
-        del ws, wp
+        del ws_, wp
 
 
 if __name__ == "__main__":
