@@ -33,14 +33,6 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   skinny_tile<MT, MODE, PK, NORM, NT, RS, KR>(args, blockIdx.x, blockIdx.y, gridDim.x, lds, Flow{});
 }
 
-// 256-row tiles (MT = 16): 139 KiB of LDS, one workgroup per CU, the register budget of one wave
-// per SIMD (the accumulators go to AGPRs)
-template <int MODE, bool PK, bool RS, int KR>
-__global__ void __launch_bounds__(256, 1) skinny_wide_kernel(const GemmArgs args) {
-  __shared__ SkinnyLds<16> lds;
-  skinny_tile<16, MODE, PK, false, false, RS, KR>(args, blockIdx.x, blockIdx.y, gridDim.x, lds, Flow{});
-}
-
 // Fused decode MLP (M <= 64): gate_up + SiLU (folded norm, non-temporal packed W) and the down
 // projection's split-K slabs in ONE launch of max(gate_up tiles, down tiles) workgroups, one per
 // CU: workgroup b runs gate_up tile b (if any), then down tile b (if any).  A down tile streams
@@ -396,13 +388,6 @@ __global__ void __launch_bounds__(256) qkv_reduce_rope_cache_kernel(
 template <int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2>
 int launch(const GemmArgs& a, hipStream_t stream) {
   const dim3 grid((a.N / (64 * KR)) * a.S * a.row_tiles, a.row_offsets != nullptr ? a.groups : 1);
-  if (a.tile_rows == 256) {  // wide tiles (dispatch: packed W, modes 0-2, no norm prologue, no NT)
-    if constexpr (MODE <= kSiluMul && !NORM && PK && !NT) {
-      skinny_wide_kernel<MODE, PK, RS, KR><<<grid, 256, 0, stream>>>(a);
-      return PK_CHECK_LAUNCH();
-    }
-    return -1;
-  }
   if (a.tile_rows == 128) {  // row-tiled decode batches above 64 (dispatch: modes 0-2, no norm prologue)
     if constexpr (MODE <= kSiluMul && !NORM) {
       skinny_gemm_kernel<8, MODE, PK, NORM, NT, RS, KR><<<grid, 256, 0, stream>>>(a);
@@ -452,8 +437,6 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
   const int rows = grouped ? a.max_group_rows : a.M;
   // (bit 8: 64-row tiles regardless -- tools/bench_gemm_rows.py compares the two)
   a.tile_rows = rows > 64 && !(a.row_scale && a.nrm_nparts > 16) && !(mode & 256) ? 128 : 64;
-  // bit 9: 256-row tiles above 128 rows (packed W, no grouping; a row scale of <= 8 parts)
-  if ((mode & 512) && rows > 128 && !grouped && (mode & 16) && !(a.row_scale && a.nrm_nparts > 8)) a.tile_rows = 256;
   a.row_tiles = (rows + a.tile_rows - 1) / a.tile_rows;
   if (rows > 64 && (rows > kMaxRows || (mode & 7) > kSiluMul || (mode & 32))) return -1;
   if (a.N % 128 || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8) return -1;
@@ -461,7 +444,7 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
   const bool norm = (mode & 32) != 0;    // bit 5: RMSNorm prologue on A
   // bit 6: non-temporal weight loads (hint); not with several row tiles, whose workgroups of one
   // W tile read it through the XCD's L2 one after another
-  const bool nt = (mode & 64) != 0 && a.row_tiles == 1 && a.tile_rows != 256;
+  const bool nt = (mode & 64) != 0 && a.row_tiles == 1;
   const bool half = (mode & 128) != 0;   // bit 7: 64-row n-blocks (KR = 1)
   if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr)) return -1;
   if (half) {  // split-K projections only: fp32 slabs or the in-launch residual update

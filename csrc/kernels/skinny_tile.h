@@ -37,7 +37,7 @@ struct GemmArgs {
   int row_scale;             // output row m scaled by rinv[m] from nrm_parts (RMSNorm folded: A is the
                              //   residual stream, the norm weight is pre-multiplied into W's columns)
   int row_tiles;             // set by dispatch: row tiles of M (> 1: M > 64, see skinny_gemm_kernel)
-  int tile_rows;             // set by dispatch: rows per row tile (64, 128 for the MT = 8 variant, 256 for MT = 16)
+  int tile_rows;             // set by dispatch: rows per row tile (64, or 128 for the MT = 8 variant)
 };
 
 namespace {
@@ -272,10 +272,8 @@ constexpr int kAStride = kKC + 8;  // bf16 elements per LDS row (+16 B pad: rows
 // MT = 8 (128 A rows, decode batches above 64): A is staged per 128-deep k-step instead of per
 // 256-deep chunk, so the double-buffered tile stays 68 KiB (two workgroups per CU) and the
 // register staging half as wide (no spills at 2 waves / SIMD).
-// MT = 16 (256 A rows, decode batches above 128): the same 128-deep A steps, 139 KiB of LDS and
-// one workgroup per CU (skinny_wide_kernel, 1 wave / SIMD: the 128 accumulators per lane fit
-// beside the staging registers); every weight byte is read once for all 256 rows instead of
-// once per 128-row tile.
+// (256-row tiles -- MT = 16, one workgroup per CU, accumulators in AGPRs -- measured slower than
+// two XCD-grouped 128-row tiles at every 8B shape: profiles/r4_wide_tiles_probe.jsonl)
 // LDS of one skinny-GEMM workgroup (passed in, so two roles of one fused launch share it)
 template <int MT>
 struct SkinnyLds {
@@ -342,9 +340,9 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   // RS (row scale): the sum-of-squares parts of row `tid` are requested before the weight
   // stream starts and consumed only after the main loop, so they never delay it (unconditional
   // loads from clamped addresses: a load behind a branch would make hipcc drain vmcnt)
-  // (4 threads per row; up to 64 parts per row for 64 rows, 16 for 128 rows, 8 for 256 rows)
-  constexpr int kRsRows = MT > 4 ? MT / 4 : 1;  // 64-row groups per thread
-  constexpr int kRsLoads = MT == 16 ? 2 : 16 / (kRsRows * kRsRows);
+  // (4 threads per row; up to 64 parts per row for 64 rows, 16 for 128 rows)
+  constexpr int kRsRows = MT > 4 ? 2 : 1;  // 64-row groups per thread
+  constexpr int kRsLoads = 16 / (kRsRows * kRsRows);
   float rs_p[RS ? kRsRows * kRsLoads : 1];
   if constexpr (RS) {
     const int np = min(args.nrm_nparts, 4 * kRsLoads), sub = tid & 3;

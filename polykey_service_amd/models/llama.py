@@ -96,11 +96,6 @@ LM_HEAD_SKINNY_MAX_M = 128
 # above this many decode rows gate_up runs on hipBLASLt (+ the norm / SiLU kernels): 256 clients
 # 19,030-19,728 -> 20,177-20,218 tok/s with 192 instead of 384 (profiles/r4_gate_up_rows_ab.jsonl)
 GATE_UP_SKINNY_MAX_M = 192
-_AB_QKV_S = int(os.environ.get("POLYKEY_AB_QKV_S", "0")) or None  # A/B only (removed after)
-_AB_O_S = int(os.environ.get("POLYKEY_AB_O_S", "0")) or None
-_AB_O_HALF = os.environ.get("POLYKEY_AB_O_HALF", "1") == "1"
-_AB_TP_REDUCE = os.environ.get("POLYKEY_AB_TP_REDUCE", "0") == "1"
-_AB_QKV_HALF = os.environ.get("POLYKEY_AB_QKV_HALF", "0") == "1"
 
 
 def pack_folded(owner, name: str, norm_w: torch.Tensor, packed_only: bool) -> torch.Tensor:
@@ -472,8 +467,8 @@ class LlamaForCausalLM(nn.Module):
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read); the residual
             # update by the last split of each n-block inside the O launch measured 1 % slower
             # (profiles/r4_o_inlaunch_ab.jsonl)
-            parts = gemm.residual_parts(gemm.linear_partial(a, layer.attn.o, ws, S=_AB_O_S, packed=layer.attn.o_p,
-                                                            half=_AB_O_HALF), residual, buf2)
+            parts = gemm.residual_parts(gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p, half=True),
+                                        residual, buf2)
             d = self._decode_mlp(layer, residual, parts, ws)
             if i < last:
                 parts = gemm.residual_parts(d, residual, buf)
@@ -493,9 +488,9 @@ class LlamaForCausalLM(nn.Module):
             # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip);
             # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
             return gemm.qkv_attn_fused(residual, at.qkv_pf, rs, ws, positions, self.cos_sin, kc, vc, md, at.scale,
-                                       at.nq, at.nkv, self._flow_qkv, S=_AB_QKV_S)
-        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, packed=at.qkv_pf, half=_AB_QKV_HALF)
-        if md.num_prefill == 0 and not (_AB_TP_REDUCE and at.nkv < gemm.QKV_ATTN_MIN_KV):
+                                       at.nq, at.nkv, self._flow_qkv)
+        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, packed=at.qkv_pf)
+        if md.num_prefill == 0:
             return attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
         q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
         return attn_ops.paged_attention(q, kc, vc, md, at.scale)

@@ -231,7 +231,7 @@ def choose_split(N: int, K: int, M: int, target: Optional[int] = None) -> int:
     """Smallest power-of-two K split giving >= ``target`` workgroups (128 W rows x one row tile
     each): 192 for one row tile, 384 when several row tiles share each W tile through the L2
     (tools/bench_gemm_rows.py, profiles/r3_decode_rows.txt)."""
-    rt = 1 if M <= 64 else -(-M // (WIDE_TILE_M if WIDE_TILES and M > 128 else SKINNY_TILE_M))
+    rt = 1 if M <= 64 else -(-M // SKINNY_TILE_M)
     if target is None:
         target = _TARGET_WGS if rt == 1 else 2 * _TARGET_WGS
     blocks = N // _ROWS_PER_WG * rt
@@ -278,18 +278,10 @@ NT_MIN_BYTES = 160 << 20
 NT_BIT = 64
 
 
-# 256-row tiles (MT = 16, one workgroup per CU) for decode batches above 128 rows: every weight
-# byte read once for 256 rows (csrc/kernels/skinny_tile.h MT = 16)
-WIDE_TILES = os.environ.get("POLYKEY_WIDE_TILES", "0") == "1"
-WIDE_BIT = 512
-WIDE_TILE_M = 256
-
-
 def _wmode(packed: Optional[torch.Tensor]) -> int:
     if packed is None:
         return 0
-    return (PACKED_BIT | (NT_BIT if packed.numel() * packed.element_size() >= NT_MIN_BYTES else 0)
-            | (WIDE_BIT if WIDE_TILES else 0))
+    return PACKED_BIT | (NT_BIT if packed.numel() * packed.element_size() >= NT_MIN_BYTES else 0)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -348,10 +340,7 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         if Sg > 1 and ws is not None and ws.numel() >= Sg * M * N:
             # split over K like the fused MLP's gate_up (bit-identical: the same slabs, summed in
             # split order, the same SiLU arithmetic)
-            half = os.environ.get("POLYKEY_AB_GU_HALF", "0") == "1" and Sg % 2 == 0  # A/B only
-            p = linear_partial_rowscale(x, w_gu_interleaved, ws, rowscale, S=Sg // 2 if half else Sg, packed=packed,
-                                        half=half)
-            Sg = p.S
+            p = linear_partial_rowscale(x, w_gu_interleaved, ws, rowscale, S=Sg, packed=packed)
             native.call("pk_splitk_reduce", out.data_ptr(), p.buf.data_ptr(), Sg, M, N, out.stride(0), 1,
                         native.stream_ptr())
             return out

@@ -401,41 +401,6 @@ def test_row_tiles_above_64(M):
     assert (y.float() - exp_folded).abs().max().item() <= 0.01 * exp_folded.abs().max().item()
 
 
-@pytest.mark.parametrize("M", [129, 256, 300, 512])
-def test_wide_row_tiles(M, monkeypatch):
-    """256-row tiles (MT = 16, one workgroup per CU) above 128 rows: packed bf16 out, fp32 split-K
-    slabs, folded-norm slabs with 8 parts per row, and the SiLU gate_up, against fp32 references,
-    and slab for slab equal in sum to the 128-row tiles."""
-    H, N, I = 4096, 6144, 1792
-    res = rnd(M, H)
-    w = rnd(N, H, scale=0.02)
-    wp = gemm.pack_weight(w)
-    exp = res.float() @ w.float().t()
-    D = gemm.DECODE_MAX_M
-    ws = torch.empty(16 * M * N, dtype=torch.float32, device="cuda")
-    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
-    parts = gemm.residual_parts(None, res.clone(), torch.empty(8 * M, device="cuda"))
-    rs = gemm.RowScale(parts, 1e-5)
-    xin = ref.rms_norm(res, nw, 1e-5).float()
-    wfp = gemm.pack_weight(gemm.fold_norm(w, nw))
-    g, u = rnd(I, H, scale=0.05), rnd(I, H, scale=0.05)
-    wgu = gemm.interleave_gate_up(g, u)
-    gup = gemm.pack_weight(gemm.fold_norm(wgu, nw))
-    narrow = gemm.linear_partial(res, w, ws, packed=wp).view().sum(0).clone()
-    monkeypatch.setattr(gemm, "WIDE_TILES", True)
-    torch.testing.assert_close(gemm.linear(res, w, packed=wp, max_m=D).float(), exp, atol=2e-2, rtol=2e-2)
-    p = gemm.linear_partial(res, w, ws, packed=wp)
-    torch.testing.assert_close(p.view().sum(0), exp, atol=1e-2, rtol=1e-2)
-    torch.testing.assert_close(p.view().sum(0), narrow, atol=1e-3, rtol=1e-3)
-    p = gemm.linear_partial_rowscale(res, w, ws, rs, packed=wfp)
-    torch.testing.assert_close(p.view().sum(0), xin @ w.float().t(), atol=3e-2, rtol=3e-2)
-    y = gemm.linear_silu(res, wgu, packed=gup, rowscale=rs)
-    rinv = torch.rsqrt(res.float().pow(2).mean(-1, keepdim=True) + 1e-5)
-    h = (res.float() @ gemm.fold_norm(wgu, nw).float().t()) * rinv
-    exp_folded = ref.silu_and_mul_interleaved(h.to(torch.bfloat16)).float()
-    assert (y.float() - exp_folded).abs().max().item() <= 0.01 * exp_folded.abs().max().item()
-
-
 def test_row_tiles_refuse_in_launch_reduction():
     """The in-launch split-K modes keep M <= 64 (their per-n-block tickets are not per row tile)."""
     M, H, K = 96, 1024, 512

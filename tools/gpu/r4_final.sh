@@ -23,4 +23,3 @@ python3 $R/tools/pmc_summary.py /tmp/pmc_c $R/gpurun_out/r4_fused_pmc_c.md > /de
 cd $R
 timeout -k 10 300 python -u tools/wide_decode_probe.py > gpurun_out/final_wide.jsonl 2>&1 || { tail -20 gpurun_out/final_wide.jsonl; exit 1; }
 cat gpurun_out/final_wide.jsonl
-bash tools/gpu/r4s2_ab10.sh

@@ -17,4 +17,3 @@ for i in 1 2 3; do
     echo "{\"variant\": \"$v\", \"line\": $(tail -1 gpurun_out/ab7_$v.log)}" | tee -a gpurun_out/ab7_solo.jsonl
   done
 done
-bash $R/tools/gpu/r4s2_ab8.sh

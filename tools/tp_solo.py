@@ -92,12 +92,9 @@ def main():
     pos = cl - 1
     slots = bt[:, (a.ctx - 1) // BS] * BS + (a.ctx - 1) % BS
     po, pml = A.decode_workspace(B, at.nq, maxb, BS, dev)
-    ctr = None  # A/B: the decode attention's partitions merged in-launch (last arriver) instead of by a kernel
-    if os.environ.get("POLYKEY_AB_DECODE_MERGE_INLAUNCH", "0") == "1" and po is not None:
-        ctr = torch.zeros((B, at.nkv), dtype=torch.int32, device=dev)
     md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0, slot_mapping=slots,
                         decode_block_tables=bt, decode_context_lens=cl, decode_part_o=po, decode_part_ml=pml,
-                        decode_counters=ctr, decode_max_ctx=A._PART if a.ctx <= A._PART else 0)
+                        decode_max_ctx=A._PART if a.ctx <= A._PART else 0)
     ids = torch.randint(0, cfg.vocab_size, (B,), dtype=torch.int32, device=dev)
 
     def step():

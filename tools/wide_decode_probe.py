@@ -1,7 +1,8 @@
 """Decode GEMMs at 256 / 512 rows (Llama-3-8B shapes, cold weights rotated over 4 copies):
-hipBLASLt (torch.mm) vs the skinny decode GEMM with 128-row tiles vs 256-row tiles (gemm.WIDE_TILES,
-MT = 16), each at the split the decode chain uses (gate_up: the folded-norm SiLU launch, S = 1).
-One JSON line per shape and row count."""
+hipBLASLt (torch.mm) vs the skinny decode GEMM's XCD-grouped 128-row tiles, each at the split the
+decode chain uses (gate_up: the folded-norm SiLU launch, S = 1).  One JSON line per shape and row
+count.  (The 256-row MT = 16 tiles it also timed in round 4 were slower and are gone:
+profiles/r4_wide_tiles_probe.jsonl.)"""
 import json
 import os
 import sys
@@ -41,20 +42,16 @@ def main():
             rs = gemm.RowScale(parts.view(-1, M), 1e-5)
             row = {"shape": name, "M": M, "N": N, "K": K}
             row["hipblaslt_us"] = timeit(lambda i: torch.mm(x, ws_[i % L].t(), out=out))
-            for wide in (False, True):
-                gemm.WIDE_TILES = wide
-                tag = "wide" if wide else "rows128"
-                if name == "gate_up":
-                    fn = lambda i: gemm.linear_silu(x, ws_[i % L], packed=wp[i % L], rowscale=rs)  # noqa: E731
-                else:
-                    fn = lambda i: gemm.linear_partial(x, ws_[i % L], slab, packed=wp[i % L])  # noqa: E731
-                try:
-                    row[f"{tag}_us"] = timeit(fn)
-                except Exception as e:  # noqa: BLE001 - a probe: report and go on
-                    row[f"{tag}_us"] = f"error: {e}"
-            gemm.WIDE_TILES = False
+            if name == "gate_up":
+                fn = lambda i: gemm.linear_silu(x, ws_[i % L], packed=wp[i % L], rowscale=rs)  # noqa: E731
+            else:
+                fn = lambda i: gemm.linear_partial(x, ws_[i % L], slab, packed=wp[i % L])  # noqa: E731
+            try:
+                row["rows128_us"] = timeit(fn)
+            except Exception as e:  # noqa: BLE001 - a probe: report and go on
+                row["rows128_us"] = f"error: {e}"
             flops = 2.0 * M * N * K
-            for k in ("hipblaslt_us", "rows128_us", "wide_us"):
+            for k in ("hipblaslt_us", "rows128_us"):
                 if isinstance(row[k], float):
                     row[k.replace("_us", "_tfs")] = round(flops / row[k] / 1e6, 1)
             print(json.dumps(row), flush=True)
