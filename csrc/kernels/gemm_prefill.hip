@@ -51,6 +51,8 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
@@ -58,6 +60,17 @@ __device__ __forceinline__ void wait_vm() {
 // (non-template) device function: called directly inside the kernel template, hipcc's host pass
 // silently drops the kernel's launch stub (undefined symbol at load time).
 __device__ __forceinline__ void glds16(const bf16_t* g, bf16_t* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
+
+// buffer-resource forms (same reason: plain functions, not called from the template directly)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const bf16_t* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p), static_cast<short>(0), bytes, 0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, bf16_t* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+__device__ __forceinline__ bf16x8_t bld16(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
 
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
 
@@ -555,9 +568,263 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_deep_kernel(const Pr
     }
 }
 
+// ---- 4-wave variant (6: row-major W, 7: block-packed W): one wave per SIMD, each wave owns a
+// 128 x 128 quadrant of the 256 x 256 tile = 8 x 8 MFMA 16x16x32 accumulators (256 fp32 per lane),
+// the structure hipBLASLt's MT256x256 kernel uses (profiles/r2_prefill_gemm_pmc.md: 0.25 LDS reads
+// per MFMA instead of the 8-wave kernels' 0.38-0.44, one wave per SIMD, few barriers).  hipcc does
+// not keep a 256-float accumulator in AGPRs next to the fragment registers when it sees the MFMAs
+// (round 2: 528 v_accvgpr moves per k-tile), so the MFMAs are inline asm on "a" operands: the
+// accumulators never leave the AGPR file.  hipcc neither counts nor pads inline asm (guide §5.7):
+//   * the first k-tile's MFMAs take C = 0 (no accumulator initialisation to pad against);
+//   * fragments come straight from ds_read (the compiler waits lgkmcnt for asm operands) and
+//     each accumulator's next MFMA is 64 MFMAs later (no dependent-MFMA hazard);
+//   * the epilogue reads the AGPRs after 32 wait states (s_nop) behind the last MFMA.
+// Pipeline: BK = 32, a 4-deep LDS ring of k-tiles (A | W, 32 KiB each, 128 KiB); at k-tile kt
+// each wave (1) retires its own LDS-DMA of tile kt + 1 with a counted vmcnt (tiles kt + 2 and
+// kt + 3 stay in flight), (2) lgkmcnt(0) + one raw barrier: tile kt + 1 visible to every wave and
+// every wave done reading tile kt's slot, (3) runs tile kt's 64 MFMAs from registers, interleaving
+// the 16 ds_reads of tile kt + 1's fragments (second register set) and the 8 LDS-DMA loads of
+// tile kt + 4 into tile kt's slot.  Tile kt + 4 thus has ~2.5 k-tiles (~2,500 cycles) to land.
+__device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8_t& w, const bf16x8_t& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(a));
+}
+__device__ __forceinline__ void mfma_zero(f32x4& c, const bf16x8_t& w, const bf16x8_t& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(w), "v"(a));
+}
+
+constexpr int kW4Threads = 256;
+
+template <bool PW, bool RS, bool BUF, bool STG>
+__global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const PrefillGemmArgs args) {
+  constexpr int BK = 32, NS = 4, kSwz = 2;
+  constexpr int kPiece = 256 * BK;  // one operand of one k-tile (16 KiB)
+  constexpr int kStage = 2 * kPiece;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NS * kStage];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  Tile tl;
+  if (!tile_of(args, tl)) return;
+  const int K = args.K, nk = K / BK;
+
+  // LDS-DMA sources: instruction j (0..3) of an operand fills LDS rows 64 j .. 64 j + 63, thread t
+  // row 64 j + t / 4, physical 16-byte chunk t % 4 = logical chunk ^ (row >> 2 & 3) (64-byte rows:
+  // the 16 rows of a fragment read hit 16 distinct bank groups); row-major W likewise, packed W:
+  // fragment 4 j + w (128-row block h = f / 8, row tile f % 8) copied lane-linearly
+  const int lrow = tid >> 2;
+  const int logical = (tid & 3) ^ ((lrow >> kSwz) & 3);
+  const bf16_t* asrc[4];
+  const bf16_t* wsrc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = min(tl.m0 + 64 * j + lrow, tl.rows - 1);  // rows past the group: clamped, never stored
+    asrc[j] = args.A + static_cast<long long>(tl.row0 + m) * args.lda + logical * 8;
+    if constexpr (PW) {
+      const int f = 4 * j + w;
+      wsrc[j] = tl.W + static_cast<long long>((tl.n0 >> 7) + (f >> 3)) * 128 * K + (f & 7) * 4 * 512 + lane * 8;
+    } else {
+      wsrc[j] = tl.W + static_cast<long long>(tl.n0 + 64 * j + lrow) * K + logical * 8;
+    }
+  }
+  auto src_of = [&](int j, int kt) {
+    const long long wo = PW ? (kt >> 2) * 16384LL + (kt & 3) * 512 : static_cast<long long>(kt) * BK;
+    return j < 4 ? asrc[j] + kt * BK : wsrc[j - 4] + wo;
+  };
+  auto dst_of = [&](int j, int slot) {  // wave w's 1 KiB of instruction j
+    return lds + slot * kStage + w * 16 * BK + (j < 4 ? j * 64 * BK : kPiece + (j - 4) * 64 * BK);
+  };
+  // BUF: the same loads as buffer instructions (32-bit lane offsets, the k offset in an SGPR; A rows
+  // past the group read as zeros instead of being clamped)
+  const __amdgpu_buffer_rsrc_t arsrc =
+      rsrc_of(args.A + static_cast<long long>(tl.row0 + tl.m0) * args.lda,
+              static_cast<int>(min(static_cast<long long>(max(tl.rows - tl.m0, 0)) * args.lda * 2, 0x7fffffffLL)));
+  const __amdgpu_buffer_rsrc_t wrsrc = rsrc_of(tl.W + static_cast<long long>(PW ? (tl.n0 >> 7) * 128 : tl.n0) * K, 0x7fffffff);
+  int avoff[4], wvoff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    avoff[j] = ((64 * j + lrow) * args.lda + logical * 8) * 2;
+    const int f = 4 * j + w;
+    wvoff[j] = PW ? ((f >> 3) * 128 * K + (f & 7) * 4 * 512 + lane * 8) * 2 : ((64 * j + lrow) * K + logical * 8) * 2;
+  }
+  auto soff_of = [&](int j, int kt) {
+    return j < 4 || !PW ? kt * BK * 2 : ((kt >> 2) * 16384 + (kt & 3) * 512) * 2;
+  };
+  auto stage_one = [&](int j, int kt) {
+    if constexpr (BUF) blds16(j < 4 ? arsrc : wrsrc, dst_of(j, kt % NS), j < 4 ? avoff[j] : wvoff[j - 4], soff_of(j, kt));
+    else glds16(src_of(j, kt), dst_of(j, kt % NS));
+  };
+  // RS (register staging): the same LDS image written by ds_write_b128 from two register sets
+  bf16x8_t S[2][8];
+  auto rs_load = [&](int set, int j, int kt) {
+    if constexpr (BUF) S[set][j] = bld16(j < 4 ? arsrc : wrsrc, j < 4 ? avoff[j] : wvoff[j - 4], soff_of(j, kt));
+    else S[set][j] = ld8(src_of(j, kt));
+  };
+  auto rs_write = [&](int set, int j, int slot) { *reinterpret_cast<bf16x8_t*>(dst_of(j, slot) + lane * 8) = S[set][j]; };
+
+  // fragment reads: wave (wr, wc) = (w >> 1, w & 1) owns rows wr*128.. and W rows wc*128..; the
+  // swizzle term of row (16 f + r) is (r >> 2) & 3, so fragment f sits at a constant offset
+  const int wr = w >> 1, wc = w & 1;
+  const int r = lane & 15, g = lane >> 4;
+  const int a_lane = (wr * 128 + r) * BK + ((g ^ ((r >> kSwz) & 3)) * 8);
+  const int w_lane = PW ? kPiece + wc * 8 * 512 + lane * 8 : kPiece + (wc * 128 + r) * BK + ((g ^ ((r >> kSwz) & 3)) * 8);
+  constexpr int kFragStride = PW ? 512 : 16 * BK;
+
+  bf16x8_t fa[2][8], fw[2][8];
+  f32x4 acc[8][8];  // [n frag][m frag]
+
+  // prologue: tiles 0..3 in flight, tile 0 retired and read (RS: tiles 0, 1 in LDS, 2, 3 in the
+  // register sets)
+  if constexpr (RS) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rs_load(0, j, 0), rs_load(1, j, 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rs_write(0, j, 0), rs_write(1, j, 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rs_load(0, j, 2), rs_load(1, j, 3);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  } else {
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) stage_one(j, t);
+    wait_vm<24>();
+  }
+  barrier();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    fw[0][f] = ld8(lds + w_lane + f * kFragStride);
+    fa[0][f] = ld8(lds + a_lane + f * 16 * BK);
+  }
+
+  // one k-tile from register set C.  Z: the first (C = 0); NEXT: read tile kt + 1 (after retiring
+  // it: VM = its younger LDS-DMA loads still in flight); RESTAGE: load tile kt + 4 into kt's slot
+  // (RS: into register set C); WR (RS): write register set C (tile kt + 2) into its slot
+  // STG: the waves issue their loads at different MFMAs of a group (wave w before MFMA 2 w), so
+  // the four waves' 1 KiB requests do not reach the CU's address unit in the same cycles
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto step = [&](auto Pc, auto Cc, auto Zc, auto Nc, auto Rc, auto Vc, auto Wc, int kt) {
+    constexpr int C = decltype(Cc)::value, VM = decltype(Vc)::value;
+    constexpr bool Z = decltype(Zc)::value, NEXT = decltype(Nc)::value, RESTAGE = decltype(Rc)::value;
+    constexpr bool WR = RS && decltype(Wc)::value;
+    if constexpr (NEXT) {
+      if constexpr (!RS) wait_vm<VM>();
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to hipcc's own waitcnt bookkeeping
+      barrier();
+    }
+    const bf16_t* nb = lds + ((kt + 1) % NS) * kStage;
+    auto load = [&](int mf) {
+      if constexpr (RS) rs_load(C, mf, kt + NS);
+      else stage_one(mf, kt + NS);
+    };
+    auto groups = [&](auto Pc) {
+      constexpr int P = decltype(Pc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mf = 0; mf < 8; ++mf) {
+        if constexpr (NEXT) {
+          fw[C ^ 1][mf] = ld8(nb + w_lane + mf * kFragStride);
+          fa[C ^ 1][mf] = ld8(nb + a_lane + mf * 16 * BK);
+        }
+        if constexpr (WR) rs_write(C, mf, (kt + 2) % NS);
+        if constexpr (RESTAGE && P < 0) load(mf);
+#pragma unroll
+        for (int nf = 0; nf < 8; ++nf) {
+          if constexpr (RESTAGE && P >= 0) {
+            if (nf == 2 * P) {
+              __builtin_amdgcn_sched_barrier(0);
+              load(mf);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+          if constexpr (Z) mfma_zero(acc[nf][mf], fw[C][nf], fa[C][mf]);
+          else mfma_acc(acc[nf][mf], fw[C][nf], fa[C][mf]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    groups(Pc);
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using V0 = std::integral_constant<int, 0>;
+  using V8 = std::integral_constant<int, 8>;
+  using V16 = std::integral_constant<int, 16>;
+  using T = std::true_type;
+  using F = std::false_type;
+  // nk = K / 32 is a multiple of 8 (launcher: K % 256 == 0)
+  // the whole k-loop per load position (one code path per wave: no join inside the loop)
+  auto run = [&](auto Pc) {
+    step(Pc, I0{}, T{}, T{}, T{}, V16{}, T{}, 0);
+    step(Pc, I1{}, F{}, T{}, T{}, V16{}, T{}, 1);
+    for (int kt = 2; kt < nk - NS; kt += 2) {
+      step(Pc, I0{}, F{}, T{}, T{}, V16{}, T{}, kt);
+      step(Pc, I1{}, F{}, T{}, T{}, V16{}, T{}, kt + 1);
+    }
+    step(Pc, I0{}, F{}, T{}, F{}, V16{}, T{}, nk - 4);
+    step(Pc, I1{}, F{}, T{}, F{}, V8{}, T{}, nk - 3);
+    step(Pc, I0{}, F{}, T{}, F{}, V0{}, F{}, nk - 2);
+    step(Pc, I1{}, F{}, F{}, F{}, V0{}, F{}, nk - 1);
+  };
+  if constexpr (STG) {
+    if (wu == 0) run(std::integral_constant<int, 0>{});
+    else if (wu == 1) run(std::integral_constant<int, 1>{});
+    else if (wu == 2) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 3>{});
+  } else {
+    run(std::integral_constant<int, -1>{});
+  }
+
+  // the last MFMAs' results before any AGPR read (8-pass XDL: 12+ wait states)
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int nf = 0; nf < 8; ++nf)
+#pragma unroll
+    for (int mf = 0; mf < 8; ++mf) asm volatile("" : "+a"(acc[nf][mf]));
+
+  // acc[nf][mf][i] = C[m = wr*128 + mf*16 + r][n = wc*128 + nf*16 + 4g + i]
+#pragma unroll
+  for (int mf = 0; mf < 8; ++mf) {
+    const int m = tl.m0 + wr * 128 + mf * 16 + r;
+    if (m >= tl.rows) continue;
+    bf16_t* crow = args.C + static_cast<long long>(tl.row0 + m) * args.ldc;
+    const int nb0 = tl.n0 + wc * 128;
+    if (args.silu) {  // n frags 2p / 2p + 1 = gate / up of the same 16 output columns
+#pragma unroll
+      for (int nf = 0; nf < 8; nf += 2) {
+        float y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = rbf(silu(rbf(acc[nf][mf][i]))) * rbf(acc[nf + 1][mf][i]);
+        uint2 v;
+        v.x = pack2(y[0], y[1]);
+        v.y = pack2(y[2], y[3]);
+        *reinterpret_cast<uint2*>(crow + (nb0 + nf * 16) / 2 + 4 * g) = v;
+      }
+    } else {
+#pragma unroll
+      for (int nf = 0; nf < 8; ++nf) {
+        uint2 v;
+        v.x = pack2(acc[nf][mf][0], acc[nf][mf][1]);
+        v.y = pack2(acc[nf][mf][2], acc[nf][mf][3]);
+        *reinterpret_cast<uint2*>(crow + nb0 + nf * 16 + 4 * g) = v;
+      }
+    }
+  }
+}
+
 int launch(const PrefillGemmArgs& a, int variant, hipStream_t stream) {
   const int grid = a.tiles_m * (a.N / kBN);
   switch (variant) {
+    case 6: prefill_gemm_w4_kernel<false, false, false, false><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 7: prefill_gemm_w4_kernel<true, false, false, false><<<grid, kW4Threads, 0, stream>>>(a); break;  // block-packed W
+    case 8: prefill_gemm_w4_kernel<false, true, false, false><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 9: prefill_gemm_w4_kernel<true, true, false, false><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 10: prefill_gemm_w4_kernel<false, false, true, false><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 11: prefill_gemm_w4_kernel<true, false, true, false><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 12: prefill_gemm_w4_kernel<false, true, true, false><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 13: prefill_gemm_w4_kernel<true, true, true, false><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 14: prefill_gemm_w4_kernel<false, false, false, true><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 15: prefill_gemm_w4_kernel<true, false, false, true><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 16: prefill_gemm_w4_kernel<false, true, true, true><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 17: prefill_gemm_w4_kernel<true, true, true, true><<<grid, kW4Threads, 0, stream>>>(a); break;
     case 0: prefill_gemm_kernel<64, 2><<<grid, kThreads, 0, stream>>>(a); break;
     case 1: prefill_gemm_kernel<32, 4><<<grid, kThreads, 0, stream>>>(a); break;
     case 2: prefill_gemm_pp_kernel<false><<<grid, kThreads, 0, stream>>>(a); break;
@@ -578,6 +845,7 @@ PK_EXPORT int pk_prefill_gemm(const PrefillGemmArgs* a, int variant, hipStream_t
   if (a->M <= 0 || a->tiles_m <= 0) return 0;
   if (a->N % kBN || a->K % 64 || a->lda % 8 || a->ldc % 4) return -1;
   if ((variant == 3 || variant == 5) && a->K % 128) return -1;
+  if (variant >= 6 && a->K % 256) return -1;
   if (a->row_offsets != nullptr && a->groups <= 0) return -1;
   if (a->row_offsets == nullptr && a->tiles_m != (a->M + kBM - 1) / kBM) return -1;
   return launch(*a, variant, stream);

@@ -54,8 +54,10 @@ def _launch(a: PrefillGemmArgs, variant: Optional[int] = None) -> None:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         f.restype = ctypes.c_int
         _checked = True
-    native.check(lib.pk_prefill_gemm(ctypes.byref(a), VARIANT if variant is None else variant, native.stream_ptr()),
-                 "pk_prefill_gemm")
+    v = VARIANT if variant is None else variant
+    if v >= 6 and a.K % 256:  # the 4-wave kernel's tail schedule needs 8+ k-tiles of 32
+        v = 5 if v % 2 else 4
+    native.check(lib.pk_prefill_gemm(ctypes.byref(a), v, native.stream_ptr()), "pk_prefill_gemm")
 
 
 def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
@@ -96,8 +98,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
     if (not supported(N, K) or x.stride(1) != 1 or not src.is_contiguous() or out.stride(1) != 1
             or (packed is not None and (K % 128 or tuple(packed.shape) != (N, K)))):
         raise ValueError(f"prefill GEMM: unsupported shape/layout M={M} N={N} K={K}")
-    if packed is not None and variant not in (3, 5):
-        variant = PACKED_VARIANT
+    if packed is not None and (variant is None or variant % 2 == 0):
+        variant = PACKED_VARIANT if variant is None or variant < 6 else variant + 1
     a = PrefillGemmArgs()
     a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), src.data_ptr()
     a.M, a.N, a.K, a.lda, a.ldc = M, N, K, x.stride(0), out.stride(0)

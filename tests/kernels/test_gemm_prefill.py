@@ -13,7 +13,7 @@ def rnd(*shape, scale=1.0):
     return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 6, 8, 10, 12])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 4096), (1000, 768, 1024), (4100, 1280, 8192),
                                    (8192, 4096, 4096), (77, 256, 14336)])
 def test_dense(M, N, K, variant):
@@ -33,7 +33,7 @@ def test_dense_strided_out_and_input():
     assert torch.count_nonzero(out_full[:, 512:]) == 0
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4])
+@pytest.mark.parametrize("variant", [0, 2, 4, 6, 8])
 @pytest.mark.parametrize("M,I,K", [(513, 512, 4096), (256, 14336, 4096)])
 def test_silu_epilogue(M, I, K, variant):
     x = rnd(M, K)
@@ -45,7 +45,7 @@ def test_silu_epilogue(M, I, K, variant):
     torch.testing.assert_close(y.float(), exp, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 6, 8])
 @pytest.mark.parametrize("silu", [False, True])
 def test_grouped(silu, variant):
     G, N, K = 6, 512, 1024
@@ -63,7 +63,7 @@ def test_grouped(silu, variant):
     assert torch.all(out[lo:] == 7.0)  # rows past the last group are never written
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4])
+@pytest.mark.parametrize("variant", [0, 2, 4, 6, 8])
 def test_repeatable_bitwise(variant):
     """Race screen for the LDS-DMA pipelines (guide §5: an early read passes reference checks
     whenever the DMA happens to land first): repeated launches on a busy chip give identical
@@ -76,7 +76,7 @@ def test_repeatable_bitwise(variant):
     torch.testing.assert_close(ys[0].float(), other.float(), atol=1e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("variant", [3, 5])
+@pytest.mark.parametrize("variant", [3, 5, 7, 9])
 @pytest.mark.parametrize("M,N,K,silu", [(300, 512, 4096, False), (4100, 1280, 8192, False), (513, 1024, 4096, True),
                                         (256, 256, 128, False), (700, 512, 256, True)])
 def test_block_packed_weights(M, N, K, silu, variant):
@@ -90,6 +90,30 @@ def test_block_packed_weights(M, N, K, silu, variant):
     torch.testing.assert_close(y.float(), ref.float(), atol=1e-2, rtol=1e-2)
     if not silu:
         torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("variant", list(range(6, 18)))
+def test_four_wave_kernel_grouped_mixtral_shape(variant):
+    """The 4-wave kernel (AGPR accumulators from inline-asm MFMAs) on a Mixtral-like grouped w13
+    with ragged expert counts, against per-expert fp32 matmuls (every k-tile of K = 4096: the
+    steady loop, the tail schedule and the packed weight addressing)."""
+    E, N, K = 4, 1024, 4096
+    counts = [700, 0, 1300, 257]
+    T = sum(counts)
+    offs = torch.tensor([0] + torch.tensor(counts).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
+    x, w = rnd(T, K), rnd(E, N, K, scale=0.02)
+    if variant % 2 == 0:
+        y = gemm_prefill.grouped_linear(x, w, offs, variant=variant)
+    else:  # dense, packed
+        y = gemm_prefill.linear(x, torch.empty(N, K, dtype=torch.bfloat16, device="meta"),
+                                packed=gemm.pack_weight(w[0]), variant=variant)
+        counts, w = [T], w[:1]
+    lo = 0
+    for e, c in enumerate(counts):
+        if c:
+            exp = x[lo:lo + c].float() @ w[e].float().t()
+            torch.testing.assert_close(y[lo:lo + c].float(), exp, atol=2e-2, rtol=2e-2)
+        lo += c
 
 
 def test_native_library_has_prefill_gemm():

@@ -25,6 +25,11 @@ VARIANTS = {
     "mlp_nt": [("gemm_skinny.hip", "case 4: mlp_fused_kernel<4, SP, KR><<<", "case 4: mlp_fused_kernel<4, SP, KR, !SP><<<")],
     # the fused launches' hand-off pollers sleeping 4 instead of 16 (x 64 cycles) between polls
     "sleep4": [("flow.h", "__builtin_amdgcn_s_sleep(16);", "__builtin_amdgcn_s_sleep(4);")],
+    # ablations of the 4-wave prefill GEMM measured this round (timing only, wrong results;
+    # profiles/r4_prefill_gemm_4wave.md): no LDS-DMA in the k-loop ("pg_noglds", 1,172 vs 1,552 us
+    # at gate_up), A loads only ("pg_aonly", 1,287 vs 1,497), no vmcnt waits ("pg_novm", no change),
+    # no fragment reads ("pg_nords", -7 %), no barrier ("pg_nobar", no change), full 128-byte lines
+    # per row ("pg_fullline", -5.6 %)
     # measured and removed this round (variant builds of the sources of that time): "mlp_v0" (no NT /
     # LDS prefetch in the down tiles: 4.063 vs 4.063 ms per graph-captured 8B step), "o_ring2" (the
     # o-projection without whole-slice weight registers: 3.997 vs 4.063 ms) -- profiles/r4_variant_ab.jsonl

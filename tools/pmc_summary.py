@@ -73,6 +73,12 @@ def main(argv):
     for t_ns, k, n, mfma, hbm, busy, lds in rows[:40]:
         out.append(f"| `{k}` | {n} | {t_ns/1e6:.2f} | {100*t_ns/total:.1f} | {t_ns/max(n,1)/1e3:.1f} | "
                    f"{100*mfma:.1f}% | {hbm:.2f} | {busy:.2f} | {lds:.0f} |")
+    # every collected counter, per call, for the top kernels
+    names = sorted({c for k in agg for c in agg[k]})
+    out += ["", "Raw counters per call:", "", "| kernel | " + " | ".join(names) + " |",
+            "|---|" + "---|" * len(names)]
+    for t_ns, k, n, *_ in rows[:8]:
+        out.append(f"| `{k[:60]}` | " + " | ".join(f"{agg[k].get(c, 0.0) / max(n, 1):.4g}" for c in names) + " |")
     text = "\n".join(out) + "\n"
     if len(argv) > 1:
         with open(argv[1], "w") as fh:

@@ -33,7 +33,8 @@ def main():
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        cases.append((name, 2.0 * M * N * K, lambda v, x=x, w=w, out=out: gemm_prefill.linear(x, w, out=out, variant=v)))
+        cases.append((name, 2.0 * M * N * K, lambda v, x=x, w=w, out=out: gemm_prefill.linear(x, w, out=out, variant=v),
+                      lambda x=x, w=w, out=out: torch.mm(x, w.t(), out=out)))
     E, H, I = 8, 4096, 14336
     counts = [2048 + d for d in (40, -30, 12, -25, 0, 31, -16, -12)]
     T = sum(counts)
@@ -42,18 +43,34 @@ def main():
     w13 = torch.randn(E, 2 * I, H, device=dev, dtype=torch.bfloat16) * 0.02
     h = torch.randn(T, I, device=dev, dtype=torch.bfloat16)
     w2 = torch.randn(E, H, I, device=dev, dtype=torch.bfloat16) * 0.02
+    # hipBLASLt reference for the grouped cases: torch._grouped_mm over the same device offsets
+    # (no SiLU epilogue: it would need a separate pass)
+    gm = getattr(torch, "_grouped_mm", None)
+    offs_end = offs[1:].contiguous()
+    blas13 = (lambda: gm(x, w13.transpose(1, 2), offs=offs_end)) if gm else None
+    blas2 = (lambda: gm(h, w2.transpose(1, 2), offs=offs_end)) if gm else None
     cases.append(("moe_w13_silu", 2.0 * T * 2 * I * H,
-                  lambda v: gemm_prefill.grouped_linear(x, w13, offs, silu=True, variant=v)))
-    cases.append(("moe_w2", 2.0 * T * H * I, lambda v: gemm_prefill.grouped_linear(h, w2, offs, variant=v)))
-    for name, fl, fn in cases:
-        ra, rb = [], []
+                  lambda v: gemm_prefill.grouped_linear(x, w13, offs, silu=True, variant=v), blas13))
+    cases.append(("moe_w2", 2.0 * T * H * I, lambda v: gemm_prefill.grouped_linear(h, w2, offs, variant=v), blas2))
+    for name, fl, fn, blas in cases:
+        ra, rb, rc = [], [], []
         for _ in range(5):
             ra.append(t(lambda: fn(va)))
             rb.append(t(lambda: fn(vb)))
+            if blas is not None:
+                try:
+                    rc.append(t(blas))
+                except Exception:  # noqa: BLE001 - reference column only
+                    blas = None
         ma, mb = statistics.median(ra), statistics.median(rb)
-        print(json.dumps({"gemm": name, f"v{va}_us": round(ma, 1), f"v{vb}_us": round(mb, 1),
-                          f"v{va}_tfs": round(fl / ma / 1e6), f"v{vb}_tfs": round(fl / mb / 1e6),
-                          "gain_pct": round(100 * (ma / mb - 1), 1)}), flush=True)
+        row = {"gemm": name, f"v{va}_us": round(ma, 1), f"v{vb}_us": round(mb, 1),
+               f"v{va}_tfs": round(fl / ma / 1e6), f"v{vb}_tfs": round(fl / mb / 1e6),
+               "gain_pct": round(100 * (ma / mb - 1), 1)}
+        if rc:
+            mc = statistics.median(rc)
+            row.update({"hipblaslt_us": round(mc, 1), "hipblaslt_tfs": round(fl / mc / 1e6),
+                        f"v{vb}_vs_hipblaslt_pct": round(100 * (mb / mc - 1), 1)})
+        print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":
