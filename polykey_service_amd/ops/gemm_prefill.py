@@ -20,10 +20,9 @@ from . import native
 
 BM = 256
 BN = 256
-# 0: BK 64 x 2 LDS stages, 1: BK 32 x 4 stages, 2: ping-pong quadrant phases (6-8 %
-# faster than 0, tools/prefill_gemm_bench.py) -- csrc/kernels/gemm_prefill.hip
-# 4: ping-pong quadrant phases with three LDS-DMA pieces in flight (tools/prefill_gemm_ab.py, same
-# process: grouped MoE w13 +3.2 %, w2 +4.8 %, dense gate_up / down +2.3-2.5 % over variant 2)
+# 4: ping-pong quadrant phases with three LDS-DMA pieces in flight (csrc/kernels/gemm_prefill.hip;
+# the slower round-2 variants 0-3 and the equal round-4 4-wave kernel 6-17 are deleted:
+# profiles/r2_prefill_gemm_lab.txt, profiles/r4_prefill_gemm_4wave.md)
 VARIANT = 4
 
 
@@ -54,10 +53,8 @@ def _launch(a: PrefillGemmArgs, variant: Optional[int] = None) -> None:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         f.restype = ctypes.c_int
         _checked = True
-    v = VARIANT if variant is None else variant
-    if v >= 6 and a.K % 256:  # the 4-wave kernel's tail schedule needs 8+ k-tiles of 32
-        v = 5 if v % 2 else 4
-    native.check(lib.pk_prefill_gemm(ctypes.byref(a), v, native.stream_ptr()), "pk_prefill_gemm")
+    native.check(lib.pk_prefill_gemm(ctypes.byref(a), VARIANT if variant is None else variant, native.stream_ptr()),
+                 "pk_prefill_gemm")
 
 
 def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
@@ -69,7 +66,7 @@ def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
     return y.to(x.dtype)
 
 
-# ping-pong kernel reading the decode GEMM's block-packed W (5: its deep-pipelined form)
+# the same kernel reading the decode GEMM's block-packed W
 PACKED_VARIANT = 5
 
 
@@ -98,8 +95,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
     if (not supported(N, K) or x.stride(1) != 1 or not src.is_contiguous() or out.stride(1) != 1
             or (packed is not None and (K % 128 or tuple(packed.shape) != (N, K)))):
         raise ValueError(f"prefill GEMM: unsupported shape/layout M={M} N={N} K={K}")
-    if packed is not None and (variant is None or variant % 2 == 0):
-        variant = PACKED_VARIANT if variant is None or variant < 6 else variant + 1
+    if packed is not None:
+        variant = PACKED_VARIANT
     a = PrefillGemmArgs()
     a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), src.data_ptr()
     a.M, a.N, a.K, a.lda, a.ldc = M, N, K, x.stride(0), out.stride(0)

@@ -6,9 +6,9 @@ mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/kernels/test_gemm_prefill.py > gpurun_out/pg5_tests.log 2>&1 \
   || { tail -40 gpurun_out/pg5_tests.log; exit 1; }
 tail -2 gpurun_out/pg5_tests.log
-timeout -k 10 200 python -u tools/pg_probe.py ${PV:-4 6 8 10 12} > gpurun_out/pg5_probe.jsonl 2>&1 || { tail -20 gpurun_out/pg5_probe.jsonl; exit 1; }
+timeout -k 10 200 python -u tools/pg_probe.py ${PV:-4 5} > gpurun_out/pg5_probe.jsonl 2>&1 || { tail -20 gpurun_out/pg5_probe.jsonl; exit 1; }
 grep '^{' gpurun_out/pg5_probe.jsonl
 for v in ${ABL:-}; do
-  POLYKEY_LIB_LIBPK_KERNELS=$PWD/tools/lab/libpk_kernels_$v.so timeout -k 10 120 python -u tools/pg_probe.py 6 >> gpurun_out/pg5_probe.jsonl 2>&1 || { tail -20 gpurun_out/pg5_probe.jsonl; exit 1; }
+  POLYKEY_LIB_LIBPK_KERNELS=$PWD/tools/lab/libpk_kernels_$v.so timeout -k 10 120 python -u tools/pg_probe.py 4 >> gpurun_out/pg5_probe.jsonl 2>&1 || { tail -20 gpurun_out/pg5_probe.jsonl; exit 1; }
 done
 grep '^{' gpurun_out/pg5_probe.jsonl | tail -2

@@ -35,7 +35,7 @@ def main():
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     from polykey_service_amd.ops import gemm
     wp = gemm.pack_weight(w)  # odd variants read the block-packed copy
-    for v in [int(a) for a in sys.argv[1:]] or [6]:
+    for v in [int(a) for a in sys.argv[1:]] or [4]:
         kw = {"packed": wp} if v % 2 else {}
         us = statistics.median(t(lambda: gemm_prefill.linear(x, w, out=out, variant=v, **kw)) for _ in range(5))
         print(json.dumps({"lib": lib, "variant": v, "gate_up_us": round(us, 1),

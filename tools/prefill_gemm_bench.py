@@ -48,7 +48,7 @@ def main():
         rows.append({"gemm": name, "M": M, "N": N, "K": K, "linear_us": round(t1, 1), "linear_tfs": round(fl / t1 / 1e6, 1),
                      "matmul_out_us": round(t2, 1), "matmul_out_tfs": round(fl / t2 / 1e6, 1),
                      "mm_out_us": round(t3, 1)})
-        for v in (2, 4):
+        for v in (4,):
             tv = timeit(lambda: gemm_prefill.linear(x, w, out=out, variant=v))
             rows[-1][f"pk{v}_us"] = round(tv, 1)
             rows[-1][f"pk{v}_tfs"] = round(fl / tv / 1e6, 1)
@@ -80,7 +80,7 @@ def main():
     r["w13_tfs"] = round(fl13 / r["w13_us"] / 1e6, 1)
     r["w2_tfs"] = round(fl2 / r["w2_us"] / 1e6, 1)
     print(json.dumps(r), flush=True)
-    for v in (2, 4):
+    for v in (4,):
         g13 = timeit(lambda: gemm_prefill.grouped_linear(x, w13, offs, silu=True, variant=v), 5, 2)
         g2 = timeit(lambda: gemm_prefill.grouped_linear(h, w2, offs, variant=v), 5, 2)
         print(json.dumps({"gemm": f"pk_grouped{v}", "w13_silu_us": round(g13, 1), "w13_tfs": round(fl13 / g13 / 1e6, 1),
