@@ -52,6 +52,7 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
@@ -121,8 +122,8 @@ __device__ __forceinline__ bool tile_of(const PrefillGemmArgs& args, Tile& t) {
 // half of a k-step is 16 such fragments; they are copied linearly into the W piece (fragment
 // f = 2 tile + k-block at f KiB) and every W fragment read is one lane-linear 16-byte ds_read --
 // conflict-free without a swizzle.  So one weight layout serves decode and prefill.
-// Measured and deleted: single-buffer-phase variants (round 2, 2-5 % slower) and a 4-wave,
-// one-wave-per-SIMD kernel with AGPR accumulators (round 4, equal; profiles/r4_prefill_gemm_4wave.md).
+// Measured and deleted: single-buffer-phase variants (round 2, 2-5 % slower).  The 4-wave kernel
+// below replaces this one where K % 128 == 0 (profiles/r4_prefill_gemm_4wave.md).
 // Every wave keeps BOTH W halves of a k-tile in registers (+16 VGPRs), so each operand half is
 // read from LDS exactly once per k-tile -- quadrant order A0W0, A0W1, A1W0, A1W1 reads A0+W0,
 // W1, A1, nothing -- and its LDS slot frees early: A0 / W0 after phase 0, W1 after 1, A1 after 2.
@@ -273,11 +274,188 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_deep_kernel(const Pr
     }
 }
 
+// ---- 4-wave variant (6: row-major W, 7: block-packed W), BK = 64: one wave per SIMD, each wave
+// owns a 128 x 128 quadrant of the 256 x 256 tile = 8 x 8 MFMA 16x16x32 accumulators (256 fp32 per
+// lane) in AGPRs: the MFMAs are inline asm on "a" operands (hipcc does not keep such an
+// accumulator in AGPRs next to the fragment registers on its own).  hipcc neither counts nor pads
+// inline asm (guide §5.7): the first k-step takes C = 0, each accumulator's next MFMA is 64 MFMAs
+// later, and the epilogue reads the AGPRs 32 wait states after the last MFMA.
+// Pipeline: two 64-deep k-tile buffers (A | W, 64 KiB each; 128-byte LDS rows = whole cache lines
+// per glds row -- the BK = 32 form of this kernel doubled the L1 -> L2 requests,
+// profiles/r4_prefill_gemm_pmc.md); the k-loop runs 32-deep sub-steps u: 64 MFMAs on the
+// fragments of u (register set u & 1) while the 16 ds_reads of u + 1 go to the other set; before
+// reading the first half of a new tile (u odd) each wave retires its own LDS-DMA (vmcnt(0)),
+// lgkmcnt(0) and one raw barrier, then issues the 16 LDS-DMA loads of tile (u + 3) / 2 into the
+// buffer the barrier just freed (2 per group of 8 MFMAs): two sub-steps of latency cover them.
+__device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8_t& w, const bf16x8_t& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(a));
+}
+__device__ __forceinline__ void mfma_zero(f32x4& c, const bf16x8_t& w, const bf16x8_t& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(w), "v"(a));
+}
+
+constexpr int kW4Threads = 256;
+
+template <bool PW>
+__global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const PrefillGemmArgs args) {
+  constexpr int BK = 64, kPiece = 256 * BK, kStage = 2 * kPiece;  // 32 KiB per operand per k-tile
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kStage];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  Tile tl;
+  if (!tile_of(args, tl)) return;
+  const int K = args.K, U = K / 32;
+
+  // LDS-DMA sources: instruction j (0..7) of an operand fills rows 32 j .. 32 j + 31; thread t row
+  // 32 j + t / 8, physical chunk t % 8 = logical chunk ^ ((row >> 1) & 7) = ^ ((t >> 4) & 7).
+  // Packed W: slot 4 j + w of the W piece = (128-row half h, row tile t, k-block bb) with
+  // slot = (8 h + t) * 2 + bb, copied lane-linearly from the packed 128 x 128 blocks.
+  const int logical = (tid & 7) ^ ((tid >> 4) & 7);
+  const bf16_t* asrc[8];
+  const bf16_t* wsrc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int m = min(tl.m0 + 32 * j + (tid >> 3), tl.rows - 1);  // rows past the group: clamped, never stored
+    asrc[j] = args.A + static_cast<long long>(tl.row0 + m) * args.lda + logical * 8;
+    if constexpr (PW) {
+      const int slot = 4 * j + w, h = slot >> 4, t = (slot >> 1) & 7, bb = slot & 1;
+      wsrc[j] = tl.W + static_cast<long long>((tl.n0 >> 7) + h) * 128 * K + (t * 4 + bb) * 512 + lane * 8;
+    } else {
+      wsrc[j] = tl.W + static_cast<long long>(tl.n0 + 32 * j + (tid >> 3)) * K + logical * 8;
+    }
+  }
+  auto stage_one = [&](int j, int T) {  // instruction j (0-7 A, 8-15 W) of k-tile T
+    bf16_t* base = lds + (T & 1) * kStage + w * 8 * BK;  // wave w's 1 KiB of the instruction
+    if (j < 8) {
+      glds16(asrc[j] + T * BK, base + j * 32 * BK);
+    } else {
+      const long long wo = PW ? (T >> 1) * 16384LL + (T & 1) * 1024 : static_cast<long long>(T) * BK;
+      glds16(wsrc[j - 8] + wo, base + kPiece + (j - 8) * 32 * BK);
+    }
+  };
+
+  // fragment reads of sub-step u: tile u / 2, k-half s = u & 1 (chunk 4 s + g); the swizzle term of
+  // row (16 f + r) is (r >> 1) & 7, so fragment f sits at a constant offset
+  const int wr = w >> 1, wc = w & 1;
+  const int r = lane & 15, g = lane >> 4;
+  auto a_off = [&](int s) { return (wr * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8); };
+  auto w_off = [&](int s) {
+    if constexpr (PW) return kPiece + (wc * 8 * 2 + s) * 512 + lane * 8;
+    return kPiece + (wc * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8);
+  };
+  constexpr int kWStride = PW ? 2 * 512 : 16 * BK;  // between the W fragments of one sub-step
+
+  bf16x8_t fa[2][8], fw[2][8];
+  f32x4 acc[8][8];  // [n frag][m frag]
+
+  // prologue: tiles 0 and 1 in flight, tile 0 retired, sub-step 0's fragments read
+#pragma unroll
+  for (int j = 0; j < 16; ++j) stage_one(j, 0);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) stage_one(j, 1);
+  wait_vm<16>();
+  barrier();
+  {
+    const int ao = a_off(0), wo = w_off(0);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      fw[0][f] = ld8(lds + wo + f * kWStride);
+      fa[0][f] = ld8(lds + ao + f * 16 * BK);
+    }
+  }
+
+  // sub-step u on register set C.  Z: the first (C = 0); BAR: u odd, the next sub-step opens a new
+  // tile; NEXT: read sub-step u + 1; LOAD: stage tile (u + 3) / 2 (all 16 loads in the odd
+  // sub-step: splitting them over both sub-steps leaves the second half one sub-step to land and
+  // measured 6-11 % slower)
+  auto step = [&](auto Cc, auto Zc, auto Bc, auto Nc, auto Lc, int u) {
+    constexpr int C = decltype(Cc)::value;
+    constexpr bool Z = decltype(Zc)::value, BAR = decltype(Bc)::value, NEXT = decltype(Nc)::value,
+                   LOAD = decltype(Lc)::value;
+    if constexpr (BAR) wait_vm<0>();
+    // lgkmcnt(0) (visible to hipcc's own waitcnt bookkeeping): this sub-step's fragments, read
+    // during the previous one, have long landed -- without it hipcc waits after the first new reads
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if constexpr (BAR) barrier();
+    const int un = u + 1;
+    const bf16_t* nb = lds + ((un >> 1) & 1) * kStage;
+    const int ao = a_off(un & 1), wo = w_off(un & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mf = 0; mf < 8; ++mf) {
+      if constexpr (NEXT) {
+        fw[C ^ 1][mf] = ld8(nb + wo + mf * kWStride);
+        fa[C ^ 1][mf] = ld8(nb + ao + mf * 16 * BK);
+      }
+      if constexpr (LOAD) {
+        stage_one(2 * mf, (u + 3) >> 1);
+        stage_one(2 * mf + 1, (u + 3) >> 1);
+      }
+#pragma unroll
+      for (int nf = 0; nf < 8; ++nf) {
+        if constexpr (Z) mfma_zero(acc[nf][mf], fw[C][nf], fa[C][mf]);
+        else mfma_acc(acc[nf][mf], fw[C][nf], fa[C][mf]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using T = std::true_type;
+  using F = std::false_type;
+  // U = K / 32 is a multiple of 4 (launcher: K % 128 == 0)
+  step(I0{}, T{}, F{}, T{}, F{}, 0);
+  for (int u = 1; u < U - 3; u += 2) {
+    step(I1{}, F{}, T{}, T{}, T{}, u);
+    step(I0{}, F{}, F{}, T{}, F{}, u + 1);
+  }
+  step(I1{}, F{}, T{}, T{}, F{}, U - 3);
+  step(I0{}, F{}, F{}, T{}, F{}, U - 2);
+  step(I1{}, F{}, F{}, F{}, F{}, U - 1);
+
+  // the last MFMAs' results before any AGPR read (8-pass XDL: 12+ wait states)
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int nf = 0; nf < 8; ++nf)
+#pragma unroll
+    for (int mf = 0; mf < 8; ++mf) asm volatile("" : "+a"(acc[nf][mf]));
+
+  // acc[nf][mf][i] = C[m = wr*128 + mf*16 + r][n = wc*128 + nf*16 + 4g + i]
+#pragma unroll
+  for (int mf = 0; mf < 8; ++mf) {
+    const int m = tl.m0 + wr * 128 + mf * 16 + r;
+    if (m >= tl.rows) continue;
+    bf16_t* crow = args.C + static_cast<long long>(tl.row0 + m) * args.ldc;
+    const int nb0 = tl.n0 + wc * 128;
+    if (args.silu) {  // n frags 2p / 2p + 1 = gate / up of the same 16 output columns
+#pragma unroll
+      for (int nf = 0; nf < 8; nf += 2) {
+        float y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = rbf(silu(rbf(acc[nf][mf][i]))) * rbf(acc[nf + 1][mf][i]);
+        uint2 v;
+        v.x = pack2(y[0], y[1]);
+        v.y = pack2(y[2], y[3]);
+        *reinterpret_cast<uint2*>(crow + (nb0 + nf * 16) / 2 + 4 * g) = v;
+      }
+    } else {
+#pragma unroll
+      for (int nf = 0; nf < 8; ++nf) {
+        uint2 v;
+        v.x = pack2(acc[nf][mf][0], acc[nf][mf][1]);
+        v.y = pack2(acc[nf][mf][2], acc[nf][mf][3]);
+        *reinterpret_cast<uint2*>(crow + nb0 + nf * 16 + 4 * g) = v;
+      }
+    }
+  }
+}
+
 int launch(const PrefillGemmArgs& a, int variant, hipStream_t stream) {
   const int grid = a.tiles_m * (a.N / kBN);
   switch (variant) {
     case 4: prefill_gemm_deep_kernel<false><<<grid, kThreads, 0, stream>>>(a); break;
     case 5: prefill_gemm_deep_kernel<true><<<grid, kThreads, 0, stream>>>(a); break;  // block-packed W
+    case 6: prefill_gemm_w4_kernel<false><<<grid, kW4Threads, 0, stream>>>(a); break;
+    case 7: prefill_gemm_w4_kernel<true><<<grid, kW4Threads, 0, stream>>>(a); break;  // block-packed W
     default: return -1;
   }
   return PK_CHECK_LAUNCH();
@@ -285,13 +463,13 @@ int launch(const PrefillGemmArgs& a, int variant, hipStream_t stream) {
 
 }  // namespace
 
-// variant: 4 = row-major W, 5 = block-packed W (K % 128 == 0); the numbers of the round-2 / round-4
-// variants measured slower and deleted (0-3, 6-17) are not reused.  Requires N % 256 == 0, K % 64 == 0,
+// variant: 6 / 7 = the 4-wave kernel (default; K % 128 == 0), 4 / 5 = the 8-wave kernel (K % 64 ==
+// 0 fallback), row-major / block-packed W (packed: K % 128 == 0).  Requires N % 256 == 0, K % 64 == 0,
 // 16-byte aligned rows (lda % 8 == 0, K % 8 == 0, ldc % 4 == 0).
 PK_EXPORT int pk_prefill_gemm(const PrefillGemmArgs* a, int variant, hipStream_t stream) {
   if (a->M <= 0 || a->tiles_m <= 0) return 0;
   if (a->N % kBN || a->K % 64 || a->lda % 8 || a->ldc % 4) return -1;
-  if (variant == 5 && a->K % 128) return -1;
+  if ((variant == 5 || variant >= 6) && a->K % 128) return -1;
   if (a->row_offsets != nullptr && a->groups <= 0) return -1;
   if (a->row_offsets == nullptr && a->tiles_m != (a->M + kBM - 1) / kBM) return -1;
   return launch(*a, variant, stream);

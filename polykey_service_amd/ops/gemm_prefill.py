@@ -20,10 +20,11 @@ from . import native
 
 BM = 256
 BN = 256
-# 4: ping-pong quadrant phases with three LDS-DMA pieces in flight (csrc/kernels/gemm_prefill.hip;
-# the slower round-2 variants 0-3 and the equal round-4 4-wave kernel 6-17 are deleted:
-# profiles/r2_prefill_gemm_lab.txt, profiles/r4_prefill_gemm_4wave.md)
-VARIANT = 4
+# 6: the 4-wave, one-wave-per-SIMD kernel (AGPR accumulators, BK 64; K % 128 == 0), 4: the 8-wave
+# ping-pong kernel (the fallback for K % 128 != 0) -- csrc/kernels/gemm_prefill.hip; same process
+# vs 4: QKV +8 %, gate_up +3.5 %, O +6 %, down 0, Mixtral w13 +2.5 %, w2 -2.6 %
+# (profiles/r4_prefill_gemm_4wave.md); hipBLASLt is still 17-23 % faster on the dense shapes
+VARIANT = 6
 
 
 class PrefillGemmArgs(ctypes.Structure):
@@ -53,8 +54,10 @@ def _launch(a: PrefillGemmArgs, variant: Optional[int] = None) -> None:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         f.restype = ctypes.c_int
         _checked = True
-    native.check(lib.pk_prefill_gemm(ctypes.byref(a), VARIANT if variant is None else variant, native.stream_ptr()),
-                 "pk_prefill_gemm")
+    v = VARIANT if variant is None else variant
+    if v >= 6 and a.K % 128:
+        v -= 2  # the 8-wave kernel needs only K % 64 == 0
+    native.check(lib.pk_prefill_gemm(ctypes.byref(a), v, native.stream_ptr()), "pk_prefill_gemm")
 
 
 def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
@@ -66,8 +69,8 @@ def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
     return y.to(x.dtype)
 
 
-# the same kernel reading the decode GEMM's block-packed W
-PACKED_VARIANT = 5
+# the same kernels reading the decode GEMM's block-packed W
+PACKED_VARIANT = 7
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, silu: bool = False,
@@ -95,7 +98,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
     if (not supported(N, K) or x.stride(1) != 1 or not src.is_contiguous() or out.stride(1) != 1
             or (packed is not None and (K % 128 or tuple(packed.shape) != (N, K)))):
         raise ValueError(f"prefill GEMM: unsupported shape/layout M={M} N={N} K={K}")
-    if packed is not None:
+    if packed is not None and variant not in (5, 7):
         variant = PACKED_VARIANT
     a = PrefillGemmArgs()
     a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), src.data_ptr()

@@ -13,11 +13,12 @@ def rnd(*shape, scale=1.0):
     return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
 
 
+@pytest.mark.parametrize("variant", [4, 6])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 4096), (1000, 768, 1024), (4100, 1280, 8192),
                                    (8192, 4096, 4096), (77, 256, 14336)])
-def test_dense(M, N, K):
+def test_dense(M, N, K, variant):
     x, w = rnd(M, K), rnd(N, K, scale=0.02)
-    y = gemm_prefill.linear(x, w)
+    y = gemm_prefill.linear(x, w, variant=variant)  # 6 falls back to 4 for K % 128
     exp = x.float() @ w.float().t()
     torch.testing.assert_close(y.float(), exp, atol=2e-2, rtol=2e-2)
 
@@ -32,26 +33,28 @@ def test_dense_strided_out_and_input():
     assert torch.count_nonzero(out_full[:, 512:]) == 0
 
 
+@pytest.mark.parametrize("variant", [4, 6])
 @pytest.mark.parametrize("M,I,K", [(513, 512, 4096), (256, 14336, 4096)])
-def test_silu_epilogue(M, I, K):
+def test_silu_epilogue(M, I, K, variant):
     x = rnd(M, K)
     g, u = rnd(I, K, scale=0.05), rnd(I, K, scale=0.05)
     w = gemm.interleave_gate_up(g, u)
-    y = gemm_prefill.linear(x, w, silu=True)
+    y = gemm_prefill.linear(x, w, silu=True, variant=variant)
     bf = lambda t: t.to(torch.bfloat16).float()
     exp = bf(torch.nn.functional.silu(bf(x.float() @ g.float().t()))) * bf(x.float() @ u.float().t())
     torch.testing.assert_close(y.float(), exp, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("variant", [4, 6])
 @pytest.mark.parametrize("silu", [False, True])
-def test_grouped(silu):
+def test_grouped(silu, variant):
     G, N, K = 6, 512, 1024
     counts = [300, 0, 17, 256, 513, 1]
     T = sum(counts) + 5  # 5 trailing rows belong to no group
     offs = torch.tensor([0] + torch.tensor(counts).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
     x, w = rnd(T, K), rnd(G, N, K, scale=0.03)
     out = torch.full((T, N // 2 if silu else N), 7.0, dtype=torch.bfloat16, device="cuda")
-    gemm_prefill.grouped_linear(x, w, offs, silu=silu, out=out)
+    gemm_prefill.grouped_linear(x, w, offs, silu=silu, out=out, variant=variant)
     exp = gemm_prefill.grouped_linear(x.cpu(), w.cpu(), offs.cpu(), silu=silu)
     lo = 0
     for e, c in enumerate(counts):
@@ -60,14 +63,15 @@ def test_grouped(silu):
     assert torch.all(out[lo:] == 7.0)  # rows past the last group are never written
 
 
+@pytest.mark.parametrize("variant", [4, 6])
 @pytest.mark.parametrize("packed", [False, True])
-def test_repeatable_bitwise(packed):
+def test_repeatable_bitwise(packed, variant):
     """Race screen for the LDS-DMA pipeline (guide §5: an early read passes reference checks
     whenever the DMA happens to land first): repeated launches on a busy chip give identical
     bits, and match the fp32 reference to rounding."""
     x, w = rnd(2048, 4096), rnd(2560, 4096, scale=0.02)
     kw = {"packed": gemm.pack_weight(w)} if packed else {}
-    ys = [gemm_prefill.linear(x, w, **kw) for _ in range(6)]
+    ys = [gemm_prefill.linear(x, w, variant=variant + int(packed), **kw) for _ in range(6)]
     for y in ys[1:]:
         assert torch.equal(y, ys[0])
     torch.testing.assert_close(ys[0].float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
@@ -76,8 +80,8 @@ def test_repeatable_bitwise(packed):
 @pytest.mark.parametrize("M,N,K,silu", [(300, 512, 4096, False), (4100, 1280, 8192, False), (513, 1024, 4096, True),
                                         (256, 256, 128, False), (700, 512, 256, True)])
 def test_block_packed_weights(M, N, K, silu):
-    """The decode GEMM's block-packed layout read directly (variant 5): same result as the
-    row-major weight through the row-major kernel."""
+    """The decode GEMM's block-packed layout read directly (variant 7, 5 where K % 128): same
+    result as the row-major weight through the row-major kernel."""
     x, w = rnd(M, K), rnd(N, K, scale=0.02)
     wp = gemm.pack_weight(w)
     y = gemm_prefill.linear(x, torch.empty(N, K, dtype=torch.bfloat16, device="meta"), packed=wp, silu=silu)
@@ -85,6 +89,36 @@ def test_block_packed_weights(M, N, K, silu):
     torch.testing.assert_close(y.float(), ref.float(), atol=1e-2, rtol=1e-2)
     if not silu:
         torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("variant", [6, 7])
+@pytest.mark.parametrize("silu", [False, True])
+def test_four_wave_kernel(variant, silu):
+    """The 4-wave kernel (AGPR accumulators from inline-asm MFMAs): grouped with ragged expert
+    counts (6, row-major W) or dense over the block-packed W (7), every k-tile of K = 4096 (the
+    steady loop and the tail schedule), against the 8-wave kernel and fp32 matmuls."""
+    E, N, K = 4, 1024, 4096
+    counts = [700, 0, 1300, 257]
+    T = sum(counts)
+    offs = torch.tensor([0] + torch.tensor(counts).cumsum(0).tolist(), dtype=torch.int32, device="cuda")
+    x, w = rnd(T, K), rnd(E, N, K, scale=0.02)
+    if variant % 2 == 0:
+        y = gemm_prefill.grouped_linear(x, w, offs, silu=silu, variant=variant)
+        ref = gemm_prefill.grouped_linear(x, w, offs, silu=silu, variant=4)
+    else:
+        meta = torch.empty(N, K, dtype=torch.bfloat16, device="meta")
+        wp = gemm.pack_weight(w[0])
+        y = gemm_prefill.linear(x, meta, packed=wp, silu=silu, variant=variant)
+        ref = gemm_prefill.linear(x, meta, packed=wp, silu=silu, variant=5)
+        counts, w = [T], w[:1]
+    torch.testing.assert_close(y.float(), ref.float(), atol=1e-2, rtol=1e-2)
+    if not silu:
+        lo = 0
+        for e, c in enumerate(counts):
+            if c:
+                exp = x[lo:lo + c].float() @ w[e].float().t()
+                torch.testing.assert_close(y[lo:lo + c].float(), exp, atol=2e-2, rtol=2e-2)
+            lo += c
 
 
 def test_native_library_has_prefill_gemm():

@@ -1,5 +1,5 @@
 """A/B of two prefill GEMM variants in one process, alternating, median of rounds (guide §5.4:
-compare schedules in one process on random data).  python tools/prefill_gemm_ab.py [va] [vb] (default: variant 4 against itself, plus the hipBLASLt column)"""
+compare schedules in one process on random data).  python tools/prefill_gemm_ab.py [va] [vb] (default: the 8-wave kernel 4 against the 4-wave kernel 6, plus the hipBLASLt column)"""
 import json
 import os
 import statistics
@@ -24,7 +24,7 @@ def t(fn, reps=10):
 
 
 def main():
-    va, vb = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (4, 4)
+    va, vb = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (4, 6)
     torch.manual_seed(0)
     dev = "cuda"
     cases = []
