@@ -9,6 +9,6 @@ tail -2 gpurun_out/pg5_tests.log
 timeout -k 10 200 python -u tools/pg_probe.py ${PV:-4 5} > gpurun_out/pg5_probe.jsonl 2>&1 || { tail -20 gpurun_out/pg5_probe.jsonl; exit 1; }
 grep '^{' gpurun_out/pg5_probe.jsonl
 for v in ${ABL:-}; do
-  POLYKEY_LIB_LIBPK_KERNELS=$PWD/tools/lab/libpk_kernels_$v.so timeout -k 10 120 python -u tools/pg_probe.py 4 >> gpurun_out/pg5_probe.jsonl 2>&1 || { tail -20 gpurun_out/pg5_probe.jsonl; exit 1; }
+  POLYKEY_LIB_LIBPK_KERNELS=$PWD/tools/lab/libpk_kernels_$v.so timeout -k 10 120 python -u tools/pg_probe.py ${ABLV:-6} >> gpurun_out/pg5_probe.jsonl 2>&1 || { tail -20 gpurun_out/pg5_probe.jsonl; exit 1; }
 done
 grep '^{' gpurun_out/pg5_probe.jsonl | tail -2
