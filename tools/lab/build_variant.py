@@ -30,30 +30,9 @@ VARIANTS = {
     # at gate_up), A loads only ("pg_aonly", 1,287 vs 1,497), no vmcnt waits ("pg_novm", no change),
     # no fragment reads ("pg_nords", -7 %), no barrier ("pg_nobar", no change), full 128-byte lines
     # per row ("pg_fullline", -5.6 %)
-    # the 4-wave prefill GEMM's 16 LDS-DMA loads of a tile: all issued right after the barrier
-    # ("pg_front"), or 4 per group in the first 4 groups ("pg_first4"), instead of 2 per group
-    "pg_front": [
-        ("gemm_prefill.hip", """    const int ao = a_off(un & 1), wo = w_off(un & 1);
-    __builtin_amdgcn_sched_barrier(0);""", """    const int ao = a_off(un & 1), wo = w_off(un & 1);
-    if constexpr (LOAD) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) stage_one(j, (u + 3) >> 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);"""),
-        ("gemm_prefill.hip", """      if constexpr (LOAD) {
-        stage_one(2 * mf, (u + 3) >> 1);
-        stage_one(2 * mf + 1, (u + 3) >> 1);
-      }""", "")],
-    "pg_first4": [
-        ("gemm_prefill.hip", """      if constexpr (LOAD) {
-        stage_one(2 * mf, (u + 3) >> 1);
-        stage_one(2 * mf + 1, (u + 3) >> 1);
-      }""", """      if constexpr (LOAD) {
-        if (mf < 4) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) stage_one(4 * mf + q, (u + 3) >> 1);
-        }
-      }""")],
+    # the 4-wave prefill GEMM's 16 LDS-DMA loads of a tile, measured at gate_up against 2 per group
+    # (1,453 us): all right after the barrier ("pg_front") 1,535, 4 per group in the first 4 groups
+    # ("pg_first4") 1,443 (noise) -- profiles/r4_prefill_gemm_4wave.md
     # measured and removed this round (variant builds of the sources of that time): "mlp_v0" (no NT /
     # LDS prefetch in the down tiles: 4.063 vs 4.063 ms per graph-captured 8B step), "o_ring2" (the
     # o-projection without whole-slice weight registers: 3.997 vs 4.063 ms) -- profiles/r4_variant_ab.jsonl
