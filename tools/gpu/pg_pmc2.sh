@@ -7,7 +7,7 @@ mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 pass() {  # $1 tag, rest: counters
   local tag=$1; shift
-  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d /tmp/pmc_$tag -- python3 $R/tools/pg_pmc_driver.py 4 \
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d /tmp/pmc_$tag -- python3 $R/tools/pg_pmc_driver.py 4 6 \
     > /tmp/pmc_$tag.log 2>&1 || { tail -30 /tmp/pmc_$tag.log > $R/gpurun_out/pg_pmc_$tag.err; tail -5 /tmp/pmc_$tag.log; return 1; }
   python3 $R/tools/pmc_summary.py /tmp/pmc_$tag $R/gpurun_out/pg_pmc_$tag.md > /dev/null || return 1
   cat $R/gpurun_out/pg_pmc_$tag.md
