@@ -78,8 +78,12 @@ def parse_args(argv=None):
                          "'Llama-3-8B TP=1 / 70B TP=8'); auto: llama3-70b when --model is llama3-8b (the "
                          "BASELINE pair), else none; 'none' skips it")
     ap.add_argument("--tp-extra-timeout", type=float, default=480.0,
-                    help="seconds the TP child may take (its failure or timeout never loses the main number)")
+                    help="seconds the TP child may take at most (its failure or timeout never loses the main number)")
     ap.add_argument("--child-timeout", type=float, default=1500.0, help="seconds the main measurement child may take")
+    ap.add_argument("--deadline", type=float, default=float(os.environ.get("POLYKEY_BENCH_DEADLINE_S", "540")),
+                    help="N > 1: seconds the whole run may take, below the driver's 600 s command limit. The main "
+                         "child gets at most this minus a print margin, the TP child only what is left, so the "
+                         "JSON line is always printed in time")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)  # internal: the measuring torchrun job
     return ap.parse_args(argv)
 
@@ -145,8 +149,15 @@ def orchestrate(args, argv) -> int:
     ranks exit without touching a GPU).  The measurement runs as a fresh N-rank torchrun child
     whose JSON line is relayed; with ``--tp 1`` a second child then measures ``--tp-extra-model``
     at TP = N (70B TP=8 on an 8-GPU node) under the extra key ``tp{N}_<model>``.  Each child has
-    its own timeout, so a TP failure can never erase the replica number."""
-    rc, main_line, _ = run_child(argv + ["--child"], args.gpus, args.child_timeout)
+    its own timeout, so a TP failure can never erase the replica number, and both live inside ONE
+    ``--deadline``: the TP child gets only what the main child left (a hung TP child is killed in
+    time for the line to be printed before the driver's own limit)."""
+    t_start = time.monotonic()
+
+    def left() -> float:  # seconds a child may still take, keeping a margin to print the line
+        return args.deadline - (time.monotonic() - t_start) - 10.0
+
+    rc, main_line, _ = run_child(argv + ["--child"], args.gpus, max(1.0, min(args.child_timeout, left())))
     if main_line is None:
         print(f"bench: measurement child failed (rc {rc})", file=sys.stderr)
         return rc or 1
@@ -157,7 +168,13 @@ def orchestrate(args, argv) -> int:
         key = f"tp{args.gpus}_" + {"llama3-70b": "70b", "llama3-8b": "8b"}.get(extra, extra)
         targv = _strip(argv, {"--model", "--tp", "--ep", "--frontend", "--tp-extra-model"}) + [
             "--model", extra, "--tp", str(args.gpus), "--tp-extra-model", "none", "--child"]
-        trc, tl, wall = run_child(targv, args.gpus, args.tp_extra_timeout)
+        budget = min(args.tp_extra_timeout, left())
+        if budget < 30.0:
+            main_line[key] = {"error": f"TP child skipped: {max(budget, 0.0):.0f} s left of the "
+                                       f"{args.deadline:.0f} s deadline"}
+            print(json.dumps(main_line), flush=True)
+            return 0
+        trc, tl, wall = run_child(targv, args.gpus, budget)
         if tl is not None:
             main_line[key] = {k: tl.get(k) for k in ("value", "unit", "p50_e2e_latency_ms", "ms_per_step", "steps",
                                                      "warmup", "scaling")}
@@ -165,7 +182,7 @@ def orchestrate(args, argv) -> int:
                                   global_batch=tl["config"]["global_batch"], init_s=tl["config"].get("init_s"),
                                   wall_s=round(wall, 1))
         else:
-            main_line[key] = {"error": f"TP child rc {trc}" + (" (timeout)" if trc == 124 else ""),
+            main_line[key] = {"error": f"TP child rc {trc}" + (f" (timeout after {budget:.0f} s)" if trc == 124 else ""),
                               "wall_s": round(wall, 1)}
     print(json.dumps(main_line), flush=True)
     return 0
@@ -376,6 +393,10 @@ def main(argv=None) -> int:
     if dist.is_initialized():
         dist.barrier()
     init_s = time.perf_counter() - t_init
+    from polykey_service_amd.utils import test_hooks
+    if test_hooks.get("POLYKEY_BENCH_HANG") == "tp" and st.tp_size > 1:
+        while True:  # a hung TP child (tests: the orchestrator's deadline must still print the line)
+            time.sleep(60)
     leaders = list(range(0, st.world_size, st.tp_size))
     leaders_group = dist.new_group(leaders) if dist.is_initialized() else None
     dp_front = st.world_size > 1 and st.tp_size == 1 and not engine.lockstep

@@ -301,7 +301,7 @@ def attach_models(router, cfg, logger) -> ModelSet:
 
     import torch
 
-    from ..engine.async_llm import AsyncLLM
+    from ..engine.async_llm import AsyncLLM, device_guard
     from ..engine.llm_engine import EngineConfig, LLMEngine
     from ..parallel.state import ParallelState
     entries = parse_serve_models(cfg.serve_models)
@@ -311,14 +311,21 @@ def attach_models(router, cfg, logger) -> ModelSet:
     llms = {}
     for name, devs in entries:
         if not devs:
-            devs = [next(free, 0)]
+            d = next(free, None)
+            if d is None and n_dev:
+                raise ValueError(f"model {name!r} has no device left: every GPU of this node is taken "
+                                 f"({cfg.serve_models!r}); give it one with '@<gpu>'")
+            devs = [d or 0]
         engines = []
         for d in devs:
             if n_dev and d >= n_dev:
                 raise ValueError(f"model {name!r} asks for GPU {d}; this node has {n_dev}")
             dev = torch.device(f"cuda:{d}") if n_dev else torch.device("cpu")
             ecfg = _dc.replace(EngineConfig.from_server_config(_dc.replace(cfg, model=name)), device=str(dev))
-            engines.append(LLMEngine(ecfg, ParallelState(device=dev)))
+            # the engine's weights, KV cache and warm-up launches on ITS device (the native ops
+            # launch on the thread's current device); its AsyncLLM thread binds the same device
+            with device_guard(dev):
+                engines.append(LLMEngine(ecfg, ParallelState(device=dev)))
         llm = AsyncLLM(engines[0]) if len(engines) == 1 else ReplicaPool([AsyncLLM(e) for e in engines])
         attach_local_llm(router, _dc.replace(cfg, model=name), logger, engine=engines[0], llm=llm)
         llms[name] = llm
@@ -340,13 +347,15 @@ def attach_local_llm(router, cfg, logger, engine=None, llm=None):
 
         import torch
 
+        from ..engine.async_llm import device_guard
         from ..parallel.state import ParallelState
         n = cfg.replicas
         engines = []
         for i in range(n):
             dev = torch.device(f"cuda:{i}") if torch.cuda.is_available() else torch.device("cpu")
             ecfg = _dc.replace(EngineConfig.from_server_config(cfg), device=str(dev))
-            engines.append(LLMEngine(ecfg, ParallelState(device=dev)))
+            with device_guard(dev):
+                engines.append(LLMEngine(ecfg, ParallelState(device=dev)))
         llm = ReplicaPool([AsyncLLM(e) for e in engines])
         engine = engines[0]
     else:

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import contextlib
 import os
 import sys
 import threading
@@ -26,6 +27,25 @@ from .sequence import RequestOutput, SamplingParams
 
 class EngineDeadError(RuntimeError):
     pass
+
+
+def bind_device(dev) -> None:
+    """Make ``dev`` the calling thread's current HIP device (no-op for CPU / None)."""
+    if dev is not None and getattr(dev, "type", None) == "cuda":
+        import torch
+        torch.cuda.set_device(dev)
+
+
+@contextlib.contextmanager
+def device_guard(dev):
+    """``torch.cuda.device(dev)`` for a CUDA ``dev``, nothing otherwise: build an engine on a GPU
+    other than the thread's current one (its native launches go to the current device)."""
+    if dev is not None and getattr(dev, "type", None) == "cuda":
+        import torch
+        with torch.cuda.device(dev):
+            yield
+    else:
+        yield
 
 
 class AsyncLLM:
@@ -285,6 +305,10 @@ class AsyncLLM:
 
     def _run(self) -> None:
         eng = self.engine
+        # the HIP device is per thread: every native launch of this engine (ops/native.py, current
+        # stream of the current device) must target the engine's GPU, not cuda:0 (several
+        # engines of one process on different GPUs: attach_models / ReplicaPool)
+        bind_device(getattr(eng, "device", None))
         prof = self._profiler()
         try:
             while True:

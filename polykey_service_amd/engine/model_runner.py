@@ -128,7 +128,8 @@ class ModelRunner:
         self.short_ctx = attn_ops._PART if cfg.max_model_len > attn_ops._PART else 0
         self.graph_pool = None
         a0 = model.layers[0].attn
-        self.part_o, self.part_ml = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks, self.bs, device)
+        self.part_o, self.part_ml = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks, self.bs, device,
+                                                              kv_heads=a0.nkv)
         self.stats = {"steps": 0, "graph_steps": 0, "short_graph_steps": 0, "tokens": 0}
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None

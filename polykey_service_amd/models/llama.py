@@ -43,6 +43,7 @@ from ..ops import moe as moe_ops
 from ..ops import reference
 from ..parallel import comm
 from ..parallel.state import ParallelState, get_state
+from ..utils import test_hooks
 from .config import ModelConfig
 from .weights import SafetensorsIndex, random_full, random_shard, shard_cols, shard_rows
 
@@ -216,8 +217,9 @@ class LlamaForCausalLM(nn.Module):
         self.vocab_start = self.st.tp_rank * self.vocab_local
         self.layers = nn.ModuleList([LlamaLayer(cfg, self.st, self._make_mlp(i)) for i in range(cfg.num_layers)])
         # POLYKEY_FAULT_DROP_PARTIAL=<layer>,<tp rank>: a deliberately wrong TP model (that rank's
-        # attention partial of that layer is dropped) -- the TP=8 correctness test must fail on it
-        fault = os.environ.get("POLYKEY_FAULT_DROP_PARTIAL")
+        # attention partial of that layer is dropped) -- the TP=8 correctness test must fail on it.
+        # Honoured only with POLYKEY_TEST_HOOKS=1, and logged at ERROR (utils/test_hooks.py)
+        fault = test_hooks.get("POLYKEY_FAULT_DROP_PARTIAL")
         if fault:
             li, rk = (int(v) for v in fault.split(","))
             if rk == self.st.tp_rank and 0 <= li < cfg.num_layers:

@@ -43,14 +43,30 @@ _PART = 512  # must match kDecodePart in csrc/kernels/attention.hip
 _PART_MIN = 128  # kDecodePartSmall: launches whose (seq, kv head) pairs cannot fill the chip
 
 
-def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, device, n_kv: int = 0) -> tuple:
-    """Partition slabs (+ arrival counters when ``n_kv``) for split-K decode attention, sized for
-    the smallest partition a launch may pick (the slab stride is the launch's partition count)."""
-    n_parts = (max_blocks * block_size + _PART_MIN - 1) // _PART_MIN
-    if n_parts <= 1:
+_DECODE_FILL = 256  # kDecodeFill: fewer (seq, kv head, partition) workgroups than this -> 128-key partitions
+
+
+def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, device, n_kv: int = 0,
+                     kv_heads: Optional[int] = None) -> tuple:
+    """Partition slabs (+ arrival counters when ``n_kv``) for split-K decode attention.  A launch
+    strides the slabs by its OWN partition count, so they are sized for the largest launch:
+    ``n_seqs`` sequences at 512-key partitions, or the few sequences that take 128-key ones
+    (csrc attention.hip decode_part: fewer than 256 (seq, kv head) workgroups, i.e. at most
+    255 // kv_heads sequences).  ``kv_heads`` (kv heads per rank; else ``n_kv``) None: every
+    launch sized at 128-key partitions (4x the full-batch need: ~4.3 GB at 256 seqs x 128k ctx
+    for Llama-3-8B, taken from the KV-cache budget -- ADVICE r4)."""
+    ctx = max_blocks * block_size
+    n_small = (ctx + _PART_MIN - 1) // _PART_MIN
+    if n_small <= 1:
         return (None, None, None) if n_kv else (None, None)
-    o = torch.empty((n_seqs, n_q, n_parts, 128), dtype=torch.float32, device=device)
-    ml = torch.empty((n_seqs, n_q, n_parts, 2), dtype=torch.float32, device=device)
+    kvh = kv_heads or n_kv
+    if kvh:
+        seqs_small = min(n_seqs, (_DECODE_FILL - 1) // kvh)
+        rows = max(n_seqs * ((ctx + _PART - 1) // _PART), seqs_small * n_small)
+    else:
+        rows = n_seqs * n_small
+    o = torch.empty((rows * n_q, 128), dtype=torch.float32, device=device)
+    ml = torch.empty((rows * n_q, 2), dtype=torch.float32, device=device)
     if n_kv:
         return o, ml, torch.zeros((n_seqs, n_kv), dtype=torch.int32, device=device)
     return o, ml

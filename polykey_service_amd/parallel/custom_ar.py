@@ -134,6 +134,11 @@ class CustomAllReduce:
         """Shapes the fused decode collective takes (:meth:`reduce_residual`)."""
         return M > 0 and N % 1024 == 0 and M * N * 2 <= self.max_bytes
 
+    def nparts(self, M: int, N: int) -> int:
+        """Rows of the norm parts :meth:`reduce_residual` writes for an [M, N] residual: N / 256
+        (two-shot form) or N / 1024 (one-shot)."""
+        return int(self.lib.pk_car_reduce_residual_nparts(self.ctx, M, N))
+
     def reduce_residual(self, pending, residual: torch.Tensor, parts: torch.Tensor) -> torch.Tensor:
         """Fused TP collective of a row-parallel decode projection, one launch: this rank's
         split-K slabs (a :class:`~polykey_service_amd.ops.gemm.Partial`) or bf16 partial [M, N]

@@ -19,7 +19,9 @@ one-rank-per-GPU run on a new node is diagnosable from its log alone.
 from __future__ import annotations
 
 import json
+import os
 import sys
+import threading
 import time
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -72,25 +74,40 @@ def check_rccl(rc, rank: int, world: int, dev: torch.device) -> Dict[str, bool]:
     return out
 
 
+def reduce_residual_widths(world: int) -> List[int]:
+    """Residual widths that drive every form of the fused collective: 1024 columns (one-shot for
+    W < 4 and for W > 4, whose two-shot needs 256 W-column chunk groups) and the smallest
+    multiple of 1024 that holds 256 W columns (two-shot from W = 4; 2048 at W = 8 -- the form a
+    70B TP=8 decode step takes)."""
+    two = -(-256 * world // 1024) * 1024
+    return [1024] if two == 1024 else [1024, two]
+
+
 def check_custom_ar(car, rank: int, world: int, dev: torch.device) -> Dict[str, bool]:
-    """The IPC all-gather and the fused decode collective (reduce_residual) of custom_ar."""
+    """The IPC all-gather and the fused decode collective (reduce_residual, one-shot and two-shot
+    forms: parts per 1024 / 256 columns, sized by ``car.nparts``) of custom_ar."""
     out = {}
     x = _pattern(rank, 4 * 64, device=dev, salt=3).view(4, 64)
     if car.supports_gather(x):
         g = car.all_gather_last(x)
         _sync(dev)
         out["all_gather_1shot"] = _close(g, torch.cat([_pattern(r, 256, salt=3).view(4, 64) for r in range(world)], -1))
-    M, N = 2, 1024
-    if car.supports_reduce_residual(M, N):
+    M = 2
+    for N in reduce_residual_widths(world):
+        if not car.supports_reduce_residual(M, N):
+            continue
+        nparts = car.nparts(M, N)
         part = _pattern(rank, M * N, device=dev, salt=4).view(M, N)
         res0 = _pattern(0, M * N, salt=5).view(M, N)
         residual = res0.to(dev).clone()
-        parts = torch.zeros((N // 1024) * M, dtype=torch.float32, device=dev)
+        parts = torch.zeros(nparts * M, dtype=torch.float32, device=dev)
         p = car.reduce_residual(part.contiguous(), residual, parts)
         _sync(dev)
         want = res0.float() + sum(_pattern(r, M * N, salt=4).view(M, N).float() for r in range(world))
-        out["reduce_residual"] = _close(residual, want.to(torch.bfloat16)) and bool(
-            torch.allclose(p.float().cpu(), want.pow(2).sum(-1).view(1, M), rtol=1e-5))
+        want_parts = want.view(M, nparts, N // nparts).pow(2).sum(-1).t()
+        form = "2shot" if N // nparts == 256 else "1shot"
+        out[f"reduce_residual_{form}_{N}"] = _close(residual, want.to(torch.bfloat16)) and tuple(p.shape) == (
+            nparts, M) and bool(torch.allclose(p.float().cpu(), want_parts, rtol=1e-5))
     return out
 
 
@@ -134,6 +151,55 @@ def _safe(fn: Callable[[], Dict[str, bool]]) -> Tuple[Dict[str, bool], Optional[
         return {}, f"{type(e).__name__}: {e}"
 
 
+# A check that has not returned after HANG_S seconds is hung (a collective whose peer never
+# arrives, a device sync on a kernel that never ends).  The watchdog then records it, emits the
+# report line at once (the log names the hung path even if nothing after it ever runs) and
+# aborts the path (ncclCommAbort / the custom all-reduce's sticky error word), which makes the
+# collective return; the check is failed and the group vote disables the path on every rank.
+# A check still stuck GRACE_S after the abort ends the process: the line is printed again with
+# "exit" and the process exits with HANG_EXIT -- never a silent hang, never an exec.
+HANG_S = float(os.environ.get("POLYKEY_PREFLIGHT_HANG_S", "30"))
+GRACE_S = float(os.environ.get("POLYKEY_PREFLIGHT_GRACE_S", "15"))
+HANG_EXIT = 75
+
+
+def _guarded(name: str, fn: Callable[[], Dict[str, bool]], abort: Callable[[], None], report: dict,
+             emit: Callable[[str], None], hang_s: Optional[float] = None,
+             grace_s: Optional[float] = None) -> Tuple[Dict[str, bool], Optional[str]]:
+    """:func:`_safe` of ``fn`` under the hang watchdog (see HANG_S)."""
+    hang_s = HANG_S if hang_s is None else hang_s
+    grace_s = GRACE_S if grace_s is None else grace_s
+    done = threading.Event()
+    hung = threading.Event()
+
+    def watch():
+        if done.wait(hang_s):
+            return
+        hung.set()
+        report.setdefault("hung", []).append(name)
+        emit(json.dumps(report))
+        try:
+            abort()
+        except Exception as e:  # noqa: BLE001 - the exit below is the backstop
+            report.setdefault("abort_errors", {})[name] = f"{type(e).__name__}: {e}"
+        if done.wait(grace_s):
+            return
+        report["exit"] = f"check {name!r} still hung {grace_s:.0f} s after its abort"
+        emit(json.dumps(report))
+        os._exit(HANG_EXIT)
+
+    t = threading.Thread(target=watch, name=f"pk-preflight-watch-{name}", daemon=True)
+    t.start()
+    try:
+        res, err = _safe(fn)
+    finally:
+        done.set()
+    t.join()
+    if hung.is_set():
+        return res, f"hung: no result within {hang_s:.0f} s (path aborted)" + (f"; {err}" if err else "")
+    return res, err
+
+
 def peer_access(st: ParallelState) -> Optional[List[List[int]]]:
     """Row r: can rank r's device read each rank's device (hipDeviceCanAccessPeer)?  None when
     the ranks do not all see each other's devices (per-rank visibility) or run on the CPU."""
@@ -158,9 +224,13 @@ def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit:
     t0 = time.perf_counter()
     report = {"event": "multi_gpu_preflight", "rank": st.rank, "world": st.world_size, "backend": st.backend,
               "ranks_per_device": st.ranks_per_device, "checks": {}, "disabled": []}
+    emit = emit or (lambda s: print(s, file=sys.stderr, flush=True))
     if "rccl" in paths or "custom_ar" in paths:
         report["peer_access"] = peer_access(st)
     dev = st.device
+
+    def _abort(obj, method):
+        return lambda: getattr(obj, method)() if obj is not None and hasattr(obj, method) else None
 
     def verdict(name, res, err, group, world, disable):
         ok = bool(res) and all(res.values()) and err is None
@@ -172,7 +242,9 @@ def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit:
             report["disabled"].append(name)
 
     if "rccl" in paths and st.rccl_tp is not None and st.tp_size > 1:
-        res, err = _safe(lambda: check_rccl(st.rccl_tp, st.tp_rank, st.tp_size, dev))
+        rc = st.rccl_tp
+        res, err = _guarded("rccl_tp", lambda: check_rccl(rc, st.tp_rank, st.tp_size, dev), _abort(rc, "abort"),
+                            report, emit)
 
         def off_tp():
             if st.rccl_ep is st.rccl_tp:
@@ -180,11 +252,14 @@ def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit:
             st.rccl_tp = None
         verdict("rccl_tp", res, err, st.tp_cpu_group, st.tp_size, off_tp)
     if "rccl" in paths and st.rccl_ep is not None and st.rccl_ep is not st.rccl_tp and st.ep_size > 1:
-        res, err = _safe(lambda: check_rccl(st.rccl_ep, st.ep_rank, st.ep_size, dev))
+        rce = st.rccl_ep
+        res, err = _guarded("rccl_ep", lambda: check_rccl(rce, st.ep_rank, st.ep_size, dev), _abort(rce, "abort"),
+                            report, emit)
         verdict("rccl_ep", res, err, st.ep_cpu_group, st.ep_size, lambda: setattr(st, "rccl_ep", None))
     if "custom_ar" in paths and st.custom_ar is not None:
         car = st.custom_ar
-        res, err = _safe(lambda: check_custom_ar(car, st.tp_rank, st.tp_size, dev))
+        res, err = _guarded("custom_ar", lambda: check_custom_ar(car, st.tp_rank, st.tp_size, dev),
+                            _abort(car, "fail"), report, emit)
 
         def off_car():
             car.close()
@@ -192,7 +267,8 @@ def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit:
         verdict("custom_ar", res, err, st.tp_cpu_group, st.tp_size, off_car)
     if "ep_ipc" in paths and st.ep_a2a is not None:
         a2a = st.ep_a2a
-        res, err = _safe(lambda: check_ep_ipc(a2a, st.ep_rank, st.ep_size, dev))
+        res, err = _guarded("ep_ipc", lambda: check_ep_ipc(a2a, st.ep_rank, st.ep_size, dev), _abort(a2a, "fail"),
+                            report, emit)
 
         def off_ep():
             for x in (st.ep_a2a, st.ep_a2a_prefill):
@@ -202,6 +278,5 @@ def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit:
         verdict("ep_ipc", res, err, st.ep_cpu_group, st.ep_size, off_ep)
     report["seconds"] = round(time.perf_counter() - t0, 3)
     if st.rank == 0 or report["disabled"] or any(not c["ok"] for c in report["checks"].values()):
-        line = json.dumps(report)
-        (emit or (lambda s: print(s, file=sys.stderr, flush=True)))(line)
+        emit(json.dumps(report))
     return report

@@ -92,3 +92,26 @@ def test_bench_world8_reports_tp_child():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["value"] > 0 and "error" in out["tp8_no-such-model"]
+
+
+def test_bench_world8_hung_tp_child_meets_the_deadline():
+    """a TP child that hangs (test hook) is killed inside the ONE --deadline,
+    and the main JSON line -- the replica number plus the TP key's error -- is printed before it."""
+    import time
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               POLYKEY_TEST_HOOKS="1", POLYKEY_BENCH_HANG="tp")
+    deadline = 150
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8", "--master-addr",
+           "127.0.0.1", "--master-port", "0", os.path.join(REPO, "bench.py"), "--gpus", "8", "--model",
+           "tiny-llama-g8", "--steps", "1", "--warmup", "1", "--concurrency", "2", "--prompt-len", "8",
+           "--max-tokens", "3", "--no-graphs", "--tp-extra-model", "tiny-llama-g8", "--deadline", str(deadline)]
+    t0 = time.monotonic()
+    r = _run(cmd, REPO, env, timeout=deadline + 120)
+    wall = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["value"] > 0 and out["config"]["parallelism"] == "dp8"
+    assert "timeout" in out["tp8_tiny-llama-g8"]["error"], out["tp8_tiny-llama-g8"]
+    assert wall < deadline + 30, wall  # torchrun's own teardown aside, the line came within the deadline

@@ -60,6 +60,7 @@ class FakeCar:
 
     def __init__(self, group, world):
         self.g, self.world, self.closed = group, world, False
+        self.forms = set()
 
     def supports_gather(self, x):
         return True
@@ -72,13 +73,21 @@ class FakeCar:
     def supports_reduce_residual(self, M, N):
         return N % 1024 == 0
 
+    def nparts(self, M, N):
+        # csrc/comm/custom_allreduce.hip pk_car_reduce_residual_nparts: two-shot (parts per 256
+        # columns) from 4 ranks when 256-column chunk groups tile N, else one-shot (per 1024)
+        return N // 256 if self.world >= 4 and N % (256 * self.world) == 0 else N // 1024
+
     def reduce_residual(self, pending, residual, parts):
         s = pending.float().clone()
         dist.all_reduce(s, group=self.g)
         residual.copy_((residual.float() + s).to(residual.dtype))
         M, N = residual.shape
-        pv = parts.view(-1)[: (N // 1024) * M].view(N // 1024, M)
-        pv.copy_(residual.float().view(M, N // 1024, 1024).pow(2).sum(-1).t())
+        n = self.nparts(M, N)
+        assert parts.numel() >= n * M  # the real reduce_residual's check
+        pv = parts.view(-1)[: n * M].view(n, M)
+        pv.copy_(residual.float().view(M, n, N // n).pow(2).sum(-1).t())
+        self.forms.add("2shot" if N // n == 256 else "1shot")
         return pv
 
     def close(self):
@@ -96,9 +105,107 @@ def _worker(rank, world, port, out, faulty_rank):
     lines = []
     rep = preflight.run(st, emit=lines.append)
     torch.save({"report": rep, "lines": lines, "rccl": st.rccl_tp is not None, "car": st.custom_ar is not None,
-                "car_closed": car.closed}, f"{out}.{rank}")
+                "car_closed": car.closed, "forms": sorted(car.forms)}, f"{out}.{rank}")
     st.rccl_tp = st.custom_ar = None
     destroy_parallel()
+
+
+class SlowComm(GlooComm):
+    """A collective whose peer arrives late (a hung RCCL call until the watchdog aborts it)."""
+
+    aborted = False
+
+    def all_reduce(self, x, op="sum", out=None):
+        import time
+        time.sleep(4.0)
+        return super().all_reduce(x, op, out)
+
+    def abort(self):
+        SlowComm.aborted = True
+
+
+def _hang_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), POLYKEY_PREFLIGHT="0")
+    from polykey_service_amd.parallel import preflight
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    preflight.HANG_S = 1.0
+    st = init_parallel(tp=world, device="cpu", backend="gloo")
+    st.rccl_tp = (SlowComm if rank == 1 else GlooComm)(st.tp_cpu_group, world)
+    st.custom_ar = FakeCar(st.tp_cpu_group, world)
+    lines = []
+    rep = preflight.run(st, emit=lines.append)
+    torch.save({"report": rep, "lines": lines, "rccl": st.rccl_tp is not None, "car": st.custom_ar is not None,
+                "aborted": SlowComm.aborted}, f"{out}.{rank}")
+    st.rccl_tp = st.custom_ar = None
+    destroy_parallel()
+
+
+def test_preflight_watchdog_aborts_a_hung_check_and_disables_it(tmp_path):
+    """a direct-RCCL check that does not return within HANG_S (rank 1's
+    all-reduce stalls; rank 0 waits in it) is reported as hung in a line emitted at once, aborted
+    (ncclCommAbort's stand-in), failed, and disabled on BOTH ranks; the healthy path stays."""
+    out = str(tmp_path / "pf")
+    mp.start_processes(_hang_worker, args=(2, _port(), out), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        d = torch.load(f"{out}.{r}", weights_only=True)
+        rep = d["report"]
+        assert rep["hung"] == ["rccl_tp"] and "hung" in rep["checks"]["rccl_tp"]["error"], rep
+        assert rep["disabled"] == ["rccl_tp"] and not d["rccl"] and d["car"], rep
+        assert d["aborted"] == (r == 1)
+        # the first line is the watchdog's (emitted while the check was still stuck)
+        assert json.loads(d["lines"][0])["hung"] == ["rccl_tp"]
+
+
+def test_preflight_watchdog_exits_when_the_abort_does_not_unblock(tmp_path):
+    """A check that stays stuck after its abort: the process prints the report line with "exit"
+    and leaves with HANG_EXIT instead of hanging the job."""
+    import subprocess
+    import sys
+    code = ("import threading, json\n"
+            "from polykey_service_amd.parallel import preflight as p\n"
+            "rep = {'event': 'multi_gpu_preflight'}\n"
+            "p._guarded('rccl_tp', lambda: threading.Event().wait(), lambda: None, rep,\n"
+            "           lambda s: print(s, flush=True), hang_s=0.5, grace_s=0.5)\n"
+            "print('unreachable')\n")
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=60)
+    from polykey_service_amd.parallel.preflight import HANG_EXIT
+    assert r.returncode == HANG_EXIT, (r.returncode, r.stdout, r.stderr)
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines[0]["hung"] == ["rccl_tp"] and "still hung" in lines[-1]["exit"]
+    assert "unreachable" not in r.stdout
+
+
+def _car_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), POLYKEY_PREFLIGHT="0")
+    from polykey_service_amd.parallel import preflight
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    st = init_parallel(tp=world, device="cpu", backend="gloo")
+    car = st.custom_ar = FakeCar(st.tp_cpu_group, world)
+    rep = preflight.run(st, paths=("custom_ar",), emit=lambda s: None)
+    torch.save({"report": rep, "car": st.custom_ar is not None, "forms": sorted(car.forms)}, f"{out}.{rank}")
+    st.custom_ar = None
+    destroy_parallel()
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_preflight_checks_both_forms_of_the_fused_collective(tmp_path, world):
+    """at TP=4 the 1024-column check took the two-shot form with parts sized for the
+    one-shot one, failed its own assert and disabled the custom all-reduce on every rank; at TP=8
+    the two-shot form a 70B decode step uses was never checked.  Both forms now run, each with
+    parts sized by car.nparts, and the path stays enabled."""
+    out = str(tmp_path / "pf")
+    mp.start_processes(_car_worker, args=(world, _port(), out), nprocs=world, join=True, start_method="spawn")
+    for r in range(world):
+        d = torch.load(f"{out}.{r}", weights_only=True)
+        chk = d["report"]["checks"]["custom_ar"]
+        assert chk["ok"] and chk["group_ok"] and d["car"], chk
+        assert d["forms"] == ["1shot", "2shot"] if world == 8 else d["forms"] == ["2shot"], d["forms"]
+        names = {k for k in chk if k.startswith("reduce_residual")}
+        assert names == ({"reduce_residual_1shot_1024", "reduce_residual_2shot_2048"} if world == 8
+                         else {"reduce_residual_2shot_1024"}), names
 
 
 @pytest.mark.parametrize("faulty_rank", [-1, 1])
@@ -109,7 +216,7 @@ def test_preflight_disables_a_faulty_collective_on_every_rank(tmp_path, faulty_r
     for r, d in enumerate(res):
         rep = d["report"]
         assert rep["checks"]["custom_ar"]["ok"] and d["car"] and not d["car_closed"], rep
-        assert set(rep["checks"]["custom_ar"]) >= {"all_gather_1shot", "reduce_residual"}
+        assert set(rep["checks"]["custom_ar"]) >= {"all_gather_1shot", "reduce_residual_1shot_1024"}
         rc = rep["checks"]["rccl_tp"]
         assert rc.get("all_reduce") and rc.get("reduce_scatter") and rc.get("all_to_allv"), rc
         if faulty_rank < 0:

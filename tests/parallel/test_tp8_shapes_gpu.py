@@ -49,6 +49,6 @@ def test_llama3_70b_tp8_shapes_on_one_gpu(tmp_path):
 def test_llama3_70b_tp8_dropped_partial_is_caught(tmp_path):
     """Fault injection: rank 3 drops its attention partial in layer 1 (POLYKEY_FAULT_DROP_PARTIAL);
     every comparison prompt's logits must leave the noise band."""
-    env = dict(os.environ, POLYKEY_FAULT_DROP_PARTIAL="1,3")
+    env = dict(os.environ, POLYKEY_FAULT_DROP_PARTIAL="1,3", POLYKEY_TEST_HOOKS="1")
     res = _rehearse(str(tmp_path / "tp8f"), ["--check-only"], env=env)
     assert res["ref_noise_band"] > 0 and len(res["ref_rows_outside_noise"]) == 4, res
