@@ -214,9 +214,22 @@ struct DecodeLds {
   bf16_t q_s[16][kHD] __attribute__((aligned(16)));
 };
 
+// bf16 store of the attention output; WT: write-through (sc1) -- the output is handed off in-launch
+// to the o-projection tiles of the same launch (decode_fused.hip), which read it with sc1 loads
+template <bool WT>
+__device__ __forceinline__ void st_out(bf16_t* base, int64_t idx, bf16_t v) {
+  if constexpr (WT)
+    __builtin_amdgcn_raw_buffer_store_b16(
+        v, __builtin_amdgcn_make_buffer_rsrc(base, static_cast<short>(0), 0x7ffffff0, 0x00020000),
+        static_cast<int>(idx * 2), 0, 16);
+  else
+    base[idx] = v;
+}
+
 // One decode-attention workgroup (seq = by, kv head = bx, partition = bz of gdz).  FL & 2: the
 // QKV slabs are handed over in-launch (decode_fused.hip): wait on kv head bx's tickets in fin
-// before reading them, and read them with sc1 loads.
+// before reading them, and read them with sc1 loads.  FL & 1: the output is handed over in-launch
+// (to the o-projection tiles): write-through stores; the caller takes the tickets.
 // PRE = 1 / 2 (fused launch): the first partition's first one / two K/V steps per wave are
 // requested before the hand-off wait, so they stream in while the QKV tiles finish.
 template <int kPart, int NW, bool FROM_QKV, int SS = 0, int FL = 0, int PRE = 0>
@@ -275,7 +288,7 @@ __device__ __forceinline__ void decode_tile(
   if (ctx <= 0) {
     if (bz == 0)  // a padded (graph) row -> zeros
       for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW)
-        out[static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD] = 0;
+        st_out<(FL & 1) != 0>(out, static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD, 0);
     return;
   }
   // n_parts comes from the launch's context bound; the clamp keeps a violated bound in-bounds
@@ -456,7 +469,7 @@ __device__ __forceinline__ void decode_tile(
     }
     const int hq = h * G + c;
     if (n_eff == 1) {
-      out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
+      st_out<(FL & 1) != 0>(out, static_cast<int64_t>(seq) * out_stride + hq * kHD + d, f2bf(L > 0.f ? O / L : 0.f));
     } else {
       const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + bz;
       part_o[pi * kHD + d] = O;
@@ -508,7 +521,7 @@ __device__ __forceinline__ void decode_tile(
       O += f * part_o[(base + p) * kHD + d];
       L += f * part_ml[2 * (base + p) + 1];
     }
-    out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
+    st_out<(FL & 1) != 0>(out, static_cast<int64_t>(seq) * out_stride + hq * kHD + d, f2bf(L > 0.f ? O / L : 0.f));
   }
 }
 

@@ -21,6 +21,7 @@
 //     (tools/gemm_lab.hip: LM head 5.1 -> 5.9 TB/s with non-temporal loads).
 #include <cstring>
 
+#include "phase.h"
 #include "skinny_tile.h"
 
 using namespace pk;
@@ -47,13 +48,19 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 // DKR: the down projection's n-block height (2: 128 rows; 1: 64 rows -- twice the tiles at the
 // same split when 128-row tiles would leave CUs idle: 8B 32 x 4, 70B TP=8 64 x 2 -> 256).
 // DNT: non-temporal down weights (A/B builds: tools/lab/build_variant.py)
-template <int MT, bool SPLIT, int DKR, bool DNT = false>
+// RES: the TP = 1 residual update of the o-projection's slabs runs as phase 0 (phase.h res_phase)
+// and the gate_up tiles take their A and row scale from it in-launch (skinny_tile FL & 4).
+template <int MT, bool SPLIT, int DKR, bool DNT = false, bool RES = false>
 __global__ void __launch_bounds__(256, 2) mlp_fused_kernel(const GemmArgs gu, const GemmArgs dn, const Flow fgu,
-                                                           const Flow fdn, int n_gu, int n_dn) {
+                                                           const Flow fdn, int n_gu, int n_dn, const ResArgs ra,
+                                                           const Flow fres, int n_res) {
   __shared__ SkinnyLds<MT> lds;
   const int b = blockIdx.x;
+  if constexpr (RES)
+    if (b < n_res) res_phase(ra, b, fres);
   if (b < n_gu) {
-    skinny_tile<MT, SPLIT ? kSiluSplit : kSiluMul, true, false, true, true, 2, 1>(gu, b, 0, n_gu, lds, fgu);
+    skinny_tile<MT, SPLIT ? kSiluSplit : kSiluMul, true, false, true, true, 2, RES ? 5 : 1>(gu, b, 0, n_gu, lds, fgu,
+                                                                                          fres);
     __syncthreads();  // the LDS tiles are reused by the down tile
   }
   if (b < n_dn) skinny_tile<MT, kPartial, true, false, DNT, false, DKR, 2>(dn, b, 0, n_dn, lds, fdn);
@@ -520,9 +527,17 @@ constexpr int kFlowWords = kFlowCounters + 1024;
 // 128-row tiles at split S would be fewer than 192 workgroups
 static int down_kr(int N, int S) { return (N / 128) * S < 192 ? 1 : 2; }
 
-PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, hipStream_t stream) {
+// res (may be null): the residual update of the previous projection's slabs as phase 0 --
+// gu.A must be res->residual and gu.nrm_parts res->parts (ResArgs, phase.h).
+PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, const ResArgs* res,
+                           hipStream_t stream) {
   GemmArgs gu = *gu_in, dn = *dn_in;
   if (gu.M <= 0) return 0;
+  if (res != nullptr && (res->residual == nullptr || res->parts == nullptr || res->flow == nullptr || res->M != gu.M ||
+                         res->H != gu.K || res->H % kResCols || (res->slabs != nullptr && res->S < 1) ||
+                         static_cast<const void*>(res->residual) != static_cast<const void*>(gu.A) ||
+                         res->parts != gu.nrm_parts || gu.nrm_nparts != res->H / kResCols || gu.lda != res->H))
+    return -1;
   // up to 128 rows (one row tile; MT = 8 above 64 rows, whose row scale reads <= 16 parts)
   if (gu.M > 128 || (gu.M > 64 && gu.nrm_nparts > 16) || dn.M != gu.M || gu.N % 128 || gu.S < 1 || gu.K % (kKC * gu.S) || !gu.row_scale ||
       gu.nrm_parts == nullptr || gu.nrm_nparts < 1 || gu.nrm_nparts > 64 || gu.out == nullptr || dn.K != gu.N / 2 ||
@@ -541,24 +556,39 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   Flow fgu{flow, done, err, 0, 0, dn.K / dn.S, 1, 0, 0, fused_spin_limit()};
   Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / (64 * dkr), dn.K / dn.S, 2, 0, 0, fused_spin_limit()};
   const int n_gu = (gu.N / 128) * gu.S, n_dn = (dn.N / (64 * dkr)) * dn.S;
-  const dim3 grid(n_gu > n_dn ? n_gu : n_dn);
-  auto go = [&](auto sp, auto kr) {
+  const ResArgs ra = res != nullptr ? *res : ResArgs{};
+  const int n_res = res != nullptr ? res_workgroups(ra) : 0;
+  const Flow fres = res != nullptr ? res_flow(ra, n_gu, err, fused_spin_limit()) : Flow{};
+  int nwg = n_gu > n_dn ? n_gu : n_dn;
+  if (n_res > nwg) return -1;  // every residual producer is also a GEMM workgroup (resident anyway)
+  const dim3 grid(nwg);
+  auto go = [&](auto sp, auto kr, auto rs) {
     constexpr bool SP = decltype(sp)::value;
     constexpr int KR = decltype(kr)::value;
+    constexpr bool RS = decltype(rs)::value;
+#define PK_MLPF(MT) \
+  mlp_fused_kernel<MT, SP, KR, false, RS><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn, ra, fres, n_res)
     switch ((gu.M + 15) / 16) {
-      case 1: mlp_fused_kernel<1, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      case 2: mlp_fused_kernel<2, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      case 3: mlp_fused_kernel<3, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      case 4: mlp_fused_kernel<4, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
-      default: mlp_fused_kernel<8, SP, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn); break;
+      case 1: PK_MLPF(1); break;
+      case 2: PK_MLPF(2); break;
+      case 3: PK_MLPF(3); break;
+      case 4: PK_MLPF(4); break;
+      default: PK_MLPF(8); break;
     }
+#undef PK_MLPF
   };
   using K1 = std::integral_constant<int, 1>;
   using K2 = std::integral_constant<int, 2>;
+  auto go_r = [&](auto sp, auto kr) {
+    if (res != nullptr)
+      go(sp, kr, std::true_type{});
+    else
+      go(sp, kr, std::false_type{});
+  };
   if (split)
-    dkr == 1 ? go(std::true_type{}, K1{}) : go(std::true_type{}, K2{});
+    dkr == 1 ? go_r(std::true_type{}, K1{}) : go_r(std::true_type{}, K2{});
   else
-    dkr == 1 ? go(std::false_type{}, K1{}) : go(std::false_type{}, K2{});
+    dkr == 1 ? go_r(std::false_type{}, K1{}) : go_r(std::false_type{}, K2{});
   return PK_CHECK_LAUNCH();
 }
 

@@ -283,9 +283,21 @@ struct SkinnyLds {
   int last;
 };
 
+// FL: in-launch hand-off roles (bits) --
+//   1  producer: output stores write-through (sc1), one ticket per finished n-block on `fl`
+//   2  consumer of per-K-slice tickets on `fl` (slice = this tile's split): weights requested first,
+//      A (the producers' output) read with sc1 loads after the wait
+//   4  consumer of ONE all-to-all hand-off on `fw` (slice 0: the in-launch residual update of
+//      phase.h res_phase): weights requested first, then the wait, then A (the residual stream)
+//      and the row-scale parts, both with sc1 loads
 template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2, int FL = 0>
 __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_in, const int by, const int gdx,
-                                            SkinnyLds<MT>& L, const Flow& fl) {
+                                            SkinnyLds<MT>& L, const Flow& fl, const Flow& fw = Flow{}) {
+  constexpr bool kProd = (FL & 1) != 0;
+  constexpr bool kWaitSlice = (FL & 2) != 0;
+  constexpr bool kWaitRes = (FL & 4) != 0;
+  constexpr bool kWait = kWaitSlice || kWaitRes;
+  static_assert(!(kWaitSlice && kWaitRes), "one wait per tile");
   constexpr int kR = KR;
   constexpr int kKA = SkinnyLds<MT>::kKA;  // k per staged A tile
   constexpr int kPPR = kKA / 8;             // 16-byte pieces per A row
@@ -344,16 +356,29 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   constexpr int kRsRows = MT > 4 ? 2 : 1;  // 64-row groups per thread
   constexpr int kRsLoads = 16 / (kRsRows * kRsRows);
   float rs_p[RS ? kRsRows * kRsLoads : 1];
-  if constexpr (RS) {
+  auto load_rs = [&]() {
     const int np = min(args.nrm_nparts, 4 * kRsLoads), sub = tid & 3;
 #pragma unroll
     for (int h = 0; h < kRsRows; ++h) {
       const int rr = min(64 * h + (tid >> 2), M - 1);
 #pragma unroll
-      for (int q = 0; q < kRsLoads; ++q)
-        rs_p[h * kRsLoads + q] = args.nrm_parts[min(sub + 4 * q, np - 1) * args.M + row0 + rr];
+      for (int q = 0; q < kRsLoads; ++q) {
+        const float* p = args.nrm_parts + min(sub + 4 * q, np - 1) * args.M + row0 + rr;
+        // parts written in this launch (res_phase): sc1 loads after the hand-off wait
+        rs_p[h * kRsLoads + q] = kWaitRes ? ldf_sc1(args.nrm_parts, p) : *p;
+      }
     }
-  }
+  };
+  if constexpr (RS && !kWaitRes) load_rs();
+  // the consumer's wait (after its first weight k-steps are requested); the residual hand-off
+  // also makes the row-scale parts readable
+  auto wait_in = [&](int split_) {
+    if constexpr (kWaitSlice) flow_wait(fl, split_);
+    if constexpr (kWaitRes) {
+      flow_wait(fw, 0);
+      if constexpr (RS) load_rs();
+    }
+  };
 
   const bf16_t* wp[kR];
 #pragma unroll
@@ -376,7 +401,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
 #pragma unroll
     for (int p = 0; p < kPieces; ++p) {
       const int col = ((tid + 256 * p) % kPPR) * 8;
-      if constexpr (FL == 2)  // the producers' output, handed off in-launch: sc1 loads
+      if constexpr (kWait)  // the producers' output, handed off in-launch: sc1 loads
         stage[p] = __builtin_amdgcn_raw_buffer_load_b128(
             __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(args.A), static_cast<short>(0), 0x7ffffff0, 0x00020000),
             static_cast<int>((arow[p] + kc + col - args.A) * 2), 0, 16);
@@ -446,10 +471,10 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
     const int nsteps = 2 * nchunks;  // even
     const int rot2 = 2 * rot;
     auto ks = [&](int j) { return k0 + ((min(j, nsteps - 1) + rot2) % nsteps) * 128; };
-    if constexpr (FL == 2) {  // consumer of an in-launch hand-off: weights first, A after the wait
+    if constexpr (kWait) {  // consumer of an in-launch hand-off: weights first, A after the wait
       load_w(wa, ks(0));
       load_w(wb, ks(1));
-      flow_wait(fl, split);
+      wait_in(split);
       load_a(ks(0));
     } else {
       load_a(ks(0));
@@ -473,12 +498,12 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       buf ^= 1;
     }
   } else {
-  if constexpr (FL == 2) {
+  if constexpr (kWait) {
     // consumer: this workgroup's first two weight k-steps are requested before the wait, so
     // they stream in while the producers finish; A (the producers' output) is read after it
     load_w(wa, ck(0));
     load_w(wb, ck(0) + 128);
-    flow_wait(fl, split);
+    wait_in(split);
     load_a(ck(0));
   } else {
     load_a(ck(0));
@@ -520,7 +545,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   // the in-launch residual update hands its slabs over write-through (measured faster than plain
   // stores + release: tools/gemm_lab.hip o_res / down_res); the plain split-K slabs are read by
   // the next kernel and stay plain (write-through made those slower)
-  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kSiluSplit || (MODE == kPartial && FL == 1);
+  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kSiluSplit || (MODE == kPartial && kProd);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = 16 * mt + r;
@@ -562,7 +587,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       uint2 v;
       v.x = pack2(y[0], y[1]);
       v.y = pack2(y[2], y[3]);
-      if constexpr (FL == 1) {  // handed off in-launch: write-through (sc1) stores
+      if constexpr (kProd) {  // handed off in-launch: write-through (sc1) stores
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(args.out, static_cast<short>(0), 0x7ffffff0, 0x00020000);
         typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{v.x, v.y}, rsrc, static_cast<int>((o - args.out) * 2), 0, 16);
@@ -571,7 +596,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       }
     }
   }
-  if constexpr ((MODE == kSiluMul || MODE == kPartial) && FL == 1)  // output columns of n-block nb
+  if constexpr ((MODE == kSiluMul || MODE == kPartial) && kProd)  // output columns of n-block nb
     flow_signal(fl, flow_slice(fl, nb, MODE == kSiluMul ? 64 * kR / 2 : 64 * kR));
   if constexpr (MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit) {
     // ---- in-launch split-K reduction by the last split of this n-block to arrive
@@ -603,7 +628,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       case 16: epilogue<MODE, 16, KR>(args, nb); break;
       default: epilogue<MODE, 0, KR>(args, nb); break;
     }
-    if constexpr (MODE == kSiluSplit && FL == 1)  // h columns of n-block nb are out: one ticket
+    if constexpr (MODE == kSiluSplit && kProd)  // h columns of n-block nb are out: one ticket
       flow_signal(fl, flow_slice(fl, nb, 64));
   }
 }

@@ -459,47 +459,98 @@ class LlamaForCausalLM(nn.Module):
             self._parts_buf2 = torch.zeros_like(self._parts_buf)
         buf, buf2 = self._parts_buf, self._parts_buf2
         residual = x
-        parts = gemm.residual_parts(None, residual, buf)
-        last = len(self.layers) - 1
         if self.st.tp_size > 1:
+            parts = gemm.residual_parts(None, residual, buf)
             return self._forward_rowscale_tp(residual, parts, positions, md, kv_caches, ws, buf, buf2)
+        # every residual update (+ norm parts) is phase 0 of the fused launch that consumes it
+        # when that launch is taken (RES_PHASE: the 2 residual_parts launches per layer go)
+        pending = None  # the previous layer's down slabs, not yet added to the residual
         for i, layer in enumerate(self.layers):
-            a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws)
+            oph = self._o_phase(layer, residual, md)
+            if self._res_phase_attn(layer, residual, md):
+                a = self._decode_attn(layer, residual, None, positions, md, kv_caches[i], ws,
+                                      res=gemm.ResIn(pending, residual, buf, self._flow_res), o=oph)
+            else:
+                parts = gemm.residual_parts(pending, residual, buf)
+                a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws, o=oph)
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read); the residual
             # update by the last split of each n-block inside the O launch measured 1 % slower
-            # (profiles/r4_o_inlaunch_ab.jsonl)
-            parts = gemm.residual_parts(gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p, half=True),
-                                        residual, buf2)
-            d = self._decode_mlp(layer, residual, parts, ws)
-            if i < last:
-                parts = gemm.residual_parts(d, residual, buf)
+            # (profiles/r4_o_inlaunch_ab.jsonl).  With the o phase the fused launch returned them.
+            o = a if isinstance(a, gemm.Partial) else gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p,
+                                                                          half=True)
+            if self._res_phase_mlp(layer, residual):
+                pending = self._decode_mlp(layer, residual, None, ws,
+                                           res=gemm.ResIn(o, residual, buf2, self._flow_res))
             else:
-                x, _ = gemm.partial_add_rms_norm(d, residual, self.norm, self.cfg.rms_eps)
+                parts = gemm.residual_parts(o, residual, buf2)
+                pending = self._decode_mlp(layer, residual, parts, ws)
+        x, _ = gemm.partial_add_rms_norm(pending, residual, self.norm, self.cfg.rms_eps)
         return x
 
-    def _decode_attn(self, layer, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
-                     md: attn_ops.AttnMetadata, kv: Tuple[torch.Tensor, torch.Tensor], ws: torch.Tensor) -> torch.Tensor:
-        """Folded-norm QKV projection + RoPE + KV write + attention of one layer -> [T, nq * 128]."""
+    def _o_phase(self, layer, residual: torch.Tensor, md) -> Optional[gemm.OProj]:
+        """The o-projection as phase 3 of the fused QKV -> attention launch (gemm.O_PHASE): its slab
+        buffer, hand-off buffer and partition-merge counters -- used only if _decode_attn takes that
+        launch (it then returns the o slabs, a gemm.Partial)."""
+        T = residual.shape[0]
+        at = layer.attn
+        if not (gemm.O_PHASE and at.o_p is not None and md.num_prefill == 0 and T <= gemm.FUSED_MAX_M
+                and gemm.o_phase_ok(at.o.shape[0], at.nq, at.nkv, T) and getattr(self, "_ws_o", None) is not None):
+            return None
+        return gemm.OProj(at.o_p, self._ws_o, self._flow_o, self._attn_counters)
+
+    def _res_phase_attn(self, layer, residual: torch.Tensor, md) -> bool:
+        """The fused QKV -> attention launch is taken AND can run the residual update as its phase 0."""
+        T, H = residual.shape
+        at = layer.attn
+        return (gemm.RES_PHASE and self.st.tp_size == 1 and self._qkv_attn_fused_ok(at, T, H // gemm.PART_COLS, md)
+                and gemm.res_workgroups(T, H) <= max((at.qkv.shape[0] // 128) * gemm.choose_split(
+                    at.qkv.shape[0], H, T), T * at.nkv))
+
+    def _res_phase_mlp(self, layer, residual: torch.Tensor) -> bool:
+        T, H = residual.shape
+        mlp = layer.mlp
+        return (gemm.RES_PHASE and self.st.tp_size == 1 and not self.st.shared_device
+                and gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, H // gemm.PART_COLS)
+                and gemm.res_workgroups(T, H) <= gemm.mlp_fused_grid(residual, mlp.gate_up_pf, mlp.down_p))
+
+    @staticmethod
+    def _qkv_attn_fused_ok(at, T: int, nparts: int, md) -> bool:
+        return (md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and at.nkv >= gemm.QKV_ATTN_MIN_KV
+                and gemm.fused_rows_ok(T, nparts) and md.num_decode == T)
+
+    def _decode_attn(self, layer, residual: torch.Tensor, parts: Optional[torch.Tensor], positions: torch.Tensor,
+                     md: attn_ops.AttnMetadata, kv: Tuple[torch.Tensor, torch.Tensor], ws: torch.Tensor,
+                     res: Optional[gemm.ResIn] = None, o: Optional[gemm.OProj] = None):
+        """Folded-norm QKV projection + RoPE + KV write + attention of one layer -> [T, nq * 128]
+        (``res``: the fused launch's phase 0 updates the residual and makes the norm parts; ``o``:
+        its phase 3 is the o-projection, whose slabs (a :class:`gemm.Partial`) are returned)."""
         at = layer.attn
         kc, vc = kv
         T = residual.shape[0]
+        if res is not None:
+            return gemm.qkv_attn_fused(residual, at.qkv_pf, None, ws, positions, self.cos_sin, kc, vc, md, at.scale,
+                                       at.nq, at.nkv, self._flow_qkv, res=res, eps=layer.eps, o=o)
         rs = gemm.RowScale(parts, layer.eps)
-        if (md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and at.nkv >= gemm.QKV_ATTN_MIN_KV
-                and gemm.fused_rows_ok(T, parts.shape[0]) and md.num_decode == T):
+        if self._qkv_attn_fused_ok(at, T, parts.shape[0], md):
             # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip);
             # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
             return gemm.qkv_attn_fused(residual, at.qkv_pf, rs, ws, positions, self.cos_sin, kc, vc, md, at.scale,
-                                       at.nq, at.nkv, self._flow_qkv)
+                                       at.nq, at.nkv, self._flow_qkv, o=o)
         p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, packed=at.qkv_pf)
         if md.num_prefill == 0:
             return attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
         q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
         return attn_ops.paged_attention(q, kc, vc, md, at.scale)
 
-    def _decode_mlp(self, layer, residual: torch.Tensor, parts: torch.Tensor, ws: torch.Tensor) -> gemm.Partial:
-        """Folded-norm gate_up + SiLU and the down projection of one layer -> down's split-K slabs."""
+    def _decode_mlp(self, layer, residual: torch.Tensor, parts: Optional[torch.Tensor], ws: torch.Tensor,
+                    res: Optional[gemm.ResIn] = None) -> gemm.Partial:
+        """Folded-norm gate_up + SiLU and the down projection of one layer -> down's split-K slabs
+        (``res``: the fused launch's phase 0 updates the residual and makes the norm parts)."""
         mlp = layer.mlp
+        if res is not None:
+            return gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, None, ws, self._flow, ws_gu=self._ws_gu,
+                                  res=res, eps=layer.eps)
         rs = gemm.RowScale(parts, layer.eps)
         if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, parts.shape[0]) and not self.st.shared_device:
             # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
@@ -532,9 +583,11 @@ class LlamaForCausalLM(nn.Module):
         launch (2 x 80 all-reduces per 70B TP=8 step)."""
         car = self.st.custom_ar
         for i, layer in enumerate(self.layers):
-            a = layer.attn.drop(self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws))
-            parts = car.reduce_residual(gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p, half=True),
-                                        residual, buf2)
+            oph = None if layer.attn.fault_drop else self._o_phase(layer, residual, md)
+            a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws, o=oph)
+            if not isinstance(a, gemm.Partial):
+                a = gemm.linear_partial(layer.attn.drop(a), layer.attn.o, ws, packed=layer.attn.o_p, half=True)
+            parts = car.reduce_residual(a, residual, buf2)
             parts = car.reduce_residual(self._decode_mlp(layer, residual, parts, ws), residual, buf)
         return gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
 
@@ -548,6 +601,17 @@ class LlamaForCausalLM(nn.Module):
             self._flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
             gemm.fused_err_word()  # before the first fused launch (engine polls gemm.check_fused)
             self._flow_qkv = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
+            # the residual phase's hand-off (gemm.ResIn: phase 0 of either fused launch)
+            self._flow_res = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
+            # the o-projection phase of the fused QKV -> attention launch (gemm.OProj): its own slab
+            # buffer, hand-off buffer and the attention's in-launch partition-merge counters
+            at = self.layers[0].attn
+            if at.o is not None and at.o.dim() == 2:
+                No, Ko = at.o.shape
+                n = max(gemm.o_phase_split(No, Ko, m) * m * No for m in range(1, gemm.FUSED_MAX_M + 1))
+                self._ws_o = torch.empty(n, dtype=torch.float32, device=self.device)
+                self._flow_o = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
+                self._attn_counters = torch.zeros((gemm.FUSED_MAX_M, at.nkv), dtype=torch.int32, device=self.device)
             # slabs of a gate_up split over K (gemm.gate_up_split > 1: the 70B TP=8 shard)
             n = self._gate_up_split_elems()
             self._ws_gu = torch.empty(n, dtype=torch.float32, device=self.device) if n else None

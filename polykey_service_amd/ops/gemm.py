@@ -47,7 +47,7 @@ MLP_FUSED_SPLIT = os.environ.get("POLYKEY_MLP_FUSED_SPLIT", "0") == "1"
 # tiles (8B: 8 kv heads); with one or two kv heads per rank (70B TP=8 / TP=4) every attention tile
 # waits for the whole projection and the launch measured slower (26.6 vs ~20 us per layer at
 # 70B TP=8, profiles/r4_tp_solo.md)
-QKV_ATTN_MIN_KV = 4
+QKV_ATTN_MIN_KV = int(os.environ.get("POLYKEY_QKV_MIN_KV", "4"))
 PACKED_BIT = 16
 
 
@@ -72,6 +72,37 @@ class GemmArgs(ctypes.Structure):
 
 
 _ARGS_CHECKED = False
+
+
+class ResArgs(ctypes.Structure):
+    """Mirror of ``struct ResArgs`` in csrc/kernels/phase.h: the in-launch residual phase."""
+    _fields_ = [("residual", ctypes.c_void_p), ("slabs", ctypes.c_void_p), ("parts", ctypes.c_void_p),
+                ("S", ctypes.c_int), ("M", ctypes.c_int), ("H", ctypes.c_int), ("flow", ctypes.c_void_p)]
+
+
+class ResIn(NamedTuple):
+    """Phase 0 of a fused decode launch (TP = 1): ``residual`` += sum of ``pending``'s slabs (None:
+    unchanged) and ``parts`` [H / 512, M] = the new rows' sums of squares -- the work of
+    :func:`residual_parts`, done inside the launch whose first GEMM consumes both (its tiles wait on
+    ``flow``, an int32 hand-off buffer of its own: >= :data:`FLOW_WORDS`, zeroed once, left zeroed)."""
+    pending: Optional["Partial"]
+    residual: torch.Tensor
+    parts: torch.Tensor
+    flow: torch.Tensor
+
+    def args(self) -> "ResArgs":
+        M, H = self.residual.shape
+        assert self.residual.is_contiguous() and H % PART_COLS == 0 and self.parts.numel() >= (H // PART_COLS) * M
+        assert self.flow.numel() >= FLOW_WORDS and self.flow.dtype == torch.int32
+        p = self.pending
+        if p is not None:
+            assert p.M == M and p.N == H
+        return ResArgs(self.residual.data_ptr(), 0 if p is None else p.buf.data_ptr(), self.parts.data_ptr(),
+                       0 if p is None else p.S, M, H, self.flow.data_ptr())
+
+    def parts_view(self) -> torch.Tensor:
+        M, H = self.residual.shape
+        return self.parts.view(-1)[: (H // PART_COLS) * M].view(H // PART_COLS, M)
 
 
 class RowScale(NamedTuple):
@@ -507,15 +538,42 @@ def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_p
             and (down_packed.shape[0] // (64 * down_kr(down_packed.shape[0], I, M))) * S <= device_cus(x.device))
 
 
-def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: RowScale,
-              ws: torch.Tensor, flow: torch.Tensor, ws_gu: Optional[torch.Tensor] = None) -> Partial:
+# TP = 1 decode: every residual update runs as phase 0 of the fused launch that consumes it
+# (ResIn, csrc/kernels/phase.h) instead of a residual_parts launch of its own
+RES_PHASE = os.environ.get("POLYKEY_RES_PHASE", "1") == "1"
+# decode: the o-projection as phase 3 of the fused QKV -> attention launch (OProj)
+O_PHASE = os.environ.get("POLYKEY_O_PHASE", "1") == "1"
+
+
+def res_workgroups(M: int, H: int) -> int:
+    """Producer workgroups of the residual phase (phase.h res_workgroups: one wave per (row, part))."""
+    return (M * (H // PART_COLS) + 3) // 4
+
+
+def mlp_fused_grid(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor) -> int:
+    """Workgroups of a :func:`mlp_fused` launch (pk_mlp_fused: max of its gate_up and down tiles)."""
+    M, K = x.shape
+    N2, I = gate_up_packed.shape[0], down_packed.shape[1]
+    N = down_packed.shape[0]
+    S = choose_split(N, I, M)
+    return max((N2 // 128) * gate_up_split(N2, K, M), (N // (64 * down_kr(N, I, M))) * S)
+
+
+def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: Optional[RowScale],
+              ws: torch.Tensor, flow: torch.Tensor, ws_gu: Optional[torch.Tensor] = None,
+              res: Optional[ResIn] = None, eps: float = 1e-5) -> Partial:
     """Decode MLP in ONE launch (csrc/kernels/gemm_skinny.hip mlp_fused_kernel):
     h = silu/mul of rinv * (x @ Wgu'^T) (folded norm, interleaved packed gate/up), then the down
     projection's fp32 split-K slabs of h @ Wd^T in ``ws``.  Down workgroups stream their first
     weight k-steps while gate_up finishes and wait on per-K-slice tickets in ``flow`` (int32,
     >= :data:`FLOW_WORDS`, zeroed once; every launch leaves it zeroed).  When gate_up is split
     over K (:func:`gate_up_split` > 1) its slabs go to ``ws_gu`` and the last split of each
-    n-block applies SiLU.  Returns the down slabs."""
+    n-block applies SiLU.  ``res`` (TP = 1): phase 0 of the launch is the residual update of the
+    o-projection's slabs (:class:`ResIn`; ``x`` must be ``res.residual``), whose parts are the row
+    scale (``rowscale`` None, ``eps`` its epsilon).  Returns the down slabs."""
+    if res is not None:
+        assert x is res.residual and rowscale is None
+        rowscale = RowScale(res.parts_view(), eps)
     M, K = x.shape
     N2, I = gate_up_packed.shape[0], down_packed.shape[1]
     N = down_packed.shape[0]
@@ -533,21 +591,56 @@ def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.
     dn = GemmArgs()
     dn.partial, dn.A, dn.W = ws.data_ptr(), h.data_ptr(), down_packed.data_ptr()
     dn.M, dn.N, dn.K, dn.lda, dn.ldo, dn.S = M, N, I, h.stride(0), N, S
-    native.call("pk_mlp_fused", ctypes.byref(gu), ctypes.byref(dn), flow.data_ptr(), native.stream_ptr())
+    ra = res.args() if res is not None else None
+    native.call("pk_mlp_fused", ctypes.byref(gu), ctypes.byref(dn), flow.data_ptr(),
+                ctypes.byref(ra) if ra is not None else None, native.stream_ptr())
     return Partial(ws, S, M, N)
 
 
 QKV_ATTN_FUSED = os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1") == "1"
 
 
-def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: RowScale, ws: torch.Tensor,
+class OProj(NamedTuple):
+    """The o-projection as phase 3 of :func:`qkv_attn_fused`: split-K slabs of attn @ Wo^T
+    (``packed`` = :func:`pack_weight` (Wo), 64-row n-blocks at half the default split, as
+    :func:`linear_partial` ``half=True``) into ``ws`` -- a buffer of its own (the QKV slabs are still
+    being read when the first o tiles store); ``flow`` its hand-off buffer (>= :data:`FLOW_WORDS`,
+    zeroed once, left zeroed); ``counters`` [M, n_kv] int32 zeroed (the attention partitions are
+    merged in-launch)."""
+    packed: torch.Tensor
+    ws: torch.Tensor
+    flow: torch.Tensor
+    counters: torch.Tensor
+
+
+def o_phase_split(N: int, K: int, M: int) -> int:
+    """K split of the o-projection phase: :func:`linear_partial` ``half=True``'s."""
+    return max(1, choose_split(N, K, M) // 2)
+
+
+def o_phase_ok(N: int, nq: int, nkv: int, M: int) -> bool:
+    """The o-projection phase's K slices must be whole kv heads or whole fractions of one."""
+    S = o_phase_split(N, nq * 128, M)
+    G = nq // nkv
+    hps = nq // S if nq % S == 0 else 0
+    return hps > 0 and (hps % G == 0 if hps >= G else G % hps == 0) and S <= 64
+
+
+def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: Optional[RowScale], ws: torch.Tensor,
                    positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, md,
-                   scale: float, nq: int, nkv: int, flow: torch.Tensor, S: Optional[int] = None) -> torch.Tensor:
+                   scale: float, nq: int, nkv: int, flow: torch.Tensor, S: Optional[int] = None,
+                   res: Optional[ResIn] = None, eps: float = 1e-5, o: Optional[OProj] = None):
     """Decode layer front half in ONE launch (csrc/kernels/decode_fused.hip): the folded-norm
     QKV projection's split-K slabs (``ws``), handed in-launch to the decode attention that
     reduces them, applies RoPE, writes the new k / v to the paged cache and attends.  Same
     result as :func:`linear_partial_rowscale` + ``attention.paged_decode_from_qkv``.  ``flow``:
-    int32 >= :data:`FLOW_WORDS`, zeroed once, left zeroed.  Returns [M, nq * 128] bf16."""
+    int32 >= :data:`FLOW_WORDS`, zeroed once, left zeroed.  ``res`` (TP = 1): phase 0 is the residual
+    update of the previous layer's down slabs (:class:`ResIn`, ``x`` is ``res.residual``; its parts
+    are the row scale, ``eps`` its epsilon).  Returns [M, nq * 128] bf16, or with ``o``
+    (:class:`OProj`) the o-projection's slabs (:class:`Partial`) computed in the same launch."""
+    if res is not None:
+        assert x is res.residual and rowscale is None
+        rowscale = RowScale(res.parts_view(), eps)
     M, K = x.shape
     N = qkv_packed.shape[0]
     S = S or choose_split(N, K, M)
@@ -560,12 +653,25 @@ def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: RowScale
     a.row_scale, a.nrm_parts, a.nrm_nparts, a.eps = 1, rowscale.parts.data_ptr(), rowscale.parts.shape[0], \
         float(rowscale.eps)
     bt = md.decode_block_tables
+    ra = res.args() if res is not None else None
+    oa, op = None, None
+    if o is not None:
+        No = o.packed.shape[0]
+        So = o_phase_split(No, nq * 128, M)
+        assert o.packed.shape[1] == nq * 128 and o.ws.numel() >= So * M * No and o.ws.data_ptr() != ws.data_ptr()
+        assert o.flow.numel() >= FLOW_WORDS and o.counters.numel() >= M * nkv and o.counters.dtype == torch.int32
+        oa = GemmArgs()
+        oa.partial, oa.A, oa.W = o.ws.data_ptr(), out.data_ptr(), o.packed.data_ptr()
+        oa.M, oa.N, oa.K, oa.lda, oa.ldo, oa.S = M, No, nq * 128, out.stride(0), No, So
+        op = Partial(o.ws, So, M, No)
     native.call("pk_qkv_attn_fused", ctypes.byref(a), out.data_ptr(), positions.data_ptr(), cos_sin.data_ptr(),
                 md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), bt.data_ptr(),
                 md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,
                 native.ptr(md.decode_part_ml) or 0, nq, nkv, k_cache.shape[2], bt.stride(0), out.stride(0),
-                float(scale), int(md.decode_max_ctx), flow.data_ptr(), native.stream_ptr())
-    return out
+                float(scale), int(md.decode_max_ctx), flow.data_ptr(), ctypes.byref(ra) if ra is not None else None,
+                ctypes.byref(oa) if oa is not None else None, o.flow.data_ptr() if o is not None else None,
+                o.counters.data_ptr() if o is not None else None, native.stream_ptr())
+    return op if op is not None else out
 
 
 def fold_norm(w: torch.Tensor, norm_weight: torch.Tensor) -> torch.Tensor:

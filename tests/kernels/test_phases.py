@@ -1,0 +1,185 @@
+"""In-launch phases of the fused decode launches (csrc/kernels/phase.h): the TP = 1 residual update
+(+ norm parts) as phase 0 of the launch that consumes it.  Everything it touches -- residual stream,
+norm parts, the launch's outputs, the K / V cache -- must be bit-identical to residual_parts +
+the same fused launch without the phase, over repeated launches with new inputs (a consumer
+reading a stale residual or parts would show), and every hand-off buffer left zeroed."""
+import math
+
+import pytest
+import torch
+
+from polykey_service_amd.ops import attention as A
+from polykey_service_amd.ops import gemm
+from polykey_service_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+HD = 128
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M", [1, 17, 64, 128])
+@pytest.mark.parametrize("H,I", [(4096, 14336), (1024, 4096)])
+@pytest.mark.parametrize("S_o", [0, 2, 4])
+def test_mlp_fused_residual_phase(M, H, I, S_o):
+    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wgu = gemm.interleave_gate_up(rnd(I, H, scale=0.05), rnd(I, H, scale=0.05))
+    gup = gemm.pack_weight(gemm.fold_norm(wgu, nw))
+    dp = gemm.pack_weight(rnd(H, I, scale=0.02))
+    nparts = H // gemm.PART_COLS
+    assert gemm.mlp_fused_ok(rnd(M, H), gup, dp, nparts)
+    S = gemm.choose_split(H, I, M)
+    ws_a = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
+    ws_b = torch.empty_like(ws_a)
+    flow_a = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda")
+    flow_b = torch.zeros_like(flow_a)
+    flow_r = torch.zeros_like(flow_a)
+    for it in range(5):
+        res0 = rnd(M, H)
+        # the o-projection's slabs (S_o = 0: no pending projection, parts only)
+        o = None
+        if S_o:
+            ob = torch.empty(S_o * M * H, dtype=torch.float32, device="cuda")
+            ob.copy_(torch.randn(S_o * M * H, device="cuda") * 0.3)
+            o = gemm.Partial(ob, S_o, M, H)
+        r1 = res0.clone()
+        p1 = gemm.residual_parts(o, r1, torch.empty(nparts * 128, device="cuda"))
+        exp = gemm.mlp_fused(r1, gup, dp, gemm.RowScale(p1, 1e-5), ws_a, flow_a).view().clone()
+        r2 = res0.clone()
+        pbuf = torch.full((nparts * 128,), float("nan"), device="cuda")
+        ws_b.fill_(float("nan"))
+        ri = gemm.ResIn(o, r2, pbuf, flow_r)
+        got = gemm.mlp_fused(r2, gup, dp, None, ws_b, flow_b, res=ri, eps=1e-5).view()
+        torch.testing.assert_close(got, exp, atol=0, rtol=0)
+        assert torch.equal(r1, r2)
+        torch.testing.assert_close(ri.parts_view(), p1, atol=0, rtol=0)
+    torch.cuda.synchronize()
+    for f in (flow_a, flow_b, flow_r):
+        assert int(f.abs().sum()) == 0, f.nonzero().tolist()
+
+
+def _block_tables(ctxs, bs, num_blocks, max_blocks):
+    g = torch.Generator().manual_seed(10)
+    perm = torch.randperm(num_blocks, generator=g).tolist()
+    bt = torch.zeros(len(ctxs), max_blocks, dtype=torch.int32)
+    i = 0
+    for s, c in enumerate(ctxs):
+        nb = (c + bs - 1) // bs
+        bt[s, :nb] = torch.tensor(perm[i:i + nb], dtype=torch.int32)
+        i += nb
+    return bt
+
+
+@pytest.mark.parametrize("nq,nkv,H", [(32, 8, 4096), (16, 4, 1024)])
+@pytest.mark.parametrize("ctxs", [[1, 5, 33, 300], [384] * 64, [40 + 3 * i for i in range(100)]])
+@pytest.mark.parametrize("pending", [False, True])
+def test_qkv_attn_fused_residual_phase(nq, nkv, H, ctxs, pending):
+    d, bs = "cuda", 32
+    B = len(ctxs)
+    N = (nq + 2 * nkv) * HD
+    max_blocks = (max(ctxs) + bs - 1) // bs + 3
+    nb = sum((c + bs - 1) // bs for c in ctxs) + 4
+    bt = _block_tables(ctxs, bs, nb, max_blocks).to(d)
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=d)
+    pos = cl - 1
+    slots = (bt.gather(1, ((cl - 1) // bs).long()[:, None])[:, 0] * bs + (cl - 1) % bs).to(torch.int32)
+    cs = ref.rope_cos_sin_cache(4096, HD, 500000.0).to(d)
+    po, pml = A.decode_workspace(B, nq, max_blocks, bs, d, kv_heads=nkv)
+    md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0, slot_mapping=slots,
+                        decode_block_tables=bt, decode_context_lens=cl, decode_part_o=po, decode_part_ml=pml)
+    wp = gemm.pack_weight(rnd(N, H, scale=0.05))
+    S = gemm.choose_split(N, H, B)
+    ws1 = torch.empty(S * B * N, dtype=torch.float32, device=d)
+    ws2 = torch.empty_like(ws1)
+    fa = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=d)
+    fb, fr = torch.zeros_like(fa), torch.zeros_like(fa)
+    nparts = H // gemm.PART_COLS
+    k0 = torch.randn(nb, nkv, bs, HD, device=d).to(torch.bfloat16)
+    v0 = torch.randn(nb, nkv, HD, bs, device=d).to(torch.bfloat16)
+    k1, v1, k2, v2 = k0.clone(), v0.clone(), k0.clone(), v0.clone()
+    scale = 1 / math.sqrt(HD)
+    for it in range(4):
+        res0 = rnd(B, H)
+        dn = None
+        if pending:  # the previous layer's down slabs
+            db = (torch.randn(4 * B * H, device=d) * 0.3)
+            dn = gemm.Partial(db, 4, B, H)
+        r1 = res0.clone()
+        p1 = gemm.residual_parts(dn, r1, torch.empty(nparts * 128, device=d))
+        exp = gemm.qkv_attn_fused(r1, wp, gemm.RowScale(p1, 1e-5), ws1, pos, cs, k1, v1, md, scale, nq, nkv, fa)
+        r2 = res0.clone()
+        ri = gemm.ResIn(dn, r2, torch.full((nparts * 128,), float("nan"), device=d), fr)
+        ws2.fill_(float("nan"))
+        got = gemm.qkv_attn_fused(r2, wp, None, ws2, pos, cs, k2, v2, md, scale, nq, nkv, fb, res=ri, eps=1e-5)
+        torch.testing.assert_close(got, exp, atol=0, rtol=0)
+        assert torch.equal(r1, r2) and torch.equal(k1, k2) and torch.equal(v1, v2)
+        torch.testing.assert_close(ri.parts_view(), p1, atol=0, rtol=0)
+    torch.cuda.synchronize()
+    for f in (fa, fb, fr):
+        assert int(f.abs().sum()) == 0, f.nonzero().tolist()
+
+
+@pytest.mark.parametrize("nq,nkv,H,No", [(32, 8, 4096, 4096), (8, 1, 8192, 8192), (16, 4, 1024, 1024)])
+@pytest.mark.parametrize("ctxs", [[384] * 64, [1, 5, 33, 300], [600, 1300, 7, 2100], [40 + 3 * i for i in range(100)]])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_qkv_attn_fused_o_phase(nq, nkv, H, No, ctxs, with_res):
+    """The o-projection as phase 3 of the fused QKV -> attention launch (gemm.OProj): its tiles wait
+    on their K slice's attention tiles (8B: 2 kv heads per slice; the 70B TP=8 shard: one kv head
+    spanning 2 slices) and the partitions are merged in-launch.  The o slabs are bit-identical to
+    the attention launch followed by linear_partial(half=True); K / V cache too."""
+    d, bs = "cuda", 32
+    B = len(ctxs)
+    N = (nq + 2 * nkv) * HD
+    max_blocks = (max(ctxs) + bs - 1) // bs + 3
+    nb = sum((c + bs - 1) // bs for c in ctxs) + 4
+    bt = _block_tables(ctxs, bs, nb, max_blocks).to(d)
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=d)
+    pos = cl - 1
+    slots = (bt.gather(1, ((cl - 1) // bs).long()[:, None])[:, 0] * bs + (cl - 1) % bs).to(torch.int32)
+    cs = ref.rope_cos_sin_cache(4096, HD, 500000.0).to(d)
+    po, pml = A.decode_workspace(B, nq, max_blocks, bs, d, kv_heads=nkv)
+    md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0, slot_mapping=slots,
+                        decode_block_tables=bt, decode_context_lens=cl, decode_part_o=po, decode_part_ml=pml)
+    wp = gemm.pack_weight(rnd(N, H, scale=0.05))
+    wo = rnd(No, nq * HD, scale=0.05)
+    wop = gemm.pack_weight(wo)
+    assert gemm.o_phase_ok(No, nq, nkv, B)
+    S = gemm.choose_split(N, H, B)
+    So = gemm.o_phase_split(No, nq * HD, B)
+    ws1 = torch.empty(S * B * N, dtype=torch.float32, device=d)
+    ws2 = torch.empty_like(ws1)
+    wso1 = torch.empty(So * B * No, dtype=torch.float32, device=d)
+    wso2 = torch.empty_like(wso1)
+    fa, fb, fo, fr = (torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=d) for _ in range(4))
+    ctr = torch.zeros((B, nkv), dtype=torch.int32, device=d)
+    nparts = H // gemm.PART_COLS
+    k0 = torch.randn(nb, nkv, bs, HD, device=d).to(torch.bfloat16)
+    v0 = torch.randn(nb, nkv, HD, bs, device=d).to(torch.bfloat16)
+    k1, v1, k2, v2 = k0.clone(), v0.clone(), k0.clone(), v0.clone()
+    scale = 1 / math.sqrt(HD)
+    for it in range(3):
+        res0 = rnd(B, H)
+        r1 = res0.clone()
+        p1 = gemm.residual_parts(None, r1, torch.empty(nparts * 128, device=d))
+        a = gemm.qkv_attn_fused(r1, wp, gemm.RowScale(p1, 1e-5), ws1, pos, cs, k1, v1, md, scale, nq, nkv, fa)
+        exp = gemm.linear_partial(a, wo, wso1, packed=wop, half=True)
+        assert exp.S == So
+        r2 = res0.clone()
+        wso2.fill_(float("nan"))
+        op = gemm.OProj(wop, wso2, fo, ctr)
+        if with_res:
+            ri = gemm.ResIn(None, r2, torch.empty(nparts * 128, device=d), fr)
+            got = gemm.qkv_attn_fused(r2, wp, None, ws2, pos, cs, k2, v2, md, scale, nq, nkv, fb, res=ri, o=op)
+        else:
+            p2 = gemm.residual_parts(None, r2, torch.empty(nparts * 128, device=d))
+            got = gemm.qkv_attn_fused(r2, wp, gemm.RowScale(p2, 1e-5), ws2, pos, cs, k2, v2, md, scale, nq, nkv, fb,
+                                      o=op)
+        assert isinstance(got, gemm.Partial) and got.S == So
+        torch.testing.assert_close(got.view(), exp.view(), atol=0, rtol=0)
+        assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    torch.cuda.synchronize()
+    for f in (fa, fb, fo, fr):
+        assert int(f.abs().sum()) == 0, f.nonzero().tolist()
+    assert int(ctr.abs().sum()) == 0

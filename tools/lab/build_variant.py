@@ -19,10 +19,10 @@ from polykey_service_amd._native.build import HIP_FLAGS, HIPCC  # noqa: E402
 
 VARIANTS = {
     # the fused QKV -> attention launch without the K/V prefetch before the hand-off wait
-    "pre0": [("decode_fused.hip", "decode_tile<P, kDecodeWaves, true, SS, 2, 2>(",
-              "decode_tile<P, kDecodeWaves, true, SS, 2, 0>(")],
+    "pre0": [("decode_fused.hip", "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 2>(",
+              "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 0>(")],
     # the fused MLP's down tiles with non-temporal weight loads
-    "mlp_nt": [("gemm_skinny.hip", "case 4: mlp_fused_kernel<4, SP, KR><<<", "case 4: mlp_fused_kernel<4, SP, KR, !SP><<<")],
+    "mlp_nt": [("gemm_skinny.hip", "mlp_fused_kernel<MT, SP, KR, false, RS><<<", "mlp_fused_kernel<MT, SP, KR, !SP, RS><<<")],
     # the fused launches' hand-off pollers sleeping 4 instead of 16 (x 64 cycles) between polls
     "sleep4": [("flow.h", "__builtin_amdgcn_s_sleep(16);", "__builtin_amdgcn_s_sleep(4);")],
     # ablations of the 4-wave prefill GEMM measured this round (timing only, wrong results;
