@@ -194,13 +194,13 @@ class ReplicaPool:
     request goes to the replica with the fewest unfinished requests.  Replicas are in-process
     :class:`AsyncLLM` engines (one thread and HIP device each) or
     :class:`~polykey_service_amd.engine.remote.RemoteEngine` handles of engine processes (one
-    rank per GPU: :func:`~polykey_service_amd.engine.remote.dp_gateway`); the first replica must
-    be local.  Duck-types :class:`AsyncLLM`."""
+    rank per GPU: :func:`~polykey_service_amd.engine.remote.dp_gateway`, or the TP groups of
+    :func:`attach_model_groups`).  Duck-types :class:`AsyncLLM`."""
 
     def __init__(self, replicas):
         self.replicas = list(replicas)
         self.tokenizer = self.replicas[0].tokenizer
-        self.engine = self.replicas[0].engine
+        self.engine = getattr(self.replicas[0], "engine", None)  # None: every replica is remote
         self.on_fatal = None
         self.watchdog_s = 0.0
 
@@ -227,9 +227,12 @@ class ReplicaPool:
 
     def shutdown(self, timeout: float = 10.0) -> None:
         # remote handles first: their "stop" frames release the other ranks' engine servers
-        for r in self.replicas[1:]:
+        local = [r for r in self.replicas if hasattr(r, "engine")]
+        for r in self.replicas:
+            if r not in local:
+                r.shutdown(timeout)
+        for r in local:
             r.shutdown(timeout)
-        self.replicas[0].shutdown(timeout)
 
     async def aclose(self) -> None:
         for r in self.replicas:
@@ -269,11 +272,31 @@ class ModelSet:
 
 def parse_serve_models(spec: str) -> List[tuple]:
     """``"llama3-8b@0-3,mixtral-8x7b@4,tiny"`` -> [("llama3-8b", [0, 1, 2, 3]), ("mixtral-8x7b", [4]),
-    ("tiny", [])] (no ``@``: the next free device)."""
+    ("tiny", [])] (no ``@``: the next free device).  Entries of one process: TP = 1 only (a
+    ``:tp<N>`` entry needs one process per GPU: :func:`plan_model_groups`)."""
+    out = []
+    for name, devs, tp in parse_serve_plan(spec):
+        if tp != 1:
+            raise ValueError(f"serve_models entry {name!r} asks for tp={tp}: tensor parallel models are served by "
+                             "one process per GPU (torchrun), not by a single process")
+        out.append((name, devs))
+    return out
+
+
+def parse_serve_plan(spec: str) -> List[tuple]:
+    """``"llama3-70b@0-3:tp4,llama3-8b@4,mixtral-8x7b@5-6"`` -> [("llama3-70b", [0..3], 4),
+    ("llama3-8b", [4], 1), ("mixtral-8x7b", [5, 6], 1)]: model, devices (no ``@``: the next free
+    ones) and its TP degree (``:tp<N>``, default 1; the devices form len(devices) / N replicas)."""
     out = []
     for item in (x.strip() for x in spec.split(",")):
         if not item:
             continue
+        item, _, tps = item.partition(":")
+        tp = 1
+        if tps:
+            if not tps.startswith("tp") or not tps[2:].isdigit() or int(tps[2:]) < 1:
+                raise ValueError(f"serve_models entry {item!r}: bad TP suffix {tps!r} (':tp<N>')")
+            tp = int(tps[2:])
         name, _, dev = item.partition("@")
         if not name:
             raise ValueError(f"serve_models entry {item!r} has no model name")
@@ -286,11 +309,41 @@ def parse_serve_models(spec: str) -> List[tuple]:
             devs = list(range(a, b + 1))
         else:
             devs = [int(dev)]
-        out.append((name, devs))
-    names = [n for n, _ in out]
+        if devs and len(devs) % tp:
+            raise ValueError(f"serve_models entry {item!r}: {len(devs)} devices are not a multiple of tp={tp}")
+        out.append((name, devs, tp))
+    names = [n for n, _, _ in out]
     if len(set(names)) != len(names):
         raise ValueError(f"serve_models names a model twice: {spec!r}")
     return out
+
+
+def plan_model_groups(spec: str, world: int) -> List[tuple]:
+    """The TP groups of a one-process-per-GPU job serving ``spec`` on ``world`` ranks (rank r on GPU
+    r): [(model, [ranks]), ...], each group TP over consecutive ranks, the lowest its leader.  An
+    entry without ``@`` takes the next free ranks (tp of them); every rank must serve exactly one
+    group, and rank 0 -- the front end -- leads the first group it is in."""
+    entries = parse_serve_plan(spec)
+    taken = sorted(d for _, devs, _ in entries for d in devs)
+    if len(set(taken)) != len(taken):
+        raise ValueError(f"serve_models gives a GPU to two models: {spec!r}")
+    free = [r for r in range(world) if r not in taken]
+    groups = []
+    for name, devs, tp in entries:
+        if not devs:
+            if len(free) < tp:
+                raise ValueError(f"model {name!r} needs {tp} more GPU(s); the job has {world} ranks ({spec!r})")
+            devs, free = free[:tp], free[tp:]
+        for i in range(0, len(devs), tp):
+            g = devs[i:i + tp]
+            if g != list(range(g[0], g[0] + tp)):
+                raise ValueError(f"model {name!r}: a TP group must be consecutive GPUs, got {g}")
+            groups.append((name, g))
+    used = sorted(r for _, g in groups for r in g)
+    if used != list(range(world)):
+        raise ValueError(f"serve_models {spec!r} covers ranks {used}, the job has {world} (one per GPU, each "
+                         "serving exactly one model)")
+    return groups
 
 
 def attach_models(router, cfg, logger) -> ModelSet:
@@ -331,6 +384,86 @@ def attach_models(router, cfg, logger) -> ModelSet:
         llms[name] = llm
     router.llm = ModelSet(llms)
     return router.llm
+
+
+def attach_model_groups(router, cfg, logger, timeout_s: float = 600.0) -> Optional[ModelSet]:
+    """Several models behind ONE front end on a one-process-per-GPU job (torchrun), each model
+    served by TP groups of its own (``serve_models`` entries ``name@<gpus>[:tp<N>]``, e.g.
+    ``llama3-70b@0-3:tp4,llama3-8b@4,mixtral-8x7b@5-6``): the world is split into the groups of
+    :func:`plan_model_groups`, every rank builds its group's engine, each group's leader serves its
+    engine to rank 0 over the engine wire (engine/remote.py), the other ranks of a group follow
+    their leader's steps (TP workers), and rank 0 registers ``llm.*:<model>`` for every model,
+    routed least-loaded over that model's groups.  Rank 0 returns the :class:`ModelSet`; the other
+    ranks return None once the front end has stopped them (the caller exits)."""
+    import dataclasses as _dc
+    import os
+    import secrets
+    import socket as _socket
+
+    import torch.distributed as dist
+
+    from ..engine.async_llm import AsyncLLM
+    from ..engine.llm_engine import EngineConfig, LLMEngine, tokenizer_for
+    from ..engine.remote import EngineServer, RemoteEngine
+    from ..parallel.state import init_parallel
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    groups = plan_model_groups(cfg.serve_models, world)
+    name = next(n for n, g in groups if rank in g)
+    st = init_parallel(tp_groups=[g for _, g in groups], timeout_s=timeout_s,
+                       device=None if cfg.device in ("", "cuda") else cfg.device)
+    ecfg = EngineConfig.from_server_config(_dc.replace(cfg, model=name))
+    engine = LLMEngine(ecfg, st)
+    # the leaders' engine-server addresses, exchanged before the workers enter their step loops
+    single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+    bind = "127.0.0.1" if single_node else "0.0.0.0"
+    advertise = os.environ.get("POLYKEY_GATEWAY_HOST") or ("127.0.0.1" if single_node else _socket.gethostname())
+    tok = [secrets.token_hex(16) if rank == 0 else None]
+    dist.broadcast_object_list(tok, src=0, group=st.world_cpu_group)
+    llm = AsyncLLM(engine) if st.tp_rank == 0 else None
+    server = EngineServer(llm, host=bind, token=tok[0]) if llm is not None and rank != 0 else None
+    addrs: List = [None] * world
+    dist.all_gather_object(addrs, (advertise, server.port) if server is not None else None, group=st.world_cpu_group)
+    if st.tp_rank != 0:
+        try:
+            engine.runner.worker_loop()  # until the group's leader stops it
+        except BaseException as e:  # noqa: BLE001 - leader died / collective failed
+            logger.error("TP worker failed", error=repr(e), rank=rank, model=name)
+            raise
+        return None
+    if server is not None:
+        logger.info("model group leader serving", model=name, rank=rank, tp=st.tp_size, port=server.port)
+        try:
+            server.serve()  # until the front end stops it
+        finally:
+            llm.shutdown()  # (stops the group's TP workers too)
+        return None
+    # rank 0: the front end
+    llms: Dict[str, object] = {}
+    for mname in dict.fromkeys(n for n, _ in groups):
+        tk = tokenizer_for(_dc.replace(ecfg, model=mname))
+        reps = []
+        for n, g in groups:
+            if n != mname:
+                continue
+            reps.append(llm if g[0] == 0 else RemoteEngine(tuple(addrs[g[0]]), tk, name=f"{n}@rank{g[0]}",
+                                                         token=tok[0]))
+        pool = reps[0] if len(reps) == 1 else ReplicaPool(reps)
+        mcfg = _dc.replace(cfg, model=mname)
+        _register_tools(router, mcfg, pool)
+        llms[mname] = pool
+        logger.info("model group ready", model=mname, groups=[g for n, g in groups if n == mname])
+    router.llm = ModelSet(llms)
+    return router.llm
+
+
+def _register_tools(router, cfg, llm) -> None:
+    name = cfg.model if isinstance(cfg.model, str) else "model"
+    router.register_model_tool("llm.generate", name, LLMTool("llm.generate", name, llm, chat=False))
+    chat_tool = LLMTool("llm.chat", name, llm, chat=True)
+    chat_tool.router = router
+    router.register_model_tool("llm.chat", name, chat_tool)
 
 
 def attach_local_llm(router, cfg, logger, engine=None, llm=None):

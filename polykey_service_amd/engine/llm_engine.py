@@ -62,6 +62,15 @@ class EngineConfig:
                    num_layers=getattr(sc, "num_layers", 0))
 
 
+def tokenizer_for(cfg: EngineConfig, mcfg: Optional[ModelConfig] = None):
+    """The tokenizer an engine for ``cfg`` uses (a front end routing to an engine in another
+    process builds the same one without the engine)."""
+    from .chat_template import family_for
+    mcfg = mcfg or get_config(cfg.model_path or cfg.model)
+    return get_tokenizer(cfg.tokenizer, mcfg.vocab_size, mcfg.bos_token_id, mcfg.eos_token_id,
+                         family_for(mcfg.name, mcfg.is_moe))
+
+
 class LLMEngine:
     def __init__(self, cfg: EngineConfig, st: Optional[ParallelState] = None, model=None):
         self.cfg = cfg
@@ -113,9 +122,7 @@ class LLMEngine:
         self.model = model
         if hasattr(model, "pack_decode_weights"):
             model.pack_decode_weights()
-        from .chat_template import family_for
-        self.tokenizer = get_tokenizer(cfg.tokenizer, mcfg.vocab_size, mcfg.bos_token_id, mcfg.eos_token_id,
-                                       family_for(mcfg.name, mcfg.is_moe))
+        self.tokenizer = tokenizer_for(cfg, mcfg)
         rcfg = RunnerConfig(block_size=cfg.block_size, max_num_seqs=cfg.max_num_seqs,
                             max_num_batched_tokens=cfg.max_num_batched_tokens, max_model_len=cfg.max_model_len,
                             num_kv_blocks=cfg.num_kv_blocks, gpu_mem_fraction=cfg.gpu_mem_fraction,

@@ -19,7 +19,7 @@ import dataclasses
 import datetime
 import logging
 import os
-from typing import Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -96,9 +96,12 @@ def pick_backend(dev_type: str, n_dev: int, local_world: int, override: Optional
 
 
 def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backend: Optional[str] = None,
-                  timeout_s: float = 600.0) -> ParallelState:
+                  timeout_s: float = 600.0, tp_groups: Optional[List[List[int]]] = None) -> ParallelState:
     """Initialise from torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*).
-    Without WORLD_SIZE (or WORLD_SIZE=1) returns a single-process state and creates no group."""
+    Without WORLD_SIZE (or WORLD_SIZE=1) returns a single-process state and creates no group.
+    ``tp_groups``: explicit TP groups of consecutive ranks, possibly of different sizes (several
+    models behind one front end, adapters/local_llm.py plan_model_groups); ``tp`` is then this
+    rank's group size and ``dp`` counts the groups."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -109,16 +112,27 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
     dev = torch.device(f"cuda:{local % max(n_dev, 1)}") if device == "cuda" else torch.device(device)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    if world % tp:
-        raise ValueError(f"world size {world} not divisible by tp={tp}")
+    if tp_groups is not None:
+        if sorted(r for g in tp_groups for r in g) != list(range(world)) or any(
+                g != list(range(g[0], g[0] + len(g))) for g in tp_groups):
+            raise ValueError(f"tp_groups {tp_groups} must split ranks 0..{world - 1} into consecutive runs")
+        if ep != 1:
+            raise ValueError("explicit TP groups serve dense / TP-sharded models only (ep = 1)")
+        mine = next(g for g in tp_groups if rank in g)
+        tp = len(mine)
+    else:
+        if world % tp:
+            raise ValueError(f"world size {world} not divisible by tp={tp}")
+        tp_groups = [list(range(r * tp, (r + 1) * tp)) for r in range(world // tp)]
+        mine = tp_groups[rank // tp]
     dp_attn = tp == 1 and ep > 1
     if dp_attn and ep != world:
         raise ValueError(f"DP attention + EP needs ep == world size ({world}), got ep={ep}")
     if not dp_attn and ep not in (1, tp):
         raise ValueError("expert parallelism must be 1, equal to tp (EP inside the TP group), or the world size "
                          "with tp=1 (DP attention + expert all-to-all)")
-    st = ParallelState(world_size=world, rank=rank, local_rank=local, tp_size=tp, tp_rank=rank % tp,
-                       dp_size=world // tp, dp_rank=rank // tp, ep_size=ep,
+    st = ParallelState(world_size=world, rank=rank, local_rank=local, tp_size=tp, tp_rank=rank - mine[0],
+                       dp_size=len(tp_groups), dp_rank=tp_groups.index(mine), ep_size=ep,
                        ep_rank=rank if dp_attn else ((rank % tp) if ep > 1 else 0), device=dev)
     if world > 1:
         # POLYKEY_DIST_BACKEND overrides (gloo: several ranks on one GPU, which RCCL refuses)
@@ -137,9 +151,8 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
         st.world_cpu_group = dist.group.WORLD if be == "gloo" else dist.new_group(list(range(world)), backend="gloo")
         st.ranks_per_device = _ranks_on_my_device(st)
         st.shared_device = dev.type == "cuda" and st.ranks_per_device > 1
-        for r in range(world // tp):
-            ranks = list(range(r * tp, (r + 1) * tp))
-            g = dist.new_group(ranks) if tp < world else dist.group.WORLD
+        for ranks in tp_groups:  # every rank creates every group, in the same order (collective)
+            g = dist.new_group(ranks) if len(ranks) < world else dist.group.WORLD
             gc = dist.new_group(ranks, backend="gloo") if be != "gloo" else g
             if rank in ranks:
                 st.tp_group, st.tp_cpu_group = g, gc

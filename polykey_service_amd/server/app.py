@@ -171,14 +171,23 @@ class PolykeyServer:
 
 
 def build_service(cfg, logger: slog.Logger):
-    """Mock router, or router + on-node LLM backend (``cfg.backend == "local"``)."""
+    """Mock router, or router + on-node LLM backend (``cfg.backend == "local"``); None on the ranks
+    of a multi-model torchrun job that are not its front end (after they have been stopped)."""
     from ..service.router import ToolRouter
     from ..adapters.security.secret_store import SecretStore
 
     router = ToolRouter(secret_store=SecretStore.from_env())
     if cfg.backend == "local" and getattr(cfg, "serve_models", ""):
-        from ..adapters.local_llm import attach_models  # several models, one front end
-        attach_models(router, cfg, logger)
+        import os
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            # one process per GPU: every model on TP groups of its own, rank 0 the front end; the
+            # other ranks return here once the front end has stopped them (no server of their own)
+            from ..adapters.local_llm import attach_model_groups
+            if attach_model_groups(router, cfg, logger) is None:
+                return None
+        else:
+            from ..adapters.local_llm import attach_models  # several models, one front end
+            attach_models(router, cfg, logger)
     elif cfg.backend == "local":
         from ..adapters.local_llm import attach_local_llm
         attach_local_llm(router, cfg, logger)
@@ -198,6 +207,8 @@ async def amain(argv=None) -> int:
         from ..utils.metrics import Metrics
         metrics = Metrics.start(cfg.metrics_addr)
     service = build_service(cfg, logger)
+    if service is None:  # a model-group rank other than the front end: its engine has been stopped
+        return 0
     srv = PolykeyServer(service, logger, cfg.listen_addr, metrics=metrics, tls_cert=cfg.tls_cert,
                         tls_key=cfg.tls_key)
     await srv.start()
