@@ -321,7 +321,7 @@ def tp_broadcast_object(obj=None):
     if st.tp_size == 1:
         return obj
     lst = [obj]
-    src = st.dp_rank * st.tp_size
+    src = st.tp_leader
     dist.broadcast_object_list(lst, src=src, group=st.tp_cpu_group)
     return lst[0]
 
@@ -333,7 +333,7 @@ def tp_broadcast_tensor(t: torch.Tensor) -> torch.Tensor:
     rc = _direct(st.rccl_tp, t)
     if rc is not None and t.is_contiguous():
         return rc.broadcast(t, root=0)  # the group's first rank is its leader
-    dist.broadcast(t, src=st.dp_rank * st.tp_size, group=st.tp_cpu_group if not t.is_cuda else st.tp_group)
+    dist.broadcast(t, src=st.tp_leader, group=st.tp_cpu_group if not t.is_cuda else st.tp_group)
     return t
 
 

@@ -34,6 +34,7 @@ class ParallelState:
     local_rank: int = 0
     tp_size: int = 1
     tp_rank: int = 0
+    tp_leader: int = 0                     # global rank of this TP group's first rank (its leader)
     dp_size: int = 1
     dp_rank: int = 0
     ep_size: int = 1
@@ -132,6 +133,7 @@ def init_parallel(tp: int = 1, ep: int = 1, device: Optional[str] = None, backen
         raise ValueError("expert parallelism must be 1, equal to tp (EP inside the TP group), or the world size "
                          "with tp=1 (DP attention + expert all-to-all)")
     st = ParallelState(world_size=world, rank=rank, local_rank=local, tp_size=tp, tp_rank=rank - mine[0],
+                       tp_leader=mine[0],
                        dp_size=len(tp_groups), dp_rank=tp_groups.index(mine), ep_size=ep,
                        ep_rank=rank if dp_attn else ((rank % tp) if ep > 1 else 0), device=dev)
     if world > 1:

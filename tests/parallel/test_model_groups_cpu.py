@@ -12,6 +12,8 @@ import torch
 import torch.multiprocessing as mp
 
 SPEC = "tiny-llama-gqa4@0-1:tp2,tiny-llama@2"
+# the TP group away from rank 0: its leader is rank 1 (not dp_rank * tp_size)
+SPEC2 = "tiny-llama@0,tiny-llama-gqa4@1-2:tp2"
 PROMPTS = [[1, 5, 6, 7, 8, 9], [1] + list(range(20, 60)), [1, 2, 3]]
 MAXTOK = 5
 
@@ -24,13 +26,13 @@ def _port():
     return p
 
 
-def _cfg():
+def _cfg(spec=SPEC):
     from polykey_service_amd.config.server_config import ServerConfig
-    return ServerConfig(backend="local", serve_models=SPEC, device="cpu", max_num_seqs=8, max_num_batched_tokens=128,
+    return ServerConfig(backend="local", serve_models=spec, device="cpu", max_num_seqs=8, max_num_batched_tokens=128,
                         max_model_len=256, hip_graphs=False)
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, spec):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), POLYKEY_PREFLIGHT="0",
                       POLYKEY_DIST_BACKEND="gloo")
@@ -42,7 +44,7 @@ def _worker(rank, world, port, out):
     from polykey_service_amd.server.app import build_service
     from polykey_service_amd.utils import slog
     from tests.helpers import ServerThread
-    router = build_service(_cfg(), slog.Logger(open(os.devnull, "w")))
+    router = build_service(_cfg(spec), slog.Logger(open(os.devnull, "w")))
     if router is None:  # ranks 1 and 2: stopped by the front end
         destroy_parallel()
         return
@@ -66,13 +68,15 @@ def _worker(rank, world, port, out):
     destroy_parallel()
 
 
-def test_two_models_on_tp_groups_behind_one_front_end(tmp_path):
+@pytest.mark.parametrize("spec", [SPEC, SPEC2])
+def test_two_models_on_tp_groups_behind_one_front_end(tmp_path, spec):
     from polykey_service_amd.adapters.local_llm import plan_model_groups
     from polykey_service_amd.engine import EngineConfig, LLMEngine, SamplingParams
     from polykey_service_amd.parallel.state import ParallelState
     assert plan_model_groups(SPEC, 3) == [("tiny-llama-gqa4", [0, 1]), ("tiny-llama", [2])]
+    assert plan_model_groups(SPEC2, 3) == [("tiny-llama", [0]), ("tiny-llama-gqa4", [1, 2])]
     out = str(tmp_path / "fe.pt")
-    mp.start_processes(_worker, args=(3, _port(), out), nprocs=3, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(3, _port(), out, spec), nprocs=3, join=True, start_method="spawn")
     got = torch.load(out, weights_only=True)
     cfg = _cfg()
     for model in ("tiny-llama", "tiny-llama-gqa4"):
