@@ -555,15 +555,21 @@ class LlamaForCausalLM(nn.Module):
         if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, parts.shape[0]) and not self.st.shared_device:
             # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
             return gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, rs, ws, self._flow, ws_gu=self._ws_gu)
+        h = self._decode_gate_up(layer, residual, parts)
+        return gemm.linear_down(h, mlp.down, ws, mlp.down_p)  # tiled as the fused launch tiles it
+
+    def _decode_gate_up(self, layer, residual: torch.Tensor, parts: torch.Tensor) -> torch.Tensor:
+        """Folded-norm gate_up + SiLU of the two-launch decode MLP -> h [T, I] bf16."""
+        mlp = layer.mlp
+        rs = gemm.RowScale(parts, layer.eps)
         if residual.shape[0] > GATE_UP_SKINNY_MAX_M and not mlp.gate_up.is_meta:
             # hipBLASLt's MFMA GEMM wins on the 235 MB gate_up above 192 rows (67 vs 85 us at 256,
             # 97 vs 155 at 512: profiles/r4_wide_decode_probe.jsonl) even with the norm and SiLU as
             # separate kernels
             x = gemm.norm_apply(residual, parts, layer.ln2, layer.eps)
-            h = gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
-        else:  # split over K like the fused launch's gate_up when its n-blocks cannot fill the chip
-            h = gemm.linear_silu(residual, mlp.gate_up, ws=self._ws_gu, packed=mlp.gate_up_pf, rowscale=rs)
-        return gemm.linear_down(h, mlp.down, ws, mlp.down_p)  # tiled as the fused launch tiles it
+            return gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
+        # split over K like the fused launch's gate_up when its n-blocks cannot fill the chip
+        return gemm.linear_silu(residual, mlp.gate_up, ws=self._ws_gu, packed=mlp.gate_up_pf, rowscale=rs)
 
     def _forward_rowscale_tp(self, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
                              md: attn_ops.AttnMetadata, kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
@@ -583,13 +589,49 @@ class LlamaForCausalLM(nn.Module):
         launch (2 x 80 all-reduces per 70B TP=8 step)."""
         car = self.st.custom_ar
         for i, layer in enumerate(self.layers):
-            oph = None if layer.attn.fault_drop else self._o_phase(layer, residual, md)
+            at, mlp = layer.attn, layer.mlp
+            oph = None if at.fault_drop else self._o_phase(layer, residual, md)
             a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws, o=oph)
-            if not isinstance(a, gemm.Partial):
-                a = gemm.linear_partial(layer.attn.drop(a), layer.attn.o, ws, packed=layer.attn.o_p, half=True)
-            parts = car.reduce_residual(a, residual, buf2)
-            parts = car.reduce_residual(self._decode_mlp(layer, residual, parts, ws), residual, buf)
+            if isinstance(a, gemm.Partial):
+                parts = car.reduce_residual(a, residual, buf2)
+            else:
+                a = at.drop(a)
+                parts = self._tp_row_collective(
+                    lambda sig: gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True, signal=sig), residual, buf2)
+            if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, parts.shape[0]) and not self.st.shared_device:
+                parts = car.reduce_residual(self._decode_mlp(layer, residual, parts, ws), residual, buf)
+            else:
+                h = self._decode_gate_up(layer, residual, parts)
+                parts = self._tp_row_collective(
+                    lambda sig: gemm.linear_down(h, mlp.down, ws, mlp.down_p, signal=sig), residual, buf)
         return gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
+
+    def _tp_row_collective(self, launch, residual: torch.Tensor, buf: torch.Tensor) -> torch.Tensor:
+        """A row-parallel decode projection + its fused TP collective.  ``launch(signal)`` runs the
+        split-K GEMM and returns its gemm.Partial.  With gemm.TP_DECODE_CHUNKS > 1 the collective
+        is that many column-chunk collectives on the comm stream, started BEFORE the GEMM ends:
+        each waits for its chunk's tiles (gemm.ChunkSignal tickets), so the xGMI exchange of the
+        first chunks runs under the GEMM of the later ones (SURVEY.md §2.3 / BASELINE.json:5
+        "all-reduce over xGMI overlapped with the GEMMs"); the compute stream joins before the
+        residual's next reader.  Otherwise one collective after the GEMM."""
+        car = self.st.custom_ar
+        M, N = residual.shape
+        C = gemm.TP_DECODE_CHUNKS
+        flow = getattr(self, "_flow_tp", None)
+        if (C < 2 or flow is None or not residual.is_cuda or not hasattr(car, "reduce_residual_chunks")
+                or M > gemm.FUSED_MAX_M or not car.chunks_ok(M, N, C)):
+            return car.reduce_residual(launch(None), residual, buf)
+        main = torch.cuda.current_stream(residual.device)
+        cs = comm.comm_stream(residual.device)
+        ev = torch.cuda.Event()
+        ev.record(main)  # what the collective depends on (the previous collective runs on cs itself)
+        p = launch(gemm.ChunkSignal(flow, N // C))
+        need = int(round(p.tiles_per_col * (N // C)))
+        cs.wait_event(ev)
+        with torch.cuda.stream(cs):
+            parts = car.reduce_residual_chunks(p, residual, buf, C, flow, need)
+        main.wait_stream(cs)
+        return parts
 
     def workspace(self, M: int) -> Optional[torch.Tensor]:
         """fp32 split-K slab buffer for decode-sized batches (fixed address: graph-safe)."""
@@ -603,6 +645,8 @@ class LlamaForCausalLM(nn.Module):
             self._flow_qkv = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
             # the residual phase's hand-off (gemm.ResIn: phase 0 of either fused launch)
             self._flow_res = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
+            # TP: the row-parallel GEMMs' per-column-chunk tickets for the overlapped collective
+            self._flow_tp = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
             # the o-projection phase of the fused QKV -> attention launch (gemm.OProj): its own slab
             # buffer, hand-off buffer and the attention's in-launch partition-merge counters
             at = self.layers[0].attn

@@ -50,6 +50,11 @@ def _comm_stream(device: torch.device) -> "torch.cuda.Stream":
     return s
 
 
+def comm_stream(device: torch.device) -> "torch.cuda.Stream":
+    """The dedicated HIP stream collectives overlap compute on (one per device)."""
+    return _comm_stream(device)
+
+
 OVERLAP_MIN_ROWS = 256
 
 

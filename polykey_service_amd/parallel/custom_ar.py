@@ -42,6 +42,7 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_allgather.argtypes = [_P, _P, _P, _LL, _LL, _I, _P]
         lib.pk_car_reduce_residual.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _P]
         lib.pk_car_reduce_residual_nparts.argtypes = [_P, _I, _I]
+        lib.pk_car_reduce_residual_ex.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P]
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_clear_error.argtypes = [_P]
         lib.pk_car_set_error.argtypes = [_P]
@@ -164,6 +165,39 @@ class CustomAllReduce:
         if rc != 0:
             raise RuntimeError(f"fused TP reduce launch failed ({rc})")
         return parts.view(-1)[: nparts * M].view(nparts, M)
+
+    def chunks_ok(self, M: int, N: int, chunks: int) -> bool:
+        """Can the fused collective of an [M, N] residual run as ``chunks`` column chunks with the
+        same norm-parts layout as the whole (both forms: chunk widths multiples of 1024)?"""
+        if chunks < 2 or N % (1024 * chunks) or not self.supports_reduce_residual(M, N):
+            return False
+        return self.nparts(M, N // chunks) * chunks == self.nparts(M, N)
+
+    def reduce_residual_chunks(self, pending, residual: torch.Tensor, parts: torch.Tensor, chunks: int,
+                               flow: torch.Tensor, need: int) -> torch.Tensor:
+        """:meth:`reduce_residual` as ``chunks`` column-chunk collectives, each launched WITHOUT
+        waiting for the split-K GEMM that produces ``pending`` (a ``gemm.Partial``): chunk c's
+        workgroups wait for ``need`` tiles' tickets at ``flow[64 c]`` (the GEMM's
+        ``gemm.ChunkSignal``) and read the slabs as they land, so chunk c's xGMI exchange runs
+        under the GEMM of the later chunks (the TP decode collective overlapped
+        with its GEMM).  Same arithmetic per element as the whole: bit-identical."""
+        M, N = residual.shape
+        if not (residual.is_contiguous() and residual.dtype == torch.bfloat16 and self.chunks_ok(M, N, chunks)):
+            raise ValueError(f"reduce_residual_chunks: unsupported residual {tuple(residual.shape)} x {chunks}")
+        assert pending.M == M and pending.N == N and pending.S >= 1 and flow.dtype == torch.int32
+        Nc = N // chunks
+        npc = self.nparts(M, Nc)
+        assert parts.numel() >= npc * chunks * M and parts.dtype == torch.float32
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        fb = flow.data_ptr()
+        for c in range(chunks):
+            rc = self.lib.pk_car_reduce_residual_ex(
+                self.ctx, pending.buf.data_ptr() + c * Nc * 4, pending.S, None,
+                residual.data_ptr() + c * Nc * 2, parts.data_ptr() + c * npc * M * 4, M, Nc, N, self.fused_blocks,
+                fb + 4 * 64 * c, fb + 4 * (64 * 64 + 64 * c), int(need), stream)
+            if rc != 0:
+                raise RuntimeError(f"fused TP reduce (chunk {c}) launch failed ({rc})")
+        return parts.view(-1)[: npc * chunks * M].view(npc * chunks, M)
 
     def set_timeout(self, seconds: float) -> None:
         self.lib.pk_car_set_timeout_ms(self.ctx, max(1, int(seconds * 1000)))
