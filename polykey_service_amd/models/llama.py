@@ -89,7 +89,8 @@ def _proj_out(x: torch.Tensor, w: torch.Tensor, ws: Optional[torch.Tensor], wp: 
     if x.shape[0] > gemm.SKINNY_MAX_M:
         # prefill: the all-reduce of one row chunk overlaps the GEMM of the next
         return comm.tp_row_parallel_overlapped(x, w.shape[0],
-                                               lambda rows, out: gemm.linear(rows, w, out=out, packed=wp))
+                                               lambda rows, out: gemm.linear(rows, w, out=out, packed=wp),
+                                               chunks=comm.overlap_chunks(x.shape[0]))
     return comm.tp_all_reduce(_proj(x, w, ws, wp))
 
 
@@ -401,7 +402,7 @@ class LlamaForCausalLM(nn.Module):
 
         and the final-normed shard is all-gathered for the LM head."""
         T = input_ids.shape[0]
-        chunks = 2 if input_ids.is_cuda and T >= 2 * comm.OVERLAP_MIN_ROWS else 1
+        chunks = comm.overlap_chunks(T) if input_ids.is_cuda else 1
         lay = comm.SPLayout(T, chunks)
         emb = ops.embedding(input_ids, self.embed, self.vocab_start, self.vocab_local)
         residual = comm.sp_reduce_scatter(emb, lay)

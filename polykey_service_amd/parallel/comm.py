@@ -56,6 +56,17 @@ def comm_stream(device: torch.device) -> "torch.cuda.Stream":
 
 
 OVERLAP_MIN_ROWS = 256
+# row chunks of an overlapped prefill projection: with 2 at best half of each collective hides
+# under the next chunk's GEMM; 4 where every chunk keeps >= OVERLAP_MIN_ROWS rows
+OVERLAP_MAX_CHUNKS = int(os.environ.get("POLYKEY_OVERLAP_CHUNKS", "4"))
+
+
+def overlap_chunks(T: int) -> int:
+    """Row chunks for a T-token overlapped prefill collective (1: no overlap)."""
+    c = 1
+    while c * 2 <= OVERLAP_MAX_CHUNKS and T >= c * 2 * OVERLAP_MIN_ROWS:
+        c *= 2
+    return c
 
 
 def tp_row_parallel_overlapped(x: torch.Tensor, n_out: int, fn, chunks: int = 2,

@@ -35,3 +35,12 @@ def test_shards_partition_padded_rows(T, tp, chunks):
                 owner[row] = (r, slo + j)
         assert seen == lay.rows
     assert sorted(owner) == list(range(_layout(T, tp, 0, chunks).Tp))
+
+
+def test_overlap_chunks_grow_with_the_prefill():
+    """Prefill collectives overlap with up to 4 row chunks, each of >= OVERLAP_MIN_ROWS rows."""
+    from polykey_service_amd.parallel import comm
+    m = comm.OVERLAP_MIN_ROWS
+    assert comm.overlap_chunks(m) == 1 and comm.overlap_chunks(2 * m - 1) == 1
+    assert comm.overlap_chunks(2 * m) == 2 and comm.overlap_chunks(4 * m - 1) == 2
+    assert comm.overlap_chunks(4 * m) == 4 and comm.overlap_chunks(64 * m) == 4
