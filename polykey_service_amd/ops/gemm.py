@@ -585,10 +585,12 @@ def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_p
 
 
 # TP = 1 decode: every residual update runs as phase 0 of the fused launch that consumes it
-# (ResIn, csrc/kernels/phase.h) instead of a residual_parts launch of its own
-RES_PHASE = os.environ.get("POLYKEY_RES_PHASE", "1") == "1"
-# decode: the o-projection as phase 3 of the fused QKV -> attention launch (OProj)
-O_PHASE = os.environ.get("POLYKEY_O_PHASE", "1") == "1"
+# (ResIn, csrc/kernels/phase.h) instead of a residual_parts launch of its own.  Measured SLOWER
+# (8B step 4.12-4.16 vs 4.00-4.02 ms, profiles/r5_phase_ab.jsonl): off by default
+RES_PHASE = os.environ.get("POLYKEY_RES_PHASE", "0") == "1"
+# decode: the o-projection as phase 3 of the fused QKV -> attention launch (OProj).  Measured
+# slower too (+0.4 % on top of the residual phase; 70B TP=8 with the fused launch 7.86 vs 6.70 ms)
+O_PHASE = os.environ.get("POLYKEY_O_PHASE", "0") == "1"
 
 
 def res_workgroups(M: int, H: int) -> int:

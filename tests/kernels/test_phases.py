@@ -23,7 +23,9 @@ def rnd(*shape, scale=1.0):
 @pytest.mark.parametrize("M", [1, 17, 64, 128])
 @pytest.mark.parametrize("H,I", [(4096, 14336), (1024, 4096)])
 @pytest.mark.parametrize("S_o", [0, 2, 4])
-def test_mlp_fused_residual_phase(M, H, I, S_o):
+def test_mlp_fused_residual_phase(M, H, I, S_o, monkeypatch):
+    # (1024, 4096): gate_up split over K (kSiluSplit), which serving keeps on two launches
+    monkeypatch.setattr(gemm, "MLP_FUSED_SPLIT", True)
     nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
     wgu = gemm.interleave_gate_up(rnd(I, H, scale=0.05), rnd(I, H, scale=0.05))
     gup = gemm.pack_weight(gemm.fold_norm(wgu, nw))
@@ -31,6 +33,8 @@ def test_mlp_fused_residual_phase(M, H, I, S_o):
     nparts = H // gemm.PART_COLS
     assert gemm.mlp_fused_ok(rnd(M, H), gup, dp, nparts)
     S = gemm.choose_split(H, I, M)
+    Sg = gemm.gate_up_split(2 * I, H, M)
+    ws_gu = torch.empty(Sg * M * 2 * I, dtype=torch.float32, device="cuda") if Sg > 1 else None
     ws_a = torch.empty(S * M * H, dtype=torch.float32, device="cuda")
     ws_b = torch.empty_like(ws_a)
     flow_a = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda")
@@ -46,12 +50,12 @@ def test_mlp_fused_residual_phase(M, H, I, S_o):
             o = gemm.Partial(ob, S_o, M, H)
         r1 = res0.clone()
         p1 = gemm.residual_parts(o, r1, torch.empty(nparts * 128, device="cuda"))
-        exp = gemm.mlp_fused(r1, gup, dp, gemm.RowScale(p1, 1e-5), ws_a, flow_a).view().clone()
+        exp = gemm.mlp_fused(r1, gup, dp, gemm.RowScale(p1, 1e-5), ws_a, flow_a, ws_gu=ws_gu).view().clone()
         r2 = res0.clone()
         pbuf = torch.full((nparts * 128,), float("nan"), device="cuda")
         ws_b.fill_(float("nan"))
         ri = gemm.ResIn(o, r2, pbuf, flow_r)
-        got = gemm.mlp_fused(r2, gup, dp, None, ws_b, flow_b, res=ri, eps=1e-5).view()
+        got = gemm.mlp_fused(r2, gup, dp, None, ws_b, flow_b, ws_gu=ws_gu, res=ri, eps=1e-5).view()
         torch.testing.assert_close(got, exp, atol=0, rtol=0)
         assert torch.equal(r1, r2)
         torch.testing.assert_close(ri.parts_view(), p1, atol=0, rtol=0)

@@ -18,6 +18,12 @@ sys.path.insert(0, REPO)
 from polykey_service_amd._native.build import HIP_FLAGS, HIPCC  # noqa: E402
 
 VARIANTS = {
+    # timing only (NOT coherent): the residual-phase consumers read A / the row-scale parts with
+    # plain loads instead of sc1 loads -- what the sc1 hand-off of a widely re-read A costs
+    "res_plain": [("skinny_tile.h", "      if constexpr (kWait)  // the producers' output, handed off in-launch: sc1 loads",
+                   "      if constexpr (kWaitSlice)  // the producers' output, handed off in-launch: sc1 loads"),
+                  ("skinny_tile.h", "rs_p[h * kRsLoads + q] = kWaitRes ? ldf_sc1(args.nrm_parts, p) : *p;",
+                   "rs_p[h * kRsLoads + q] = *p;")],
     # the fused QKV -> attention launch without the K/V prefetch before the hand-off wait
     "pre0": [("decode_fused.hip", "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 2>(",
               "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 0>(")],
