@@ -398,6 +398,20 @@ PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, 
                        n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
 }
 
+// ... with counters ([n_seqs, n_kv] int32, zeroed once, re-armed by the kernel): the partitions of
+// a sequence are merged in-launch by the last one to arrive (no reduce kernel after)
+PK_EXPORT int pk_paged_decode_qkv2(void* out, const void* partial, int S, int M, const void* positions,
+                                   const void* cos_sin, const void* slots, void* k_cache, void* v_cache,
+                                   const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
+                                   void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks,
+                                   int out_stride, float scale, int max_ctx, hipStream_t stream) {
+  if (partial == nullptr || S < 1 || M < n_seqs) return -1;
+  QkvIn qi{static_cast<const float*>(partial), static_cast<const int*>(positions), static_cast<const float*>(cos_sin),
+           static_cast<const int*>(slots), S, M};
+  return decode_launch(out, nullptr, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, counters,
+                       n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
+}
+
 int pk_get_decode_z() { return g_decode_z; }  // the fused QKV -> attention launch (decode_fused.hip)
 
 PK_EXPORT int pk_set_decode_z(int z) {

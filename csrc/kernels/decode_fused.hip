@@ -87,7 +87,7 @@ __global__ void __launch_bounds__(256, 2) qkv_attn_fused_kernel(const GemmArgs q
     const int x = b % aa.n_kv, y = (b / aa.n_kv) % aa.n_seqs, z = b / (aa.n_kv * aa.n_seqs);
     decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 2>(
         aa.out, nullptr, aa.kc, aa.vc, aa.block_tables, aa.context_lens, aa.part_o, aa.part_ml,
-        OPH ? aa.counters : nullptr, aa.n_q, aa.n_kv, aa.bs, aa.max_blocks, 0, aa.out_stride, aa.n_parts, aa.scale2,
+        aa.counters, aa.n_q, aa.n_kv, aa.bs, aa.max_blocks, 0, aa.out_stride, aa.n_parts, aa.scale2,
         aa.qi, x, y, z, aa.z, lds.a, fa);
     if constexpr (OPH) o_signal(fo, os, x);  // (its barrier also frees the LDS for the o tile)
   }
@@ -150,8 +150,9 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   const int n_res = res != nullptr ? res_workgroups(ra) : 0;
   const Flow fres = res != nullptr ? res_flow(ra, n_qkv, err, fused_spin_limit()) : Flow{};
   // o_in (may be null): the o-projection phase -- its split-K slabs [o.S, M, o.N] of out @ Wo^T
-  // (packed W, 64-row n-blocks), out handed over in-launch; counters: [n_seqs, n_kv] zeroed
-  // (partitions merged in-launch; no reduce kernel after)
+  // (packed W, 64-row n-blocks), out handed over in-launch (needs counters when partitioned).
+  // counters (may be null): [n_seqs, n_kv] zeroed -- partitions merged in-launch by the last
+  // partition workgroup to arrive instead of by a reduce kernel after the launch
   const bool oph = o_in != nullptr;
   GemmArgs oa = oph ? *o_in : GemmArgs{};
   OSlices os{1, 1};
@@ -209,7 +210,7 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
     default: go_mt(std::integral_constant<int, 0>{}); break;
   }
   int rc = PK_CHECK_LAUNCH();
-  if (rc || n_parts == 1 || oph) return rc;  // (oph: merged in-launch)
+  if (rc || n_parts == 1 || counters != nullptr) return rc;  // (counters: partitions merged in-launch)
   if (P == kDecodePartSmall)
     paged_decode_reduce_kernel<kDecodePartSmall><<<dim3(n_q, n_seqs), 128, 0, stream>>>(
         static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),

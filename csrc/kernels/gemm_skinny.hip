@@ -499,6 +499,13 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
     case kQkvRope:
       if (a.counters == nullptr || a.N != (a.nq + 2 * a.nkv) * 128 || a.bs <= 0 || a.bs % 32) return -1;
       return norm ? launch_pk<kQkvRope, true>(a, packed, nt, stream) : launch_pk<kQkvRope, false>(a, packed, nt, stream);
+    case kSiluSplit:
+      // interleaved gate / up split over K, reduced in-launch by the last split of each n-block
+      // (SiLU applied there): folded-norm row scale, packed W, one 64-row tile, counters [N / 128]
+      if (norm || !packed || !a.row_scale || a.S < 2 || a.M > 64 || a.row_tiles > 1 || a.counters == nullptr ||
+          a.partial == nullptr || a.out == nullptr)
+        return -1;
+      return nt ? launch<kSiluSplit, true, false, true, true>(a, stream) : launch<kSiluSplit, true, false, false, true>(a, stream);
     default: return -1;
   }
 }

@@ -538,7 +538,9 @@ class LlamaForCausalLM(nn.Module):
             # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
             return gemm.qkv_attn_fused(residual, at.qkv_pf, rs, ws, positions, self.cos_sin, kc, vc, md, at.scale,
                                        at.nq, at.nkv, self._flow_qkv, o=o)
-        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, packed=at.qkv_pf)
+        # (64-row n-blocks at half the split: half the slabs the attention prologue sums -- the 70B
+        # TP=8 shard's 10 n-blocks otherwise take split 16)
+        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, packed=at.qkv_pf, half=gemm.QKV_HALF)
         if md.num_prefill == 0:
             return attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
         q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
@@ -570,7 +572,8 @@ class LlamaForCausalLM(nn.Module):
             x = gemm.norm_apply(residual, parts, layer.ln2, layer.eps)
             return gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
         # split over K like the fused launch's gate_up when its n-blocks cannot fill the chip
-        return gemm.linear_silu(residual, mlp.gate_up, ws=self._ws_gu, packed=mlp.gate_up_pf, rowscale=rs)
+        return gemm.linear_silu(residual, mlp.gate_up, ws=self._ws_gu, packed=mlp.gate_up_pf, rowscale=rs,
+                                counters=self._gu_counters)
 
     def _forward_rowscale_tp(self, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
                              md: attn_ops.AttnMetadata, kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
@@ -660,6 +663,10 @@ class LlamaForCausalLM(nn.Module):
             # slabs of a gate_up split over K (gemm.gate_up_split > 1: the 70B TP=8 shard)
             n = self._gate_up_split_elems()
             self._ws_gu = torch.empty(n, dtype=torch.float32, device=self.device) if n else None
+            # arrival counters of that gate_up's in-launch split-K reduction (gemm.GATE_UP_INLAUNCH)
+            gu = self.layers[0].mlp.gate_up if hasattr(self.layers[0].mlp, "gate_up") else None
+            self._gu_counters = (torch.zeros(gu.shape[0] // 128, dtype=torch.int32, device=self.device)
+                                 if n and gu is not None else None)
         return self._ws
 
     def _gate_up_split_elems(self) -> int:

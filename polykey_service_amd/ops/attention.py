@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from typing import Optional
 
 import torch
@@ -40,6 +41,11 @@ class AttnMetadata:
 
 
 _PART = 512  # must match kDecodePart in csrc/kernels/attention.hip
+# decode: a sequence's partitions merged by its last partition workgroup (in-launch) instead of a
+# reduce launch after the attention (the engine passes AttnMetadata.decode_counters).  Measured
+# slower: 70B TP=8 per-rank step 7.21 vs 6.68 ms (the merge's release / acquire fences,
+# profiles/r5_tp_ab.jsonl) -- off by default
+INLAUNCH_MERGE = os.environ.get("POLYKEY_DECODE_INLAUNCH_MERGE", "0") == "1"
 _PART_MIN = 128  # kDecodePartSmall: launches whose (seq, kv head) pairs cannot fill the chip
 
 
@@ -145,6 +151,14 @@ def paged_decode_from_qkv(p, positions: torch.Tensor, cos_sin: torch.Tensor, k_c
     T = p.M
     out = torch.empty((T, nq * 128), dtype=torch.bfloat16, device=p.buf.device)
     bt = md.decode_block_tables
+    if md.decode_counters is not None:  # partitions merged in-launch (no reduce kernel after)
+        native.call("pk_paged_decode_qkv2", out.data_ptr(), p.buf.data_ptr(), p.S, p.M, positions.data_ptr(),
+                    cos_sin.data_ptr(), md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                    bt.data_ptr(), md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,
+                    native.ptr(md.decode_part_ml) or 0, md.decode_counters.data_ptr(), md.num_decode, nq, nkv,
+                    k_cache.shape[2], bt.stride(0), out.stride(0), float(scale), int(md.decode_max_ctx),
+                    native.stream_ptr())
+        return out
     native.call("pk_paged_decode_qkv", out.data_ptr(), p.buf.data_ptr(), p.S, p.M, positions.data_ptr(),
                 cos_sin.data_ptr(), md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                 bt.data_ptr(), md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,

@@ -48,10 +48,17 @@ MLP_FUSED_SPLIT = os.environ.get("POLYKEY_MLP_FUSED_SPLIT", "0") == "1"
 # waits for the whole projection and the launch measured slower (26.6 vs ~20 us per layer at
 # 70B TP=8, profiles/r4_tp_solo.md)
 QKV_ATTN_MIN_KV = int(os.environ.get("POLYKEY_QKV_MIN_KV", "4"))
+# the two-launch decode QKV (TP shards with few kv heads) as 64-row n-blocks at half the split:
+# half the fp32 slabs the attention prologue sums (70B TP=8: 6.66-6.67 vs 6.68 ms, neutral)
+QKV_HALF = os.environ.get("POLYKEY_QKV_HALF", "1") == "1"
 PACKED_BIT = 16
 
 
-MODE_BF16, MODE_PARTIAL, MODE_SILU, MODE_ADD_RES_NORM, MODE_QKV_ROPE = 0, 1, 2, 3, 4
+MODE_BF16, MODE_PARTIAL, MODE_SILU, MODE_ADD_RES_NORM, MODE_QKV_ROPE, MODE_SILU_SPLIT = 0, 1, 2, 3, 4, 5
+# a decode gate_up split over K (70B TP=8: 56 n-blocks) reduced + SiLU'd in-launch by the last split
+# of each n-block (MODE_SILU_SPLIT) instead of by a splitk_reduce launch after it.  Measured slower
+# (70B TP=8 per-rank step 6.78 vs 6.68 ms, profiles/r5_tp_ab.jsonl): off by default
+GATE_UP_INLAUNCH = os.environ.get("POLYKEY_GATE_UP_INLAUNCH", "0") == "1"
 NORM_BIT = 32
 
 
@@ -392,7 +399,8 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
 
 def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[torch.Tensor] = None,
                 packed: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None,
-                rowscale: Optional[RowScale] = None, max_m: int = SKINNY_MAX_M) -> torch.Tensor:
+                rowscale: Optional[RowScale] = None, max_m: int = SKINNY_MAX_M,
+                counters: Optional[torch.Tensor] = None) -> torch.Tensor:
     """silu(x @ Wg^T) * (x @ Wu^T) with interleaved gate/up rows → [M, I].  With ``norm``,
     ``x`` is the residual stream and the RMSNorm is applied in the kernel's prologue (S = 1);
     with ``rowscale`` the norm is folded (W pre-multiplied, rows scaled in the epilogue)."""
@@ -402,6 +410,13 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
         Sg = gate_up_split(N, K, M) if rowscale is not None and M <= FUSED_MAX_M else 1
         if Sg > 1 and ws is not None and ws.numel() >= Sg * M * N:
+            if (GATE_UP_INLAUNCH and counters is not None and packed is not None and M <= SKINNY_MAX_M
+                    and counters.numel() >= N // 128):
+                # the last split of each n-block sums the slabs and applies SiLU in the same launch
+                # (the fused MLP's kSiluSplit epilogue; bit-identical to the reduce launch)
+                _launch_ex(MODE_SILU_SPLIT, x, w_gu_interleaved, packed, Sg, out=out, ws=ws, counters=counters,
+                           rowscale=rowscale)
+                return out
             # split over K like the fused MLP's gate_up (bit-identical: the same slabs, summed in
             # split order, the same SiLU arithmetic)
             p = linear_partial_rowscale(x, w_gu_interleaved, ws, rowscale, S=Sg, packed=packed)
@@ -718,7 +733,7 @@ def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: Optional
                 native.ptr(md.decode_part_ml) or 0, nq, nkv, k_cache.shape[2], bt.stride(0), out.stride(0),
                 float(scale), int(md.decode_max_ctx), flow.data_ptr(), ctypes.byref(ra) if ra is not None else None,
                 ctypes.byref(oa) if oa is not None else None, o.flow.data_ptr() if o is not None else None,
-                o.counters.data_ptr() if o is not None else None, native.stream_ptr())
+                o.counters.data_ptr() if o is not None else native.ptr(md.decode_counters), native.stream_ptr())
     return op if op is not None else out
 
 

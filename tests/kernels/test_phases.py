@@ -187,3 +187,61 @@ def test_qkv_attn_fused_o_phase(nq, nkv, H, No, ctxs, with_res):
     for f in (fa, fb, fo, fr):
         assert int(f.abs().sum()) == 0, f.nonzero().tolist()
     assert int(ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("nq,nkv,S", [(8, 1, 8), (8, 1, 16), (32, 8, 4)])
+@pytest.mark.parametrize("ctxs", [[384] * 64, [600, 1300, 7, 2100, 1], [1, 5, 33, 300]])
+def test_decode_inlaunch_partition_merge(nq, nkv, S, ctxs):
+    """Decode attention from QKV slabs with the partitions merged by the last partition workgroup
+    to arrive (AttnMetadata.decode_counters) is bit-identical to the merge by a reduce launch."""
+    d, bs = "cuda", 32
+    B = len(ctxs)
+    N = (nq + 2 * nkv) * HD
+    max_blocks = (max(ctxs) + bs - 1) // bs + 3
+    nb = sum((c + bs - 1) // bs for c in ctxs) + 4
+    bt = _block_tables(ctxs, bs, nb, max_blocks).to(d)
+    cl = torch.tensor(ctxs, dtype=torch.int32, device=d)
+    pos = cl - 1
+    slots = (bt.gather(1, ((cl - 1) // bs).long()[:, None])[:, 0] * bs + (cl - 1) % bs).to(torch.int32)
+    cs = ref.rope_cos_sin_cache(4096, HD, 500000.0).to(d)
+    po, pml = A.decode_workspace(B, nq, max_blocks, bs, d, kv_heads=nkv)
+    ctr = torch.zeros((B, nkv), dtype=torch.int32, device=d)
+    k0 = torch.randn(nb, nkv, bs, HD, device=d).to(torch.bfloat16)
+    v0 = torch.randn(nb, nkv, HD, bs, device=d).to(torch.bfloat16)
+    k1, v1, k2, v2 = k0.clone(), v0.clone(), k0.clone(), v0.clone()
+    for it in range(3):
+        ws = torch.randn(S * B * N, device=d) * (0.5 / S)
+        p = gemm.Partial(ws, S, B, N)
+        outs = []
+        for counters, (kc, vc) in ((None, (k1, v1)), (ctr, (k2, v2))):
+            md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0,
+                                slot_mapping=slots, decode_block_tables=bt, decode_context_lens=cl, decode_part_o=po,
+                                decode_part_ml=pml, decode_counters=counters)
+            outs.append(A.paged_decode_from_qkv(p, pos, cs, kc, vc, md, 1 / math.sqrt(HD), nq, nkv))
+        torch.testing.assert_close(outs[1], outs[0], atol=0, rtol=0)
+        assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    torch.cuda.synchronize()
+    assert int(ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("H,I", [(8192, 3584), (1024, 4096)])
+def test_gate_up_split_inlaunch_silu(M, H, I):
+    """A decode gate_up split over K (70B TP=8: 56 n-blocks, split 4) with the slabs summed and
+    SiLU applied by the last split of each n-block (MODE_SILU_SPLIT) equals the splitk_reduce launch."""
+    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wgu = gemm.interleave_gate_up(rnd(I, H, scale=0.05), rnd(I, H, scale=0.05))
+    gup = gemm.pack_weight(gemm.fold_norm(wgu, nw))
+    Sg = gemm.gate_up_split(2 * I, H, M)
+    assert Sg > 1
+    ws = torch.empty(Sg * M * 2 * I, dtype=torch.float32, device="cuda")
+    ctr = torch.zeros(2 * I // 128, dtype=torch.int32, device="cuda")
+    for it in range(4):
+        res = rnd(M, H)
+        parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
+        rs = gemm.RowScale(parts, 1e-5)
+        exp = gemm.linear_silu(res, wgu, ws=ws, packed=gup, rowscale=rs)
+        got = gemm.linear_silu(res, wgu, ws=ws, packed=gup, rowscale=rs, counters=ctr)
+        torch.testing.assert_close(got, exp, atol=0, rtol=0)
+    torch.cuda.synchronize()
+    assert int(ctr.abs().sum()) == 0

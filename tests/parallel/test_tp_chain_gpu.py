@@ -73,6 +73,9 @@ def test_tp8_shard_fused_chain_bit_identical_to_two_launches(monkeypatch):
         # QKV_ATTN_MIN_KV); the launches must still be exact where they are allowed
         monkeypatch.setattr(gemm, "MLP_FUSED_SPLIT", True)
         monkeypatch.setattr(gemm, "QKV_ATTN_MIN_KV", 1)
+        # the fused launch's QKV tiles are 128-row n-blocks at the full split: compare with the same
+        # tiling (the two-launch chain's half-split QKV sums its slabs in another grouping)
+        monkeypatch.setattr(gemm, "QKV_HALF", False)
         outs = []
         for fused in (False, True):
             gemm.MLP_FUSED = gemm.QKV_ATTN_FUSED = fused

@@ -91,10 +91,12 @@ def main():
     cl = torch.full((B,), a.ctx, dtype=torch.int32, device=dev)
     pos = cl - 1
     slots = bt[:, (a.ctx - 1) // BS] * BS + (a.ctx - 1) % BS
-    po, pml = A.decode_workspace(B, at.nq, maxb, BS, dev)
+    po, pml = A.decode_workspace(B, at.nq, maxb, BS, dev, kv_heads=at.nkv)
+    # the engine's metadata (engine/model_runner.py): in-launch partition merge counters
+    ctr = torch.zeros((B, at.nkv), dtype=torch.int32, device=dev) if A.INLAUNCH_MERGE and po is not None else None
     md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0, slot_mapping=slots,
                         decode_block_tables=bt, decode_context_lens=cl, decode_part_o=po, decode_part_ml=pml,
-                        decode_max_ctx=A._PART if a.ctx <= A._PART else 0)
+                        decode_counters=ctr, decode_max_ctx=A._PART if a.ctx <= A._PART else 0)
     ids = torch.randint(0, cfg.vocab_size, (B,), dtype=torch.int32, device=dev)
 
     def step():
@@ -130,7 +132,8 @@ def main():
                       "ms_per_step": round(ms, 3), "us_per_layer": round(ms * 1000 / cfg.num_layers, 2),
                       "graph": not a.eager, "init_s": round(init_s, 1),
                       "mlp_fused": os.environ.get("POLYKEY_MLP_FUSED", "1"),
-                      "qkv_attn_fused": os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1")}), flush=True)
+                      "qkv_attn_fused": os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1"),
+                      "env": {k: v for k, v in os.environ.items() if k.startswith("POLYKEY_")}}), flush=True)
 
 
 if __name__ == "__main__":
