@@ -93,53 +93,6 @@ __device__ __forceinline__ void spin_wait(uint32_t* flag, uint32_t e, Signals* m
   }
 }
 
-// The fused collective overlapped with its GEMM: the row-parallel projection's
-// split-K tiles run on the compute stream and take one ticket per finished tile on the column
-// chunk they belong to (ready[64 * chunk], write-through slab stores); this chunk's collective,
-// launched on the comm stream without waiting for the GEMM, starts its workgroups at once, and
-// one lane of each polls the chunk's tickets (bounded by the same wall-clock timeout) before the
-// workgroup reads the slabs with sc1 loads.  The chunk's last workgroup past the wait re-arms both
-// counters (a graph replay starts from zero).
-struct LocalWait {
-  int* ready;  // null: the slabs were finished before this launch (no wait, plain loads)
-  int* done;
-  int need;    // GEMM tiles of this column chunk
-};
-
-__device__ __forceinline__ bool local_wait(const LocalWait& w, Signals* my_sig, const Fail& f) {
-  __shared__ uint32_t lbad_s;
-  if (threadIdx.x == 0) {
-    lbad_s = 0u;
-    const long long t0 = wall_clock64();
-    uint32_t it = 0;
-    while (__hip_atomic_load(w.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < w.need) {
-      __builtin_amdgcn_s_sleep(2);
-      if ((++it & 255u) == 0 && wall_clock64() - t0 > f.timeout) {
-        __hip_atomic_store(&my_sig->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(f.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        lbad_s = 1u;
-        break;
-      }
-    }
-    if (__hip_atomic_fetch_add(w.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == static_cast<int>(gridDim.x) - 1) {
-      __hip_atomic_store(w.ready, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(w.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  return lbad_s == 0u;
-}
-
-// 16-byte load of slab element `off` (floats): sc1 when handed over in-launch-style by a running GEMM
-template <bool SC1>
-__device__ __forceinline__ float4 ld_slab(const float* slabs, int64_t off) {
-  if constexpr (SC1)
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(slabs), static_cast<short>(0), 0x7ffffff0, 0x00020000),
-        static_cast<int>(off * 4), 0, 16));
-  return *reinterpret_cast<const float4*>(slabs + off);
-}
-
 // Call epilogue: workgroup b stores the call's epoch into entries b, b + nb, ... of the epoch
 // array, so every entry holds the same value whatever grid the next call launches.
 __device__ __forceinline__ void end_call(Signals* my_sig, uint32_t e) {
@@ -387,15 +340,15 @@ __device__ __forceinline__ float wave_sum64(float v) {
   return v;
 }
 
-// ld: row stride of the slabs / residual / partial (>= N: a column chunk of a wider projection,
-// the slabs [S, M, ld]); lw.ready != null: wait for the GEMM's tiles of this chunk first (SC1).
-template <int W, bool SC1 = false>
+// ld: row stride of the residual / partial (>= N: a column chunk of a wider residual); lds: row
+// stride of the slabs [S, M, lds] (a chunk's own GEMM: lds = N).
+template <int W>
 __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __restrict__ peers, int rank,
                                                                size_t data_bytes, const float* __restrict__ slabs,
                                                                int S, const uint4* __restrict__ partial,
                                                                uint16_t* __restrict__ residual,
                                                                float* __restrict__ parts, int M, int N, int ld,
-                                                               const Fail fail, const LocalWait lw) {
+                                                               int lds, const Fail fail) {
   const int b = blockIdx.x, nb = gridDim.x;
   Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
   __shared__ uint32_t e_s, err_s;
@@ -410,21 +363,20 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
   const size_t slot = kSigBytes + (e & 1u) * data_bytes;
   const int nchunk = N >> 10;
   const int items = M * nchunk;
-  const int64_t slab = static_cast<int64_t>(M) * ld;
+  const int64_t slab = static_cast<int64_t>(M) * lds;
   uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + slot);
-  if constexpr (SC1)
-    if (!local_wait(lw, my_sig, fail)) return;
   // 1. local split-K reduction -> bf16 partial in this rank's slot (slot rows of N, source rows of ld)
   for (int it = b; it < items; it += nb) {
     const int r = it / nchunk, c = it - r * nchunk;
     const int64_t off = static_cast<int64_t>(r) * N + (c << 10) + threadIdx.x * 8;  // element offset
     const int64_t goff = static_cast<int64_t>(r) * ld + (c << 10) + threadIdx.x * 8;
+    const int64_t soff = static_cast<int64_t>(r) * lds + (c << 10) + threadIdx.x * 8;
     uint4 pk;
     if (S > 0) {
       float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       for (int sidx = 0; sidx < S; ++sidx) {
-        const float4 p0 = ld_slab<SC1>(slabs, sidx * slab + goff);
-        const float4 p1 = ld_slab<SC1>(slabs, sidx * slab + goff + 4);
+        const float4 p0 = *reinterpret_cast<const float4*>(slabs + sidx * slab + soff);
+        const float4 p1 = *reinterpret_cast<const float4*>(slabs + sidx * slab + soff + 4);
         a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w;
         a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
       }
@@ -500,13 +452,13 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
 // owner's bits.
 constexpr int kRrChunk = 256;
 
-template <int W, bool SC1 = false>
+template <int W>
 __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPtrs* __restrict__ peers, int rank,
                                                                      size_t data_bytes, const float* __restrict__ slabs,
                                                                      int S, const uint4* __restrict__ partial,
                                                                      uint16_t* __restrict__ residual,
                                                                      float* __restrict__ parts, int M, int N, int ld,
-                                                                     const Fail fail, const LocalWait lw) {
+                                                                     int lds, const Fail fail) {
   const int b = blockIdx.x, nb = gridDim.x;
   Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
   __shared__ uint32_t e_s, err_s;
@@ -521,12 +473,10 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
   const size_t res_slot = kSigBytes + (2 + (e & 1u)) * data_bytes;
   const int nchunk = N / kRrChunk, ngroups = nchunk / W;
   const int items = M * ngroups;
-  const int64_t slab = static_cast<int64_t>(M) * ld;
+  const int64_t slab = static_cast<int64_t>(M) * lds;
   const int64_t parts_off = static_cast<int64_t>(M) * N * 2;  // byte offset of the parts in a result slot
   uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + in_slot);
   const int t = threadIdx.x;
-  if constexpr (SC1)
-    if (!local_wait(lw, my_sig, fail)) return;
   // 0. stage the local partial of every chunk of my items (W chunks x 256 columns = 32 W uint4)
   for (int it = b; it < items; it += nb) {
     const int r = it / ngroups, j = it - r * ngroups;
@@ -534,12 +484,13 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
       const int c = j * W + u / 32;
       const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + (u % 32) * 8;  // element offset
       const int64_t goff = static_cast<int64_t>(r) * ld + c * kRrChunk + (u % 32) * 8;
+      const int64_t soff = static_cast<int64_t>(r) * lds + c * kRrChunk + (u % 32) * 8;
       uint4 pk;
       if (S > 0) {
         float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         for (int sidx = 0; sidx < S; ++sidx) {
-          const float4 p0 = ld_slab<SC1>(slabs, sidx * slab + goff);
-          const float4 p1 = ld_slab<SC1>(slabs, sidx * slab + goff + 4);
+          const float4 p0 = *reinterpret_cast<const float4*>(slabs + sidx * slab + soff);
+          const float4 p1 = *reinterpret_cast<const float4*>(slabs + sidx * slab + soff + 4);
           a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w;
           a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
         }
@@ -833,35 +784,28 @@ PK_EXPORT int pk_car_reduce_residual_nparts(void* ctx, int M, int N) {
 }
 
 PK_EXPORT int pk_car_reduce_residual_ex(void* ctx, const void* slabs, int S, const void* partial, void* residual,
-                                        void* parts, int M, int N, int ld, int blocks, int* ready, int* done,
-                                        int need, hipStream_t stream);
+                                        void* parts, int M, int N, int ld, int lds, int blocks, hipStream_t stream);
 
 PK_EXPORT int pk_car_reduce_residual(void* ctx, const void* slabs, int S, const void* partial, void* residual,
                                      void* parts, int M, int N, int blocks, hipStream_t stream) {
-  return pk_car_reduce_residual_ex(ctx, slabs, S, partial, residual, parts, M, N, N, blocks, nullptr, nullptr, 0,
-                                   stream);
+  return pk_car_reduce_residual_ex(ctx, slabs, S, partial, residual, parts, M, N, N, N, blocks, stream);
 }
 
-// The same collective over a column chunk [M, N] of a wider projection: slabs [S, M, ld] /
-// residual [M, ld] / partial [M, ld] pointers already offset to the chunk's first column, parts
-// offset to its first part row.  ready != null (the overlapped form, LocalWait): the GEMM that
-// produces the slabs may still be running -- wait for `need` tickets at ready[0] (its tiles of
-// this chunk; done[0] the re-arm count) and read the slabs with sc1 loads.
+// The same collective over a column chunk [M, N] of a wider residual (row stride ld) -- the TP
+// decode collective overlapped with its GEMM runs one per column chunk on the comm stream while
+// the compute stream runs the GEMM of the next chunk (parallel/custom_ar.py reduce_residual_chunk):
+// residual / partial pointers offset to the chunk's first column, parts to its first part row,
+// slabs [S, M, lds] (the chunk GEMM's own, lds = N).
 PK_EXPORT int pk_car_reduce_residual_ex(void* ctx, const void* slabs, int S, const void* partial, void* residual,
-                                        void* parts, int M, int N, int ld, int blocks, int* ready, int* done,
-                                        int need, hipStream_t stream) {
+                                        void* parts, int M, int N, int ld, int lds, int blocks, hipStream_t stream) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (c == nullptr || c->d_peers == nullptr) return -1;
   if (M <= 0) return 0;
-  if (N <= 0 || N % 1024 || ld < N || ld % 8 || S < 0 || (S == 0 && partial == nullptr) ||
-      (S > 0 && slabs == nullptr) || residual == nullptr || parts == nullptr ||
-      (ready != nullptr && (done == nullptr || need <= 0 || S == 0 ||
-                            static_cast<size_t>(S) * M * ld * 4 >= (static_cast<size_t>(1) << 31))))
+  if (N <= 0 || N % 1024 || ld < N || ld % 8 || lds < N || lds % 8 || S < 0 || (S == 0 && partial == nullptr) ||
+      (S > 0 && slabs == nullptr) || residual == nullptr || parts == nullptr)
     return -2;
   if (static_cast<size_t>(M) * N * 2 > c->data_bytes) return -2;
   const Fail fail{c->d_err, c->timeout_ticks};
-  const LocalWait lw{ready, done, need};
-  const bool sc1 = ready != nullptr;
   const float* sl = static_cast<const float*>(slabs);
   const uint4* pt = static_cast<const uint4*>(partial);
   uint16_t* rs = static_cast<uint16_t*>(residual);
@@ -873,12 +817,8 @@ PK_EXPORT int pk_car_reduce_residual_ex(void* ctx, const void* slabs, int S, con
     switch (c->world) {
 #define PK_CRR2_CASE(WW)                                                                                       \
   case WW:                                                                                                   \
-    if (sc1)                                                                                                 \
-      reduce_residual_2shot_kernel<WW, true><<<nb, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, sl, S, pt, \
-                                                                     rs, ps, M, N, ld, fail, lw);             \
-    else                                                                                                     \
-      reduce_residual_2shot_kernel<WW, false><<<nb, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, sl, S,  \
-                                                                      pt, rs, ps, M, N, ld, fail, lw);        \
+    reduce_residual_2shot_kernel<WW><<<nb, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, sl, S, pt, rs, ps, \
+                                                             M, N, ld, lds, fail);                            \
     break;
       PK_CRR2_CASE(4)
       PK_CRR2_CASE(5)
@@ -896,12 +836,8 @@ PK_EXPORT int pk_car_reduce_residual_ex(void* ctx, const void* slabs, int S, con
   switch (c->world) {
 #define PK_CRR_CASE(WW)                                                                                          \
   case WW:                                                                                                     \
-    if (sc1)                                                                                                   \
-      reduce_residual_kernel<WW, true><<<blocks, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, sl, S, pt, rs, \
-                                                                   ps, M, N, ld, fail, lw);                    \
-    else                                                                                                       \
-      reduce_residual_kernel<WW, false><<<blocks, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, sl, S, pt,    \
-                                                                    rs, ps, M, N, ld, fail, lw);               \
+    reduce_residual_kernel<WW><<<blocks, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, sl, S, pt, rs, ps, M, \
+                                                           N, ld, lds, fail);                                  \
     break;
     PK_CRR_CASE(2)
     PK_CRR_CASE(3)

@@ -34,16 +34,6 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
   skinny_tile<MT, MODE, PK, NORM, NT, RS, KR>(args, blockIdx.x, blockIdx.y, gridDim.x, lds, Flow{});
 }
 
-// Split-K slabs of a row-parallel TP projection whose collective overlaps it:
-// write-through slab stores and one ticket per finished tile on the column chunk of its n-block
-// (flow slice = n-block columns / cols_per_slice); the chunk's fused collective
-// (csrc/comm/custom_allreduce.hip LocalWait), launched on the comm stream, starts on the tickets.
-template <int MT, int KR>
-__global__ void __launch_bounds__(256, 2) skinny_partial_signal_kernel(const GemmArgs args, const Flow fl) {
-  __shared__ SkinnyLds<MT> lds;
-  skinny_tile<MT, kPartial, true, false, false, false, KR, 1>(args, blockIdx.x, 0, gridDim.x, lds, fl);
-}
-
 // Fused decode MLP (M <= 64): gate_up + SiLU (folded norm, non-temporal packed W) and the down
 // projection's split-K slabs in ONE launch of max(gate_up tiles, down tiles) workgroups, one per
 // CU: workgroup b runs gate_up tile b (if any), then down tile b (if any).  A down tile streams
@@ -610,42 +600,6 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
 }
 
 PK_EXPORT int pk_flow_words() { return kFlowWords; }
-
-// a.partial <- slabs [S, M, N] of A @ W^T (packed W, M <= 128: one row tile; half: 64-row n-blocks)
-// with one ticket per tile at flow[64 * (n-block columns / cols_per_slice)] (<= 64 chunks).
-PK_EXPORT int pk_skinny_partial_signal(const GemmArgs* in, int half, int* flow, int cols_per_slice,
-                                       hipStream_t stream) {
-  GemmArgs a = *in;
-  if (a.M <= 0) return 0;
-  const int KR = half ? 1 : 2;
-  if (a.M > 128 || a.partial == nullptr || a.W == nullptr || a.S < 1 || a.K % (kKC * a.S) || a.lda % 8 ||
-      a.N % (64 * KR) || cols_per_slice <= 0 || cols_per_slice % (64 * KR) || a.N % cols_per_slice ||
-      a.N / cols_per_slice > 64 || flow == nullptr || a.row_scale || a.row_offsets != nullptr)
-    return -1;
-  a.row_tiles = 1;
-  a.tile_rows = a.M > 64 ? 128 : 64;
-  a.max_group_rows = 0;
-  int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
-  const Flow fl{flow, flow + 64 * kFlowPad, err, 0, 0, cols_per_slice, 1, 0, 0, fused_spin_limit()};
-  const dim3 grid((a.N / (64 * KR)) * a.S);
-#define PK_SPS(MT, KK) skinny_partial_signal_kernel<MT, KK><<<grid, 256, 0, stream>>>(a, fl)
-#define PK_SPS_MT(KK)                        \
-  switch ((a.M + 15) / 16) {                 \
-    case 1: PK_SPS(1, KK); break;            \
-    case 2: PK_SPS(2, KK); break;            \
-    case 3: PK_SPS(3, KK); break;            \
-    case 4: PK_SPS(4, KK); break;            \
-    default: PK_SPS(8, KK); break;           \
-  }
-  if (half) {
-    PK_SPS_MT(1)
-  } else {
-    PK_SPS_MT(2)
-  }
-#undef PK_SPS_MT
-#undef PK_SPS
-  return PK_CHECK_LAUNCH();
-}
 
 static int* g_fused_err = nullptr;
 int* fused_err_word() { return g_fused_err; }

@@ -599,43 +599,55 @@ class LlamaForCausalLM(nn.Module):
             if isinstance(a, gemm.Partial):
                 parts = car.reduce_residual(a, residual, buf2)
             else:
-                a = at.drop(a)
-                parts = self._tp_row_collective(
-                    lambda sig: gemm.linear_partial(a, at.o, ws, packed=at.o_p, half=True, signal=sig), residual, buf2)
+                parts = self._tp_row_collective(at.drop(a), at.o, at.o_p, ws, residual, buf2)
             if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, parts.shape[0]) and not self.st.shared_device:
                 parts = car.reduce_residual(self._decode_mlp(layer, residual, parts, ws), residual, buf)
             else:
                 h = self._decode_gate_up(layer, residual, parts)
-                parts = self._tp_row_collective(
-                    lambda sig: gemm.linear_down(h, mlp.down, ws, mlp.down_p, signal=sig), residual, buf)
+                parts = self._tp_row_collective(h, mlp.down, mlp.down_p, ws, residual, buf, down=True)
         return gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
 
-    def _tp_row_collective(self, launch, residual: torch.Tensor, buf: torch.Tensor) -> torch.Tensor:
-        """A row-parallel decode projection + its fused TP collective.  ``launch(signal)`` runs the
-        split-K GEMM and returns its gemm.Partial.  With gemm.TP_DECODE_CHUNKS > 1 the collective
-        is that many column-chunk collectives on the comm stream, started BEFORE the GEMM ends:
-        each waits for its chunk's tiles (gemm.ChunkSignal tickets), so the xGMI exchange of the
-        first chunks runs under the GEMM of the later ones (SURVEY.md §2.3 / BASELINE.json:5
-        "all-reduce over xGMI overlapped with the GEMMs"); the compute stream joins before the
-        residual's next reader.  Otherwise one collective after the GEMM."""
+    def _tp_row_collective(self, x: torch.Tensor, w: torch.Tensor, wp: Optional[torch.Tensor], ws: torch.Tensor,
+                           residual: torch.Tensor, buf: torch.Tensor, down: bool = False) -> torch.Tensor:
+        """A row-parallel decode projection x @ w^T + its fused TP collective (custom_ar
+        reduce_residual: slab sum, xGMI exchange, residual add, norm parts) -> the parts.
+
+        With gemm.TP_DECODE_CHUNKS = C > 1 the projection runs as C column-chunk GEMMs on the
+        compute stream (w's packed rows are n-block-major, so a chunk is a contiguous row range);
+        after each, an event forks the chunk's collective onto the comm stream, so the xGMI
+        exchange of chunk c runs while the compute stream computes chunk c + 1 (SURVEY.md §2.3 /
+        BASELINE.json:5: all-reduce over xGMI overlapped with the GEMMs on HIP streams).  Every
+        collective waits only on a finished GEMM: no in-kernel wait on a producer that a shared
+        hardware queue could order behind it.  The compute stream joins before the residual's next
+        reader.  ``down``: tiled as gemm.linear_down (else linear_partial, half)."""
         car = self.st.custom_ar
         M, N = residual.shape
+
+        def gemm_of(xx, ww, pp, out):
+            return gemm.linear_down(xx, ww, out, pp) if down else gemm.linear_partial(xx, ww, out, packed=pp, half=True)
         C = gemm.TP_DECODE_CHUNKS
-        flow = getattr(self, "_flow_tp", None)
-        if (C < 2 or flow is None or not residual.is_cuda or not hasattr(car, "reduce_residual_chunks")
-                or M > gemm.FUSED_MAX_M or not car.chunks_ok(M, N, C)):
-            return car.reduce_residual(launch(None), residual, buf)
+        if (C < 2 or wp is None or not residual.is_cuda or not hasattr(car, "reduce_residual_chunk")
+                or M > gemm.FUSED_MAX_M or (N // C) % 128 or not car.chunks_ok(M, N, C)):
+            return car.reduce_residual(gemm_of(x, w, wp, ws), residual, buf)
+        Nc = N // C
+        K = x.shape[1]
+        S_c = gemm.choose_split(Nc, K, M) if down else max(1, gemm.choose_split(Nc, K, M) // 2)
+        if ws.numel() < C * S_c * M * Nc:  # the chunks' slabs side by side in the workspace
+            return car.reduce_residual(gemm_of(x, w, wp, ws), residual, buf)
         main = torch.cuda.current_stream(residual.device)
         cs = comm.comm_stream(residual.device)
-        ev = torch.cuda.Event()
-        ev.record(main)  # what the collective depends on (the previous collective runs on cs itself)
-        p = launch(gemm.ChunkSignal(flow, N // C))
-        need = int(round(p.tiles_per_col * (N // C)))
-        cs.wait_event(ev)
-        with torch.cuda.stream(cs):
-            parts = car.reduce_residual_chunks(p, residual, buf, C, flow, need)
+        off = 0
+        for c in range(C):
+            rows = slice(c * Nc, (c + 1) * Nc)
+            p = gemm_of(x, w[rows], wp[rows], ws[off:])
+            off += p.S * M * Nc
+            ev = torch.cuda.Event()
+            ev.record(main)
+            cs.wait_event(ev)
+            with torch.cuda.stream(cs):
+                car.reduce_residual_chunk(p, residual, buf, c, C)
         main.wait_stream(cs)
-        return parts
+        return buf.view(-1)[: car.nparts(M, N) * M].view(-1, M)
 
     def workspace(self, M: int) -> Optional[torch.Tensor]:
         """fp32 split-K slab buffer for decode-sized batches (fixed address: graph-safe)."""
@@ -649,8 +661,6 @@ class LlamaForCausalLM(nn.Module):
             self._flow_qkv = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
             # the residual phase's hand-off (gemm.ResIn: phase 0 of either fused launch)
             self._flow_res = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
-            # TP: the row-parallel GEMMs' per-column-chunk tickets for the overlapped collective
-            self._flow_tp = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
             # the o-projection phase of the fused QKV -> attention launch (gemm.OProj): its own slab
             # buffer, hand-off buffer and the attention's in-launch partition-merge counters
             at = self.layers[0].attn

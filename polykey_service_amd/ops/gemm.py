@@ -242,13 +242,11 @@ def norm_apply(residual: torch.Tensor, parts: torch.Tensor, weight: torch.Tensor
 
 @dataclasses.dataclass
 class Partial:
-    """fp32 split-K slabs ``buf[:S*M*N]`` viewed as [S, M, N] (not yet summed); ``tiles_per_col``:
-    a :class:`ChunkSignal` GEMM's tiles per output column (its tickets per chunk = cols x this)."""
+    """fp32 split-K slabs ``buf[:S*M*N]`` viewed as [S, M, N] (not yet summed)."""
     buf: torch.Tensor
     S: int
     M: int
     N: int
-    tiles_per_col: float = 0.0
 
     def view(self) -> torch.Tensor:
         return self.buf[: self.S * self.M * self.N].view(self.S, self.M, self.N)
@@ -348,37 +346,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
     return out
 
 
-class ChunkSignal(NamedTuple):
-    """Tickets of a split-K GEMM whose consumer overlaps it (the TP decode collective over column
-    chunks, parallel/custom_ar.py reduce_residual_chunks): every tile takes one ticket at
-    ``flow[64 * chunk]`` for the ``cols``-wide column chunk of its n-block (int32, >=
-    :data:`FLOW_WORDS`, zeroed once, re-armed by the consumer)."""
-    flow: torch.Tensor
-    cols: int
-
-
-# TP decode: each row-parallel projection's fused collective runs as this many column-chunk
-# collectives on the comm stream, overlapped with the GEMM (ChunkSignal; 1: after it, one launch)
+# TP decode: each row-parallel projection runs as this many column-chunk GEMMs on the compute stream,
+# each chunk's fused collective on the comm stream behind an event after ITS GEMM -- the collective
+# of chunk c overlaps the GEMM of chunk c + 1 (1: one GEMM, then one collective)
 TP_DECODE_CHUNKS = int(os.environ.get("POLYKEY_TP_DECODE_CHUNKS", "2"))
 
 
-def _linear_partial_signal(x: torch.Tensor, packed: torch.Tensor, ws: torch.Tensor, S: int, half: bool,
-                           sig: ChunkSignal) -> None:
-    M, K = x.shape
-    N = packed.shape[0]
-    a = GemmArgs()
-    a.partial, a.A, a.W = ws.data_ptr(), x.data_ptr(), packed.data_ptr()
-    a.M, a.N, a.K, a.lda, a.ldo, a.S = M, N, K, x.stride(0), N, S
-    native.call("pk_skinny_partial_signal", ctypes.byref(a), int(half), sig.flow.data_ptr(), int(sig.cols),
-                native.stream_ptr())
-
-
 def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Optional[int] = None,
-                   packed: Optional[torch.Tensor] = None, half: bool = False,
-                   signal: Optional[ChunkSignal] = None) -> Partial:
+                   packed: Optional[torch.Tensor] = None, half: bool = False) -> Partial:
     """Split-K fp32 slabs into workspace ``ws`` (fp32, >= S*M*N).  ``half`` (packed W): 64-row
-    n-blocks at half the default split -- the same grid, half the slab bytes.  ``signal``: the
-    tiles also take per-column-chunk tickets (:class:`ChunkSignal`; packed W, M <= 128)."""
+    n-blocks at half the default split -- the same grid, half the slab bytes."""
     M, K = x.shape
     N = w.shape[0]
     half = half and packed is not None and packed.numel() * packed.element_size() < NT_MIN_BYTES
@@ -387,10 +364,6 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
         if half:
             S = max(1, S // 2)
     assert ws.numel() >= S * M * N, "split-K workspace too small"
-    if signal is not None:
-        assert packed is not None and M <= FUSED_MAX_M
-        _linear_partial_signal(x, packed, ws, S, half, signal)
-        return Partial(ws, S, M, N, S / (64 if half else 128))
     src = packed if packed is not None else w
     native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), src.data_ptr(), M, N, K, x.stride(0), N, S,
                 1 | _wmode(packed) | (HALF_BIT if half else 0), native.stream_ptr())
@@ -538,31 +511,18 @@ def down_kr(N: int, K: int, M: int) -> int:
     return 1 if (N // _ROWS_PER_WG) * choose_split(N, K, M) < _TARGET_WGS else 2
 
 
-def linear_down(h: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, packed: Optional[torch.Tensor],
-                signal: Optional[ChunkSignal] = None) -> Partial:
+def linear_down(h: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, packed: Optional[torch.Tensor]) -> Partial:
     """The decode down projection as the fused MLP launch tiles it (split :func:`choose_split`,
-    n-blocks of :func:`down_kr` x 64 rows) -> fp32 slabs (``signal``: see :func:`linear_partial`)."""
+    n-blocks of :func:`down_kr` x 64 rows) -> fp32 slabs."""
     M, K = h.shape
     N = w.shape[0]
     S = choose_split(N, K, M)
     if packed is not None and down_kr(N, K, M) == 1 and M <= FUSED_MAX_M:
         assert ws.numel() >= S * M * N, "split-K workspace too small"
-        if signal is not None:
-            _linear_partial_signal(h, packed, ws, S, True, signal)
-            return Partial(ws, S, M, N, S / 64)
         native.call("pk_skinny_gemm", 0, ws.data_ptr(), h.data_ptr(), packed.data_ptr(), M, N, K, h.stride(0), N, S,
                     1 | PACKED_BIT | HALF_BIT, native.stream_ptr())
         return Partial(ws, S, M, N)
-    if signal is not None:
-        assert packed is not None and M <= FUSED_MAX_M
-        _linear_partial_signal(h, packed, ws, S, False, signal)
-        return Partial(ws, S, M, N, S / 128)
     return linear_partial(h, w, ws, S, packed=packed)
-
-
-def down_half(N: int, K: int, M: int, packed: Optional[torch.Tensor]) -> bool:
-    """Does :func:`linear_down` tile with 64-row n-blocks?"""
-    return packed is not None and down_kr(N, K, M) == 1 and M <= FUSED_MAX_M
 
 
 def gate_up_split(N2: int, K: int, M: int) -> int:

@@ -57,7 +57,6 @@ SIGNATURES = {
     "pk_qkv_reduce_rope_cache": [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, P],
     "pk_skinny_gemm_ex": [P, I32, P],
     "pk_mlp_fused": [P, P, P, P, P],
-    "pk_skinny_partial_signal": [P, I32, P, I32, P],
     "pk_qkv_attn_fused": [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, P, P, P, P, P],
     "pk_gemm_args_size": [],
     "pk_norm_apply": [P, P, P, I32, P, I32, I32, F32, P],

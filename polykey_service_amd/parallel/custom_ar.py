@@ -42,7 +42,7 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_allgather.argtypes = [_P, _P, _P, _LL, _LL, _I, _P]
         lib.pk_car_reduce_residual.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _P]
         lib.pk_car_reduce_residual_nparts.argtypes = [_P, _I, _I]
-        lib.pk_car_reduce_residual_ex.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P]
+        lib.pk_car_reduce_residual_ex.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_clear_error.argtypes = [_P]
         lib.pk_car_set_error.argtypes = [_P]
@@ -173,31 +173,26 @@ class CustomAllReduce:
             return False
         return self.nparts(M, N // chunks) * chunks == self.nparts(M, N)
 
-    def reduce_residual_chunks(self, pending, residual: torch.Tensor, parts: torch.Tensor, chunks: int,
-                               flow: torch.Tensor, need: int) -> torch.Tensor:
-        """:meth:`reduce_residual` as ``chunks`` column-chunk collectives, each launched WITHOUT
-        waiting for the split-K GEMM that produces ``pending`` (a ``gemm.Partial``): chunk c's
-        workgroups wait for ``need`` tiles' tickets at ``flow[64 c]`` (the GEMM's
-        ``gemm.ChunkSignal``) and read the slabs as they land, so chunk c's xGMI exchange runs
-        under the GEMM of the later chunks (the TP decode collective overlapped
-        with its GEMM).  Same arithmetic per element as the whole: bit-identical."""
+    def reduce_residual_chunk(self, pending, residual: torch.Tensor, parts: torch.Tensor, chunk: int,
+                              chunks: int) -> None:
+        """:meth:`reduce_residual` of column chunk ``chunk`` of ``chunks``: ``pending`` (a
+        ``gemm.Partial``) holds that chunk's own slabs [S, M, N / chunks]; the chunk's columns of
+        ``residual`` and its rows of the norm parts are updated.  Same arithmetic per element as
+        the whole-width call (bit-identical).  The TP decode chain runs one per chunk on the comm
+        stream while the compute stream runs the next chunk's GEMM (models/llama.py)."""
         M, N = residual.shape
         if not (residual.is_contiguous() and residual.dtype == torch.bfloat16 and self.chunks_ok(M, N, chunks)):
-            raise ValueError(f"reduce_residual_chunks: unsupported residual {tuple(residual.shape)} x {chunks}")
-        assert pending.M == M and pending.N == N and pending.S >= 1 and flow.dtype == torch.int32
+            raise ValueError(f"reduce_residual_chunk: unsupported residual {tuple(residual.shape)} / {chunks}")
         Nc = N // chunks
+        assert pending.M == M and pending.N == Nc and pending.S >= 1 and 0 <= chunk < chunks
         npc = self.nparts(M, Nc)
         assert parts.numel() >= npc * chunks * M and parts.dtype == torch.float32
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        fb = flow.data_ptr()
-        for c in range(chunks):
-            rc = self.lib.pk_car_reduce_residual_ex(
-                self.ctx, pending.buf.data_ptr() + c * Nc * 4, pending.S, None,
-                residual.data_ptr() + c * Nc * 2, parts.data_ptr() + c * npc * M * 4, M, Nc, N, self.fused_blocks,
-                fb + 4 * 64 * c, fb + 4 * (64 * 64 + 64 * c), int(need), stream)
-            if rc != 0:
-                raise RuntimeError(f"fused TP reduce (chunk {c}) launch failed ({rc})")
-        return parts.view(-1)[: npc * chunks * M].view(npc * chunks, M)
+        rc = self.lib.pk_car_reduce_residual_ex(
+            self.ctx, pending.buf.data_ptr(), pending.S, None, residual.data_ptr() + chunk * Nc * 2,
+            parts.data_ptr() + chunk * npc * M * 4, M, Nc, N, Nc, self.fused_blocks,
+            torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"fused TP reduce (chunk {chunk}) launch failed ({rc})")
 
     def set_timeout(self, seconds: float) -> None:
         self.lib.pk_car_set_timeout_ms(self.ctx, max(1, int(seconds * 1000)))

@@ -187,10 +187,10 @@ def _fused_phase(car, rank, world, dev):
 
 
 def _overlap_phase(car, rank, world, dev):
-    """The fused collective overlapped with its GEMM: the split-K GEMM takes one
-    ticket per tile on its column chunk (gemm.ChunkSignal) and the chunk collectives, launched on
-    a side stream BEFORE the GEMM is done, start on those tickets.  Residual, parts and slabs
-    bit-identical to GEMM-then-collective, eager and graph-replayed; tickets left zeroed."""
+    """The fused collective overlapped with its GEMM: the projection as C column-
+    chunk GEMMs on the compute stream, each chunk's collective on a side stream behind an event
+    after its GEMM (reduce_residual_chunk).  Residual and parts bit-identical to one GEMM + one
+    collective, eager and graph-replayed (the side-stream fork / join inside the graph)."""
     from polykey_service_amd.ops import gemm
     car.fused_blocks = 32
     g = torch.Generator().manual_seed(11)
@@ -201,31 +201,31 @@ def _overlap_phase(car, rank, world, dev):
     x = torch.randn(M, K, generator=gr).to(torch.bfloat16).to(dev)
     w = (torch.randn(N, K, generator=gr) * 0.05).to(torch.bfloat16).to(dev)
     wp = gemm.pack_weight(w)
-    S = max(1, gemm.choose_split(N, K, M) // 2)
-    ws1 = torch.empty(S * M * N, dtype=torch.float32, device=dev)
+    ws1 = torch.empty(8 * M * N, dtype=torch.float32, device=dev)
     ws2 = torch.empty_like(ws1)
-    flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=dev)
     np_ = car.nparts(M, N)
     p1 = torch.zeros(np_ * M, dtype=torch.float32, device=dev)
     p2 = torch.zeros_like(p1)
     r1, r2 = res0.clone(), res0.clone()
     cs = torch.cuda.Stream()
+    Nc = N // C
 
     def ref():
         r1.copy_(res0)
-        pa = gemm.linear_partial(x, w, ws1, packed=wp, half=True)
-        car.reduce_residual(pa, r1, p1)
+        car.reduce_residual(gemm.linear_partial(x, w, ws1, packed=wp, half=True), r1, p1)
 
     def overlapped():
         r2.copy_(res0)
         main = torch.cuda.current_stream()
-        ev = torch.cuda.Event()
-        ev.record(main)
-        pb = gemm.linear_partial(x, w, ws2, packed=wp, half=True, signal=gemm.ChunkSignal(flow, N // C))
-        need = int(round(pb.tiles_per_col * (N // C)))
-        cs.wait_event(ev)
-        with torch.cuda.stream(cs):
-            car.reduce_residual_chunks(pb, r2, p2, C, flow, need)
+        off = 0
+        for c in range(C):
+            pc = gemm.linear_partial(x, w[c * Nc:(c + 1) * Nc], ws2[off:], packed=wp[c * Nc:(c + 1) * Nc], half=True)
+            off += pc.S * M * Nc
+            ev = torch.cuda.Event()
+            ev.record(main)
+            cs.wait_event(ev)
+            with torch.cuda.stream(cs):
+                car.reduce_residual_chunk(pc, r2, p2, c, C)
         main.wait_stream(cs)
 
     for it in range(2):
@@ -233,14 +233,10 @@ def _overlap_phase(car, rank, world, dev):
         ref()
         torch.cuda.synchronize()
         dist.barrier()
-        ws2.fill_(float("nan"))
         overlapped()
         torch.cuda.synchronize()
-        assert torch.equal(ws1[: S * M * N], ws2[: S * M * N]), "slabs"
         assert torch.equal(r1, r2), ("residual", it, car.error())
         assert torch.equal(p1, p2), ("parts", it)
-        assert int(flow.abs().sum()) == 0, flow.nonzero().tolist()
-    # captured: the side-stream fork / join inside the graph
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     dist.barrier()
@@ -260,7 +256,7 @@ def _overlap_phase(car, rank, world, dev):
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(r1, r2) and torch.equal(p1, p2), ("graph", it)
-    assert car.error() == 0 and int(flow.abs().sum()) == 0
+    assert car.error() == 0
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

@@ -28,6 +28,11 @@ from polykey_service_amd.parallel import comm  # noqa: E402
 from polykey_service_amd.parallel.state import ParallelState, set_state  # noqa: E402
 
 
+# SOLO_AR_NOOP=1: every collective does nothing (not even the local slab sum): times the GEMM side of
+# the TP chain alone, chunked (POLYKEY_TP_DECODE_CHUNKS > 1) or not, like for like
+NOOP = os.environ.get("SOLO_AR_NOOP") == "1"
+
+
 class SoloAR:
     """The local half of every TP collective (no peers)."""
 
@@ -51,7 +56,19 @@ class SoloAR:
         return N % 1024 == 0
 
     def reduce_residual(self, pending, residual, parts):
+        if NOOP:
+            return parts.view(-1)[: (residual.shape[1] // 512) * residual.shape[0]].view(-1, residual.shape[0])
         return gemm.residual_parts(pending, residual, parts)
+
+    # column-chunk collectives of the overlapped TP chain (models/llama.py _tp_row_collective)
+    def nparts(self, M, N):
+        return N // 512
+
+    def chunks_ok(self, M, N, chunks):
+        return NOOP and chunks > 1 and N % (1024 * chunks) == 0
+
+    def reduce_residual_chunk(self, pending, residual, parts, chunk, chunks):
+        pass  # SOLO_AR_NOOP: only the GEMM side of the chunked chain is timed
 
     def check(self):
         pass
