@@ -316,7 +316,15 @@ PK_EXPORT int pk_decode_num_parts(int max_context) { return (max_context + kDeco
 int decode_part(int n_seqs, int n_kv, int max_ctx) {
   const int big = (max_ctx + kDecodePart - 1) / kDecodePart;
   const int z = big < g_decode_z ? big : g_decode_z;
-  return n_seqs * n_kv * z < kDecodeFill ? kDecodePartSmall : kDecodePart;
+  return n_seqs * n_kv * z < g_decode_fill ? kDecodePartSmall : kDecodePart;
+}
+
+// Workgroup count below which decode takes 128-key partitions (default 256; 0: always 512 keys;
+// never above 256: ops/attention.py decode_workspace sizes the partition slabs for that bound).
+PK_EXPORT int pk_set_decode_fill(int n) {
+  if (n < 0 || n > 256) return -1;
+  g_decode_fill = n;
+  return 0;
 }
 
 template <int P>

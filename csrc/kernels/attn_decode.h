@@ -14,7 +14,7 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1e30f;
 constexpr int kDecodeWaves = 4;  // waves per (seq, kv head, partition); 8 measured ~10 % slower at 384 keys
 constexpr int kDecodePartSmall = 128;  // keys per partition when (seq, kv head) pairs cannot fill the chip
-constexpr int kDecodeFill = 256;       // ... i.e. fewer workgroups than this at the full partition
+int g_decode_fill = 256;  // ... i.e. fewer workgroups than this at the full partition (pk_set_decode_fill)
 int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
 
 // K/V stream loads: plain (non-temporal measured slower: in-situ decode step 4.43 vs 4.45 ms,

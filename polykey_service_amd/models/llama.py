@@ -627,7 +627,8 @@ class LlamaForCausalLM(nn.Module):
             return gemm.linear_down(xx, ww, out, pp) if down else gemm.linear_partial(xx, ww, out, packed=pp, half=True)
         C = gemm.TP_DECODE_CHUNKS
         if (C < 2 or wp is None or not residual.is_cuda or not hasattr(car, "reduce_residual_chunk")
-                or M > gemm.FUSED_MAX_M or (N // C) % 128 or not car.chunks_ok(M, N, C)):
+                or M > gemm.FUSED_MAX_M or (N // C) % 128 or not car.chunks_ok(M, N, C)
+                or not self._overlap_streams_ok()):
             return car.reduce_residual(gemm_of(x, w, wp, ws), residual, buf)
         Nc = N // C
         K = x.shape[1]
@@ -648,6 +649,15 @@ class LlamaForCausalLM(nn.Module):
                 car.reduce_residual_chunk(p, residual, buf, c, C)
         main.wait_stream(cs)
         return buf.view(-1)[: car.nparts(M, N) * M].view(-1, M)
+
+    def _overlap_streams_ok(self) -> bool:
+        """The overlapped TP chain forks a comm stream inside the captured decode graph.  Ranks
+        sharing one GPU (rehearsals) gain nothing from it, and under a single hardware queue per
+        process (GPU_MAX_HW_QUEUES=1, the rehearsals' setting) replaying such a graph crashed the
+        HIP runtime (profiles/r5_tp_overlap.md); POLYKEY_TP_OVERLAP_FORCE=1 lifts the check."""
+        if os.environ.get("POLYKEY_TP_OVERLAP_FORCE") == "1":
+            return True
+        return not self.st.shared_device and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 2
 
     def workspace(self, M: int) -> Optional[torch.Tensor]:
         """fp32 split-K slab buffer for decode-sized batches (fixed address: graph-safe)."""

@@ -47,6 +47,16 @@ _PART = 512  # must match kDecodePart in csrc/kernels/attention.hip
 # profiles/r5_tp_ab.jsonl) -- off by default
 INLAUNCH_MERGE = os.environ.get("POLYKEY_DECODE_INLAUNCH_MERGE", "0") == "1"
 _PART_MIN = 128  # kDecodePartSmall: launches whose (seq, kv head) pairs cannot fill the chip
+_FILL_SET = False
+
+
+def apply_decode_fill() -> None:
+    """POLYKEY_DECODE_FILL (A/B): the workgroup count below which decode attention takes 128-key
+    partitions (csrc attention.hip decode_part; 0: always 512)."""
+    global _FILL_SET
+    if not _FILL_SET and os.environ.get("POLYKEY_DECODE_FILL") is not None:
+        native.call("pk_set_decode_fill", int(os.environ["POLYKEY_DECODE_FILL"]))
+    _FILL_SET = True
 
 
 _DECODE_FILL = 256  # kDecodeFill: fewer (seq, kv head, partition) workgroups than this -> 128-key partitions
@@ -105,6 +115,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         _reference(q, k_cache, v_cache, md, scale, out)
         return out
     assert hd == 128 and q.stride(-1) == 1 and q.stride(1) == hd
+    apply_decode_fill()
     stream = native.stream_ptr()
     nd = md.num_decode
     if nd > 0:
@@ -148,6 +159,7 @@ def paged_decode_from_qkv(p, positions: torch.Tensor, cos_sin: torch.Tensor, k_c
     k / v into the paged cache and attends — one kernel instead of reduce+RoPE+cache then
     attention.  Returns [T, nq*128] bf16."""
     assert md.num_prefill == 0 and k_cache.shape[-1] == 128
+    apply_decode_fill()
     T = p.M
     out = torch.empty((T, nq * 128), dtype=torch.bfloat16, device=p.buf.device)
     bt = md.decode_block_tables

@@ -349,7 +349,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
 # TP decode: each row-parallel projection runs as this many column-chunk GEMMs on the compute stream,
 # each chunk's fused collective on the comm stream behind an event after ITS GEMM -- the collective
 # of chunk c overlaps the GEMM of chunk c + 1 (1: one GEMM, then one collective)
-TP_DECODE_CHUNKS = int(os.environ.get("POLYKEY_TP_DECODE_CHUNKS", "2"))
+# Measured: the chunked GEMMs + stream fork / join cost 16 us per 70B TP=8 layer on the GEMM side
+# alone (per-rank step 7.38 vs 6.07 ms with 2 chunks, 10.1 ms with 4; profiles/r5_tp_overlap.md) --
+# more than the xGMI time they could hide: one GEMM + one collective by default
+TP_DECODE_CHUNKS = int(os.environ.get("POLYKEY_TP_DECODE_CHUNKS", "1"))
 
 
 def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Optional[int] = None,
@@ -669,6 +672,8 @@ def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: Optional
     S = S or choose_split(N, K, M)
     assert ws.numel() >= S * M * N and flow.numel() >= FLOW_WORDS and flow.dtype == torch.int32
     assert md.num_prefill == 0 and md.num_decode == M and k_cache.shape[-1] == 128
+    from . import attention as _attn
+    _attn.apply_decode_fill()
     out = torch.empty((M, nq * 128), dtype=torch.bfloat16, device=x.device)
     a = GemmArgs()
     a.partial, a.A, a.W = ws.data_ptr(), x.data_ptr(), qkv_packed.data_ptr()
