@@ -100,11 +100,31 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def kill_tree(p: "subprocess.Popen") -> None:
+    """SIGKILL ``p``, its process group and every descendant.  torchrun's ranks run in sessions
+    of their own: killing the launcher's group alone orphans them -- they keep the stdout pipe
+    open (so a ``communicate`` after the kill never sees EOF) and, hung, never exit."""
+    import signal
+    try:
+        import psutil
+        kids = psutil.Process(p.pid).children(recursive=True)
+    except Exception:  # psutil missing or the launcher already gone
+        kids = []
+    try:
+        os.killpg(p.pid, signal.SIGKILL)
+    except (ProcessLookupError, PermissionError):
+        pass
+    for k in kids:
+        try:
+            k.kill()
+        except Exception:
+            pass
+
+
 def run_child(argv, n: int, timeout: float):
     """One measurement as a fresh torchrun job of ``n`` ranks (a child process, never an exec;
     its own session, so a timeout kills the whole tree and frees every GPU).  Returns
     (rc, the child's JSON line as a dict or None, wall seconds)."""
-    import signal
     env = {k: v for k, v in os.environ.items() if k not in _LAUNCH_ENV and not k.startswith("TORCHELASTIC_")}
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
@@ -114,8 +134,11 @@ def run_child(argv, n: int, timeout: float):
         out, _ = p.communicate(timeout=timeout)
         rc = p.returncode
     except subprocess.TimeoutExpired:
-        os.killpg(p.pid, signal.SIGKILL)
-        out, _ = p.communicate()
+        kill_tree(p)
+        try:
+            out, _ = p.communicate(timeout=30)
+        except subprocess.TimeoutExpired:  # a descendant that escaped still holds the pipe
+            out = ""
         rc = 124
     line = None
     for ln in out.splitlines():

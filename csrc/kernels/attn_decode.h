@@ -14,12 +14,41 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1e30f;
 constexpr int kDecodeWaves = 4;  // waves per (seq, kv head, partition); 8 measured ~10 % slower at 384 keys
 constexpr int kDecodePartSmall = 128;  // keys per partition when (seq, kv head) pairs cannot fill the chip
-int g_decode_fill = 256;  // ... i.e. fewer workgroups than this at the full partition (pk_set_decode_fill)
+// ... i.e. fewer workgroups than this at the full partition (pk_set_decode_fill).  64: the 70B TP=8
+// rank's 64 sequences x 1 kv head stay at 512 keys (one workgroup per sequence, no merge launch):
+// per-rank step 6.52 vs 6.54 ms at 256 (128-key partitions + merge), profiles/r5_attn_ab4.jsonl
+int g_decode_fill = 64;
 int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
+// K/V prefetch across the q slab reduction in launches of <= 1 workgroup per CU (pk_set_decode_pre):
+// measured slower with the one-round prologue (6.62 vs 6.54 ms, profiles/r5_attn_ab4.jsonl)
+int g_decode_pre = 0;
 
 // K/V stream loads: plain (non-temporal measured slower: in-situ decode step 4.43 vs 4.45 ms,
 // tools/ab_decode.py)
 __device__ __forceinline__ bf16x8_t ldkv(const bf16_t* p) { return ld8(p); }
+
+// 16-byte load of QKV slab floats p..p+3; SC1: handed over in-launch (sc1 buffer load, base < 2 GiB)
+template <bool SC1>
+__device__ __forceinline__ float4 ld_slab4(const float* base, const float* p) {
+  if constexpr (SC1)
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), static_cast<short>(0), 0x7ffffff0, 0x00020000),
+        static_cast<int>((p - base) * 4), 0, 16));
+  return *reinterpret_cast<const float4*>(p);
+}
+
+// uniform int through the vector memory path (raw buffer load), see decode_tile's prologue
+__device__ __forceinline__ int ld_vmem(const int* p) {
+  return __builtin_amdgcn_raw_buffer_load_b32(
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p), static_cast<short>(0), 0x7ffffff0, 0x00020000), 0, 0, 0);
+}
+
+__device__ __forceinline__ void add4f(float4& a, const float4& b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
 
 __device__ __forceinline__ bf16x8_t zero8() {
   u32x4 z = {0u, 0u, 0u, 0u};
@@ -248,14 +277,52 @@ __device__ __forceinline__ void decode_tile(
   auto& sn_s = L.sn_s;
   static_assert(64 * NW >= 256, "the new-token scores use 16 lanes per query head, G <= 16");
   const int h = bx, seq = by;
-  // the first partition's block-table window, requested before anything else so its round
-  // trip overlaps the context / q preparation instead of following it (entries past the
-  // sequence's blocks are in-bounds of the row and never used)
+  // QKV slab item `it` (FROM_QKV): 4 consecutive columns j..j+3 of a head and their rotation
+  // partners j+64..j+67 (16-byte slab loads); the G q heads + k + v of kv head h are 16 (G + 2) items
+  auto item_col = [&](int it, int& j) {
+    const int Gq = n_q / n_kv;
+    if (it < Gq * 16) {
+      j = (it & 15) * 4;
+      return (h * Gq + (it >> 4)) * kHD + j;
+    }
+    if (it < Gq * 16 + 16) {
+      j = (it - Gq * 16) * 4;
+      return (n_q + h) * kHD + j;
+    }
+    j = (it - Gq * 16 - 16) * 4;
+    return (n_q + n_kv + h) * kHD + j;
+  };
+  // Prologue loads in ONE round trip: the context / position / slot (vector loads: scalar ones
+  // were waited for with lgkmcnt(0) together with the kernel-argument loads the slab addresses
+  // need), the first partition's block-table window, and -- slabs complete at launch, i.e. not a
+  // fused launch's in-launch hand-off -- this thread's first QKV slab item, ahead of the writer /
+  // fold decision (which only selects what is stored; the first pass of the q loop consumes it).
+  int ctx = ld_vmem(context_lens + seq);
+  int pos_q = FROM_QKV ? ld_vmem(qi.positions + seq) : 0;
+  int slot_q = FROM_QKV ? ld_vmem(qi.slots + seq) : -1;
+  // (entries of the block-table window past the sequence's blocks are in-bounds of the row and
+  // never used)
   const int pre_b0 = static_cast<int>(bz) * (kPart / bs);
   int bt_pre = 0;
   if (static_cast<int>(threadIdx.x) <= kPart / bs && pre_b0 + static_cast<int>(threadIdx.x) < max_blocks)
     bt_pre = block_tables[static_cast<int64_t>(seq) * max_blocks + pre_b0 + threadIdx.x];
-  const int ctx = context_lens[seq];
+  constexpr bool kHoist = FROM_QKV && SS > 0 && (FL & 2) == 0;
+  float4 hva[kHoist ? SS : 1], hvb[kHoist ? SS : 1];
+  if constexpr (kHoist) {
+    const int N = (n_q + 2 * n_kv) * kHD;
+    const int64_t slab = static_cast<int64_t>(qi.M) * N;
+    const float* base = qi.partial + static_cast<int64_t>(seq) * N;
+    int j;
+    const int col = item_col(min(static_cast<int>(threadIdx.x), (n_q / n_kv) * 16 + 31), j);
+#pragma unroll
+    for (int sp = 0; sp < SS; ++sp) {
+      hva[sp] = *reinterpret_cast<const float4*>(base + sp * slab + col);
+      hvb[sp] = *reinterpret_cast<const float4*>(base + sp * slab + col + 64);
+    }
+  }
+  // the three scalars are needed from here on: their wait (issued first) leaves the slab loads in
+  // flight, and the memory clobber keeps the slab loads above it
+  asm volatile("" : "+v"(ctx), "+v"(pos_q), "+v"(slot_q) :: "memory");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t blk_stride = static_cast<int64_t>(n_kv) * bs * kHD;
   const bf16_t* kch = kc + static_cast<int64_t>(h) * bs * kHD;
@@ -268,8 +335,8 @@ __device__ __forceinline__ void decode_tile(
     // not produced by the QKV tiles)
     const int n_used0 = min((ctx + kPart - 1) / kPart, n_parts);
     if (ctx > 0 && static_cast<int>(bz) < n_used0) {
-      const bool writer0 = qi.slots[seq] >= 0 && static_cast<int>(bz) == (n_used0 - 1) % static_cast<int>(gdz);
-      const bool fold0 = writer0 && qi.positions[seq] == ctx - 1;
+      const bool writer0 = slot_q >= 0 && static_cast<int>(bz) == (n_used0 - 1) % static_cast<int>(gdz);
+      const bool fold0 = writer0 && pos_q == ctx - 1;
       const int ctx_c0 = fold0 ? ctx - 1 : ctx;
       const int begin = bz * kPart, end = min(ctx_c0, begin + kPart);
       // (a writer that does not fold stores the new row into the cache before attending: no prefetch)
@@ -312,75 +379,86 @@ __device__ __forceinline__ void decode_tile(
     const int N = (n_q + 2 * n_kv) * kHD;
     const int64_t slab = static_cast<int64_t>(qi.M) * N;
     const float* base = qi.partial + static_cast<int64_t>(seq) * N;
-    const float* cs = qi.cos_sin + static_cast<int64_t>(qi.positions[seq]) * kHD;
-    slot = qi.slots[seq];
+    const float* cs = qi.cos_sin + static_cast<int64_t>(pos_q) * kHD;
+    slot = slot_q;
     const bool writer = slot >= 0 && static_cast<int>(bz) == (n_used - 1) % static_cast<int>(gdz);
-    fold = writer && qi.positions[seq] == ctx - 1;
-    const int n_items = G * 64 + (writer ? 128 : 0);
+    fold = writer && pos_q == ctx - 1;
+    // one pass of 16-byte slab loads per thread for G <= 14 (1-column items took 3 dependent
+    // rounds at G = 8)
+    const int n_items = G * 16 + (writer ? 32 : 0);
     for (int it = threadIdx.x; it < n_items; it += 64 * NW) {
-      int col, j;
-      if (it < G * 64) {
-        j = it & 63;
-        col = (h * G + (it >> 6)) * kHD + j;
-      } else if (it < G * 64 + 64) {
-        j = it - G * 64;
-        col = (n_q + h) * kHD + j;
-      } else {
-        j = it - G * 64 - 64;
-        col = (n_q + n_kv + h) * kHD + j;
-      }
-      float a = 0.f, b = 0.f;
+      int j;
+      const int col = item_col(it, j);
+      float4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
       if constexpr (SS > 0) {  // all slab loads in flight before the first add
-        float va[SS], vb[SS];
+        float4 va[SS], vb[SS];
+        if (kHoist && it == static_cast<int>(threadIdx.x)) {
 #pragma unroll
-        for (int sp = 0; sp < SS; ++sp) {
-          if constexpr ((FL & 2) != 0) {
-            va[sp] = ldf_sc1(qi.partial, base + sp * slab + col);
-            vb[sp] = ldf_sc1(qi.partial, base + sp * slab + col + 64);
-          } else {
-            va[sp] = base[sp * slab + col];
-            vb[sp] = base[sp * slab + col + 64];
+          for (int sp = 0; sp < SS; ++sp) {
+            va[sp] = hva[sp];
+            vb[sp] = hvb[sp];
+          }
+        } else {
+#pragma unroll
+          for (int sp = 0; sp < SS; ++sp) {
+            va[sp] = ld_slab4<(FL & 2) != 0>(qi.partial, base + sp * slab + col);
+            vb[sp] = ld_slab4<(FL & 2) != 0>(qi.partial, base + sp * slab + col + 64);
           }
         }
 #pragma unroll
         for (int sp = 0; sp < SS; ++sp) {
-          a += va[sp];
-          b += vb[sp];
+          add4f(a, va[sp]);
+          add4f(b, vb[sp]);
         }
       } else {
         for (int sp = 0; sp < qi.S; ++sp) {
-          if constexpr ((FL & 2) != 0) {
-            a += ldf_sc1(qi.partial, base + sp * slab + col);
-            b += ldf_sc1(qi.partial, base + sp * slab + col + 64);
-          } else {
-            a += base[sp * slab + col];
-            b += base[sp * slab + col + 64];
-          }
+          add4f(a, ld_slab4<(FL & 2) != 0>(qi.partial, base + sp * slab + col));
+          add4f(b, ld_slab4<(FL & 2) != 0>(qi.partial, base + sp * slab + col + 64));
         }
       }
-      if (it < G * 64 + 64) {  // q or k: round (the GEMM output), rotate (neox)
-        a = bf2f(f2bf(a));
-        b = bf2f(f2bf(b));
-        const float co = cs[j], si = cs[64 + j];
-        const bf16_t ra = f2bf(a * co - b * si), rb = f2bf(b * co + a * si);
-        if (it < G * 64) {
-          q_s[it >> 6][j] = ra;
-          q_s[it >> 6][j + 64] = rb;
-        } else if (fold) {
-          kn_s[j] = ra;
-          kn_s[j + 64] = rb;
-        } else {
-          bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * n_kv + h) * bs * kHD;
-          d[kcache_off(slot % bs, j)] = ra;
-          d[kcache_off(slot % bs, j + 64)] = rb;
+      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+      if (it < G * 16 + 16) {  // q or k: round (the GEMM output), rotate (neox)
+        const float4 co4 = *reinterpret_cast<const float4*>(cs + j), si4 = *reinterpret_cast<const float4*>(cs + 64 + j);
+        const float co[4] = {co4.x, co4.y, co4.z, co4.w}, si[4] = {si4.x, si4.y, si4.z, si4.w};
+        float ra[4], rb[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = bf2f(f2bf(av[e])), y = bf2f(f2bf(bv[e]));
+          ra[e] = x * co[e] - y * si[e];
+          rb[e] = y * co[e] + x * si[e];
         }
+        uint2 pa, pb;
+        pa.x = pack2(ra[0], ra[1]);
+        pa.y = pack2(ra[2], ra[3]);
+        pb.x = pack2(rb[0], rb[1]);
+        pb.y = pack2(rb[2], rb[3]);
+        bf16_t* dst;
+        if (it < G * 16) {
+          dst = &q_s[it >> 4][j];
+        } else if (fold) {
+          dst = &kn_s[j];
+        } else {  // fragment-native K tile: 4-dim groups stay contiguous (common.h kcache_off)
+          bf16_t* d = kc + (static_cast<int64_t>(slot / bs) * n_kv + h) * bs * kHD;
+          *reinterpret_cast<uint2*>(d + kcache_off(slot % bs, j)) = pa;
+          *reinterpret_cast<uint2*>(d + kcache_off(slot % bs, j + 64)) = pb;
+          continue;
+        }
+        *reinterpret_cast<uint2*>(dst) = pa;
+        *reinterpret_cast<uint2*>(dst + 64) = pb;
       } else if (fold) {
-        vn_s[j] = bf2f(f2bf(a));
-        vn_s[j + 64] = bf2f(f2bf(b));
-      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vn_s[j + e] = bf2f(f2bf(av[e]));
+          vn_s[j + 64 + e] = bf2f(f2bf(bv[e]));
+        }
+      } else {  // transposed V tile: channels j..j+3 are 8 elements apart (common.h vcache_off)
         bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs;
-        d[vcache_off(slot % bs, j)] = f2bf(a);
-        d[vcache_off(slot % bs, j + 64)] = f2bf(b);
+        const int va0 = vcache_off(slot % bs, j), vb0 = vcache_off(slot % bs, j + 64);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          d[va0 + 8 * e] = f2bf(av[e]);
+          d[vb0 + 8 * e] = f2bf(bv[e]);
+        }
       }
     }
     if (!fold) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new k/v rows are in L2 before any wave reads them
@@ -470,6 +548,17 @@ __device__ __forceinline__ void decode_tile(
     const int hq = h * G + c;
     if (n_eff == 1) {
       st_out<(FL & 1) != 0>(out, static_cast<int64_t>(seq) * out_stride + hq * kHD + d, f2bf(L > 0.f ? O / L : 0.f));
+    } else if (counters != nullptr) {
+      // merged in-launch: write-through (sc1) stores relative to this sequence's slab (< 2 GiB),
+      // read back by the merging workgroup with sc1 loads -- no release / acquire fences (an L2
+      // write-back / invalidate per workgroup measured +6.6 us per 70B TP=8 layer)
+      const int pl = hq * n_parts + bz;
+      stf_sc1(part_o + static_cast<int64_t>(seq) * n_q * n_parts * kHD, pl * kHD + d, O);
+      if (d == 0) {
+        float* ml = part_ml + static_cast<int64_t>(seq) * n_q * n_parts * 2;
+        stf_sc1(ml, 2 * pl, M);
+        stf_sc1(ml, 2 * pl + 1, L);
+      }
     } else {
       const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + bz;
       part_o[pi * kHD + d] = O;
@@ -491,35 +580,31 @@ __device__ __forceinline__ void decode_tile(
   }
   if (n_eff == 1 || counters == nullptr) return;
   // ---- in-launch split-K merge: the last workgroup to arrive combines the partials
-  // (guide §5 "In-launch split-K reduction": plain slab stores, every wave drains, one agent
-  // release + ticket; the last arriver acquires, merges and re-arms the counter).
+  // (write-through partials, every wave drains them, one lane takes the ticket; the last arriver
+  // reads them back with sc1 loads, merges and re-arms the counter -- flow.h's hand-off rule).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int* ctr = counters + seq * n_kv + h;
     const int t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = (t == n_eff - 1);
-    if (last) {
-      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!last) return;
+  const float* so = part_o + static_cast<int64_t>(seq) * n_q * n_parts * kHD;
+  const float* sml = part_ml + static_cast<int64_t>(seq) * n_q * n_parts * 2;
   for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
     const int c = idx / kHD, d = idx % kHD;
     const int hq = h * G + c;
-    const int64_t base = (static_cast<int64_t>(seq) * n_q + hq) * n_parts;
+    const int base = hq * n_parts;
     float M = kNegBig;
-    for (int p = 0; p < n_eff; ++p) M = fmaxf(M, part_ml[2 * (base + p)]);
+    for (int p = 0; p < n_eff; ++p) M = fmaxf(M, ldf_sc1(sml, sml + 2 * (base + p)));
     float O = 0.f, L = 0.f;
     for (int p = 0; p < n_eff; ++p) {
-      const float f = exp2f(part_ml[2 * (base + p)] - M);
-      O += f * part_o[(base + p) * kHD + d];
-      L += f * part_ml[2 * (base + p) + 1];
+      const float f = exp2f(ldf_sc1(sml, sml + 2 * (base + p)) - M);
+      O += f * ldf_sc1(so, so + (base + p) * kHD + d);
+      L += f * ldf_sc1(sml, sml + 2 * (base + p) + 1);
     }
     st_out<(FL & 1) != 0>(out, static_cast<int64_t>(seq) * out_stride + hq * kHD + d, f2bf(L > 0.f ? O / L : 0.f));
   }

@@ -47,6 +47,13 @@ __device__ __forceinline__ float ldf_sc1(const float* base, const float* p) {
       static_cast<int>((p - base) * 4), 0, 16));
 }
 
+// write-through (sc1) 4-byte store of element i of the buffer at base (< 2 GiB)
+__device__ __forceinline__ void stf_sc1(float* base, int i, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(
+      __builtin_bit_cast(unsigned, v),
+      __builtin_amdgcn_make_buffer_rsrc(base, static_cast<short>(0), 0x7ffffff0, 0x00020000), i * 4, 0, 16);
+}
+
 // The hand-off needs no fence (guide, "Hand-offs measured with sc1 loads", first row): the
 // producer's output stores are write-through (sc1), every wave drains them (vmcnt(0)) before ONE
 // lane takes the ticket; the consumer's single polling lane matches, the workgroup joins it at a

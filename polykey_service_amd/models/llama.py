@@ -540,7 +540,8 @@ class LlamaForCausalLM(nn.Module):
                                        at.nq, at.nkv, self._flow_qkv, o=o)
         # (64-row n-blocks at half the split: half the slabs the attention prologue sums -- the 70B
         # TP=8 shard's 10 n-blocks otherwise take split 16)
-        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, packed=at.qkv_pf, half=gemm.QKV_HALF)
+        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, S=gemm.QKV_SPLIT or None, packed=at.qkv_pf,
+                                         half=gemm.QKV_HALF)
         if md.num_prefill == 0:
             return attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
         q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)

@@ -51,15 +51,21 @@ _FILL_SET = False
 
 
 def apply_decode_fill() -> None:
-    """POLYKEY_DECODE_FILL (A/B): the workgroup count below which decode attention takes 128-key
-    partitions (csrc attention.hip decode_part; 0: always 512)."""
+    """A/B knobs of the decode attention launch, applied once per process:
+    POLYKEY_DECODE_FILL -- the workgroup count below which decode attention takes 128-key
+    partitions (csrc attention.hip decode_part; 0: always 512); POLYKEY_DECODE_PRE=1 -- K/V
+    prefetch across the q slab reduction in launches of at most one workgroup per CU (=1: on)."""
     global _FILL_SET
-    if not _FILL_SET and os.environ.get("POLYKEY_DECODE_FILL") is not None:
-        native.call("pk_set_decode_fill", int(os.environ["POLYKEY_DECODE_FILL"]))
+    if not _FILL_SET:
+        if os.environ.get("POLYKEY_DECODE_FILL") is not None:
+            native.call("pk_set_decode_fill", int(os.environ["POLYKEY_DECODE_FILL"]))
+        if os.environ.get("POLYKEY_DECODE_PRE") is not None:
+            native.call("pk_set_decode_pre", int(os.environ["POLYKEY_DECODE_PRE"]))
     _FILL_SET = True
 
 
-_DECODE_FILL = 256  # kDecodeFill: fewer (seq, kv head, partition) workgroups than this -> 128-key partitions
+# g_decode_fill (csrc attn_decode.h): fewer (seq, kv head, partition) workgroups than this -> 128-key partitions
+_DECODE_FILL = int(os.environ.get("POLYKEY_DECODE_FILL", "256"))
 
 
 def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, device, n_kv: int = 0,

@@ -32,7 +32,7 @@ FUSED_MAX_M = 128
 FUSED_MT8_MAX_PARTS = 16
 SKINNY_TILE_M = 128  # rows per row tile above 64 (the kernel's MT = 8 variant)
 # measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
-_TARGET_WGS = 192
+_TARGET_WGS = int(os.environ.get("POLYKEY_SKINNY_TARGET", "192"))  # (A/B knob)
 _ROWS_PER_WG = 128
 _KCHUNK = 256
 # The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see
@@ -51,6 +51,7 @@ QKV_ATTN_MIN_KV = int(os.environ.get("POLYKEY_QKV_MIN_KV", "4"))
 # the two-launch decode QKV (TP shards with few kv heads) as 64-row n-blocks at half the split:
 # half the fp32 slabs the attention prologue sums (70B TP=8: 6.66-6.67 vs 6.68 ms, neutral)
 QKV_HALF = os.environ.get("POLYKEY_QKV_HALF", "1") == "1"
+QKV_SPLIT = int(os.environ.get("POLYKEY_QKV_SPLIT", "0"))  # A/B: the decode QKV's K split (0: choose_split)
 PACKED_BIT = 16
 
 

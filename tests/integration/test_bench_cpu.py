@@ -3,7 +3,6 @@ from rank 0 with the BASELINE metric, whole-job value, and the DP parallelism / 
 of the launch; 2 ranks go through the torchrun child launch the driver itself uses."""
 import json
 import os
-import signal
 import subprocess
 import sys
 
@@ -18,8 +17,13 @@ def _run(cmd, cwd, env, timeout=300):
     try:
         out, err = p.communicate(timeout=timeout)
     except subprocess.TimeoutExpired:
-        os.killpg(p.pid, signal.SIGKILL)
-        out, err = p.communicate()
+        sys.path.insert(0, REPO)
+        from bench import kill_tree
+        kill_tree(p)
+        try:
+            out, err = p.communicate(timeout=30)
+        except subprocess.TimeoutExpired:
+            out, err = "", ""
         pytest.fail(f"bench.py timed out after {timeout} s\n{err[-3000:]}")
     return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
