@@ -30,7 +30,7 @@ using namespace pk;
 namespace {
 
 template <int kPart, int NW, bool FROM_QKV, int SS = 0, int PRE = 0>
-__global__ void __launch_bounds__(64 * NW, PRE ? 1 : 3) paged_decode_kernel(
+__global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, bf16_t* __restrict__ kc,
     bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
     float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int n_q, int n_kv, int bs,

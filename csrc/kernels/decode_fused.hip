@@ -175,7 +175,7 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   }
   int nwg = n_attn > n_qkv ? n_attn : n_qkv;
   nwg = n_o > nwg ? n_o : nwg;
-  if (n_res > nwg) return -1;
+  nwg = n_res > nwg ? n_res : nwg;  // (the residual workgroups come first and never wait)
   const dim3 grid(nwg);
   auto go = [&](auto mt, auto ss) {
     constexpr int MT = decltype(mt)::value, SS = decltype(ss)::value;
