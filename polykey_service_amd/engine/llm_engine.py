@@ -212,7 +212,10 @@ class LLMEngine:
         hand-off (FusedHandoffError: co-tenant on the GPU), the runner falls back to the
         two-launch path and the step is launched again -- the sequences' state is untouched until
         a step completes and the re-run rewrites the same KV slots.  A TP / lockstep group cannot
-        re-run one rank alone: there the error stays fatal.  Returns (done, redone)."""
+        re-run one rank alone, so TP ranks that share a GPU (where a co-tenant can starve a
+        hand-off) never take the fused launches (models/llama.py _qkv_attn_fused_ok, the fused
+        MLP's shared_device check); on a dedicated GPU a lost hand-off is a fault and stays fatal.
+        Returns (done, redone)."""
         from ..ops.gemm import FusedHandoffError
         try:
             return self._complete(batch, sampling, handle), False

@@ -515,10 +515,12 @@ class LlamaForCausalLM(nn.Module):
                 and gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, H // gemm.PART_COLS)
                 and gemm.res_workgroups(T, H) <= gemm.mlp_fused_grid(residual, mlp.gate_up_pf, mlp.down_p))
 
-    @staticmethod
-    def _qkv_attn_fused_ok(at, T: int, nparts: int, md) -> bool:
+    def _qkv_attn_fused_ok(self, at, T: int, nparts: int, md) -> bool:
+        # (a TP rank sharing its GPU keeps the two launches: a hand-off lost to a co-tenant has a
+        # fallback only at TP = 1 -- a TP group cannot re-run one rank's step, llm_engine.py)
         return (md.num_prefill == 0 and gemm.QKV_ATTN_FUSED and at.nkv >= gemm.QKV_ATTN_MIN_KV
-                and gemm.fused_rows_ok(T, nparts) and md.num_decode == T)
+                and gemm.fused_rows_ok(T, nparts) and md.num_decode == T
+                and not (self.st.shared_device and self.st.tp_size > 1))
 
     def _decode_attn(self, layer, residual: torch.Tensor, parts: Optional[torch.Tensor], positions: torch.Tensor,
                      md: attn_ops.AttnMetadata, kv: Tuple[torch.Tensor, torch.Tensor], ws: torch.Tensor,
