@@ -71,6 +71,17 @@ def main(argv):
             a[3] += overlap(b, e, gemm_spans) > 0
         for n, (c, tot, ov, g) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
             lines.append(f"| {s} | `{n}` | {c} | {tot / 1e3:.1f} | {ov / 1e3:.1f} | {100 * ov / max(tot, 1):.0f} | {g} |")
+    # timeline around the first kernel of the busiest side stream: what the main stream was doing
+    side = [s for s in by_stream if s != main_s]
+    if side:
+        s = max(side, key=lambda q: sum(e - b for b, e, _ in by_stream[q]))
+        t0 = by_stream[s][0][0] if by_stream[s] else 0
+        allk = sorted((b, e, st, n) for st, v in by_stream.items() for b, e, n in v)
+        i0 = max(0, next((i for i, k in enumerate(allk) if k[0] >= t0), 0) - 12)
+        lines += ["", f"timeline from 12 kernels before the first stream-{s} kernel (us from there)", "",
+                  "| start | end | stream | kernel |", "|---|---|---|---|"]
+        for b, e, st, n in allk[i0:i0 + 48]:
+            lines.append(f"| {(b - t0) / 1e3:.1f} | {(e - t0) / 1e3:.1f} | {st} | `{n}` |")
     text = "\n".join(lines) + "\n"
     if len(argv) > 1:
         open(argv[1], "w").write(text)
