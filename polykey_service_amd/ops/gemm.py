@@ -313,7 +313,7 @@ def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
 
 
 # weights at least this large are streamed with non-temporal loads (gate_up, MoE w13, LM head)
-NT_MIN_BYTES = 160 << 20
+NT_MIN_BYTES = int(os.environ.get("POLYKEY_NT_MIN_MB", "160")) << 20
 NT_BIT = 64
 
 
