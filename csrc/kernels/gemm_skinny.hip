@@ -454,8 +454,14 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
   const bool nt = (mode & 64) != 0 && a.row_tiles == 1;
   const bool half = (mode & 128) != 0;   // bit 7: 64-row n-blocks (KR = 1)
   if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr)) return -1;
-  if (half) {  // split-K projections only: fp32 slabs or the in-launch residual update
+  if (half) {  // split-K projections (fp32 slabs, the in-launch residual update) and the unsplit SiLU
     if (grouped || norm || nt) return -1;
+    if ((mode & 7) == kSiluMul) {  // folded-norm gate_up + SiLU, no K split: N / 64 workgroups
+      if (!packed || !a.row_scale || a.S != 1 || a.row_tiles > 1 || a.nrm_parts == nullptr || a.nrm_nparts < 1 ||
+          a.nrm_nparts > 64)
+        return -1;
+      return launch<kSiluMul, true, false, false, true, 1>(a, stream);
+    }
     if (a.row_scale) {  // folded-norm QKV slabs (packed W only)
       if ((mode & 7) != kPartial || !packed || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64)
         return -1;

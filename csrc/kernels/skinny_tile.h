@@ -541,6 +541,38 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   }
 
   // C^T tile: rows = W rows (n), cols = m:  acc[t][mt][i] = C[m = 16*mt + r][n = n0 + 16*t + 4*g + i]
+  if constexpr (MODE == kSiluMul && kR == 1) {
+    // 64-row n-blocks: wave w holds the 16 gate (w even) or up (w odd) rows of the same 16 h
+    // columns as its partner w ^ 1 (interleave block 16); the up waves hand their (row-scaled)
+    // accumulators to the gate waves through the LDS the A tiles no longer need
+    static_assert(!kProd, "KR = 1 SiLU: no in-launch hand-off");
+    __syncthreads();  // every wave is done reading the A tiles
+    float* xch = reinterpret_cast<float*>(&a_lds[0][0][0]) + (w >> 1) * MT * 256 + lane * 4;
+    if constexpr (RS)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[0][mt] *= rinv_s[min(16 * mt + r, M - 1)];
+    if (w & 1) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<f32x4*>(xch + mt * 256) = acc[0][mt];
+    }
+    __syncthreads();
+    if ((w & 1) == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + r;
+        if (m >= M) continue;
+        const f32x4 u = *reinterpret_cast<const f32x4*>(xch + mt * 256);
+        float y[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = rbf(silu(rbf(acc[0][mt][i]))) * rbf(u[i]);
+        uint2 v;
+        v.x = pack2(y[0], y[1]);
+        v.y = pack2(y[2], y[3]);
+        *reinterpret_cast<uint2*>(args.out + static_cast<int64_t>(row0 + m) * args.ldo + (n0 >> 1) + 4 * g) = v;
+      }
+    }
+    return;
+  }
   constexpr bool kSlab = MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit;
   // the in-launch residual update hands its slabs over write-through (measured faster than plain
   // stores + release: tools/gemm_lab.hip o_res / down_res); the plain split-K slabs are read by

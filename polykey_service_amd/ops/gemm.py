@@ -60,6 +60,12 @@ MODE_BF16, MODE_PARTIAL, MODE_SILU, MODE_ADD_RES_NORM, MODE_QKV_ROPE, MODE_SILU_
 # of each n-block (MODE_SILU_SPLIT) instead of by a splitk_reduce launch after it.  Measured slower
 # (70B TP=8 per-rank step 6.78 vs 6.68 ms, profiles/r5_tp_ab.jsonl): off by default
 GATE_UP_INLAUNCH = os.environ.get("POLYKEY_GATE_UP_INLAUNCH", "0") == "1"
+# a folded-norm gate_up whose 128-row n-blocks cannot fill the chip (70B TP=8: 56) as 64-row
+# n-blocks WITHOUT a K split (112 workgroups, SiLU in the epilogue: no slabs, no reduce launch)
+# instead of split over K + the SiLU reduce launch.  Measured slower: 45 us vs 26 + 5 us per layer,
+# per-rank step 7.75 vs 6.51-6.54 ms (profiles/r5_kr1.jsonl: 112 workgroups cannot stream the 117 MB
+# shard) -- off by default
+GATE_UP_KR1 = os.environ.get("POLYKEY_GATE_UP_KR1", "0") == "1"
 NORM_BIT = 32
 
 
@@ -386,6 +392,9 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         N = w_gu_interleaved.shape[0]
         out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
         Sg = gate_up_split(N, K, M) if rowscale is not None and M <= FUSED_MAX_M else 1
+        if Sg > 1 and GATE_UP_KR1 and packed is not None and M <= SKINNY_MAX_M:
+            _launch_ex(MODE_SILU | HALF_BIT, x, w_gu_interleaved, packed, 1, out=out, rowscale=rowscale)
+            return out
         if Sg > 1 and ws is not None and ws.numel() >= Sg * M * N:
             if (GATE_UP_INLAUNCH and counters is not None and packed is not None and M <= SKINNY_MAX_M
                     and counters.numel() >= N // 128):

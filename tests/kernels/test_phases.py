@@ -254,3 +254,36 @@ def test_gate_up_split_inlaunch_silu(M, H, I):
         torch.testing.assert_close(got, exp, atol=0, rtol=0)
     torch.cuda.synchronize()
     assert int(ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+@pytest.mark.parametrize("H,I", [(8192, 3584), (1024, 4096)])
+def test_gate_up_kr1_unsplit_matches_split(M, H, I, monkeypatch):
+    """The 70B TP=8 gate_up as 64-row n-blocks without a K split (GATE_UP_KR1: 112 workgroups, the
+    up waves hand their accumulators to the gate waves through LDS, SiLU in the epilogue) agrees
+    with the split-K slabs + SiLU reduce launch to bf16 rounding (one fp32 accumulation chain
+    instead of four summed slabs), and with an fp32 reference."""
+    nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
+    wg, wu = rnd(I, H, scale=0.05), rnd(I, H, scale=0.05)
+    wgu = gemm.interleave_gate_up(wg, wu)
+    gup = gemm.pack_weight(gemm.fold_norm(wgu, nw))
+    Sg = gemm.gate_up_split(2 * I, H, M)
+    assert Sg > 1
+    ws = torch.empty(Sg * M * 2 * I, dtype=torch.float32, device="cuda")
+    for it in range(3):
+        res = rnd(M, H)
+        parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 64, device="cuda"))
+        rs = gemm.RowScale(parts, 1e-5)
+        monkeypatch.setattr(gemm, "GATE_UP_KR1", False)
+        exp = gemm.linear_silu(res, wgu, ws=ws, packed=gup, rowscale=rs)
+        monkeypatch.setattr(gemm, "GATE_UP_KR1", True)
+        got = gemm.linear_silu(res, wgu, ws=ws, packed=gup, rowscale=rs)
+        scale = exp.float().abs().max().item()
+        torch.testing.assert_close(got.float(), exp.float(), atol=0.02 * scale, rtol=0.02)
+        # fp32 reference: rinv * (x @ (W diag(nw))^T), then SiLU(gate) * up
+        x = res.float()
+        rinv = torch.rsqrt((x * x).mean(dim=1, keepdim=True) + 1e-5)
+        xn = (x * rinv) * nw.float()
+        ref32 = torch.nn.functional.silu(xn @ wg.float().t()) * (xn @ wu.float().t())
+        torch.testing.assert_close(got.float(), ref32, atol=0.03 * scale, rtol=0.05)
+        assert (got.float() - exp.float()).abs().max().item() <= 0.02 * scale

@@ -85,6 +85,17 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&sink, 64 << 20));
   CHECK(hipMemset(buf, 1, bytes));
   CHECK(hipDeviceSynchronize());
+  if (argc > 1 && std::string(argv[1]) == "few") {
+    // how fast can FEWER workgroups than CUs stream 112 MiB (a 70B TP=8 gate_up shard without
+    // split-K: 56-112 n-blocks)?  us per launch, 256 / 512 threads, depth 8 / 16
+    std::printf("grid | 256 thr d8 d16 | 512 thr d8 d16 (us, 112 MiB)\n");
+    const int grids[] = {56, 64, 112, 128, 160, 224, 256};
+    for (int g : grids)
+      std::printf("%4d | %7.2f %7.2f | %7.2f %7.2f\n", g, run_sized<8, false>(buf, n_vec, sink, 112, g, 256, 40),
+                  run_sized<16, false>(buf, n_vec, sink, 112, g, 256, 40), run_sized<8, false>(buf, n_vec, sink, 112, g, 512, 40),
+                  run_sized<16, false>(buf, n_vec, sink, 112, g, 512, 40));
+    return 0;
+  }
   if (argc > 1 && std::string(argv[1]) == "sized") {
     // us per launch for the decode GEMM weight sizes (MiB) over grids / depths
     const size_t sizes[] = {32, 48, 112, 224, 1002};
