@@ -29,14 +29,14 @@ using namespace pk;
 
 namespace {
 
-template <int kPart, int NW, bool FROM_QKV, int SS = 0, int PRE = 0>
+template <int kPart, int NW, bool FROM_QKV, int SS = 0>
 __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, bf16_t* __restrict__ kc,
     bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
     float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int n_q, int n_kv, int bs,
     int max_blocks, int q_stride, int out_stride, int n_parts, float scale2, const QkvIn qi) {
   __shared__ DecodeLds<kPart, NW> lds;
-  decode_tile<kPart, NW, FROM_QKV, SS, 0, PRE>(out, q, kc, vc, block_tables, context_lens, part_o, part_ml, counters, n_q, n_kv,
+  decode_tile<kPart, NW, FROM_QKV, SS>(out, q, kc, vc, block_tables, context_lens, part_o, part_ml, counters, n_q, n_kv,
                                        bs, max_blocks, q_stride, out_stride, n_parts, scale2, qi, blockIdx.x, blockIdx.y,
                                        blockIdx.z, gridDim.z, lds, Flow{});
 }
@@ -319,10 +319,9 @@ int decode_part(int n_seqs, int n_kv, int max_ctx) {
   return n_seqs * n_kv * z < g_decode_fill ? kDecodePartSmall : kDecodePart;
 }
 
-// 1: standalone decode attention launches of at most one workgroup per CU prefetch their first
-// K/V step(s) across the q slab reduction (decode_launch_p); 0: never
-PK_EXPORT int pk_set_decode_pre(int on) {
-  g_decode_pre = on != 0;
+// 1: standalone decode attention launches of at most 128 workgroups run 8-wave workgroups
+PK_EXPORT int pk_set_decode_wide(int on) {
+  g_decode_wide = on != 0;
   return 0;
 }
 
@@ -350,19 +349,19 @@ static int decode_launch_p(void* out, const void* q, const QkvIn& qi, const void
       static_cast<bf16_t*>(const_cast<void*>(v_cache)), static_cast<const int*>(block_tables),                  \
       static_cast<const int*>(context_lens), static_cast<float*>(part_o), static_cast<float*>(part_ml),          \
       static_cast<int*>(counters), n_q, n_kv, bs, max_blocks, q_stride, out_stride, n_parts, scale * kLog2e, qi
-  // PRE (pk_set_decode_pre, off by default): at most one workgroup per CU (the 70B TP=8 shard: one
-  // kv head per rank), so the first K/V step(s) could be requested before the q slab reduction
-  // (registers are no constraint at one wave per SIMD); measured slower than the one-round prologue
-  const bool pre = g_decode_pre && static_cast<long>(grid.x) * grid.y * grid.z <= 256 && P % bs == 0;
-  constexpr int kPre = P > 128 ? 2 : 1;
+  // WIDE (pk_set_decode_wide): launches of at most 128 workgroups (the 70B TP=8 shard: 64 sequences
+  // x one kv head) as 8-wave workgroups -- twice the K/V loads in flight per CU when most CUs idle
+  // (the K/V prefetch across the slab reduction for such launches, PRE, measured slower:
+  // profiles/r5_attn_ab4.jsonl)
+  const bool wide = g_decode_wide && static_cast<long>(grid.x) * grid.y * grid.z <= 128;
   if (qi.partial != nullptr) {
-    switch (qi.S * (pre ? -1 : 1)) {
+    switch (qi.S * (wide ? -1 : 1)) {
       case 2: paged_decode_kernel<P, kDecodeWaves, true, 2><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       case 4: paged_decode_kernel<P, kDecodeWaves, true, 4><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       case 8: paged_decode_kernel<P, kDecodeWaves, true, 8><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       case 16: paged_decode_kernel<P, kDecodeWaves, true, 16><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
-      case -8: paged_decode_kernel<P, kDecodeWaves, true, 8, kPre><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
-      case -16: paged_decode_kernel<P, kDecodeWaves, true, 16, kPre><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
+      case -8: paged_decode_kernel<P, 8, true, 8><<<grid, 64 * 8, 0, stream>>>(PK_DECODE_ARGS); break;
+      case -16: paged_decode_kernel<P, 8, true, 16><<<grid, 64 * 8, 0, stream>>>(PK_DECODE_ARGS); break;
       default: paged_decode_kernel<P, kDecodeWaves, true, 0><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
     }
   } else

@@ -53,14 +53,14 @@ _FILL_SET = False
 def apply_decode_fill() -> None:
     """A/B knobs of the decode attention launch, applied once per process:
     POLYKEY_DECODE_FILL -- the workgroup count below which decode attention takes 128-key
-    partitions (csrc attention.hip decode_part; 0: always 512); POLYKEY_DECODE_PRE=1 -- K/V
-    prefetch across the q slab reduction in launches of at most one workgroup per CU (=1: on)."""
+    partitions (csrc attention.hip decode_part; 0: always 512); POLYKEY_DECODE_WIDE=1 -- 8-wave
+    workgroups for launches of at most 128 workgroups."""
     global _FILL_SET
     if not _FILL_SET:
         if os.environ.get("POLYKEY_DECODE_FILL") is not None:
             native.call("pk_set_decode_fill", int(os.environ["POLYKEY_DECODE_FILL"]))
-        if os.environ.get("POLYKEY_DECODE_PRE") is not None:
-            native.call("pk_set_decode_pre", int(os.environ["POLYKEY_DECODE_PRE"]))
+        if os.environ.get("POLYKEY_DECODE_WIDE") is not None:
+            native.call("pk_set_decode_wide", int(os.environ["POLYKEY_DECODE_WIDE"]))
     _FILL_SET = True
 
 

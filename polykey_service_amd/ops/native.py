@@ -38,7 +38,7 @@ SIGNATURES = {
     "pk_paged_decode": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, F32, I32, P],
     "pk_set_decode_z": [I32],
     "pk_set_decode_fill": [I32],
-    "pk_set_decode_pre": [I32],
+    "pk_set_decode_wide": [I32],
     "pk_paged_decode_qkv2": [P, P, I32, I32, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, I32, P],
     "pk_paged_decode_qkv": [P, P, I32, I32, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, I32, P],
     "pk_paged_prefill": [P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, F32, P],

@@ -193,9 +193,8 @@ def test_qkv_attn_fused_o_phase(nq, nkv, H, No, ctxs, with_res):
 @pytest.mark.parametrize("ctxs", [[384] * 64, [600, 1300, 7, 2100, 1], [1, 5, 33, 300]])
 def test_decode_inlaunch_partition_merge(nq, nkv, S, ctxs):
     """Decode attention from QKV slabs with the partitions merged by the last partition workgroup
-    to arrive (AttnMetadata.decode_counters) is bit-identical to the merge by a reduce launch, and
-    so is the launch that prefetches its first K/V step across the q slab reduction (one
-    workgroup per CU or fewer: pk_set_decode_pre)."""
+    to arrive (AttnMetadata.decode_counters) is bit-identical to the merge by a reduce launch; the
+    launch of 8-wave workgroups (at most 128 workgroups: pk_set_decode_wide) agrees to rounding."""
     d, bs = "cuda", 32
     B = len(ctxs)
     N = (nq + 2 * nkv) * HD
@@ -217,16 +216,17 @@ def test_decode_inlaunch_partition_merge(nq, nkv, S, ctxs):
         outs = []
         kv0 = (k1.clone(), v1.clone())
         try:
-            for pre, counters, (kc, vc) in ((0, None, (k1, v1)), (1, ctr, (k2, v2)), (1, None, kv0)):
-                native.call("pk_set_decode_pre", pre)
+            for wide, counters, (kc, vc) in ((0, None, (k1, v1)), (0, ctr, (k2, v2)), (1, None, kv0)):
+                native.call("pk_set_decode_wide", wide)
                 md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0,
                                     slot_mapping=slots, decode_block_tables=bt, decode_context_lens=cl,
                                     decode_part_o=po, decode_part_ml=pml, decode_counters=counters)
                 outs.append(A.paged_decode_from_qkv(p, pos, cs, kc, vc, md, 1 / math.sqrt(HD), nq, nkv))
         finally:
-            native.call("pk_set_decode_pre", 0)
+            native.call("pk_set_decode_wide", 1)
         torch.testing.assert_close(outs[1], outs[0], atol=0, rtol=0)
-        torch.testing.assert_close(outs[2], outs[0], atol=0, rtol=0)
+        # 8 waves split the keys differently: the same softmax, merged in another order
+        torch.testing.assert_close(outs[2].float(), outs[0].float(), atol=2e-2, rtol=2e-2)
         assert torch.equal(k1, k2) and torch.equal(v1, v2)
         assert torch.equal(k1, kv0[0]) and torch.equal(v1, kv0[1])
     torch.cuda.synchronize()

@@ -6,7 +6,7 @@ launches over 80 layers' KV caches (cold, like a decode step) and reported in us
   q                  q given in bf16 (no slab reduction / RoPE / cache write)
   ctx 32             one 32-key step per sequence: the launch's fixed cost
   fill 0             512-key partitions (64 workgroups, no merge launch) instead of 128-key ones
-  pre 0              no K/V prefetch across the q slab reduction
+  wide               8-wave workgroups (launches of <= 128 workgroups)
   merge              partitions merged in-launch by the last to arrive (no reduce launch)
 
     python tools/attn70_probe.py [--ctx 384] [--batch 64] [--heads 8,1]
@@ -89,24 +89,23 @@ def main():
     A.apply_decode_fill()
     kv_mb = a.batch * a.ctx * NKV * HD * 2 * 2 / 1e6
     rows = []
-    for name, S, mode, ctx, fill, pre, merge in (("qkv S16", 16, "qkv", a.ctx, 256, 1, 0), ("qkv S16 pre0", 16, "qkv", a.ctx, 256, 0, 0),
-                                                 ("qkv S16 merge", 16, "qkv", a.ctx, 256, 0, 1),
-                                                 ("qkv S8", 8, "qkv", a.ctx, 256, 1, 0), ("qkv S1", 1, "qkv", a.ctx, 256, 1, 0),
-                                                 ("q", 1, "q", a.ctx, 256, 1, 0), ("qkv S16 ctx32", 16, "qkv", 32, 256, 1, 0),
-                                                 ("q ctx32", 1, "q", 32, 256, 1, 0), ("qkv S16 fill0", 16, "qkv", a.ctx, 0, 1, 0),
-                                                 ("qkv S16 fill0 pre0", 16, "qkv", a.ctx, 0, 0, 0),
-                                                 ("q fill0", 1, "q", a.ctx, 0, 1, 0),
-                                                 ("qkv S4", 4, "qkv", a.ctx, 256, 0, 0),
-                                                 ("qkv S4 fill4096", 4, "qkv", a.ctx, 4096, 0, 0),
-                                                 ("qkv S4 fill4096 merge", 4, "qkv", a.ctx, 4096, 0, 1),
-                                                 ("q fill4096", 1, "q", a.ctx, 4096, 0, 0)):
+    for name, S, mode, ctx, fill, wide, merge in (("qkv S16", 16, "qkv", a.ctx, 256, 0, 0),
+                                                  ("qkv S16 merge", 16, "qkv", a.ctx, 256, 0, 1),
+                                                  ("qkv S16 fill0", 16, "qkv", a.ctx, 0, 0, 0),
+                                                  ("qkv S16 fill0 wide", 16, "qkv", a.ctx, 0, 1, 0),
+                                                  ("qkv S8 fill0", 8, "qkv", a.ctx, 0, 0, 0),
+                                                  ("qkv S8 fill0 wide", 8, "qkv", a.ctx, 0, 1, 0),
+                                                  ("qkv S4", 4, "qkv", a.ctx, 256, 0, 0),
+                                                  ("q", 1, "q", a.ctx, 256, 0, 0), ("q fill0", 1, "q", a.ctx, 0, 0, 0),
+                                                  ("qkv S16 ctx32", 16, "qkv", 32, 256, 0, 0),
+                                                  ("q ctx32", 1, "q", 32, 256, 0, 0)):
         native.call("pk_set_decode_fill", fill)
-        native.call("pk_set_decode_pre", pre)
+        native.call("pk_set_decode_wide", wide)
         us = run(a.batch, ctx, S, mode, merge=bool(merge))
         rows.append({"heads": a.heads, "variant": name, "ctx": ctx, "us": us, "kv_tbs": round(kv_mb * ctx / a.ctx / us, 2)})
         print(json.dumps(rows[-1]), flush=True)
     native.call("pk_set_decode_fill", 256)
-    native.call("pk_set_decode_pre", 1)
+    native.call("pk_set_decode_wide", 1)
 
 
 if __name__ == "__main__":
