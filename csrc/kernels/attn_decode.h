@@ -19,9 +19,11 @@ constexpr int kDecodePartSmall = 128;  // keys per partition when (seq, kv head)
 // per-rank step 6.52 vs 6.54 ms at 256 (128-key partitions + merge), profiles/r5_attn_ab4.jsonl
 int g_decode_fill = 64;
 int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
-// 8-wave workgroups for launches of <= 128 workgroups (pk_set_decode_wide): 70B TP=8 rank attention
-// 10.5 -> 10.1 us, step 6.52-6.53 -> 6.51 ms (profiles/r5_wide_attn.jsonl, r5_attn70_probe3.jsonl)
-int g_decode_wide = 1;
+// 8-wave workgroups for launches of <= 128 workgroups (pk_set_decode_wide, A/B): 70B TP=8 rank
+// attention 10.5 -> 10.1 us, step 6.52-6.53 -> 6.51 ms (profiles/r5_wide_attn.jsonl,
+// r5_attn70_probe3.jsonl).  Off: within noise, and the 4-wave tile keeps the standalone launch
+// bit-identical to the fused QKV -> attention launch (whose fallback re-runs a step through it)
+int g_decode_wide = 0;
 
 // K/V stream loads: plain (non-temporal measured slower: in-situ decode step 4.43 vs 4.45 ms,
 // tools/ab_decode.py)

@@ -223,7 +223,7 @@ def test_decode_inlaunch_partition_merge(nq, nkv, S, ctxs):
                                     decode_part_o=po, decode_part_ml=pml, decode_counters=counters)
                 outs.append(A.paged_decode_from_qkv(p, pos, cs, kc, vc, md, 1 / math.sqrt(HD), nq, nkv))
         finally:
-            native.call("pk_set_decode_wide", 1)
+            native.call("pk_set_decode_wide", 0)
         torch.testing.assert_close(outs[1], outs[0], atol=0, rtol=0)
         # 8 waves split the keys differently: the same softmax, merged in another order
         torch.testing.assert_close(outs[2].float(), outs[0].float(), atol=2e-2, rtol=2e-2)

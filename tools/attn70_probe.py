@@ -105,7 +105,7 @@ def main():
         rows.append({"heads": a.heads, "variant": name, "ctx": ctx, "us": us, "kv_tbs": round(kv_mb * ctx / a.ctx / us, 2)})
         print(json.dumps(rows[-1]), flush=True)
     native.call("pk_set_decode_fill", 256)
-    native.call("pk_set_decode_wide", 1)
+    native.call("pk_set_decode_wide", 0)
 
 
 if __name__ == "__main__":
