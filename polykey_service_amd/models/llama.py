@@ -541,9 +541,10 @@ class LlamaForCausalLM(nn.Module):
             return gemm.qkv_attn_fused(residual, at.qkv_pf, rs, ws, positions, self.cos_sin, kc, vc, md, at.scale,
                                        at.nq, at.nkv, self._flow_qkv, o=o)
         # (64-row n-blocks at half the split: half the slabs the attention prologue sums -- the 70B
-        # TP=8 shard's 10 n-blocks otherwise take split 16)
+        # TP=8 shard's 10 n-blocks otherwise take split 16; one 64-row tile only: the row-tiled wide
+        # batches keep 128-row n-blocks, 8B at 256 rows 34.5 vs 26 us, profiles/r5_wide_256_kgrid.md)
         p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, S=gemm.QKV_SPLIT or None, packed=at.qkv_pf,
-                                         half=gemm.QKV_HALF)
+                                         half=gemm.QKV_HALF and T <= gemm.SKINNY_MAX_M)
         if md.num_prefill == 0:
             return attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
         q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
