@@ -52,6 +52,10 @@ QKV_ATTN_MIN_KV = int(os.environ.get("POLYKEY_QKV_MIN_KV", "4"))
 # half the fp32 slabs the attention prologue sums (70B TP=8: 6.66-6.67 vs 6.68 ms, neutral)
 QKV_HALF = os.environ.get("POLYKEY_QKV_HALF", "1") == "1"
 QKV_SPLIT = int(os.environ.get("POLYKEY_QKV_SPLIT", "0"))  # A/B: the decode QKV's K split (0: choose_split)
+# A/B: the half-split (64-row n-block) decode projections (the o-projection) at this multiple of
+# their split -- more, smaller workgroups, more slab bytes (x2: 8B 4.04-4.05 vs 3.98-3.99 ms, 70B
+# TP=8 6.54 vs 6.50, profiles/r5_osplit.jsonl)
+HALF_SPLIT_MUL = int(os.environ.get("POLYKEY_HALF_SPLIT_MUL", "1"))
 PACKED_BIT = 16
 
 
@@ -373,6 +377,8 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
         S = choose_split(N, K, M)
         if half:
             S = max(1, S // 2)
+            if HALF_SPLIT_MUL > 1 and M <= SKINNY_MAX_M and K % (_KCHUNK * S * HALF_SPLIT_MUL) == 0:
+                S *= HALF_SPLIT_MUL
     assert ws.numel() >= S * M * N, "split-K workspace too small"
     src = packed if packed is not None else w
     native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), src.data_ptr(), M, N, K, x.stride(0), N, S,
