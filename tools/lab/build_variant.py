@@ -39,7 +39,9 @@ VARIANTS = {
     # the 4-wave prefill GEMM's 16 LDS-DMA loads of a tile, measured at gate_up against 2 per group
     # (1,453 us): all right after the barrier ("pg_front") 1,535, 4 per group in the first 4 groups
     # ("pg_first4") 1,443 (noise) -- profiles/r4_prefill_gemm_4wave.md
-    # round 5, measured and removed: "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
+    # round 5, measured and removed: "mt8_chunk256" (128-row decode tiles staging A per 256-deep chunk,
+    # one workgroup per CU: 8B at 128 rows 6.36 vs 5.62-5.65 ms, 256 rows 10.07-10.09 vs 9.21-9.22,
+    # profiles/r5_mt8.jsonl); "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
     # in flight per wave instead of two: 8B step 4.22-4.23 vs 3.99-4.00 ms, 70B TP=8 rank 6.77 vs
     # 6.54-6.57 -- profiles/r5_wdepth.jsonl)
     # measured and removed this round (variant builds of the sources of that time): "mlp_v0" (no NT /
