@@ -454,8 +454,16 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
   const bool nt = (mode & 64) != 0 && a.row_tiles == 1;
   const bool half = (mode & 128) != 0;   // bit 7: 64-row n-blocks (KR = 1)
   if (norm && (a.nrm_parts == nullptr || a.nrm_w == nullptr)) return -1;
-  if (half) {  // split-K projections (fp32 slabs, the in-launch residual update) and the unsplit SiLU
-    if (grouped || norm || nt) return -1;
+  if (half) {  // split-K projections (fp32 slabs, the in-launch residual update); bf16 out with too
+               // few 128-row n-blocks to fill the chip (the 70B TP=8 LM-head shard: 126)
+    if (grouped || norm) return -1;
+    if ((mode & 7) == kBF16) {
+      if (a.S != 1 || a.row_scale || a.row_tiles > 1) return -1;
+      if (nt) return packed ? launch<kBF16, true, false, true, false, 1>(a, stream) : -1;
+      return packed ? launch<kBF16, true, false, false, false, 1>(a, stream)
+                    : launch<kBF16, false, false, false, false, 1>(a, stream);
+    }
+    if (nt) return -1;
     if ((mode & 7) == kSiluMul) {  // folded-norm gate_up + SiLU, no K split: N / 64 workgroups
       if (!packed || !a.row_scale || a.S != 1 || a.row_tiles > 1 || a.nrm_parts == nullptr || a.nrm_nparts < 1 ||
           a.nrm_nparts > 64)

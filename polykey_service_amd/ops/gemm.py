@@ -52,6 +52,9 @@ QKV_ATTN_MIN_KV = int(os.environ.get("POLYKEY_QKV_MIN_KV", "4"))
 # half the fp32 slabs the attention prologue sums (70B TP=8: 6.66-6.67 vs 6.68 ms, neutral)
 QKV_HALF = os.environ.get("POLYKEY_QKV_HALF", "1") == "1"
 QKV_SPLIT = int(os.environ.get("POLYKEY_QKV_SPLIT", "0"))  # A/B: the decode QKV's K split (0: choose_split)
+# bf16-out decode GEMMs whose 128-row n-blocks cannot fill the chip run as 64-row n-blocks (the 70B
+# TP=8 LM-head shard: 126 -> 252 workgroups; per-rank step 6.52 vs 6.54 ms, profiles/r5_lmhalf.jsonl)
+LINEAR_HALF = os.environ.get("POLYKEY_LINEAR_HALF", "1") == "1"
 # A/B: the half-split (64-row n-block) decode projections (the o-projection) at this multiple of
 # their split -- more, smaller workgroups, more slab bytes (x2: 8B 4.04-4.05 vs 3.98-3.99 ms, 70B
 # TP=8 6.54 vs 6.50, profiles/r5_osplit.jsonl)
@@ -352,8 +355,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
     if out is None:
         out = torch.empty((M, N), dtype=x.dtype, device=x.device)
     src = packed if packed is not None else w
+    # too few 128-row n-blocks for the chip (the 70B TP=8 LM-head shard: 126): 64-row n-blocks
+    half = LINEAR_HALF and packed is not None and M <= SKINNY_MAX_M and N // _ROWS_PER_WG < _TARGET_WGS
     native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), src.data_ptr(), M, N, K, x.stride(0),
-                out.stride(0), 1, 0 | _wmode(packed), native.stream_ptr())
+                out.stride(0), 1, 0 | _wmode(packed) | (HALF_BIT if half else 0), native.stream_ptr())
     return out
 
 
