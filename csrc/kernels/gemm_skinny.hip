@@ -86,38 +86,35 @@ __global__ void __launch_bounds__(256) norm_apply_kernel(bf16_t* __restrict__ x,
 }
 
 // Sum S fp32 slabs [S, M, N] -> bf16 [M, ldo]; SILU: N = 2I interleaved (16 gate | 16 up).
-template <bool SILU>
+// One thread per 4 output columns: with SILU its 4 gate columns and the 4 up columns 16 further,
+// so every thread works (SS > 0: all 2 SS slab loads issued before the first add -- one round
+// trip; a runtime loop whose up loads followed the gate loads of half the threads took two).
+template <bool SILU, int SS>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__ out, const float* __restrict__ partial,
                                                             int S, int M, int N, int ldo) {
   const int m = blockIdx.y;
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;  // 4-column group
-  if (v * 4 >= N) return;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = 0; s < S; ++s) {
-    const float4 p = *reinterpret_cast<const float4*>(partial + (static_cast<int64_t>(s) * M + m) * N + 4 * v);
-    acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
-  }
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;  // 4-column group of the output
+  const int nout = SILU ? N / 2 : N;
+  if (v * 4 >= nout) return;
+  // SILU: output columns 4v..4v+3 = h block b, offset j; gate slab column 32 b + j, up + 16
+  const int c = SILU ? ((4 * v) >> 4) * 32 + ((4 * v) & 15) : 4 * v;
+  const float* src = partial + static_cast<int64_t>(m) * N + c;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  float4 g = slab_sum<SS>(src, slab, S);
   if (!SILU) {
     uint2 o;
-    o.x = pack2(acc.x, acc.y);
-    o.y = pack2(acc.z, acc.w);
+    o.x = pack2(g.x, g.y);
+    o.y = pack2(g.z, g.w);
     *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * ldo + 4 * v) = o;
   } else {
-    // column c = 4v; block b = c / 32, within-block j = c % 32; gate if j < 16
-    const int c = 4 * v, b = c >> 5, j = c & 31;
-    if (j >= 16) return;
-    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int s = 0; s < S; ++s) {
-      const float4 p = *reinterpret_cast<const float4*>(partial + (static_cast<int64_t>(s) * M + m) * N + c + 16);
-      u.x += p.x; u.y += p.y; u.z += p.z; u.w += p.w;
-    }
-    float g4[4] = {acc.x, acc.y, acc.z, acc.w}, u4[4] = {u.x, u.y, u.z, u.w}, y[4];
+    const float4 u = slab_sum<SS>(src + 16, slab, S);
+    float g4[4] = {g.x, g.y, g.z, g.w}, u4[4] = {u.x, u.y, u.z, u.w}, y[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) y[i] = bf2f(f2bf(silu(bf2f(f2bf(g4[i]))))) * bf2f(f2bf(u4[i]));
     uint2 o;
     o.x = pack2(y[0], y[1]);
     o.y = pack2(y[2], y[3]);
-    *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * ldo + b * 16 + j) = o;
+    *reinterpret_cast<uint2*>(out + static_cast<int64_t>(m) * ldo + 4 * v) = o;
   }
 }
 
@@ -658,11 +655,23 @@ PK_EXPORT int pk_splitk_reduce(void* out, const void* partial, int S, int M, int
                                hipStream_t stream) {
   if (M <= 0) return 0;
   if (N % 4) return -1;
-  dim3 grid((N / 4 + 255) / 256, M);
-  if (silu)
-    splitk_reduce_kernel<true><<<grid, 256, 0, stream>>>(static_cast<bf16_t*>(out), static_cast<const float*>(partial), S, M, N, ldo);
-  else
-    splitk_reduce_kernel<false><<<grid, 256, 0, stream>>>(static_cast<bf16_t*>(out), static_cast<const float*>(partial), S, M, N, ldo);
+  if (silu && N % 32) return -1;
+  dim3 grid(((silu ? N / 2 : N) / 4 + 255) / 256, M);
+  bf16_t* o = static_cast<bf16_t*>(out);
+  const float* p = static_cast<const float*>(partial);
+#define PK_SKR(SI)                                                                                   \
+  switch (S) {                                                                                       \
+    case 2: splitk_reduce_kernel<SI, 2><<<grid, 256, 0, stream>>>(o, p, S, M, N, ldo); break;        \
+    case 4: splitk_reduce_kernel<SI, 4><<<grid, 256, 0, stream>>>(o, p, S, M, N, ldo); break;        \
+    case 8: splitk_reduce_kernel<SI, 8><<<grid, 256, 0, stream>>>(o, p, S, M, N, ldo); break;        \
+    default: splitk_reduce_kernel<SI, 0><<<grid, 256, 0, stream>>>(o, p, S, M, N, ldo); break;       \
+  }
+  if (silu) {
+    PK_SKR(true)
+  } else {
+    PK_SKR(false)
+  }
+#undef PK_SKR
   return PK_CHECK_LAUNCH();
 }
 
