@@ -36,27 +36,23 @@
 
 #define PK_EXPORT extern "C" __attribute__((visibility("default")))
 
+#include "comm/signals.h"
+
 namespace {
 
-constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 1024;  // workgroups of one call (flag rows)
+using pkcomm::kMaxBlocks;
+using pkcomm::kMaxRanks;
+using pkcomm::kRrChunk;
+using pkcomm::kSigBytes;
+using pkcomm::Signals;
 constexpr int kArBlocks = 256;    // grid cap of the one-shot / two-shot all-reduce and all-gather
 constexpr int kThreads = 512;
-
-struct Signals {                                 // at the start of every rank's IPC buffer
-  uint32_t flag[kMaxBlocks][kMaxRanks];          // written by peers (remote stores)
-  uint32_t flag2[kMaxBlocks][kMaxRanks];         // two-shot: reduce-scatter results published
-  uint32_t epoch[kMaxBlocks];                    // this rank's call counter (all entries equal between calls)
-  uint32_t error;                                // device-side copy of the sticky error word
-};
 
 // per-call failure state handed to the kernels
 struct Fail {
   uint32_t* host_err;      // host-mapped pinned word: polled by the engine, sticky
   long long timeout;       // wall-clock ticks a wait may take
 };
-
-constexpr size_t kSigBytes = (sizeof(Signals) + 4095) / 4096 * 4096;
 
 struct PeerPtrs {
   char* base[kMaxRanks];  // every rank's IPC buffer as mapped in this process (own included)
@@ -450,8 +446,6 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
 // the parts are per 256-column chunk: [N / 256, M].  Arithmetic per element as the one-shot
 // (fp32 rank-order sum of bf16 partials, bf16 round, bf16 residual add); every rank ends with the
 // owner's bits.
-constexpr int kRrChunk = 256;
-
 template <int W>
 __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPtrs* __restrict__ peers, int rank,
                                                                      size_t data_bytes, const float* __restrict__ slabs,
@@ -559,10 +553,114 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
   end_call(my_sig, e);
 }
 
+// Pushed form of the two-shot fused collective (the decode GEMM drives the
+// exchange).  The projection's GEMM (kernels/skinny_tile.h kPush) has already done stage 0 of
+// reduce_residual_2shot ACROSS the fabric: the last split of every n-block summed its slabs and
+// stored the bf16 tile straight into the input slot of the chunk's owner -- remote stores over
+// xGMI, issued while the GEMM's other tiles still stream -- then stamped the owner's
+// pflag[n-block][source].  This launch therefore starts at the reduce-scatter and reads only its
+// OWN slot there:
+//   1. owner: wait for the push flags of the chunk's n-blocks from every source, sum the W tiles
+//      in rank order, add into the residual, publish the new chunk and its parts (result slot);
+//   2. all-gather: as the two-shot form.
+// Bit-identical to reduce_residual_2shot over the same slabs (the same slab order into the bf16
+// partial, the same rank-order sum).  nbc: columns per GEMM n-block (64 or 128).
+template <int W>
+__global__ void __launch_bounds__(128) reduce_residual_pushed_kernel(const PeerPtrs* __restrict__ peers, int rank,
+                                                                      size_t data_bytes, uint16_t* __restrict__ residual,
+                                                                      float* __restrict__ parts, int M, int N, int nbc,
+                                                                      const Fail fail) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
+  __shared__ uint32_t e_s, err_s, bad_s;
+  if (threadIdx.x == 0) {
+    e_s = my_sig->epoch[b] + 1;
+    err_s = my_sig->error;
+  }
+  __syncthreads();
+  if (err_s) return;
+  const uint32_t e = e_s;
+  const size_t in_slot = kSigBytes + (e & 1u) * data_bytes;
+  const size_t res_slot = kSigBytes + (2 + (e & 1u)) * data_bytes;
+  const int nchunk = N / kRrChunk, ngroups = nchunk / W;
+  const int items = M * ngroups;
+  const int per = kRrChunk / nbc;  // n-blocks per chunk
+  const int64_t parts_off = static_cast<int64_t>(M) * N * 2;
+  const uint16_t* own = reinterpret_cast<const uint16_t*>(peers->base[rank] + in_slot);
+  uint4* res_mine = reinterpret_cast<uint4*>(peers->base[rank] + res_slot);
+  float* parts_mine = reinterpret_cast<float*>(peers->base[rank] + res_slot + parts_off);
+  const int t = threadIdx.x;
+  int waited = -1;
+  for (int it = b; it < items; it += nb) {
+    const int r = it / ngroups, j = it - r * ngroups;
+    const int c = j * W + rank;
+    if (j != waited) {  // the chunk's W x per tiles have landed in my slot
+      if (t == 0) bad_s = 0u;
+      __syncthreads();
+      if (t < W * per) {
+        spin_wait(&my_sig->pflag[c * per + t % per][t / per], e, my_sig, fail);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (__hip_atomic_load(&my_sig->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) bad_s = 1u;
+      }
+      __syncthreads();
+      if (bad_s) return;  // a peer never pushed: residual untouched, the engine fails the step
+      waited = j;
+    }
+    if (t < 32) {
+      const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + t * 8;
+      uint4 v[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q)
+        v[q] = *reinterpret_cast<const uint4*>(own + pkcomm::push_off(q, r, j, t * 8, M, ngroups));
+      const uint4 rr = *reinterpret_cast<const uint4*>(residual + off);
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) acc8(acc, v[q]);
+      float res[8];
+      unpack8f(rr, res);
+      float ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        res[q] = rbf(rbf(acc[q]) + res[q]);
+        ss += res[q] * res[q];
+      }
+      const uint4 out = make_uint4(pack2(res[0], res[1]), pack2(res[2], res[3]), pack2(res[4], res[5]),
+                                   pack2(res[6], res[7]));
+      *reinterpret_cast<uint4*>(residual + off) = out;
+      res_mine[off >> 3] = out;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 32);
+      if (t == 0) {
+        parts[static_cast<int64_t>(c) * M + r] = ss;
+        parts_mine[static_cast<int64_t>(c) * M + r] = ss;
+      }
+    }
+  }
+  publish<W>(peers, rank, b, e, true);
+  if (!wait_all<W>(my_sig->flag2, b, e, my_sig, fail)) return;
+  for (int it = b; it < items; it += nb) {
+    const int r = it / ngroups, j = it - r * ngroups;
+    for (int u = t; u < 32 * W; u += 128) {
+      const int q = u / 32;
+      if (q == rank) continue;
+      const int c = j * W + q;
+      const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + (u % 32) * 8;
+      *reinterpret_cast<uint4*>(residual + off) = reinterpret_cast<const uint4*>(peers->base[q] + res_slot)[off >> 3];
+      if (u % 32 == 0)
+        parts[static_cast<int64_t>(c) * M + r] =
+            reinterpret_cast<const float*>(peers->base[q] + res_slot + parts_off)[static_cast<int64_t>(c) * M + r];
+    }
+  }
+  end_call(my_sig, e);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------- host API
 PK_EXPORT int pk_car_abi_version() { return 1; }
+
+// bytes before the first data slot of an IPC buffer (tools/push_probe.py lays out stand-ins)
+PK_EXPORT long long pk_car_sig_bytes() { return static_cast<long long>(kSigBytes); }
 
 PK_EXPORT int pk_car_ipc_handle_size() { return static_cast<int>(sizeof(hipIpcMemHandle_t)); }
 
@@ -785,6 +883,53 @@ PK_EXPORT int pk_car_reduce_residual_nparts(void* ctx, int M, int N) {
 
 PK_EXPORT int pk_car_reduce_residual_ex(void* ctx, const void* slabs, int S, const void* partial, void* residual,
                                         void* parts, int M, int N, int ld, int lds, int blocks, hipStream_t stream);
+
+// Where the decode GEMM's kPush epilogue writes (kernels/skinny_tile.h GemmArgs push_*): the
+// device array of every rank's IPC buffer, this rank, the group size and the slot size.
+PK_EXPORT int pk_car_push_target(void* ctx, void** peers, int* rank, int* world, long long* slot_bytes) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr || c->d_peers == nullptr) return -1;
+  *peers = c->d_peers;
+  *rank = c->rank;
+  *world = c->world;
+  *slot_bytes = static_cast<long long>(c->data_bytes);
+  return 0;
+}
+
+// The fused collective after a kPush GEMM (reduce_residual_pushed_kernel): residual [M, N] bf16
+// (contiguous), parts [N / 256, M]; nbc = the GEMM's n-block width (64: KR = 1, 128).
+PK_EXPORT int pk_car_reduce_residual_pushed(void* ctx, void* residual, void* parts, int M, int N, int nbc, int blocks,
+                                            hipStream_t stream) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr || c->d_peers == nullptr) return -1;
+  if (M <= 0) return 0;
+  if (c->world < 2 || (nbc != 64 && nbc != 128) || N % (kRrChunk * c->world) || N / nbc > kMaxBlocks ||
+      residual == nullptr || parts == nullptr || static_cast<size_t>(M) * N * 2 > c->data_bytes)
+    return -2;
+  const Fail fail{c->d_err, c->timeout_ticks};
+  const int items = M * (N / kRrChunk / c->world);
+  int nb = blocks <= 0 ? std::min(items, 512) : blocks;
+  nb = std::max(1, std::min({nb, items, kMaxBlocks}));
+  uint16_t* rs = static_cast<uint16_t*>(residual);
+  float* ps = static_cast<float*>(parts);
+  switch (c->world) {
+#define PK_CRP_CASE(WW)                                                                                         \
+  case WW:                                                                                                    \
+    reduce_residual_pushed_kernel<WW><<<nb, 128, 0, stream>>>(c->d_peers, c->rank, c->data_bytes, rs, ps, M, N, nbc, \
+                                                              fail);                                           \
+    break;
+    PK_CRP_CASE(2)
+    PK_CRP_CASE(3)
+    PK_CRP_CASE(4)
+    PK_CRP_CASE(5)
+    PK_CRP_CASE(6)
+    PK_CRP_CASE(7)
+    PK_CRP_CASE(8)
+#undef PK_CRP_CASE
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
 
 PK_EXPORT int pk_car_reduce_residual(void* ctx, const void* slabs, int S, const void* partial, void* residual,
                                      void* parts, int M, int N, int blocks, hipStream_t stream) {

@@ -428,6 +428,15 @@ int launch_pk(const GemmArgs& a, bool packed, bool nt, hipStream_t stream) {
   return packed ? launch<MODE, true, NORM, false>(a, stream) : launch<MODE, false, NORM, false>(a, stream);
 }
 
+// kPush: one 64-row tile, split-K tickets, a TP group whose owner chunks split N evenly, and
+// n-blocks (of ncol columns) that the owners' push-flag rows can index
+bool push_ok(const GemmArgs& a, int ncol) {
+  return a.counters != nullptr && a.partial != nullptr && a.push_peers != nullptr && a.push_world >= 2 &&
+         a.push_world <= pkcomm::kMaxRanks && a.push_rank >= 0 && a.push_rank < a.push_world && a.M <= 64 &&
+         a.row_tiles == 1 && !a.row_scale && a.N % (pkcomm::kRrChunk * a.push_world) == 0 &&
+         a.N / ncol <= pkcomm::kMaxBlocks && static_cast<long long>(a.M) * a.N * 2 <= a.push_bytes;
+}
+
 int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
   if (args.M <= 0) return 0;
   GemmArgs a = args;
@@ -480,6 +489,11 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
       return packed ? launch<kAddResNorm, true, false, false, false, 1>(a, stream)
                     : launch<kAddResNorm, false, false, false, false, 1>(a, stream);
     }
+    if ((mode & 7) == kPush) {
+      if (!push_ok(a, 64)) return -1;
+      return packed ? launch<kPush, true, false, false, false, 1>(a, stream)
+                    : launch<kPush, false, false, false, false, 1>(a, stream);
+    }
     return -1;
   }
   if (a.row_scale && (grouped || norm || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64))
@@ -500,6 +514,9 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
     case kQkvRope:
       if (a.counters == nullptr || a.N != (a.nq + 2 * a.nkv) * 128 || a.bs <= 0 || a.bs % 32) return -1;
       return norm ? launch_pk<kQkvRope, true>(a, packed, nt, stream) : launch_pk<kQkvRope, false>(a, packed, nt, stream);
+    case kPush:
+      if (norm || !push_ok(a, 128)) return -1;
+      return packed ? launch<kPush, true, false, false>(a, stream) : launch<kPush, false, false, false>(a, stream);
     case kSiluSplit:
       // interleaved gate / up split over K, reduced in-launch by the last split of each n-block
       // (SiLU applied there): folded-norm row scale, packed W, one 64-row tile, counters [N / 128]
@@ -528,7 +545,7 @@ PK_EXPORT int pk_skinny_gemm(void* out, void* partial, const void* A, const void
   return dispatch(a, mode, stream);
 }
 
-// Full-featured entry: modes 0-4 (see Mode), bit 4 packed W, bit 5 RMSNorm prologue, bit 6 NT W.
+// Full-featured entry: modes 0-6 (see Mode), bit 4 packed W, bit 5 RMSNorm prologue, bit 6 NT W.
 PK_EXPORT int pk_skinny_gemm_ex(const GemmArgs* args, int mode, hipStream_t stream) {
   return dispatch(*args, mode, stream);
 }

@@ -3,6 +3,7 @@
 #pragma once
 #include <type_traits>
 
+#include "comm/signals.h"
 #include "common.h"
 #include "flow.h"
 
@@ -38,6 +39,9 @@ struct GemmArgs {
                              //   residual stream, the norm weight is pre-multiplied into W's columns)
   int row_tiles;             // set by dispatch: row tiles of M (> 1: M > 64, see skinny_gemm_kernel)
   int tile_rows;             // set by dispatch: rows per row tile (64, or 128 for the MT = 8 variant)
+  const char* const* push_peers;  // kPush: every TP rank's IPC buffer (custom_ar PeerPtrs, device)
+  long long push_bytes;      // kPush: bytes of one IPC data slot
+  int push_rank, push_world; // kPush: this rank, TP group size
 };
 
 namespace {
@@ -58,7 +62,12 @@ namespace {
 //   kSiluSplit:  interleaved gate / up split over K (the fused MLP's gate_up when N / 128 tiles
 //                alone cannot fill the chip, e.g. 70B TP=8: 56 n-blocks): silu(gate) * up of the
 //                summed slabs -> h, stored write-through for the in-launch hand-off.
-enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4, kSiluSplit = 5 };
+//   kPush:       a row-parallel TP projection whose epilogue drives its collective: bf16(sum) of
+//                the n-block is stored straight into the input slot of the rank that owns its
+//                256-column chunk (remote stores over xGMI while the other tiles still stream),
+//                then that rank's push flag [n-block][this rank] is stamped with the call's
+//                epoch (custom_allreduce.hip reduce_residual_pushed_kernel consumes them).
+enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4, kSiluSplit = 5, kPush = 6 };
 constexpr int kMaxRows = 1024;  // decode batch bound of the row-tiled modes
 constexpr int kPartCols = 512;  // columns per sum-of-squares part (residual_parts_kernel)
 
@@ -179,6 +188,42 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
         for (int off = TPR / 2; off > 0; off >>= 1) sq += __shfl_xor(sq, off, TPR);
         if (tid % TPR == 0) args.sumsq_parts[static_cast<int64_t>(nb) * M + m] = sq;
       }
+    }
+  } else if constexpr (MODE == kPush) {
+    constexpr int TPR = NCOL / 4, RPP = 256 / TPR;
+    const int W = args.push_world, me = args.push_rank;
+    // the call's epoch: this rank's counter + 1 (every entry is equal between calls)
+    auto* mine = reinterpret_cast<pkcomm::Signals*>(const_cast<char*>(args.push_peers[me]));
+    const uint32_t e = __hip_atomic_load(&mine->epoch[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+    const int chunk = nbase / pkcomm::kRrChunk, owner = chunk % W, ng = N / pkcomm::kRrChunk / W;
+    char* obase = const_cast<char*>(args.push_peers[owner]);
+    bf16_t* dst = reinterpret_cast<bf16_t*>(obase + pkcomm::kSigBytes + (e & 1u) * args.push_bytes);
+    const int x = nbase % pkcomm::kRrChunk + (tid % TPR) * 4;
+    const int c = nbase + (tid % TPR) * 4;
+    for (int m0 = tid / TPR; m0 < M; m0 += RPP * RB) {
+      float4 a[RB];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int m = min(m0 + RPP * i, M - 1);
+        a[i] = slab_sum<SS, true>(args.partial + static_cast<int64_t>(m) * N + c, slab, S, args.partial);
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int m = m0 + RPP * i;
+        if (m >= M) break;
+        uint2 o;
+        o.x = pack2(a[i].x, a[i].y);
+        o.y = pack2(a[i].z, a[i].w);
+        *reinterpret_cast<uint2*>(dst + pkcomm::push_off(me, m, chunk / W, x, M, ng)) = o;
+      }
+    }
+    // every push drained, system release, then the owner's flag (custom_allreduce.hip publish)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(&reinterpret_cast<pkcomm::Signals*>(obase)->pflag[nb][me], e, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     }
   } else {  // kQkvRope: n-block nb is head nb of q | k | v
     const int nq = args.nq, nkv = args.nkv, bs = args.bs;
@@ -573,11 +618,12 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
     }
     return;
   }
-  constexpr bool kSlab = MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit;
+  constexpr bool kSlab =
+      MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit || MODE == kPush;
   // the in-launch residual update hands its slabs over write-through (measured faster than plain
   // stores + release: tools/gemm_lab.hip o_res / down_res); the plain split-K slabs are read by
   // the next kernel and stay plain (write-through made those slower)
-  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kSiluSplit || (MODE == kPartial && kProd);
+  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kSiluSplit || MODE == kPush || (MODE == kPartial && kProd);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = 16 * mt + r;
@@ -630,7 +676,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   }
   if constexpr ((MODE == kSiluMul || MODE == kPartial) && kProd)  // output columns of n-block nb
     flow_signal(fl, flow_slice(fl, nb, MODE == kSiluMul ? 64 * kR / 2 : 64 * kR));
-  if constexpr (MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit) {
+  if constexpr (MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit || MODE == kPush) {
     // ---- in-launch split-K reduction by the last split of this n-block to arrive
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -55,7 +55,8 @@ def _g(pattern: str) -> List[str]:
 
 def targets() -> List[Target]:
     return [
-        Target("libpk_kernels", "hip", _g("csrc/kernels/*.hip"), _g("csrc/kernels/*.h") + _g("csrc/kernels/*.cuh")),
+        Target("libpk_kernels", "hip", _g("csrc/kernels/*.hip"), _g("csrc/kernels/*.h") + _g("csrc/kernels/*.cuh")
+               + _g("csrc/comm/signals.h")),
         Target("libpk_comm", "hip", _g("csrc/comm/*.hip"), _g("csrc/comm/*.h")),
         Target("_pk_aesgcm", "pybind", _g("csrc/security/*.cpp"), _g("csrc/security/*.h"), ["crypto"]),
         Target("_pk_runtime", "pybind", _g("csrc/runtime/*.cpp"), _g("csrc/runtime/*.h")),

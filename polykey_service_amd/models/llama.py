@@ -626,6 +626,13 @@ class LlamaForCausalLM(nn.Module):
         reader.  ``down``: tiled as gemm.linear_down (else linear_partial, half)."""
         car = self.st.custom_ar
         M, N = residual.shape
+        if (gemm.TP_PUSH and wp is not None and residual.is_cuda and hasattr(car, "push_ok")
+                and getattr(self, "_push_counters", None) is not None and car.push_ok(M, N, 64)):
+            # the GEMM's epilogue stores each finished tile into its owner's slot (xGMI under the
+            # GEMM's tail); the collective starts at the reduce-scatter
+            nbc = gemm.push_projection(x, w, ws, wp, self._push_counters, car.push_target(), down=down)
+            self._push_calls = getattr(self, "_push_calls", 0) + 1  # tools/tp_rehearsal.py reports it
+            return car.reduce_residual_pushed(residual, buf, nbc)
 
         def gemm_of(xx, ww, pp, out):
             return gemm.linear_down(xx, ww, out, pp) if down else gemm.linear_partial(xx, ww, out, packed=pp, half=True)
@@ -691,6 +698,9 @@ class LlamaForCausalLM(nn.Module):
             gu = self.layers[0].mlp.gate_up if hasattr(self.layers[0].mlp, "gate_up") else None
             self._gu_counters = (torch.zeros(gu.shape[0] // 128, dtype=torch.int32, device=self.device)
                                  if n and gu is not None else None)
+            # split-K arrival counters of the push GEMMs (gemm.TP_PUSH: o / down, N = hidden)
+            self._push_counters = (torch.zeros(self.cfg.hidden_size // 64, dtype=torch.int32, device=self.device)
+                                   if self.st.tp_size > 1 else None)
         return self._ws
 
     def _gate_up_split_elems(self) -> int:

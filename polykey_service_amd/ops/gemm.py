@@ -62,7 +62,12 @@ HALF_SPLIT_MUL = int(os.environ.get("POLYKEY_HALF_SPLIT_MUL", "1"))
 PACKED_BIT = 16
 
 
-MODE_BF16, MODE_PARTIAL, MODE_SILU, MODE_ADD_RES_NORM, MODE_QKV_ROPE, MODE_SILU_SPLIT = 0, 1, 2, 3, 4, 5
+MODE_BF16, MODE_PARTIAL, MODE_SILU, MODE_ADD_RES_NORM, MODE_QKV_ROPE, MODE_SILU_SPLIT, MODE_PUSH = 0, 1, 2, 3, 4, 5, 6
+# TP decode: the row-parallel projections' GEMM epilogue pushes its finished tiles into the owner
+# ranks' IPC slots (MODE_PUSH, :func:`push_projection`) and the collective starts at the
+# reduce-scatter (custom_ar.reduce_residual_pushed).  Bit-identical to GEMM + fused collective; off
+# by default until an 8-GPU run has timed it (one GPU cannot show the xGMI traffic it hides)
+TP_PUSH = os.environ.get("POLYKEY_TP_PUSH", "0") == "1"
 # a decode gate_up split over K (70B TP=8: 56 n-blocks) reduced + SiLU'd in-launch by the last split
 # of each n-block (MODE_SILU_SPLIT) instead of by a splitk_reduce launch after it.  Measured slower
 # (70B TP=8 per-rank step 6.78 vs 6.68 ms, profiles/r5_tp_ab.jsonl): off by default
@@ -89,7 +94,8 @@ class GemmArgs(ctypes.Structure):
                 ("nkv", ctypes.c_int), ("bs", ctypes.c_int), ("row_offsets", ctypes.c_void_p),
                 ("w_stride", ctypes.c_longlong), ("groups", ctypes.c_int), ("max_group_rows", ctypes.c_int),
                 ("a_rows", ctypes.c_void_p), ("a_row_div", ctypes.c_int), ("row_scale", ctypes.c_int),
-                ("row_tiles", ctypes.c_int), ("tile_rows", ctypes.c_int)]
+                ("row_tiles", ctypes.c_int), ("tile_rows", ctypes.c_int), ("push_peers", ctypes.c_void_p),
+                ("push_bytes", ctypes.c_longlong), ("push_rank", ctypes.c_int), ("push_world", ctypes.c_int)]
 
 
 _ARGS_CHECKED = False
@@ -547,6 +553,45 @@ def linear_down(h: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, packed: Opti
                     1 | PACKED_BIT | HALF_BIT, native.stream_ptr())
         return Partial(ws, S, M, N)
     return linear_partial(h, w, ws, S, packed=packed)
+
+
+class PushTarget(NamedTuple):
+    """Where a MODE_PUSH epilogue stores (custom_ar.CustomAllReduce.push_target): the device array
+    of every TP rank's IPC buffer, this rank, the group size, the bytes of one data slot."""
+    peers: int
+    rank: int
+    world: int
+    slot_bytes: int
+
+
+def push_projection(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, packed: torch.Tensor,
+                    counters: torch.Tensor, target: PushTarget, down: bool = False,
+                    split: Optional[int] = None) -> int:
+    """A row-parallel TP decode projection x @ w^T whose epilogue drives its collective: tiled and
+    split exactly as :func:`linear_down` (``down``) or :func:`linear_partial` ``half=True`` (the o
+    projection), so its slabs are bit-identical; the last split of every n-block stores bf16(sum of
+    the slabs) into the owner rank's input slot and stamps the owner's push flag.  ``counters``:
+    int32 >= N / 64, zeroed once (left zeroed).  Returns the n-block width the owners' collective
+    needs (custom_ar.reduce_residual_pushed)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if down:
+        S = choose_split(N, K, M)
+        half = down_kr(N, K, M) == 1 and M <= FUSED_MAX_M
+    else:
+        half = packed.numel() * packed.element_size() < NT_MIN_BYTES
+        S = choose_split(N, K, M)
+        if half:
+            S = max(1, S // 2)
+            if HALF_SPLIT_MUL > 1 and M <= SKINNY_MAX_M and K % (_KCHUNK * S * HALF_SPLIT_MUL) == 0:
+                S *= HALF_SPLIT_MUL
+    S = split or S  # (tools/push_probe.py: other splits, not bit-identical to the serving chain)
+    nbc = 64 if half else 128
+    assert ws.numel() >= S * M * N and counters.numel() >= N // 64 and counters.dtype == torch.int32
+    _launch_ex(MODE_PUSH | (HALF_BIT if half else 0), x, w, packed, S, ws=ws, counters=counters,
+               push_peers=target.peers, push_bytes=target.slot_bytes, push_rank=target.rank,
+               push_world=target.world)
+    return nbc
 
 
 def gate_up_split(N2: int, K: int, M: int) -> int:

@@ -43,6 +43,10 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_reduce_residual.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _P]
         lib.pk_car_reduce_residual_nparts.argtypes = [_P, _I, _I]
         lib.pk_car_reduce_residual_ex.argtypes = [_P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _P]
+        lib.pk_car_push_target.argtypes = [_P, ctypes.POINTER(_P), ctypes.POINTER(_I), ctypes.POINTER(_I),
+                                           ctypes.POINTER(_LL)]
+        lib.pk_car_reduce_residual_pushed.argtypes = [_P, _P, _P, _I, _I, _I, _I, _P]
+        lib.pk_car_sig_bytes.restype = _LL
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_clear_error.argtypes = [_P]
         lib.pk_car_set_error.argtypes = [_P]
@@ -193,6 +197,39 @@ class CustomAllReduce:
             torch.cuda.current_stream(self.device).cuda_stream)
         if rc != 0:
             raise RuntimeError(f"fused TP reduce (chunk {chunk}) launch failed ({rc})")
+
+    def push_target(self):
+        """Where a decode GEMM's push epilogue writes (gemm.push_projection)."""
+        if getattr(self, "_push_target", None) is None:
+            from ..ops.gemm import PushTarget
+            peers, rank, world, nbytes = _P(), _I(), _I(), _LL()
+            if self.lib.pk_car_push_target(self.ctx, ctypes.byref(peers), ctypes.byref(rank), ctypes.byref(world),
+                                           ctypes.byref(nbytes)) != 0:
+                raise RuntimeError("pk_car_push_target failed")
+            self._push_target = PushTarget(peers.value, rank.value, world.value, nbytes.value)
+        return self._push_target
+
+    def push_ok(self, M: int, N: int, nbc: int = 128) -> bool:
+        """Shapes the pushed collective takes: the two-shot layout (parts per 256 columns, what
+        :meth:`nparts` gives the consumers), one 64-row tile, n-blocks the flag rows index."""
+        return (0 < M <= 64 and N % (256 * self.world) == 0 and N // nbc <= 1024 and M * N * 2 <= self.max_bytes
+                and self.nparts(M, N) == N // 256)
+
+    def reduce_residual_pushed(self, residual: torch.Tensor, parts: torch.Tensor, nbc: int) -> torch.Tensor:
+        """:meth:`reduce_residual` after a push GEMM (gemm.push_projection): every rank's bf16
+        partial of this rank's chunks is already in this rank's slot, so the collective starts at
+        the reduce-scatter.  Same residual and parts bits as the two-shot :meth:`reduce_residual`."""
+        M, N = residual.shape
+        if not (residual.is_contiguous() and residual.dtype == torch.bfloat16 and self.push_ok(M, N, nbc)):
+            raise ValueError(f"reduce_residual_pushed: unsupported residual {tuple(residual.shape)} {residual.dtype}")
+        nparts = N // 256
+        assert parts.numel() >= nparts * M and parts.dtype == torch.float32
+        rc = self.lib.pk_car_reduce_residual_pushed(self.ctx, residual.data_ptr(), parts.data_ptr(), M, N, nbc,
+                                                    self.fused_blocks,
+                                                    torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"pushed TP reduce launch failed ({rc})")
+        return parts.view(-1)[: nparts * M].view(nparts, M)
 
     def set_timeout(self, seconds: float) -> None:
         self.lib.pk_car_set_timeout_ms(self.ctx, max(1, int(seconds * 1000)))

@@ -1,4 +1,4 @@
-"""One-shot / two-shot xGMI all-reduce (csrc/comm/custom_allreduce.hip) with 2 and 8 ranks.
+"""One-shot / two-shot xGMI all-reduce (csrc/comm/custom_allreduce.hip) with 2, 4 and 8 ranks.
 
 On a one-GPU box all ranks share cuda:0: IPC handles, peer flags, parity slots and graph
 replay are exercised exactly as across GPUs (the loads just do not cross xGMI); 8 ranks run
@@ -65,6 +65,7 @@ def _worker(rank, world, port, q):
         assert car.error() == 0
         _fused_phase(car, rank, world, dev)
         _overlap_phase(car, rank, world, dev)
+        _push_phase(car, rank, world, dev)
         # a rank that skips a call: every rank that waits for it times out and fails loudly
         # (sticky error word, read without a GPU sync), and later calls return at once
         car.set_timeout(1.0)
@@ -256,6 +257,81 @@ def _overlap_phase(car, rank, world, dev):
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(r1, r2) and torch.equal(p1, p2), ("graph", it)
+    assert car.error() == 0
+
+
+def _push_phase(car, rank, world, dev):
+    """The GEMM epilogue drives the collective (gemm.push_projection): the o / down
+    projections' last split of every n-block stores its bf16 tile into the owner rank's slot and
+    stamps the owner's push flag; reduce_residual_pushed starts at the reduce-scatter.  Residual and
+    parts bit-identical to GEMM + two-shot reduce_residual at the 70B TP=8 per-rank shapes, eager,
+    interleaved with other collectives, and graph-replayed."""
+    from polykey_service_amd.ops import gemm
+    M, N = 64, 8192
+    if not car.push_ok(M, N, 64):
+        assert world < 4  # the one-shot layout (parts per 1024 columns) stays unpushed
+        return
+    car.fused_blocks = 32
+    tgt = car.push_target()
+    assert tgt.rank == rank and tgt.world == world
+    g = torch.Generator().manual_seed(13)
+    gr = torch.Generator().manual_seed(3000 + rank)
+    ctr = torch.zeros(N // 64, dtype=torch.int32, device=dev)
+    np_ = car.nparts(M, N)
+    assert np_ == N // 256
+    for K, down in ((1024, False), (3584, True)):
+        res0 = (torch.randn(M, N, generator=g) * 2).to(torch.bfloat16).to(dev)
+        x = torch.randn(M, K, generator=gr).to(torch.bfloat16).to(dev)
+        w = (torch.randn(N, K, generator=gr) * 0.05).to(torch.bfloat16).to(dev)
+        wp = gemm.pack_weight(w)
+        ws1 = torch.empty(8 * M * N, dtype=torch.float32, device=dev)
+        ws2 = torch.empty_like(ws1)
+        p1 = torch.zeros(np_ * M, dtype=torch.float32, device=dev)
+        p2 = torch.zeros_like(p1)
+        r1, r2 = res0.clone(), res0.clone()
+
+        def ref():
+            r1.copy_(res0)
+            pend = gemm.linear_down(x, w, ws1, wp) if down else gemm.linear_partial(x, w, ws1, packed=wp, half=True)
+            car.reduce_residual(pend, r1, p1)
+
+        def pushed():
+            r2.copy_(res0)
+            nbc = gemm.push_projection(x, w, ws2, wp, ctr, tgt, down=down)
+            car.reduce_residual_pushed(r2, p2, nbc)
+
+        for it in range(2):
+            dist.barrier()
+            ref()
+            torch.cuda.synchronize()
+            dist.barrier()
+            pushed()
+            torch.cuda.synchronize()
+            assert car.error() == 0, ("push timeout", K, it)
+            assert torch.equal(r1, r2), ("residual", K, it, int((r1 != r2).sum()))
+            assert torch.equal(p1, p2), ("parts", K, it)
+            assert int(ctr.abs().sum()) == 0, "split-K counters must be left zeroed"
+            # another collective in between: the push GEMM reads the shared call epoch
+            car.all_reduce(torch.ones(4096, dtype=torch.bfloat16, device=dev))
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        dist.barrier()
+        with torch.cuda.stream(s):
+            pushed()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        dist.barrier()
+        with torch.cuda.graph(graph):
+            pushed()
+        for it in range(3):
+            dist.barrier()
+            ref()
+            torch.cuda.synchronize()
+            dist.barrier()
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(r1, r2) and torch.equal(p1, p2), ("graph", K, it)
     assert car.error() == 0
 
 

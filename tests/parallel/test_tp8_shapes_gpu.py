@@ -57,6 +57,17 @@ def test_llama3_70b_tp8_overlapped_collectives(tmp_path):
     assert res["graph_equals_eager"] and res["ref_rows_outside_noise"] == [], res
 
 
+def test_llama3_70b_tp8_pushed_collectives(tmp_path):
+    """The row-parallel projections' GEMM epilogues push their tiles into the owner ranks' slots
+    (POLYKEY_TP_PUSH, gemm.push_projection + custom_ar.reduce_residual_pushed): graphs equal eager,
+    logits inside the TP=1 noise band, and the decode steps really took the pushed path."""
+    env = dict(os.environ, POLYKEY_TP_PUSH="1")
+    res = _rehearse(str(tmp_path / "tp8p"), env=env)
+    assert res["fused_tp_decode"] and res["car_err"] == 0 and res["graph_steps"] > 0, res
+    assert res["tp_push_calls"] > 0, res
+    assert res["graph_equals_eager"] and res["ref_rows_outside_noise"] == [], res
+
+
 def test_llama3_70b_tp8_dropped_partial_is_caught(tmp_path):
     """Fault injection: rank 3 drops its attention partial in layer 1 (POLYKEY_FAULT_DROP_PARTIAL);
     every comparison prompt's logits must leave the noise band."""

@@ -27,3 +27,15 @@ def test_grouped_reference_matches_dense_reference():
     y = gemm_prefill.grouped_linear(x, w, offs, silu=True)
     assert y.shape == (40, 128) and torch.count_nonzero(y[33:]) == 0
     torch.testing.assert_close(y[10:33], gemm_prefill.linear(x[10:33], w[2], silu=True))
+
+
+def test_gemm_args_mirror_matches_the_native_struct():
+    """ops/gemm.py GemmArgs (ctypes) has the size of csrc/kernels/skinny_tile.h GemmArgs, including
+    the push fields of the TP decode GEMM epilogue; the comm library exports the push entry points."""
+    import ctypes
+
+    from polykey_service_amd.ops import gemm, native
+    from polykey_service_amd.parallel import custom_ar
+    assert native.lib().pk_gemm_args_size() == ctypes.sizeof(gemm.GemmArgs)
+    lib = custom_ar._lib()
+    assert lib.pk_car_push_target and lib.pk_car_reduce_residual_pushed

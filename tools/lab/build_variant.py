@@ -24,6 +24,13 @@ VARIANTS = {
                    "      if constexpr (kWaitSlice)  // the producers' output, handed off in-launch: sc1 loads"),
                   ("skinny_tile.h", "rs_p[h * kRsLoads + q] = kWaitRes ? ldf_sc1(args.nrm_parts, p) : *p;",
                    "rs_p[h * kRsLoads + q] = *p;")],
+    # timing only (NOT coherent): the TP push epilogue (MODE_PUSH) without the system release
+    # before the owner's flag, and without the pushed stores themselves (tools/push_probe.py)
+    "push_nofence": [("skinny_tile.h", """      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(&reinterpret_cast<pkcomm::Signals*>(obase)->pflag""",
+                      """      __hip_atomic_store(&reinterpret_cast<pkcomm::Signals*>(obase)->pflag""")],
+    "push_nostore": [("skinny_tile.h", "        *reinterpret_cast<uint2*>(dst + pkcomm::push_off(me, m, chunk / W, x, M, ng)) = o;",
+                      "        if (o.x == 0x7fc07fc1u) *reinterpret_cast<uint2*>(dst + pkcomm::push_off(me, m, chunk / W, x, M, ng)) = o;")],
     # the fused QKV -> attention launch without the K/V prefetch before the hand-off wait
     "pre0": [("decode_fused.hip", "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 2>(",
               "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 0>(")],
@@ -55,6 +62,7 @@ def build(name: str) -> str:
     work = tempfile.mkdtemp(prefix=f"pkvar_{name}_")
     kdir = os.path.join(work, "kernels")
     shutil.copytree(src, kdir)
+    shutil.copytree(os.path.join(REPO, "csrc", "comm"), os.path.join(work, "comm"))  # comm/signals.h
     for fname, old, new in VARIANTS[name]:
         p = os.path.join(kdir, fname)
         text = open(p).read()

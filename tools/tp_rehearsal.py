@@ -251,7 +251,8 @@ def role_rank(a) -> int:
     tn = run(1 + a.steps, 2)
     res.update(batch=a.batch, prompt=a.prompt, steps=a.steps,
                decode_ms_per_step_shared_gpu=round((tn - t1) / a.steps * 1e3, 3),
-               car_err=st.custom_ar.error(), fused_tp_decode=eng.model._rowscale_ok(
+               car_err=st.custom_ar.error(), tp_push_calls=getattr(eng.model, "_push_calls", 0),
+               fused_tp_decode=eng.model._rowscale_ok(
                    torch.zeros((a.batch, eng.mcfg.hidden_size), dtype=torch.bfloat16, device="cuda:0")))
     eng.runner.stop_workers()
     print(json.dumps(res), flush=True)
