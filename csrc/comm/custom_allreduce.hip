@@ -65,6 +65,7 @@ struct Ctx {
   PeerPtrs peers{};
   PeerPtrs* d_peers = nullptr;
   bool opened[kMaxRanks] = {};
+  char* loop[kMaxRanks] = {};  // loopback context: the stand-in peer buffers it owns
   uint32_t* h_err = nullptr;   // host-mapped error word (hipHostMalloc mapped | coherent)
   uint32_t* d_err = nullptr;   // its device alias
   long long timeout_ticks = 0;
@@ -828,8 +829,46 @@ PK_EXPORT void pk_car_destroy(void* ctx) {
     if (c->opened[j]) (void)hipIpcCloseMemHandle(c->peers.base[j]);
   if (c->d_peers) (void)hipFree(c->d_peers);
   if (c->local) (void)hipFree(c->local);
+  for (int j = 0; j < kMaxRanks; ++j)
+    if (c->loop[j]) (void)hipFree(c->loop[j]);
   if (c->h_err) (void)hipHostFree(c->h_err);
   delete c;
+}
+
+// Loopback context for one-process timing of the real collective kernels (tools/tp_solo.py
+// --car loopback): the W - 1 "peers" are stand-in buffers on this device, and every flag row of
+// every buffer is pre-stamped far ahead of any epoch this run reaches, so no wait ever blocks.  The
+// kernels do all their own work (slab reduction, publishes, stores, reads of the stand-ins' slots);
+// what is missing is the xGMI latency and the skew between real ranks.  Results are meaningless.
+PK_EXPORT void* pk_car_create_loopback(int rank, int world, long long data_bytes) {
+  Ctx* c = static_cast<Ctx*>(pk_car_create(rank, world, data_bytes));
+  if (c == nullptr) return nullptr;
+  const size_t total = kSigBytes + 4 * c->data_bytes;
+  for (int j = 0; j < world; ++j) {
+    if (j != rank) {
+      void* p = nullptr;
+      if (hipExtMallocWithFlags(&p, total, hipDeviceMallocUncached) != hipSuccess ||
+          hipMemset(p, 0, total) != hipSuccess) {
+        pk_car_destroy(c);
+        return nullptr;
+      }
+      c->loop[j] = static_cast<char*>(p);
+      c->peers.base[j] = c->loop[j];
+    }
+    // flag, flag2 and pflag rows: 3 x kMaxBlocks x kMaxRanks words from the start of Signals
+    if (hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(c->peers.base[j]), 0x40000000,
+                     3 * kMaxBlocks * kMaxRanks) != hipSuccess) {
+      pk_car_destroy(c);
+      return nullptr;
+    }
+  }
+  if (hipMalloc(&c->d_peers, sizeof(PeerPtrs)) != hipSuccess ||
+      hipMemcpy(c->d_peers, &c->peers, sizeof(PeerPtrs), hipMemcpyHostToDevice) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    pk_car_destroy(c);
+    return nullptr;
+  }
+  return c;
 }
 
 // All-gather of a [rows, row_bytes] row block per rank into out [rows, world * row_bytes]

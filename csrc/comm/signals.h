@@ -26,6 +26,8 @@ struct Signals {                                 // at the start of every rank's
 };
 
 constexpr size_t kSigBytes = (sizeof(Signals) + 4095) / 4096 * 4096;
+// the flag rows lead the struct (pk_car_create_loopback pre-stamps them in one memset)
+static_assert(offsetof(Signals, epoch) == 3 * sizeof(uint32_t) * kMaxBlocks * kMaxRanks, "flag rows first");
 
 // Element offset (bf16) in an owner's input slot of the pushed partial of source rank `src`,
 // row r, column x of the owner's local chunk lc: [src][row][local chunk][256 columns].  An owner

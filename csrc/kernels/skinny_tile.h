@@ -198,6 +198,11 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
     const int chunk = nbase / pkcomm::kRrChunk, owner = chunk % W, ng = N / pkcomm::kRrChunk / W;
     char* obase = const_cast<char*>(args.push_peers[owner]);
     bf16_t* dst = reinterpret_cast<bf16_t*>(obase + pkcomm::kSigBytes + (e & 1u) * args.push_bytes);
+    // system-scope write-through stores (sc0 sc1): complete once acknowledged, so the flag needs
+    // no release fence -- an L2 write-back per workgroup measured 3 us of a 6 us GEMM
+    // (tools/push_probe.py); slots are < 2 GiB: 32-bit buffer offsets
+    const auto drs = __builtin_amdgcn_make_buffer_rsrc(dst, static_cast<short>(0), 0x7ffffff0, 0x00020000);
+    typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
     const int x = nbase % pkcomm::kRrChunk + (tid % TPR) * 4;
     const int c = nbase + (tid % TPR) * 4;
     for (int m0 = tid / TPR; m0 < M; m0 += RPP * RB) {
@@ -211,20 +216,17 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
       for (int i = 0; i < RB; ++i) {
         const int m = m0 + RPP * i;
         if (m >= M) break;
-        uint2 o;
-        o.x = pack2(a[i].x, a[i].y);
-        o.y = pack2(a[i].z, a[i].w);
-        *reinterpret_cast<uint2*>(dst + pkcomm::push_off(me, m, chunk / W, x, M, ng)) = o;
+        const int64_t eo = pkcomm::push_off(me, m, chunk / W, x, M, ng);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack2(a[i].x, a[i].y), pack2(a[i].z, a[i].w)}, drs,
+                                              static_cast<int>(eo * 2), 0, 17);
       }
     }
-    // every push drained, system release, then the owner's flag (custom_allreduce.hip publish)
+    // every push acknowledged, then the owner's flag (its wait acquires)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (tid == 0)
       __hip_atomic_store(&reinterpret_cast<pkcomm::Signals*>(obase)->pflag[nb][me], e, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-    }
   } else {  // kQkvRope: n-block nb is head nb of q | k | v
     const int nq = args.nq, nkv = args.nkv, bs = args.bs;
     if (nb < nq + nkv) {

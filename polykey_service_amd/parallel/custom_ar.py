@@ -47,6 +47,8 @@ def _lib() -> ctypes.CDLL:
                                            ctypes.POINTER(_LL)]
         lib.pk_car_reduce_residual_pushed.argtypes = [_P, _P, _P, _I, _I, _I, _I, _P]
         lib.pk_car_sig_bytes.restype = _LL
+        lib.pk_car_create_loopback.argtypes = [_I, _I, _LL]
+        lib.pk_car_create_loopback.restype = _P
         lib.pk_car_check_error.argtypes = [_P]
         lib.pk_car_clear_error.argtypes = [_P]
         lib.pk_car_set_error.argtypes = [_P]
@@ -102,6 +104,21 @@ class CustomAllReduce:
             rc = self.lib.pk_car_open(self.ctx, blob)
         if rc != 0:
             raise RuntimeError(f"pk_car_open failed ({rc})")
+
+    @classmethod
+    def loopback(cls, rank: int, world: int, device: torch.device, max_bytes: int = 16 << 20) -> "CustomAllReduce":
+        """One-process stand-in group for timing the real collective kernels (tools/tp_solo.py
+        --car loopback; csrc pk_car_create_loopback): peers are local buffers whose flags never
+        block.  The reduced values are meaningless; the kernels' own work is all there."""
+        self = cls.__new__(cls)
+        self.lib = _lib()
+        self.rank, self.world, self.device = rank, world, device
+        self.max_bytes, self.blocks, self.fused_blocks = max_bytes, 0, 0
+        with torch.cuda.device(device):
+            self.ctx = self.lib.pk_car_create_loopback(rank, world, max_bytes)
+        if not self.ctx:
+            raise RuntimeError("pk_car_create_loopback failed")
+        return self
 
     def supports(self, x: torch.Tensor) -> bool:
         n = x.numel() * x.element_size()

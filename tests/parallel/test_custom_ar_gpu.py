@@ -347,3 +347,47 @@ def test_custom_allreduce_ranks_share_one_gpu(world):
     for p in procs:
         p.join(timeout=60)
     assert res == {r: "ok" for r in range(world)}, res
+
+
+def test_loopback_group_runs_every_collective_without_blocking():
+    """The one-process stand-in group tools/tp_solo.py --car loopback times the real collective
+    kernels with: every form (one-/two-shot all-reduce, all-gather, fused and pushed reduce) runs
+    to completion in one process, graph-replayed too, and no wait times out."""
+    from polykey_service_amd.ops import gemm
+    from polykey_service_amd.parallel.custom_ar import CustomAllReduce
+    dev = torch.device("cuda:0")
+    car = CustomAllReduce.loopback(0, 8, dev)
+    car.set_timeout(2.0)
+    try:
+        M, N, K = 64, 8192, 1024
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        wp = gemm.pack_weight((torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16))
+        ws = torch.empty(8 * M * N, dtype=torch.float32, device=dev)
+        res = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        parts = torch.zeros((N // 256) * M, dtype=torch.float32, device=dev)
+        ctr = torch.zeros(N // 64, dtype=torch.int32, device=dev)
+
+        def chain():
+            car.all_reduce(torch.ones(4096, dtype=torch.bfloat16, device=dev), algo=1)
+            car.all_reduce(torch.ones(1 << 20, dtype=torch.bfloat16, device=dev), algo=2)
+            car.all_gather_last(torch.ones(M, 256, dtype=torch.bfloat16, device=dev))
+            car.reduce_residual(gemm.linear_partial(x, wp, ws, packed=wp, half=True), res, parts)
+            nbc = gemm.push_projection(x, wp, ws, wp, ctr, car.push_target())
+            car.reduce_residual_pushed(res, parts, nbc)
+
+        chain()
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            chain()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            chain()
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        assert car.error() == 0 and int(ctr.abs().sum()) == 0
+    finally:
+        car.close()

@@ -24,13 +24,10 @@ VARIANTS = {
                    "      if constexpr (kWaitSlice)  // the producers' output, handed off in-launch: sc1 loads"),
                   ("skinny_tile.h", "rs_p[h * kRsLoads + q] = kWaitRes ? ldf_sc1(args.nrm_parts, p) : *p;",
                    "rs_p[h * kRsLoads + q] = *p;")],
-    # timing only (NOT coherent): the TP push epilogue (MODE_PUSH) without the system release
-    # before the owner's flag, and without the pushed stores themselves (tools/push_probe.py)
-    "push_nofence": [("skinny_tile.h", """      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      __hip_atomic_store(&reinterpret_cast<pkcomm::Signals*>(obase)->pflag""",
-                      """      __hip_atomic_store(&reinterpret_cast<pkcomm::Signals*>(obase)->pflag""")],
-    "push_nostore": [("skinny_tile.h", "        *reinterpret_cast<uint2*>(dst + pkcomm::push_off(me, m, chunk / W, x, M, ng)) = o;",
-                      "        if (o.x == 0x7fc07fc1u) *reinterpret_cast<uint2*>(dst + pkcomm::push_off(me, m, chunk / W, x, M, ng)) = o;")],
+    # round 5, measured and removed: "push_nofence" / "push_nostore" (the TP push epilogue without
+    # its system release / without its stores: the release was 3.2 us of the 6.5 us the epilogue
+    # added to the 70B TP=8 o projection, the stores 1.1 us -- profiles/r5_push_probe.jsonl; the
+    # epilogue now stores write-through at system scope and stamps the flag without a fence)
     # the fused QKV -> attention launch without the K/V prefetch before the hand-off wait
     "pre0": [("decode_fused.hip", "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 2>(",
               "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 0>(")],
@@ -57,7 +54,39 @@ VARIANTS = {
 }
 
 
+# variants of libpk_comm (csrc/comm), loaded with POLYKEY_LIB_LIBPK_COMM=<path>
+COMM_VARIANTS = {
+    # timing only (NOT coherent): the collectives without their system-scope release / acquire
+    # fences (tools/car_probe.py on a loopback group)
+    "car_norel": [("custom_allreduce.hip", '__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");', "")],
+    "car_noacq": [("custom_allreduce.hip", '__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");', "")],
+}
+
+
+def build_comm(name: str) -> str:
+    work = tempfile.mkdtemp(prefix=f"pkvar_{name}_")
+    cdir = os.path.join(work, "comm")
+    shutil.copytree(os.path.join(REPO, "csrc", "comm"), cdir)
+    for fname, old, new in COMM_VARIANTS[name]:
+        p = os.path.join(cdir, fname)
+        text = open(p).read()
+        if old not in text:
+            raise SystemExit(f"variant {name}: pattern not found in {fname}: {old!r}")
+        open(p, "w").write(text.replace(old, new))
+    objs = []
+    for s in sorted(glob.glob(os.path.join(cdir, "*.hip"))):
+        o = os.path.join(work, os.path.basename(s) + ".o")
+        subprocess.run([HIPCC, "-x", "hip", *HIP_FLAGS, "-I" + work, "-c", s, "-o", o], check=True)
+        objs.append(o)
+    out = os.path.join(REPO, "tools", "lab", f"libpk_comm_{name}.so")
+    subprocess.run([HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", *objs, "-o", out], check=True)
+    shutil.rmtree(work, ignore_errors=True)
+    return out
+
+
 def build(name: str) -> str:
+    if name in COMM_VARIANTS:
+        return build_comm(name)
     src = os.path.join(REPO, "csrc", "kernels")
     work = tempfile.mkdtemp(prefix=f"pkvar_{name}_")
     kdir = os.path.join(work, "kernels")
@@ -85,5 +114,5 @@ def build(name: str) -> str:
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:] or list(VARIANTS):
+    for n in sys.argv[1:] or list(VARIANTS) + list(COMM_VARIANTS):
         print(build(n), flush=True)

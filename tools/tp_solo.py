@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--ctx", type=int, default=384)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--eager", action="store_true", help="no graph (for per-kernel traces with launch gaps)")
+    ap.add_argument("--car", choices=["solo", "loopback"], default="solo",
+                    help="collectives: their local half (SoloAR) or the real kernels on local stand-in peers")
     a = ap.parse_args()
     cfg = get_config(a.model)
     if a.layers:
@@ -91,7 +93,11 @@ def main():
     dev = torch.device("cuda:0")
     st = ParallelState(tp_size=a.tp, tp_rank=0, device=dev)
     if a.tp > 1:
-        st.custom_ar = SoloAR(a.tp)
+        if a.car == "loopback":
+            from polykey_service_amd.parallel.custom_ar import CustomAllReduce
+            st.custom_ar = CustomAllReduce.loopback(0, a.tp, dev)
+        else:
+            st.custom_ar = SoloAR(a.tp)
     set_state(st)
     t0 = time.perf_counter()
     model = build_model(cfg, st, torch.bfloat16, dev).init_random(0)
@@ -145,9 +151,11 @@ def main():
         torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     gemm.check_fused()
+    if a.car == "loopback":
+        assert st.custom_ar.error() == 0, "a loopback wait timed out"
     print(json.dumps({"model": a.model, "tp": a.tp, "layers": cfg.num_layers, "batch": B, "ctx": a.ctx,
                       "ms_per_step": round(ms, 3), "us_per_layer": round(ms * 1000 / cfg.num_layers, 2),
-                      "graph": not a.eager, "init_s": round(init_s, 1),
+                      "graph": not a.eager, "init_s": round(init_s, 1), "car": a.car,
                       "mlp_fused": os.environ.get("POLYKEY_MLP_FUSED", "1"),
                       "qkv_attn_fused": os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1"),
                       "env": {k: v for k, v in os.environ.items() if k.startswith("POLYKEY_")}}), flush=True)
