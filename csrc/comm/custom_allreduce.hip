@@ -7,11 +7,15 @@
 //
 //   1. each workgroup b copies its chunk of the input into this rank's IPC buffer (slot = call
 //      parity, so a slow peer still reading the previous call is never overwritten);
-//   2. system-scope release, then it stamps flag[b][rank] = epoch in EVERY peer's signal area
-//      (remote stores over xGMI);
+//   2. once those stores are acknowledged it stamps flag[b][rank] = epoch in EVERY peer's signal
+//      area (remote stores over xGMI);
 //   3. it polls its own flag[b][j] == epoch for all peers j (relaxed system-scope loads, bounded
-//      spin), acquires, reads chunk b from all W buffers (peer reads over xGMI), sums in fp32 in
-//      a fixed rank order (bit-identical on every rank) and writes bf16 output.
+//      spin), reads chunk b from all W buffers (peer reads over xGMI), sums in fp32 in a fixed
+//      rank order (bit-identical on every rank) and writes bf16 output.
+// Every slot access is system-scope (sc0 sc1: st_sys / ld_sys): a store is performed at system
+// scope once acknowledged (s_waitcnt vmcnt(0) before the flag) and a load is served coherently,
+// so no release / acquire fence is needed -- the L2 write-back / invalidate those do per
+// workgroup measured 3.8 / 3.4 us of a 14.9 us fused collective (tools/car_probe.py).
 //
 // No grid-wide barrier: chunk b only depends on the W workgroups b of the W ranks.  The epoch
 // lives in device memory, so the kernels replay correctly inside HIP graphs.  It is ONE call
@@ -106,6 +110,25 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
 }
 
+// System-scope (sc0 sc1) slot accesses through a buffer resource on a rank's IPC buffer (< 2 GiB:
+// 32-bit byte offsets): write-through stores complete at system scope, loads bypass stale lines.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const char* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), static_cast<short>(0), 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t r, int64_t boff, const uint4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, static_cast<int>(boff), 0, 17);
+}
+__device__ __forceinline__ uint4 ld_sys(__amdgpu_buffer_rsrc_t r, int64_t boff) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(boff), 0, 17));
+}
+__device__ __forceinline__ void stf_sys(__amdgpu_buffer_rsrc_t r, int64_t boff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, static_cast<int>(boff), 0, 17);
+}
+__device__ __forceinline__ float ldf_sys(__amdgpu_buffer_rsrc_t r, int64_t boff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(boff), 0, 17));
+}
+
 // n16: message size in 16-byte vectors (8 bf16).  Each workgroup owns a contiguous chunk.
 template <int W>
 __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __restrict__ peers, int rank,
@@ -126,32 +149,30 @@ __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __re
   const int64_t lo = b * per, hi = min(n16, lo + per);
 
   // 1. stage my chunk into my own buffer
-  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + slot);
-  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) mine[i] = inp[i];
-  // 2. publish: every thread's stores drained, system release, then one lane stamps every peer
+  const auto mine = rsrc(peers->base[rank]);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) st_sys(mine, slot + i * 16, inp[i]);
+  // 2. publish: every thread's stores acknowledged, then one lane stamps every peer
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < W) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
     __hip_atomic_store(&ps->flag[b][rank], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // 3. wait for all peers' chunk b, then reduce
   if (threadIdx.x < W) {
     spin_wait(&my_sig->flag[b][threadIdx.x], e, my_sig, fail);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (__hip_atomic_load(&my_sig->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) err_s = 1u;
   }
   __syncthreads();
   if (err_s) return;  // a peer never arrived: leave the output alone (the engine fails the step)
-  const uint4* src[W];
+  __amdgpu_buffer_rsrc_t src[W];
 #pragma unroll
-  for (int j = 0; j < W; ++j) src[j] = reinterpret_cast<const uint4*>(peers->base[j] + slot);
+  for (int j = 0; j < W; ++j) src[j] = rsrc(peers->base[j]);
   for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     uint4 v[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) v[j] = src[j][i];
+    for (int j = 0; j < W; ++j) v[j] = ld_sys(src[j], slot + i * 16);
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
@@ -166,7 +187,8 @@ __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __re
   end_call(my_sig, e);
 }
 
-// Bounded relaxed poll of this rank's flag[b][j] for every peer j, then one system acquire.
+// Bounded relaxed poll of this rank's flag[b][j] for every peer j (the data behind a flag is read
+// with system-scope loads: no acquire).
 // Returns false when some peer timed out (every thread of the workgroup sees the same answer).
 template <int W>
 __device__ __forceinline__ bool wait_all(uint32_t (*flags)[kMaxRanks], int b, uint32_t e, Signals* my_sig,
@@ -176,20 +198,19 @@ __device__ __forceinline__ bool wait_all(uint32_t (*flags)[kMaxRanks], int b, ui
   __syncthreads();
   if (threadIdx.x < W) {
     spin_wait(&flags[b][threadIdx.x], e, my_sig, fail);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (__hip_atomic_load(&my_sig->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) bad_s = 1u;
   }
   __syncthreads();
   return bad_s == 0u;
 }
 
-// Drain this workgroup's stores, then stamp flags[b][rank] = e in every rank's signal area.
+// Wait until this workgroup's (system-scope) stores are acknowledged, then stamp flags[b][rank] =
+// e in every rank's signal area.
 template <int W>
 __device__ __forceinline__ void publish(const PeerPtrs* peers, int rank, int b, uint32_t e, bool second) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < W) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
     __hip_atomic_store(second ? &ps->flag2[b][rank] : &ps->flag[b][rank], e, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -232,11 +253,11 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
     hi = min(min(n16, (s + 1) * slice), lo + per);
   };
   // 1. stage chunk b of every slice
-  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + in_slot);
+  const auto mine = rsrc(peers->base[rank]);
   for (int s = 0; s < W; ++s) {
     int64_t lo, hi;
     range(s, lo, hi);
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) mine[i] = inp[i];
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) st_sys(mine, in_slot + i * 16, inp[i]);
   }
   publish<W>(peers, rank, b, e, false);
   if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
@@ -244,15 +265,15 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
   {
     int64_t lo, hi;
     range(rank, lo, hi);
-    uint4* res = reinterpret_cast<uint4*>(peers->base[rank] + res_slot);
     for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       uint4 v[W];
 #pragma unroll
-      for (int j = 0; j < W; ++j) v[j] = reinterpret_cast<const uint4*>(peers->base[j] + in_slot)[i];
+      for (int j = 0; j < W; ++j) v[j] = ld_sys(rsrc(peers->base[j]), in_slot + i * 16);
 #pragma unroll
       for (int j = 0; j < W; ++j) acc8(acc, v[j]);
-      res[i] = make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
+      st_sys(mine, res_slot + i * 16,
+             make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7])));
     }
   }
   publish<W>(peers, rank, b, e, true);
@@ -262,8 +283,8 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
   for (int s = 0; s < W; ++s) {
     int64_t lo, hi;
     range(s, lo, hi);
-    const uint4* res = reinterpret_cast<const uint4*>(peers->base[s] + res_slot);
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) out[i] = res[i];
+    const auto res = rsrc(peers->base[s]);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) out[i] = ld_sys(res, res_slot + i * 16);
   }
   end_call(my_sig, e);
 }
@@ -292,15 +313,15 @@ __global__ void __launch_bounds__(kThreads) allgather_1shot(const PeerPtrs* __re
   const int64_t n16 = rows * row16;
   const int64_t per = (n16 + nb - 1) / nb;
   const int64_t lo = b * per, hi = min(n16, lo + per);
-  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + slot);
-  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) mine[i] = inp[i];
+  const auto mine = rsrc(peers->base[rank]);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) st_sys(mine, slot + i * 16, inp[i]);
   publish<W>(peers, rank, b, e, false);
   if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
   for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
     const int64_t row = i / row16, col = i - row * row16;
     uint4 v[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) v[j] = reinterpret_cast<const uint4*>(peers->base[j] + slot)[i];
+    for (int j = 0; j < W; ++j) v[j] = ld_sys(rsrc(peers->base[j]), slot + i * 16);
 #pragma unroll
     for (int j = 0; j < W; ++j) out[(row * W + j) * row16 + col] = v[j];
   }
@@ -361,7 +382,7 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
   const int nchunk = N >> 10;
   const int items = M * nchunk;
   const int64_t slab = static_cast<int64_t>(M) * lds;
-  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + slot);
+  const auto mine = rsrc(peers->base[rank]);
   // 1. local split-K reduction -> bf16 partial in this rank's slot (slot rows of N, source rows of ld)
   for (int it = b; it < items; it += nb) {
     const int r = it / nchunk, c = it - r * nchunk;
@@ -381,27 +402,25 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
     } else {
       pk = partial[goff >> 3];
     }
-    mine[off >> 3] = pk;
+    st_sys(mine, slot + off * 2, pk);
   }
   // 2. publish (same protocol as the one-shot all-reduce), wait for every peer's workgroup b
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < W) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
     __hip_atomic_store(&ps->flag[b][rank], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (threadIdx.x < W) {
     spin_wait(&my_sig->flag[b][threadIdx.x], e, my_sig, fail);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (__hip_atomic_load(&my_sig->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) err_s = 1u;
   }
   __syncthreads();
   if (err_s) return;  // a peer never arrived: residual untouched, the engine fails the step
   // 3./4. rank-ordered sum over xGMI, residual add, per-chunk sums of squares
-  const uint4* src[W];
+  __amdgpu_buffer_rsrc_t src[W];
 #pragma unroll
-  for (int j = 0; j < W; ++j) src[j] = reinterpret_cast<const uint4*>(peers->base[j] + slot);
+  for (int j = 0; j < W; ++j) src[j] = rsrc(peers->base[j]);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int it = b; it < items; it += nb) {
     const int r = it / nchunk, c = it - r * nchunk;
@@ -409,7 +428,7 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
     const int64_t goff = static_cast<int64_t>(r) * ld + (c << 10) + threadIdx.x * 8;
     uint4 v[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) v[j] = src[j][off >> 3];
+    for (int j = 0; j < W; ++j) v[j] = ld_sys(src[j], slot + off * 2);
     const uint4 rr = *reinterpret_cast<const uint4*>(residual + goff);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -470,7 +489,7 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
   const int items = M * ngroups;
   const int64_t slab = static_cast<int64_t>(M) * lds;
   const int64_t parts_off = static_cast<int64_t>(M) * N * 2;  // byte offset of the parts in a result slot
-  uint4* mine = reinterpret_cast<uint4*>(peers->base[rank] + in_slot);
+  const auto mine = rsrc(peers->base[rank]);
   const int t = threadIdx.x;
   // 0. stage the local partial of every chunk of my items (W chunks x 256 columns = 32 W uint4)
   for (int it = b; it < items; it += nb) {
@@ -493,14 +512,12 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
       } else {
         pk = partial[goff >> 3];
       }
-      mine[off >> 3] = pk;
+      st_sys(mine, in_slot + off * 2, pk);
     }
   }
   publish<W>(peers, rank, b, e, false);
   if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
   // 1. my chunk of each item: rank-order sum over xGMI, residual add, sums of squares
-  uint4* res_mine = reinterpret_cast<uint4*>(peers->base[rank] + res_slot);
-  float* parts_mine = reinterpret_cast<float*>(peers->base[rank] + res_slot + parts_off);
   for (int it = b; it < items; it += nb) {
     const int r = it / ngroups, j = it - r * ngroups;
     const int c = j * W + rank;
@@ -509,7 +526,7 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
       const int64_t goff = static_cast<int64_t>(r) * ld + c * kRrChunk + t * 8;
       uint4 v[W];
 #pragma unroll
-      for (int q = 0; q < W; ++q) v[q] = reinterpret_cast<const uint4*>(peers->base[q] + in_slot)[off >> 3];
+      for (int q = 0; q < W; ++q) v[q] = ld_sys(rsrc(peers->base[q]), in_slot + off * 2);
       const uint4 rr = *reinterpret_cast<const uint4*>(residual + goff);
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -525,12 +542,12 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
       const uint4 out = make_uint4(pack2(res[0], res[1]), pack2(res[2], res[3]), pack2(res[4], res[5]),
                                    pack2(res[6], res[7]));
       *reinterpret_cast<uint4*>(residual + goff) = out;
-      res_mine[off >> 3] = out;
+      st_sys(mine, res_slot + off * 2, out);
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 32);
       if (t == 0) {
         parts[static_cast<int64_t>(c) * M + r] = ss;
-        parts_mine[static_cast<int64_t>(c) * M + r] = ss;
+        stf_sys(mine, res_slot + parts_off + (static_cast<int64_t>(c) * M + r) * 4, ss);
       }
     }
   }
@@ -545,10 +562,10 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
       const int c = j * W + q;
       const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + (u % 32) * 8;
       const int64_t goff = static_cast<int64_t>(r) * ld + c * kRrChunk + (u % 32) * 8;
-      *reinterpret_cast<uint4*>(residual + goff) = reinterpret_cast<const uint4*>(peers->base[q] + res_slot)[off >> 3];
+      const auto rq = rsrc(peers->base[q]);
+      *reinterpret_cast<uint4*>(residual + goff) = ld_sys(rq, res_slot + off * 2);
       if (u % 32 == 0)
-        parts[static_cast<int64_t>(c) * M + r] =
-            reinterpret_cast<const float*>(peers->base[q] + res_slot + parts_off)[static_cast<int64_t>(c) * M + r];
+        parts[static_cast<int64_t>(c) * M + r] = ldf_sys(rq, res_slot + parts_off + (static_cast<int64_t>(c) * M + r) * 4);
     }
   }
   end_call(my_sig, e);
@@ -587,9 +604,7 @@ __global__ void __launch_bounds__(128) reduce_residual_pushed_kernel(const PeerP
   const int items = M * ngroups;
   const int per = kRrChunk / nbc;  // n-blocks per chunk
   const int64_t parts_off = static_cast<int64_t>(M) * N * 2;
-  const uint16_t* own = reinterpret_cast<const uint16_t*>(peers->base[rank] + in_slot);
-  uint4* res_mine = reinterpret_cast<uint4*>(peers->base[rank] + res_slot);
-  float* parts_mine = reinterpret_cast<float*>(peers->base[rank] + res_slot + parts_off);
+  const auto mine = rsrc(peers->base[rank]);
   const int t = threadIdx.x;
   int waited = -1;
   for (int it = b; it < items; it += nb) {
@@ -600,7 +615,6 @@ __global__ void __launch_bounds__(128) reduce_residual_pushed_kernel(const PeerP
       __syncthreads();
       if (t < W * per) {
         spin_wait(&my_sig->pflag[c * per + t % per][t / per], e, my_sig, fail);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         if (__hip_atomic_load(&my_sig->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) bad_s = 1u;
       }
       __syncthreads();
@@ -611,8 +625,7 @@ __global__ void __launch_bounds__(128) reduce_residual_pushed_kernel(const PeerP
       const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + t * 8;
       uint4 v[W];
 #pragma unroll
-      for (int q = 0; q < W; ++q)
-        v[q] = *reinterpret_cast<const uint4*>(own + pkcomm::push_off(q, r, j, t * 8, M, ngroups));
+      for (int q = 0; q < W; ++q) v[q] = ld_sys(mine, in_slot + pkcomm::push_off(q, r, j, t * 8, M, ngroups) * 2);
       const uint4 rr = *reinterpret_cast<const uint4*>(residual + off);
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -628,12 +641,12 @@ __global__ void __launch_bounds__(128) reduce_residual_pushed_kernel(const PeerP
       const uint4 out = make_uint4(pack2(res[0], res[1]), pack2(res[2], res[3]), pack2(res[4], res[5]),
                                    pack2(res[6], res[7]));
       *reinterpret_cast<uint4*>(residual + off) = out;
-      res_mine[off >> 3] = out;
+      st_sys(mine, res_slot + off * 2, out);
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 32);
       if (t == 0) {
         parts[static_cast<int64_t>(c) * M + r] = ss;
-        parts_mine[static_cast<int64_t>(c) * M + r] = ss;
+        stf_sys(mine, res_slot + parts_off + (static_cast<int64_t>(c) * M + r) * 4, ss);
       }
     }
   }
@@ -646,10 +659,10 @@ __global__ void __launch_bounds__(128) reduce_residual_pushed_kernel(const PeerP
       if (q == rank) continue;
       const int c = j * W + q;
       const int64_t off = static_cast<int64_t>(r) * N + c * kRrChunk + (u % 32) * 8;
-      *reinterpret_cast<uint4*>(residual + off) = reinterpret_cast<const uint4*>(peers->base[q] + res_slot)[off >> 3];
+      const auto rq = rsrc(peers->base[q]);
+      *reinterpret_cast<uint4*>(residual + off) = ld_sys(rq, res_slot + off * 2);
       if (u % 32 == 0)
-        parts[static_cast<int64_t>(c) * M + r] =
-            reinterpret_cast<const float*>(peers->base[q] + res_slot + parts_off)[static_cast<int64_t>(c) * M + r];
+        parts[static_cast<int64_t>(c) * M + r] = ldf_sys(rq, res_slot + parts_off + (static_cast<int64_t>(c) * M + r) * 4);
     }
   }
   end_call(my_sig, e);
