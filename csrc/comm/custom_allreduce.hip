@@ -475,6 +475,31 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
                                                                      int lds, const Fail fail) {
   const int b = blockIdx.x, nb = gridDim.x;
   Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
+  const int t = threadIdx.x;
+  const int nchunk = N / kRrChunk, ngroups = nchunk / W;
+  const int items = M * ngroups;
+  const int64_t slab = static_cast<int64_t>(M) * lds;
+  // One item per workgroup (the decode shapes) and S <= 4: the item's slab operands are requested
+  // before the call's epoch, so that load is not a round trip of its own on the critical path.
+  constexpr int kU = (32 * W + 127) / 128;  // stage-0 units per thread
+  const bool pre = S >= 1 && S <= 4 && items <= nb && b < items;
+  float4 pv[kU][4][2];
+  if (pre) {
+    const int r = b / ngroups, j = b - r * ngroups;
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const int u = t + 128 * k;
+      if (u < 32 * W) {
+        const int64_t soff = static_cast<int64_t>(r) * lds + (j * W + u / 32) * kRrChunk + (u % 32) * 8;
+#pragma unroll
+        for (int sidx = 0; sidx < 4; ++sidx) {  // branch-free (slab S - 1 again past S): one load batch
+          const float* sp = slabs + min(sidx, S - 1) * slab + soff;
+          pv[k][sidx][0] = *reinterpret_cast<const float4*>(sp);
+          pv[k][sidx][1] = *reinterpret_cast<const float4*>(sp + 4);
+        }
+      }
+    }
+  }
   __shared__ uint32_t e_s, err_s;
   if (threadIdx.x == 0) {
     e_s = my_sig->epoch[b] + 1;
@@ -485,14 +510,30 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
   const uint32_t e = e_s;
   const size_t in_slot = kSigBytes + (e & 1u) * data_bytes;
   const size_t res_slot = kSigBytes + (2 + (e & 1u)) * data_bytes;
-  const int nchunk = N / kRrChunk, ngroups = nchunk / W;
-  const int items = M * ngroups;
-  const int64_t slab = static_cast<int64_t>(M) * lds;
   const int64_t parts_off = static_cast<int64_t>(M) * N * 2;  // byte offset of the parts in a result slot
   const auto mine = rsrc(peers->base[rank]);
-  const int t = threadIdx.x;
   // 0. stage the local partial of every chunk of my items (W chunks x 256 columns = 32 W uint4)
-  for (int it = b; it < items; it += nb) {
+  if (pre) {
+    const int r = b / ngroups, j = b - r * ngroups;
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const int u = t + 128 * k;
+      if (u < 32 * W) {
+        const int64_t off = static_cast<int64_t>(r) * N + (j * W + u / 32) * kRrChunk + (u % 32) * 8;
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // slab order, as the loop below
+#pragma unroll
+        for (int sidx = 0; sidx < 4; ++sidx)
+          if (sidx < S) {
+            const float4 p0 = pv[k][sidx][0], p1 = pv[k][sidx][1];
+            a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w;
+            a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
+          }
+        st_sys(mine, in_slot + off * 2,
+               make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7])));
+      }
+    }
+  }
+  for (int it = pre ? items : b; it < items; it += nb) {
     const int r = it / ngroups, j = it - r * ngroups;
     for (int u = t; u < 32 * W; u += 128) {
       const int c = j * W + u / 32;

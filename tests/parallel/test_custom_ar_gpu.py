@@ -126,7 +126,9 @@ def _fused_phase(car, rank, world, dev):
     car.fused_blocks = 32  # every rank's grid resident at once on the shared GPU
     g = torch.Generator().manual_seed(7)  # same residual on every rank
     gr = torch.Generator().manual_seed(1000 + rank)
-    for M, N, S in ((1, 1024, 2), (3, 4096, 0), (64, 8192, 4), (17, 2048, 1)):
+    # (4, 8192, 3) / (8, 4096, 4): one item per workgroup -- the two-shot form's slab prefetch ahead
+    # of the epoch (S = 3 re-reads slab 2 past S, unsummed)
+    for M, N, S in ((1, 1024, 2), (3, 4096, 0), (64, 8192, 4), (17, 2048, 1), (4, 8192, 3), (8, 4096, 4)):
         res = (torch.randn(M, N, generator=g) * 2).to(torch.bfloat16)
         slabs = torch.randn(max(S, 1), M, N, generator=gr) if S else None
         partial = torch.randn(M, N, generator=gr).to(torch.bfloat16) if S == 0 else None
