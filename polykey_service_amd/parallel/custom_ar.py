@@ -28,6 +28,8 @@ from .._native.loader import load_cdll
 log = logging.getLogger(__name__)
 
 _P, _I, _LL = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+# grid of the fused decode collective (0: one workgroup per (row, owner-chunk group), <= 512); A/B knob
+_FUSED_BLOCKS = int(os.environ.get("POLYKEY_CAR_FUSED_BLOCKS", "0"))
 
 
 def _lib() -> ctypes.CDLL:
@@ -73,7 +75,7 @@ class CustomAllReduce:
         # grid of the fused decode collective (0: one workgroup per (row, 1024-column chunk), up
         # to 512).  Ranks sharing ONE GPU (rehearsals, tests) need every rank's grid resident at
         # once: maybe_create caps it there.
-        self.fused_blocks = 0
+        self.fused_blocks = _FUSED_BLOCKS
         self.ctx = None
         hsz = self.lib.pk_car_ipc_handle_size()
         # the local half (allocation, IPC handle) never skips the handle exchange: a rank that
@@ -113,7 +115,7 @@ class CustomAllReduce:
         self = cls.__new__(cls)
         self.lib = _lib()
         self.rank, self.world, self.device = rank, world, device
-        self.max_bytes, self.blocks, self.fused_blocks = max_bytes, 0, 0
+        self.max_bytes, self.blocks, self.fused_blocks = max_bytes, 0, _FUSED_BLOCKS
         with torch.cuda.device(device):
             self.ctx = self.lib.pk_car_create_loopback(rank, world, max_bytes)
         if not self.ctx:
