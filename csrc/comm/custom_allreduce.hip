@@ -369,6 +369,23 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
                                                                int lds, const Fail fail) {
   const int b = blockIdx.x, nb = gridDim.x;
   Signals* my_sig = reinterpret_cast<Signals*>(peers->base[rank]);
+  const int nchunk = N >> 10;
+  const int items = M * nchunk;
+  const int64_t slab = static_cast<int64_t>(M) * lds;
+  // one item per workgroup and S <= 4: the slab operands are requested before the call's epoch
+  // (as in reduce_residual_2shot_kernel; branch-free, slab S - 1 again past S)
+  const bool pre = S >= 1 && S <= 4 && items <= nb && b < items;
+  float4 pv[4][2];
+  if (pre) {
+    const int r = b / nchunk, c = b - r * nchunk;
+    const int64_t soff = static_cast<int64_t>(r) * lds + (c << 10) + threadIdx.x * 8;
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx) {
+      const float* sp = slabs + min(sidx, S - 1) * slab + soff;
+      pv[sidx][0] = *reinterpret_cast<const float4*>(sp);
+      pv[sidx][1] = *reinterpret_cast<const float4*>(sp + 4);
+    }
+  }
   __shared__ uint32_t e_s, err_s;
   __shared__ float red[2];
   if (threadIdx.x == 0) {
@@ -379,12 +396,22 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
   if (err_s) return;
   const uint32_t e = e_s;
   const size_t slot = kSigBytes + (e & 1u) * data_bytes;
-  const int nchunk = N >> 10;
-  const int items = M * nchunk;
-  const int64_t slab = static_cast<int64_t>(M) * lds;
   const auto mine = rsrc(peers->base[rank]);
   // 1. local split-K reduction -> bf16 partial in this rank's slot (slot rows of N, source rows of ld)
-  for (int it = b; it < items; it += nb) {
+  if (pre) {
+    const int r = b / nchunk, c = b - r * nchunk;
+    const int64_t off = static_cast<int64_t>(r) * N + (c << 10) + threadIdx.x * 8;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // slab order, as the loop below
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx)
+      if (sidx < S) {
+        const float4 p0 = pv[sidx][0], p1 = pv[sidx][1];
+        a[0] += p0.x; a[1] += p0.y; a[2] += p0.z; a[3] += p0.w;
+        a[4] += p1.x; a[5] += p1.y; a[6] += p1.z; a[7] += p1.w;
+      }
+    st_sys(mine, slot + off * 2, make_uint4(pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(a[4], a[5]), pack2(a[6], a[7])));
+  }
+  for (int it = pre ? items : b; it < items; it += nb) {
     const int r = it / nchunk, c = it - r * nchunk;
     const int64_t off = static_cast<int64_t>(r) * N + (c << 10) + threadIdx.x * 8;  // element offset
     const int64_t goff = static_cast<int64_t>(r) * ld + (c << 10) + threadIdx.x * 8;
