@@ -16,6 +16,9 @@
 // scope once acknowledged (s_waitcnt vmcnt(0) before the flag) and a load is served coherently,
 // so no release / acquire fence is needed -- the L2 write-back / invalidate those do per
 // workgroup measured 3.8 / 3.4 us of a 14.9 us fused collective (tools/car_probe.py).
+// That argument has only been exercised with every "peer" on one device; the fenced protocol
+// stays available per context (pk_car_set_fenced) and the serving-shape preflight selects it when
+// the fence-free form mismatches on the group's real devices.
 //
 // No grid-wide barrier: chunk b only depends on the W workgroups b of the W ranks.  The epoch
 // lives in device memory, so the kernels replay correctly inside HIP graphs.  It is ONE call
@@ -56,7 +59,21 @@ constexpr int kThreads = 512;
 struct Fail {
   uint32_t* host_err;      // host-mapped pinned word: polled by the engine, sticky
   long long timeout;       // wall-clock ticks a wait may take
+  int fenced;              // 1: the fenced protocol (see rel_fence); 0: fence-free (default)
 };
+
+// The fenced protocol (pk_car_set_fenced): a system-scope release fence between a
+// workgroup's acknowledged slot stores and its flag store, and a system-scope acquire fence after
+// a flag wait.  The slot accesses stay system-scope as well, so this is strictly stronger than the
+// fence-free default.  Preflight (parallel/preflight.py check_custom_ar_serving) switches a group
+// to it when the fence-free form fails its serving-shape stress on the group's real devices.
+// The branch is uniform (a kernel argument): fence-free calls pay one scalar compare.
+__device__ __forceinline__ void rel_fence(const Fail& f) {
+  if (f.fenced) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+__device__ __forceinline__ void acq_fence(const Fail& f) {
+  if (f.fenced) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
 
 struct PeerPtrs {
   char* base[kMaxRanks];  // every rank's IPC buffer as mapped in this process (own included)
@@ -73,6 +90,7 @@ struct Ctx {
   uint32_t* h_err = nullptr;   // host-mapped error word (hipHostMalloc mapped | coherent)
   uint32_t* d_err = nullptr;   // its device alias
   long long timeout_ticks = 0;
+  int fenced = 0;              // pk_car_set_fenced
 };
 
 // Bounded wait for flags[b][j] >= e of every peer j (one lane per peer).  ">=", not "==": a
@@ -92,6 +110,7 @@ __device__ __forceinline__ void spin_wait(uint32_t* flag, uint32_t e, Signals* m
       break;
     }
   }
+  acq_fence(f);
 }
 
 // Call epilogue: workgroup b stores the call's epoch into entries b, b + nb, ... of the epoch
@@ -155,6 +174,7 @@ __global__ void __launch_bounds__(kThreads) allreduce_1shot(const PeerPtrs* __re
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < W) {
+    rel_fence(fail);
     Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
     __hip_atomic_store(&ps->flag[b][rank], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -207,10 +227,12 @@ __device__ __forceinline__ bool wait_all(uint32_t (*flags)[kMaxRanks], int b, ui
 // Wait until this workgroup's (system-scope) stores are acknowledged, then stamp flags[b][rank] =
 // e in every rank's signal area.
 template <int W>
-__device__ __forceinline__ void publish(const PeerPtrs* peers, int rank, int b, uint32_t e, bool second) {
+__device__ __forceinline__ void publish(const PeerPtrs* peers, int rank, int b, uint32_t e, bool second,
+                                        const Fail& fail) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < W) {
+    rel_fence(fail);
     Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
     __hip_atomic_store(second ? &ps->flag2[b][rank] : &ps->flag[b][rank], e, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -259,7 +281,7 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
     range(s, lo, hi);
     for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) st_sys(mine, in_slot + i * 16, inp[i]);
   }
-  publish<W>(peers, rank, b, e, false);
+  publish<W>(peers, rank, b, e, false, fail);
   if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
   // 2. reduce chunk b of my slice across all ranks into my result region
   {
@@ -276,7 +298,7 @@ __global__ void __launch_bounds__(kThreads) allreduce_2shot(const PeerPtrs* __re
              make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7])));
     }
   }
-  publish<W>(peers, rank, b, e, true);
+  publish<W>(peers, rank, b, e, true, fail);
   if (!wait_all<W>(my_sig->flag2, b, e, my_sig, fail)) return;
   // 3. gather chunk b of every reduced slice
 #pragma unroll
@@ -315,7 +337,7 @@ __global__ void __launch_bounds__(kThreads) allgather_1shot(const PeerPtrs* __re
   const int64_t lo = b * per, hi = min(n16, lo + per);
   const auto mine = rsrc(peers->base[rank]);
   for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) st_sys(mine, slot + i * 16, inp[i]);
-  publish<W>(peers, rank, b, e, false);
+  publish<W>(peers, rank, b, e, false, fail);
   if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
   for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
     const int64_t row = i / row16, col = i - row * row16;
@@ -435,6 +457,7 @@ __global__ void __launch_bounds__(128) reduce_residual_kernel(const PeerPtrs* __
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < W) {
+    rel_fence(fail);
     Signals* ps = reinterpret_cast<Signals*>(peers->base[threadIdx.x]);
     __hip_atomic_store(&ps->flag[b][rank], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -583,7 +606,7 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
       st_sys(mine, in_slot + off * 2, pk);
     }
   }
-  publish<W>(peers, rank, b, e, false);
+  publish<W>(peers, rank, b, e, false, fail);
   if (!wait_all<W>(my_sig->flag, b, e, my_sig, fail)) return;
   // 1. my chunk of each item: rank-order sum over xGMI, residual add, sums of squares
   for (int it = b; it < items; it += nb) {
@@ -619,7 +642,7 @@ __global__ void __launch_bounds__(128) reduce_residual_2shot_kernel(const PeerPt
       }
     }
   }
-  publish<W>(peers, rank, b, e, true);
+  publish<W>(peers, rank, b, e, true, fail);
   if (!wait_all<W>(my_sig->flag2, b, e, my_sig, fail)) return;
   // 2. the other owners' chunks: new residual and parts
   for (int it = b; it < items; it += nb) {
@@ -718,7 +741,7 @@ __global__ void __launch_bounds__(128) reduce_residual_pushed_kernel(const PeerP
       }
     }
   }
-  publish<W>(peers, rank, b, e, true);
+  publish<W>(peers, rank, b, e, true, fail);
   if (!wait_all<W>(my_sig->flag2, b, e, my_sig, fail)) return;
   for (int it = b; it < items; it += nb) {
     const int r = it / ngroups, j = it - r * ngroups;
@@ -749,6 +772,9 @@ PK_EXPORT int pk_car_ipc_handle_size() { return static_cast<int>(sizeof(hipIpcMe
 // Allocate this rank's IPC buffer (signals + 2 data slots of data_bytes) on the current device.
 PK_EXPORT void* pk_car_create(int rank, int world, long long data_bytes) {
   if (world < 2 || world > kMaxRanks || rank < 0 || rank >= world || data_bytes <= 0 || data_bytes % 16) return nullptr;
+  // every slot access is a buffer op with a 32-bit byte offset and num_records 0x7ffffff0
+  // (rsrc): the whole buffer must stay below that, or offsets wrap and accesses are dropped
+  if (static_cast<long long>(kSigBytes) + 4 * data_bytes > 0x7ffffff0LL) return nullptr;
   Ctx* c = new Ctx();
   c->rank = rank;
   c->world = world;
@@ -787,6 +813,20 @@ PK_EXPORT void* pk_car_create(int rank, int world, long long data_bytes) {
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
   c->timeout_ticks = 30LL * 1000 * khz;  // 30 s default (pk_car_set_timeout_ms)
   return c;
+}
+
+// 1: every later call of this context runs the fenced protocol (rel_fence / acq_fence); 0: fence-free.
+// All ranks of a group must agree (parallel/preflight.py switches them together).
+PK_EXPORT int pk_car_set_fenced(void* ctx, int on) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (c == nullptr) return -1;
+  c->fenced = on ? 1 : 0;
+  return 0;
+}
+
+PK_EXPORT int pk_car_get_fenced(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  return c == nullptr ? -1 : c->fenced;
 }
 
 // Wall-clock bound of every wait of this context (a peer that is this late is treated as dead).
@@ -850,7 +890,7 @@ PK_EXPORT int pk_car_allreduce_bf16_algo(void* ctx, const void* inp, void* out, 
   const uint4* in4 = static_cast<const uint4*>(inp);
   uint4* out4 = static_cast<uint4*>(out);
   if (algo == 0) algo = bytes <= kOneShotMax ? 1 : 2;
-  const Fail fail{c->d_err, c->timeout_ticks};
+  const Fail fail{c->d_err, c->timeout_ticks, c->fenced};
   switch (c->world) {
 #define PK_CAR_CASE(WW)                                                                                            \
   case WW:                                                                                                       \
@@ -963,7 +1003,7 @@ PK_EXPORT int pk_car_allgather(void* ctx, const void* inp, void* out, long long 
   const int64_t row16 = row_bytes / 16, n16 = rows * row16;
   if (blocks <= 0) blocks = static_cast<int>(std::min<int64_t>(kArBlocks, std::max<int64_t>(1, n16 / (kThreads * 2))));
   blocks = std::min(blocks, kArBlocks);
-  const Fail fail{c->d_err, c->timeout_ticks};
+  const Fail fail{c->d_err, c->timeout_ticks, c->fenced};
   const uint4* in4 = static_cast<const uint4*>(inp);
   uint4* out4 = static_cast<uint4*>(out);
   switch (c->world) {
@@ -1024,9 +1064,11 @@ PK_EXPORT int pk_car_reduce_residual_pushed(void* ctx, void* residual, void* par
   if (c == nullptr || c->d_peers == nullptr) return -1;
   if (M <= 0) return 0;
   if (c->world < 2 || (nbc != 64 && nbc != 128) || N % (kRrChunk * c->world) || N / nbc > kMaxBlocks ||
-      residual == nullptr || parts == nullptr || static_cast<size_t>(M) * N * 2 > c->data_bytes)
-    return -2;
-  const Fail fail{c->d_err, c->timeout_ticks};
+      residual == nullptr || parts == nullptr ||
+      static_cast<size_t>(M) * N * 2 + static_cast<size_t>(N / kRrChunk) * M * 4 > c->data_bytes)
+    return -2;  // (the result slot holds the new residual AND its fp32 parts)
+  if (c->fenced) return -5;  // the GEMM's push epilogue has no fenced form: the caller keeps the plain chain
+  const Fail fail{c->d_err, c->timeout_ticks, c->fenced};
   const int items = M * (N / kRrChunk / c->world);
   int nb = blocks <= 0 ? std::min(items, 512) : blocks;
   nb = std::max(1, std::min({nb, items, kMaxBlocks}));
@@ -1070,7 +1112,7 @@ PK_EXPORT int pk_car_reduce_residual_ex(void* ctx, const void* slabs, int S, con
       (S > 0 && slabs == nullptr) || residual == nullptr || parts == nullptr)
     return -2;
   if (static_cast<size_t>(M) * N * 2 > c->data_bytes) return -2;
-  const Fail fail{c->d_err, c->timeout_ticks};
+  const Fail fail{c->d_err, c->timeout_ticks, c->fenced};
   const float* sl = static_cast<const float*>(slabs);
   const uint4* pt = static_cast<const uint4*>(partial);
   uint16_t* rs = static_cast<uint16_t*>(residual);

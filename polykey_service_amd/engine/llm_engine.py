@@ -128,6 +128,7 @@ class LLMEngine:
                             num_kv_blocks=cfg.num_kv_blocks, gpu_mem_fraction=cfg.gpu_mem_fraction,
                             hip_graphs=cfg.hip_graphs, graph_batch_sizes=tuple(cfg.graph_batch_sizes))
         self.runner = ModelRunner(model, rcfg, dev)
+        self._serving_preflight(mcfg)
         nblocks = self.runner.allocate_kv_cache()
         rt = load_extension("_pk_runtime")
         self.bm = rt.BlockManager(nblocks, cfg.block_size, int(nblocks * cfg.watermark), cfg.prefix_caching)
@@ -141,6 +142,20 @@ class LLMEngine:
         self.overlap = cfg.overlap
         self._inflight = None
         self.continuation_steps = 0
+
+    def _serving_preflight(self, mcfg: ModelConfig) -> None:
+        """TP: the fused decode collective checked at the shape serving will replay it at (the
+        largest decode graph bucket x hidden, 16 back-to-back calls, graph-replayed) before any
+        graph captures it; a mismatch switches the group to the fenced slot protocol or disables
+        the custom collectives on every rank (parallel/preflight.py check_custom_ar_serving)."""
+        car = self.st.custom_ar
+        if car is None or self.st.tp_size < 2 or os.environ.get("POLYKEY_PREFLIGHT", "1") == "0":
+            return
+        rows = [g for g in self.runner.default_graph_sizes() if car.supports_reduce_residual(g, mcfg.hidden_size)]
+        if rows:
+            from ..parallel import preflight
+            self.preflight_report = preflight.run(self.st, paths=("custom_ar_serving",),
+                                                  serving=(max(rows), mcfg.hidden_size))
 
     # ------------------------------------------------------------------ API
     @property

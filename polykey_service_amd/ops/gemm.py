@@ -377,19 +377,27 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
 TP_DECODE_CHUNKS = int(os.environ.get("POLYKEY_TP_DECODE_CHUNKS", "1"))
 
 
+def partial_tiling(N: int, K: int, M: int, packed: Optional[torch.Tensor], half: bool):
+    """(split, half) of a split-K slab projection: ``half`` (64-row n-blocks at half the split)
+    holds only for packed weights below :data:`NT_MIN_BYTES`.  Shared by :func:`linear_partial`
+    and :func:`push_projection`, whose slabs must be bit-identical."""
+    half = half and packed is not None and packed.numel() * packed.element_size() < NT_MIN_BYTES
+    S = choose_split(N, K, M)
+    if half:
+        S = max(1, S // 2)
+        if HALF_SPLIT_MUL > 1 and M <= SKINNY_MAX_M and K % (_KCHUNK * S * HALF_SPLIT_MUL) == 0:
+            S *= HALF_SPLIT_MUL
+    return S, half
+
+
 def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Optional[int] = None,
                    packed: Optional[torch.Tensor] = None, half: bool = False) -> Partial:
     """Split-K fp32 slabs into workspace ``ws`` (fp32, >= S*M*N).  ``half`` (packed W): 64-row
     n-blocks at half the default split -- the same grid, half the slab bytes."""
     M, K = x.shape
     N = w.shape[0]
-    half = half and packed is not None and packed.numel() * packed.element_size() < NT_MIN_BYTES
-    if S is None:
-        S = choose_split(N, K, M)
-        if half:
-            S = max(1, S // 2)
-            if HALF_SPLIT_MUL > 1 and M <= SKINNY_MAX_M and K % (_KCHUNK * S * HALF_SPLIT_MUL) == 0:
-                S *= HALF_SPLIT_MUL
+    S_auto, half = partial_tiling(N, K, M, packed, half)
+    S = S_auto if S is None else S
     assert ws.numel() >= S * M * N, "split-K workspace too small"
     src = packed if packed is not None else w
     native.call("pk_skinny_gemm", 0, ws.data_ptr(), x.data_ptr(), src.data_ptr(), M, N, K, x.stride(0), N, S,
@@ -579,12 +587,9 @@ def push_projection(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, packed: 
         S = choose_split(N, K, M)
         half = down_kr(N, K, M) == 1 and M <= FUSED_MAX_M
     else:
-        half = packed.numel() * packed.element_size() < NT_MIN_BYTES
-        S = choose_split(N, K, M)
-        if half:
-            S = max(1, S // 2)
-            if HALF_SPLIT_MUL > 1 and M <= SKINNY_MAX_M and K % (_KCHUNK * S * HALF_SPLIT_MUL) == 0:
-                S *= HALF_SPLIT_MUL
+        # the unpushed chain's o projection is linear_partial(half=True): the same helper picks
+        # both tilings, so no threshold (POLYKEY_NT_MIN_MB) can make them differ
+        S, half = partial_tiling(N, K, M, packed, True)
     S = split or S  # (tools/push_probe.py: other splits, not bit-identical to the serving chain)
     nbc = 64 if half else 128
     assert ws.numel() >= S * M * N and counters.numel() >= N // 64 and counters.dtype == torch.int32

@@ -30,6 +30,11 @@ log = logging.getLogger(__name__)
 _P, _I, _LL = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
 # grid of the fused decode collective (0: one workgroup per (row, owner-chunk group), <= 512); A/B knob
 _FUSED_BLOCKS = int(os.environ.get("POLYKEY_CAR_FUSED_BLOCKS", "0"))
+# slot protocol: "auto" = fence-free until the serving-shape preflight finds a mismatch on this
+# group's devices (then fenced, parallel/preflight.py); "1" = fenced from the start; "0" = never fenced
+FENCED = os.environ.get("POLYKEY_CAR_FENCED", "auto")
+# the largest buffer the kernels' 32-bit buffer offsets address (csrc pk_car_create)
+MAX_DATA_BYTES = (0x7FFFFFF0 - (1 << 20)) // 4
 
 
 def _lib() -> ctypes.CDLL:
@@ -55,6 +60,8 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_clear_error.argtypes = [_P]
         lib.pk_car_set_error.argtypes = [_P]
         lib.pk_car_set_timeout_ms.argtypes = [_P, _LL]
+        lib.pk_car_set_fenced.argtypes = [_P, _I]
+        lib.pk_car_get_fenced.argtypes = [_P]
         lib.pk_car_destroy.argtypes = [_P]
         lib.pk_car_destroy.restype = None
         lib._pk_typed = True
@@ -70,6 +77,9 @@ class CustomAllReduce:
                  blocks: int = 0, timeout_s: Optional[float] = None):
         self.lib = _lib()
         self.rank, self.world, self.device = rank, world, device
+        if not 0 < max_bytes <= MAX_DATA_BYTES:
+            raise ValueError(f"custom all-reduce slot of {max_bytes} bytes: 32-bit slot offsets allow "
+                             f"at most {MAX_DATA_BYTES}")
         self.max_bytes = max_bytes
         self.blocks = blocks
         # grid of the fused decode collective (0: one workgroup per (row, 1024-column chunk), up
@@ -90,6 +100,7 @@ class CustomAllReduce:
             if timeout_s is None:
                 timeout_s = float(os.environ.get("POLYKEY_CUSTOM_AR_TIMEOUT_S", "30"))
             self.set_timeout(timeout_s)
+            self.set_fenced(FENCED == "1")
             buf = ctypes.create_string_buffer(hsz)
             if self.lib.pk_car_get_handle(self.ctx, buf) != 0:
                 raise RuntimeError("hipIpcGetMemHandle failed")
@@ -120,7 +131,19 @@ class CustomAllReduce:
             self.ctx = self.lib.pk_car_create_loopback(rank, world, max_bytes)
         if not self.ctx:
             raise RuntimeError("pk_car_create_loopback failed")
+        self.set_fenced(FENCED == "1")
         return self
+
+    @property
+    def fenced(self) -> bool:
+        """The fenced slot protocol is in use (release / acquire fences around every flag)."""
+        return bool(self.ctx) and self.lib.pk_car_get_fenced(self.ctx) == 1
+
+    def set_fenced(self, on: bool) -> None:
+        """Switch this rank's context to the fenced (``on``) or fence-free slot protocol for
+        every later call.  Every rank of the group must switch together (preflight does)."""
+        if self.lib.pk_car_set_fenced(self.ctx, 1 if on else 0) != 0:
+            raise RuntimeError("pk_car_set_fenced failed")
 
     def supports(self, x: torch.Tensor) -> bool:
         n = x.numel() * x.element_size()
@@ -231,8 +254,8 @@ class CustomAllReduce:
     def push_ok(self, M: int, N: int, nbc: int = 128) -> bool:
         """Shapes the pushed collective takes: the two-shot layout (parts per 256 columns, what
         :meth:`nparts` gives the consumers), one 64-row tile, n-blocks the flag rows index."""
-        return (0 < M <= 64 and N % (256 * self.world) == 0 and N // nbc <= 1024 and M * N * 2 <= self.max_bytes
-                and self.nparts(M, N) == N // 256)
+        return (not self.fenced and 0 < M <= 64 and N % (256 * self.world) == 0 and N // nbc <= 1024
+                and M * N * 2 + (N // 256) * M * 4 <= self.max_bytes and self.nparts(M, N) == N // 256)
 
     def reduce_residual_pushed(self, residual: torch.Tensor, parts: torch.Tensor, nbc: int) -> torch.Tensor:
         """:meth:`reduce_residual` after a push GEMM (gemm.push_projection): every rank's bf16

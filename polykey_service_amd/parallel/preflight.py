@@ -116,6 +116,113 @@ def check_custom_ar(car, rank: int, world: int, dev: torch.device) -> Dict[str, 
     return out
 
 
+class _Slabs:
+    """A split-K slab operand of the fused collective (the fields custom_ar reads of a
+    ``gemm.Partial``): ``buf`` fp32 [S * M * N]."""
+
+    def __init__(self, buf: torch.Tensor, S: int, M: int, N: int):
+        self.buf, self.S, self.M, self.N = buf, S, M, N
+
+    def view(self) -> torch.Tensor:
+        return self.buf[: self.S * self.M * self.N].view(self.S, self.M, self.N)
+
+
+SERVING_CALLS = 16
+
+
+def _serving_operands(rank: int, M: int, N: int, calls: int, dev: torch.device):
+    """Rank-seeded operands of ``calls`` fused collectives at [M, N]: even calls a bf16 partial,
+    odd calls 2 fp32 split-K slabs (p + 0.5, -0.5: the real decode chain's form).  Small integers:
+    every sum and every norm part is exact in any order, so a stale or torn slot read cannot hide."""
+    ops = []
+    for k in range(calls):
+        p = _pattern(rank, M * N, dtype=torch.float32, salt=100 + k).view(M, N)
+        if k % 2 == 0:
+            ops.append(p.to(torch.bfloat16).to(dev).contiguous())
+        else:
+            buf = torch.cat([(p + 0.5).reshape(-1), torch.full((M * N,), -0.5)]).to(dev)
+            ops.append(_Slabs(buf, 2, M, N))
+    return ops
+
+
+def check_custom_ar_serving(car, rank: int, world: int, dev: torch.device, M: int, N: int,
+                            calls: int = SERVING_CALLS, graph: Optional[bool] = None) -> Dict[str, object]:
+    """The fused decode collective at serving shape: ``calls`` back-to-back
+    ``reduce_residual`` calls at [M, N] (M = the largest decode graph bucket, N = hidden) with no
+    host synchronisation between them -- every slot parity is reused calls / 2 times while peers
+    run up to one call ahead, the window in which a read served from a stale or not-yet-visible
+    peer slot shows -- first eagerly, then (on the GPU) captured in a HIP graph and replayed, each
+    result compared bit for bit with the locally computed sum.  The timed replay gives the
+    per-call time (``collective_us``).  Returns the check dict (booleans) plus that time."""
+    graph = dev.type == "cuda" if graph is None else graph
+    if not car.supports_reduce_residual(M, N):
+        return {}
+    nparts = car.nparts(M, N)
+    ops = _serving_operands(rank, M, N, calls, dev)
+    res0 = [_pattern(0, M * N, salt=300 + k).view(M, N).to(torch.bfloat16) for k in range(calls)]
+    residuals = [r.to(dev).clone() for r in res0]
+    parts = [torch.zeros(nparts * M, dtype=torch.float32, device=dev) for _ in range(calls)]
+    wants, want_parts = [], []
+    for k in range(calls):
+        tot = res0[k].float() + sum(_pattern(r, M * N, dtype=torch.float32, salt=100 + k).view(M, N)
+                                    for r in range(world))
+        wants.append(tot.to(torch.bfloat16))
+        want_parts.append(tot.view(M, nparts, N // nparts).pow(2).sum(-1).t().contiguous())
+
+    def run_all():
+        return [car.reduce_residual(ops[k], residuals[k], parts[k]) for k in range(calls)]
+
+    def verify(outs) -> bool:
+        ok = True
+        for k in range(calls):
+            ok &= _close(residuals[k], wants[k]) and tuple(outs[k].shape) == (nparts, M)
+            ok &= bool(torch.equal(outs[k].float().cpu(), want_parts[k]))
+        return ok
+
+    def reset():
+        for k in range(calls):
+            residuals[k].copy_(res0[k].to(dev))
+            parts[k].zero_()
+
+    out: Dict[str, object] = {}
+    outs = run_all()  # eager, back to back
+    _sync(dev)
+    out["eager"] = verify(outs)
+    t0 = time.perf_counter()
+    us = None
+    if graph:
+        reset()
+        _sync(dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            gouts = run_all()
+        _sync(dev)
+        reset()  # (capture enqueues nothing; the replays below do the work)
+        g.replay()
+        _sync(dev)
+        out["graph"] = verify(gouts)
+        reset()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        g.replay()
+        ev1.record()
+        _sync(dev)
+        us = ev0.elapsed_time(ev1) * 1000.0 / calls
+        out["graph_timed"] = verify(gouts)
+        del g
+    else:
+        reset()
+        t0 = time.perf_counter()
+        outs = run_all()
+        _sync(dev)
+        us = (time.perf_counter() - t0) * 1e6 / calls
+        out["repeat"] = verify(outs)
+    return {"checks": out, "collective_us": round(us, 2) if us is not None else None,
+            "shape": [M, N], "calls": calls}
+
+
 def check_ep_ipc(a2a, rank: int, world: int, dev: torch.device) -> Dict[str, bool]:
     """Dispatch + return of the IPC expert all-to-all: rank r sends (r + j) % 2 + 1 rows to rank j
     (expert id j + 10 * row), the owners return each row doubled."""
@@ -143,6 +250,55 @@ def check_ep_ipc(a2a, rank: int, world: int, dev: torch.device) -> Dict[str, boo
 
 
 # ------------------------------------------------------------------------------------- run
+def _serving_check(st: ParallelState, serving: Tuple[int, int], report: dict, emit, verdict) -> None:
+    """:func:`check_custom_ar_serving` under the watchdog, the fence-free protocol first.  When it
+    fails on some rank and no rank saw a hang (the slot epochs are still in step), the whole group
+    switches to the fenced protocol (custom_ar.set_fenced) and runs the check again; a second
+    failure -- or a hang -- disables the custom collectives on every rank (RCCL takes over)."""
+    from . import custom_ar as _car_mod
+    car = st.custom_ar
+    M, N = serving
+    dev = st.device
+
+    def off_car():
+        car.close()
+        st.custom_ar = None
+
+    def attempt(name):
+        holder = {}
+
+        def fn():
+            r = check_custom_ar_serving(car, st.tp_rank, st.tp_size, dev, M, N)
+            holder.update(r)
+            return dict(r.get("checks", {}))
+        res, err = _guarded(name, fn, lambda: car.fail(), report, emit)
+        if holder.get("collective_us") is not None:
+            report.setdefault("collective_us", {})[name] = holder["collective_us"]
+        report.setdefault("serving_shape", [M, N])
+        return res, err
+
+    name = "custom_ar_serving_fenced" if car.fenced else "custom_ar_serving"
+    res, err = attempt(name)
+    ok = bool(res) and all(res.values()) and err is None
+    agreed = _agree(ok, st.tp_cpu_group, st.tp_size)
+    if agreed or car.fenced or _car_mod.FENCED == "0":
+        report["car_protocol"] = "fenced" if car.fenced else "fence-free"
+        verdict(name, res, err, st.tp_cpu_group, st.tp_size, off_car)
+        return
+    # the fence-free form failed somewhere: record it, then retry fenced if every rank is still in step
+    report["checks"][name] = {"ok": ok, "group_ok": False, **({"error": err} if err else {}), **res}
+    clean = err is None and not (hasattr(car, "error") and car.error())
+    if not _agree(clean, st.tp_cpu_group, st.tp_size):
+        off_car()
+        report["disabled"].append(name)
+        return
+    car.set_fenced(True)
+    report["car_protocol"] = "fenced"
+    res, err = attempt("custom_ar_serving_fenced")
+    verdict("custom_ar_serving_fenced", res, err, st.tp_cpu_group, st.tp_size, off_car)
+
+
+
 def _agree(ok: bool, group, world: int) -> bool:
     votes = [None] * world
     dist.all_gather_object(votes, bool(ok), group=group)
@@ -223,9 +379,11 @@ def peer_access(st: ParallelState) -> Optional[List[List[int]]]:
     return None if any(r is None for r in rows) else rows
 
 
-def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit: Callable[[str], None] = None) -> dict:
-    """Check every created device-collective path in ``paths`` ("rccl", "custom_ar", "ep_ipc"),
-    disable the failed ones on every rank, return (and emit) the report."""
+def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit: Callable[[str], None] = None,
+        serving: Optional[Tuple[int, int]] = None) -> dict:
+    """Check every created device-collective path in ``paths`` ("rccl", "custom_ar", "ep_ipc",
+    "custom_ar_serving" with ``serving`` = (rows, hidden)), disable the failed ones on every
+    rank, return (and emit) the report."""
     t0 = time.perf_counter()
     report = {"event": "multi_gpu_preflight", "rank": st.rank, "world": st.world_size, "backend": st.backend,
               "ranks_per_device": st.ranks_per_device, "checks": {}, "disabled": []}
@@ -270,6 +428,8 @@ def run(st: ParallelState, paths: Tuple[str, ...] = ("rccl", "custom_ar"), emit:
             car.close()
             st.custom_ar = None
         verdict("custom_ar", res, err, st.tp_cpu_group, st.tp_size, off_car)
+    if "custom_ar_serving" in paths and st.custom_ar is not None and serving is not None:
+        _serving_check(st, serving, report, emit, verdict)
     if "ep_ipc" in paths and st.ep_a2a is not None:
         a2a = st.ep_a2a
         res, err = _guarded("ep_ipc", lambda: check_ep_ipc(a2a, st.ep_rank, st.ep_size, dev), _abort(a2a, "fail"),

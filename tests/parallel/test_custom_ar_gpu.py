@@ -64,6 +64,16 @@ def _worker(rank, world, port, q):
             assert bool((yg.float() == want).all()), (it, yg[:4])
         assert car.error() == 0
         _fused_phase(car, rank, world, dev)
+        _serving_phase(car, rank, world, dev)
+        # the fenced slot protocol (preflight's fallback): the same bits, and the
+        # serving-shape check passes with it too; then back to the fence-free default
+        car.set_fenced(True)
+        assert car.fenced and not car.push_ok(64, 8192, 64)
+        dist.barrier()
+        _fused_phase(car, rank, world, dev)
+        _serving_phase(car, rank, world, dev)
+        car.set_fenced(False)
+        dist.barrier()
         _overlap_phase(car, rank, world, dev)
         _push_phase(car, rank, world, dev)
         # a rank that skips a call: every rank that waits for it times out and fails loudly
@@ -186,6 +196,19 @@ def _fused_phase(car, rank, world, dev):
         inc = torch.tensor(float(sum(r + 1 for r in range(world)))).to(torch.bfloat16).float()
         want = (res0.float() + inc).to(torch.bfloat16)
         assert torch.equal(r_dev.cpu(), want), it
+    assert car.error() == 0
+
+
+def _serving_phase(car, rank, world, dev):
+    """parallel/preflight.check_custom_ar_serving on the real kernels: 16 back-to-back fused
+    collectives at a decode shape (bf16 partials and fp32 slabs alternating), eager and graph-
+    replayed, bit-exact against the locally computed sums; the timed replay reports a per-call time."""
+    from polykey_service_amd.parallel import preflight
+    car.fused_blocks = 32  # every rank's grid resident at once on the shared GPU
+    dist.barrier()
+    r = preflight.check_custom_ar_serving(car, rank, world, dev, 64, 4096)
+    assert r["checks"] and all(r["checks"].values()), (car.fenced, r)
+    assert set(r["checks"]) == {"eager", "graph", "graph_timed"} and r["collective_us"] > 0, r
     assert car.error() == 0
 
 

@@ -231,3 +231,90 @@ def test_preflight_disables_a_faulty_collective_on_every_rank(tmp_path, faulty_r
         assert line["disabled"] == ["rccl_tp"] and line["checks"]["rccl_tp"]["all_gather"] is False
     else:
         assert res[1]["lines"] == []
+
+
+class StaleCar(FakeCar):
+    """The fused collective of FakeCar with the protocol switch of custom_ar.CustomAllReduce; on
+    ``stale_rank`` the 11th call of 16 (in the protocols listed in ``stale_in``) reads the peer
+    sum of the PREVIOUS call -- a slot served stale, the failure a fence-free protocol could
+    show on real xGMI."""
+
+    def __init__(self, group, world, stale_rank, stale_in):
+        super().__init__(group, world)
+        self.stale_rank, self.stale_in = stale_rank, stale_in
+        self.fenced, self.calls, self.prev, self.failed, self.switched = False, 0, None, False, []
+
+    def set_fenced(self, on):
+        self.fenced = bool(on)
+        self.calls = 0
+        self.switched.append(bool(on))
+
+    def error(self):
+        return 0
+
+    def fail(self):
+        self.failed = True
+
+    def reduce_residual(self, pending, residual, parts):
+        src = pending.view().sum(0) if hasattr(pending, "view") and not isinstance(pending, torch.Tensor) \
+            else pending.float()
+        s = src.float().clone()
+        dist.all_reduce(s, group=self.g)
+        self.calls += 1
+        proto = "fenced" if self.fenced else "fence-free"
+        if (dist.get_rank(self.g) == self.stale_rank and self.calls == 11 and proto in self.stale_in
+                and self.prev is not None):
+            s = self.prev  # the previous call's slot contents
+        self.prev = s
+        residual.copy_((residual.float() + s.to(torch.bfloat16).float()).to(residual.dtype))
+        M, N = residual.shape
+        n = self.nparts(M, N)
+        pv = parts.view(-1)[: n * M].view(n, M)
+        pv.copy_(residual.float().view(M, n, N // n).pow(2).sum(-1).t())
+        return pv
+
+
+def _serving_worker(rank, world, port, out, stale_in):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), POLYKEY_PREFLIGHT="0")
+    from polykey_service_amd.parallel import preflight
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    st = init_parallel(tp=world, device="cpu", backend="gloo")
+    car = st.custom_ar = StaleCar(st.tp_cpu_group, world, stale_rank=1, stale_in=stale_in)
+    lines = []
+    rep = preflight.run(st, paths=("custom_ar_serving",), emit=lines.append, serving=(8, 2048))
+    torch.save({"report": rep, "lines": lines, "car": st.custom_ar is not None, "closed": car.closed,
+                "switched": car.switched, "fenced": car.fenced}, f"{out}.{rank}")
+    st.custom_ar = None
+    destroy_parallel()
+
+
+@pytest.mark.parametrize("stale_in", [(), ("fence-free",), ("fence-free", "fenced")])
+def test_serving_preflight_catches_a_stale_slot_and_falls_back(tmp_path, stale_in):
+    """VERDICT r5 item 2 / ADVICE r5: the fused collective at serving shape, 16 back-to-back calls.
+    A stale slot read on call 11 of 16 on ONE rank fails the fence-free check on that rank; the
+    group agrees, switches to the fenced protocol on BOTH ranks and checks again.  If the fenced
+    protocol reads stale too, the custom collectives are disabled on both ranks (RCCL takes over);
+    a clean group keeps the fence-free protocol.  The report line carries the per-call time."""
+    out = str(tmp_path / "pf")
+    mp.start_processes(_serving_worker, args=(2, _port(), out, stale_in), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        d = torch.load(f"{out}.{r}", weights_only=True)
+        rep = d["report"]
+        assert rep["serving_shape"] == [8, 2048]
+        if not stale_in:
+            assert rep["checks"]["custom_ar_serving"]["ok"] and rep["car_protocol"] == "fence-free", rep
+            assert d["car"] and d["switched"] == [] and rep["disabled"] == []
+            assert rep["collective_us"]["custom_ar_serving"] > 0
+            continue
+        first = rep["checks"]["custom_ar_serving"]
+        assert first["ok"] == (r != 1) and not first["group_ok"], rep  # only rank 1 saw the stale read
+        assert d["switched"] == [True] and rep["car_protocol"] == "fenced"  # both ranks switched
+        fenced = rep["checks"]["custom_ar_serving_fenced"]
+        if stale_in == ("fence-free",):
+            assert fenced["ok"] and fenced["group_ok"] and d["car"] and not d["closed"] and rep["disabled"] == []
+        else:
+            assert not fenced["group_ok"] and not d["car"] and d["closed"], rep
+            assert rep["disabled"] == ["custom_ar_serving_fenced"]
+    line = json.loads(torch.load(f"{out}.0", weights_only=True)["lines"][-1])
+    assert line["event"] == "multi_gpu_preflight" and "collective_us" in line
