@@ -24,8 +24,10 @@ With N > 1 (plain, or rank 0 of the driver's torchrun -- the other outer ranks e
 touching a GPU) the measurement runs in a fresh N-rank torchrun child whose JSON line is relayed;
 with ``--tp 1`` a second child then serves ``--tp-extra-model`` (default Llama-3-70B) at TP = N
 over the same gRPC load and its result is added under ``tp{N}_70b`` -- the 70B TP=8 half of the
-BASELINE metric on an 8-GPU node.  Each child has its own timeout: a TP failure is reported in
-that key and never loses the replica number.
+BASELINE metric on an 8-GPU node -- and a third child serves ``--ep-extra-model`` (default
+Mixtral-8x7B) with DP attention + expert parallelism over all N GPUs (IPC expert all-to-all),
+reported under ``ep{N}_mixtral`` (BASELINE config 5).  Each child has its own timeout inside ONE
+deadline: an extra child's failure is reported in its key and never loses the replica number.
 """
 from __future__ import annotations
 
@@ -56,7 +58,9 @@ def parse_args(argv=None):
     ap.add_argument("--concurrency", type=int, default=64, help="concurrent gRPC clients per replica")
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--max-tokens", type=int, default=256)
-    ap.add_argument("--mode", choices=["unary", "stream"], default="unary")
+    ap.add_argument("--mode", choices=["unary", "stream", "openai"], default="unary",
+                    help="unary / server-streaming ExecuteTool over gRPC, or POST /v1/chat/completions on the "
+                         "OpenAI-compatible route (api/openai.py) served by the same process")
     ap.add_argument("--max-batched-tokens", type=int, default=8192)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--num-kv-blocks", type=int, default=0, help="KV blocks per replica (0: size from free HBM)")
@@ -77,8 +81,17 @@ def parse_args(argv=None):
                          "torchrun child and report it under the extra key tp{N}_<model> (BASELINE.json: "
                          "'Llama-3-8B TP=1 / 70B TP=8'); auto: llama3-70b when --model is llama3-8b (the "
                          "BASELINE pair), else none; 'none' skips it")
+    ap.add_argument("--tp-extra-mode", choices=["unary", "stream", "openai"], default="openai",
+                    help="the TP child's request path: BASELINE config 4 is '70B TP=8 over xGMI, OpenAI-compatible "
+                         "chat route'")
     ap.add_argument("--tp-extra-timeout", type=float, default=480.0,
                     help="seconds the TP child may take at most (its failure or timeout never loses the main number)")
+    ap.add_argument("--ep-extra-model", default="auto",
+                    help="N > 1 with --tp 1: after the TP child, measure this MoE model with DP attention + EP = N "
+                         "(expert all-to-all over all N GPUs) under ep{N}_<model> (BASELINE config 5); auto: "
+                         "mixtral-8x7b when --model is llama3-8b and N divides its experts, else none")
+    ap.add_argument("--ep-extra-timeout", type=float, default=300.0,
+                    help="seconds the EP child may take at most (never at the main number's expense)")
     ap.add_argument("--child-timeout", type=float, default=1500.0, help="seconds the main measurement child may take")
     ap.add_argument("--deadline", type=float, default=float(os.environ.get("POLYKEY_BENCH_DEADLINE_S", "540")),
                     help="N > 1: seconds the whole run may take, below the driver's 600 s command limit. The main "
@@ -167,14 +180,20 @@ def _strip(argv, names):
     return out
 
 
+def _extra_key(prefix: str, n: int, model: str) -> str:
+    return f"{prefix}{n}_" + {"llama3-70b": "70b", "llama3-8b": "8b", "mixtral-8x7b": "mixtral"}.get(model, model)
+
+
 def orchestrate(args, argv) -> int:
     """``--gpus N`` (N > 1), plain or under the driver's torchrun (rank 0 only: the other outer
     ranks exit without touching a GPU).  The measurement runs as a fresh N-rank torchrun child
-    whose JSON line is relayed; with ``--tp 1`` a second child then measures ``--tp-extra-model``
-    at TP = N (70B TP=8 on an 8-GPU node) under the extra key ``tp{N}_<model>``.  Each child has
-    its own timeout, so a TP failure can never erase the replica number, and both live inside ONE
-    ``--deadline``: the TP child gets only what the main child left (a hung TP child is killed in
-    time for the line to be printed before the driver's own limit)."""
+    whose JSON line is relayed; with ``--tp 1`` two more children then measure the other BASELINE
+    configs on the same N GPUs: ``--tp-extra-model`` at TP = N (70B TP=8 on an 8-GPU node) under
+    ``tp{N}_<model>`` and ``--ep-extra-model`` with DP attention + EP = N (Mixtral expert
+    all-to-all) under ``ep{N}_<model>``.  Each child has its own timeout, so an extra child's
+    failure can never erase the replica number, and all of them live inside ONE ``--deadline``:
+    a later child gets only what the earlier ones left (a hung child is killed in time for the
+    line to be printed before the driver's own limit)."""
     t_start = time.monotonic()
 
     def left() -> float:  # seconds a child may still take, keeping a margin to print the line
@@ -184,29 +203,41 @@ def orchestrate(args, argv) -> int:
     if main_line is None:
         print(f"bench: measurement child failed (rc {rc})", file=sys.stderr)
         return rc or 1
-    extra = args.tp_extra_model
-    if extra == "auto":
-        extra = "llama3-70b" if args.model == "llama3-8b" else "none"
-    if args.tp == 1 and args.ep == 1 and extra and extra != "none":
-        key = f"tp{args.gpus}_" + {"llama3-70b": "70b", "llama3-8b": "8b"}.get(extra, extra)
-        targv = _strip(argv, {"--model", "--tp", "--ep", "--frontend", "--tp-extra-model"}) + [
-            "--model", extra, "--tp", str(args.gpus), "--tp-extra-model", "none", "--child"]
-        budget = min(args.tp_extra_timeout, left())
+    strip = {"--model", "--tp", "--ep", "--frontend", "--tp-extra-model", "--ep-extra-model", "--mode",
+             "--tp-extra-mode"}
+
+    def extra_child(key: str, cargs, timeout: float) -> None:
+        budget = min(timeout, left())
         if budget < 30.0:
-            main_line[key] = {"error": f"TP child skipped: {max(budget, 0.0):.0f} s left of the "
+            main_line[key] = {"error": f"child skipped: {max(budget, 0.0):.0f} s left of the "
                                        f"{args.deadline:.0f} s deadline"}
-            print(json.dumps(main_line), flush=True)
-            return 0
-        trc, tl, wall = run_child(targv, args.gpus, budget)
+            return
+        trc, tl, wall = run_child(_strip(argv, strip) + cargs + ["--tp-extra-model", "none", "--ep-extra-model",
+                                                                 "none", "--child"], args.gpus, budget)
         if tl is not None:
             main_line[key] = {k: tl.get(k) for k in ("value", "unit", "p50_e2e_latency_ms", "ms_per_step", "steps",
                                                      "warmup", "scaling")}
             main_line[key].update(model=tl["config"]["model"], parallelism=tl["config"]["parallelism"],
+                                  rpc=tl["config"].get("rpc"),
                                   global_batch=tl["config"]["global_batch"], init_s=tl["config"].get("init_s"),
                                   wall_s=round(wall, 1))
         else:
-            main_line[key] = {"error": f"TP child rc {trc}" + (f" (timeout after {budget:.0f} s)" if trc == 124 else ""),
+            main_line[key] = {"error": f"child rc {trc}" + (f" (timeout after {budget:.0f} s)" if trc == 124 else ""),
                               "wall_s": round(wall, 1)}
+
+    if args.tp == 1 and args.ep == 1:
+        extra = args.tp_extra_model
+        if extra == "auto":
+            extra = "llama3-70b" if args.model == "llama3-8b" else "none"
+        if extra and extra != "none":
+            extra_child(_extra_key("tp", args.gpus, extra), ["--model", extra, "--tp", str(args.gpus), "--mode",
+                                                             args.tp_extra_mode], args.tp_extra_timeout)
+        moe = args.ep_extra_model
+        if moe == "auto":
+            moe = "mixtral-8x7b" if args.model == "llama3-8b" and 8 % args.gpus == 0 else "none"
+        if moe and moe != "none":
+            extra_child(_extra_key("ep", args.gpus, moe), ["--model", moe, "--tp", "1", "--ep", str(args.gpus),
+                                                           "--mode", args.mode], args.ep_extra_timeout)
     print(json.dumps(main_line), flush=True)
     return 0
 
@@ -244,6 +275,31 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
                                          stop_after=engine.lockstep or n_replicas > 1)
         finally:
             await srv.server.stop(0)
+    http = session = None
+    if args.mode == "openai":
+        # the OpenAI-compatible route on the same process and event loop as the gRPC server
+        import aiohttp
+
+        from polykey_service_amd.api.openai import serve_openai
+        hport = _free_port()
+        http = await serve_openai(router, f"127.0.0.1:{hport}", logger)
+        session = aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0),
+                                        timeout=aiohttp.ClientTimeout(total=600))
+        url = f"http://127.0.0.1:{hport}/v1/chat/completions"
+        for _ in range(600):  # the route is up once it answers
+            try:
+                async with session.get(f"http://127.0.0.1:{hport}/health") as hr:
+                    if hr.status == 200:
+                        break
+            except aiohttp.ClientError:
+                pass
+            await asyncio.sleep(0.05)
+        tok = router.llm.tokenizer
+        # prompt length in tokens after the chat template: the content is sized so the templated
+        # prompt is exactly --prompt-len tokens (byte tokenizer: one ASCII character per token)
+        overhead = len(tok.encode(tok.apply_chat_template([{"role": "user", "content": ""}])))
+        if args.prompt_len <= overhead:
+            raise SystemExit(f"--prompt-len {args.prompt_len}: the chat template alone is {overhead} tokens")
     channel = grpc.aio.insecure_channel(f"127.0.0.1:{port}", options=[
         ("grpc.max_receive_message_length", 64 << 20), ("grpc.max_send_message_length", 64 << 20)])
     unary = channel.unary_unary(proto.EXECUTE_TOOL, request_serializer=proto.ExecuteToolRequest.SerializeToString,
@@ -262,6 +318,11 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
     marks = []
 
     def build():
+        if args.mode == "openai":
+            n = max(1, args.prompt_len - overhead)
+            text = "".join(rng.choice("abcdefghijklmnopqrstuvwxyz ") for _ in range(n))
+            return {"messages": [{"role": "user", "content": text}], "max_tokens": args.max_tokens,
+                    "ignore_eos": True, "temperature": 0.0}
         req = proto.ExecuteToolRequest(tool_name=tool)
         req.parameters.update({"prompt_token_ids": [rng.randrange(0, V) for _ in range(args.prompt_len)],
                                "max_tokens": args.max_tokens, "ignore_eos": True, "temperature": 0.0,
@@ -270,6 +331,12 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
 
     async def one(req):
         t0 = time.perf_counter()  # submit time (requests are prebuilt: see `waves` below)
+        if args.mode == "openai":
+            async with session.post(url, json=req) as hr:
+                body = await hr.json()
+            if hr.status != 200:
+                raise RuntimeError(f"openai route: HTTP {hr.status}: {body}")
+            return int(body["usage"]["completion_tokens"]), time.perf_counter() - t0
         if args.mode == "unary":
             resp = await unary(req, timeout=600)
         else:
@@ -325,6 +392,9 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
         await _abarrier(leaders_group)
     elapsed = time.perf_counter() - t0
     await channel.close()
+    if session is not None:
+        await session.close()
+        await http.shutdown()
     await srv.server.stop(0)
     if engine.lockstep or n_replicas > 1:
         # DP attention + EP: leave the lockstep loop together with the other ranks; single front
@@ -409,6 +479,10 @@ def main(argv=None) -> int:
                         max_num_batched_tokens=args.max_batched_tokens, max_model_len=max_len,
                         hip_graphs=not args.no_graphs, num_kv_blocks=args.num_kv_blocks,
                         gpu_mem_fraction=args.gpu_mem_fraction)
+    if args.mode == "openai":
+        # every templated chat prompt starts with the same markup: the prefix cache would serve
+        # those blocks and skip their prefill work -- off, so no work is skipped in the timed region
+        ecfg.prefix_caching = False
     t_init = time.perf_counter()
     engine = LLMEngine(ecfg, st)
     if engine.device.type == "cuda":
@@ -477,7 +551,8 @@ def main(argv=None) -> int:
                 else f"dp{st.world_size}" + (f"_ep{st.ep_size}_a2a" if st.ep_size > 1 else "")
                 + ("_single_frontend" if args.frontend == "single" and dp_front else ""),
                 "concurrency_per_replica": args.concurrency,
-                "rpc": f"ExecuteTool ({args.mode})",
+                "rpc": "POST /v1/chat/completions (OpenAI route)" if args.mode == "openai" else
+                f"ExecuteTool ({args.mode})",
                 "clients": "load-generator process" if args.client == "process" else "server event loop",
                 "hip_graphs": not args.no_graphs,
                 # every prompt is unique, so the prefix cache must serve nothing (no skipped work)

@@ -33,10 +33,10 @@ template <int kPart, int NW, bool FROM_QKV, int SS = 0>
 __global__ void __launch_bounds__(64 * NW) paged_decode_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, bf16_t* __restrict__ kc,
     bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int n_q, int n_kv, int bs,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int n_q, int n_kv, int bs,
     int max_blocks, int q_stride, int out_stride, int n_parts, float scale2, const QkvIn qi) {
   __shared__ DecodeLds<kPart, NW> lds;
-  decode_tile<kPart, NW, FROM_QKV, SS>(out, q, kc, vc, block_tables, context_lens, part_o, part_ml, counters, n_q, n_kv,
+  decode_tile<kPart, NW, FROM_QKV, SS>(out, q, kc, vc, block_tables, context_lens, part_o, part_ml, n_q, n_kv,
                                        bs, max_blocks, q_stride, out_stride, n_parts, scale2, qi, blockIdx.x, blockIdx.y,
                                        blockIdx.z, gridDim.z, lds, Flow{});
 }
@@ -319,12 +319,6 @@ int decode_part(int n_seqs, int n_kv, int max_ctx) {
   return n_seqs * n_kv * z < g_decode_fill ? kDecodePartSmall : kDecodePart;
 }
 
-// 1: standalone decode attention launches of at most 128 workgroups run 8-wave workgroups
-PK_EXPORT int pk_set_decode_wide(int on) {
-  g_decode_wide = on != 0;
-  return 0;
-}
-
 // Workgroup count below which decode takes 128-key partitions (default 64; 0: always 512 keys).
 // The partition slabs must be sized for the bound (ops/attention.py decode_workspace reads the
 // same POLYKEY_DECODE_FILL; kv_heads=None sizes them for any).
@@ -337,7 +331,7 @@ PK_EXPORT int pk_set_decode_fill(int n) {
 template <int P>
 static int decode_launch_p(void* out, const void* q, const QkvIn& qi, const void* k_cache, const void* v_cache,
                            const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
-                           void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
+                           int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
                            int out_stride, float scale, int max_ctx, hipStream_t stream) {
   const int n_parts = (max_ctx + P - 1) / P;
   if (n_parts > 1 && (part_o == nullptr || part_ml == nullptr)) return -2;
@@ -348,27 +342,22 @@ static int decode_launch_p(void* out, const void* q, const QkvIn& qi, const void
   static_cast<bf16_t*>(out), static_cast<const bf16_t*>(q), static_cast<bf16_t*>(const_cast<void*>(k_cache)),   \
       static_cast<bf16_t*>(const_cast<void*>(v_cache)), static_cast<const int*>(block_tables),                  \
       static_cast<const int*>(context_lens), static_cast<float*>(part_o), static_cast<float*>(part_ml),          \
-      static_cast<int*>(counters), n_q, n_kv, bs, max_blocks, q_stride, out_stride, n_parts, scale * kLog2e, qi
-  // WIDE (pk_set_decode_wide): launches of at most 128 workgroups (the 70B TP=8 shard: 64 sequences
-  // x one kv head) as 8-wave workgroups -- twice the K/V loads in flight per CU when most CUs idle
-  // (the K/V prefetch across the slab reduction for such launches, PRE, measured slower:
-  // profiles/r5_attn_ab4.jsonl)
-  const bool wide = g_decode_wide && static_cast<long>(grid.x) * grid.y * grid.z <= 128;
+      n_q, n_kv, bs, max_blocks, q_stride, out_stride, n_parts, scale * kLog2e, qi
+  // (the K/V prefetch across the slab reduction for launches that leave most CUs idle, PRE,
+  // measured slower: profiles/r5_attn_ab4.jsonl)
   if (qi.partial != nullptr) {
-    switch (qi.S * (wide ? -1 : 1)) {
+    switch (qi.S) {
       case 2: paged_decode_kernel<P, kDecodeWaves, true, 2><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       case 4: paged_decode_kernel<P, kDecodeWaves, true, 4><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       case 8: paged_decode_kernel<P, kDecodeWaves, true, 8><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
       case 16: paged_decode_kernel<P, kDecodeWaves, true, 16><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
-      case -8: paged_decode_kernel<P, 8, true, 8><<<grid, 64 * 8, 0, stream>>>(PK_DECODE_ARGS); break;
-      case -16: paged_decode_kernel<P, 8, true, 16><<<grid, 64 * 8, 0, stream>>>(PK_DECODE_ARGS); break;
       default: paged_decode_kernel<P, kDecodeWaves, true, 0><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS); break;
     }
   } else
     paged_decode_kernel<P, kDecodeWaves, false><<<grid, 64 * kDecodeWaves, 0, stream>>>(PK_DECODE_ARGS);
 #undef PK_DECODE_ARGS
   int rc = PK_CHECK_LAUNCH();
-  if (rc || counters != nullptr || n_parts == 1) return rc;
+  if (rc || n_parts == 1) return rc;
   dim3 g2(n_q, n_seqs);
   paged_decode_reduce_kernel<P><<<g2, 128, 0, stream>>>(
       static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),
@@ -376,11 +365,11 @@ static int decode_launch_p(void* out, const void* q, const QkvIn& qi, const void
   return PK_CHECK_LAUNCH();
 }
 
-// counters: [n_seqs, n_kv] int32, zero-initialised once (the merging workgroup re-arms its
-// counter); with counters == null the partitions are merged by a second kernel instead.
+// Sequences with more than one partition are merged by a second kernel (an in-launch merge by
+// the last partition measured slower, profiles/r5_tp_ab.jsonl, and was removed in round 6).
 static int decode_launch(void* out, const void* q, const QkvIn& qi, const void* k_cache, const void* v_cache,
                          const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
-                         void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
+                         int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
                          int out_stride, float scale, int max_ctx, hipStream_t stream) {
   if (n_seqs <= 0) return 0;
   if (n_q % n_kv || n_q / n_kv > 16 || bs % 32 || bs <= 0) return -1;  // K tiles: 32 keys
@@ -389,20 +378,20 @@ static int decode_launch(void* out, const void* q, const QkvIn& qi, const void* 
   if (max_ctx <= 0 || max_ctx > max_blocks * bs) max_ctx = max_blocks * bs;
   if (decode_part(n_seqs, n_kv, max_ctx) == kDecodePartSmall)
     return decode_launch_p<kDecodePartSmall>(out, q, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml,
-                                             counters, n_seqs, n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale,
+                                             n_seqs, n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale,
                                              max_ctx, stream);
   return decode_launch_p<kDecodePart>(out, q, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml,
-                                      counters, n_seqs, n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale, max_ctx,
+                                      n_seqs, n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale, max_ctx,
                                       stream);
 }
 
 // max_blocks: block-table row stride; max_ctx: bound on every context of this launch (<= 0: no bound)
 PK_EXPORT int pk_paged_decode(void* out, const void* q, const void* k_cache, const void* v_cache,
                               const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
-                              void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
+                              int n_seqs, int n_q, int n_kv, int bs, int max_blocks, int q_stride,
                               int out_stride, float scale, int max_ctx, hipStream_t stream) {
   const QkvIn none{};
-  return decode_launch(out, q, none, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, counters, n_seqs,
+  return decode_launch(out, q, none, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, n_seqs,
                        n_q, n_kv, bs, max_blocks, q_stride, out_stride, scale, max_ctx, stream);
 }
 
@@ -416,21 +405,7 @@ PK_EXPORT int pk_paged_decode_qkv(void* out, const void* partial, int S, int M, 
   if (partial == nullptr || S < 1 || M < n_seqs) return -1;
   QkvIn qi{static_cast<const float*>(partial), static_cast<const int*>(positions), static_cast<const float*>(cos_sin),
            static_cast<const int*>(slots), S, M};
-  return decode_launch(out, nullptr, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, nullptr,
-                       n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
-}
-
-// ... with counters ([n_seqs, n_kv] int32, zeroed once, re-armed by the kernel): the partitions of
-// a sequence are merged in-launch by the last one to arrive (no reduce kernel after)
-PK_EXPORT int pk_paged_decode_qkv2(void* out, const void* partial, int S, int M, const void* positions,
-                                   const void* cos_sin, const void* slots, void* k_cache, void* v_cache,
-                                   const void* block_tables, const void* context_lens, void* part_o, void* part_ml,
-                                   void* counters, int n_seqs, int n_q, int n_kv, int bs, int max_blocks,
-                                   int out_stride, float scale, int max_ctx, hipStream_t stream) {
-  if (partial == nullptr || S < 1 || M < n_seqs) return -1;
-  QkvIn qi{static_cast<const float*>(partial), static_cast<const int*>(positions), static_cast<const float*>(cos_sin),
-           static_cast<const int*>(slots), S, M};
-  return decode_launch(out, nullptr, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml, counters,
+  return decode_launch(out, nullptr, qi, k_cache, v_cache, block_tables, context_lens, part_o, part_ml,
                        n_seqs, n_q, n_kv, bs, max_blocks, 0, out_stride, scale, max_ctx, stream);
 }
 

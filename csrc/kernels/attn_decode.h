@@ -19,11 +19,8 @@ constexpr int kDecodePartSmall = 128;  // keys per partition when (seq, kv head)
 // per-rank step 6.52 vs 6.54 ms at 256 (128-key partitions + merge), profiles/r5_attn_ab4.jsonl
 int g_decode_fill = 64;
 int g_decode_z = 4;  // max partition workgroups per (seq, kv head) (pk_set_decode_z)
-// 8-wave workgroups for launches of <= 128 workgroups (pk_set_decode_wide, A/B): 70B TP=8 rank
-// attention 10.5 -> 10.1 us, step 6.52-6.53 -> 6.51 ms (profiles/r5_wide_attn.jsonl,
-// r5_attn70_probe3.jsonl).  Off: within noise, and the 4-wave tile keeps the standalone launch
-// bit-identical to the fused QKV -> attention launch (whose fallback re-runs a step through it)
-int g_decode_wide = 0;
+// (8-wave workgroups for small launches, pk_set_decode_wide: within noise at the 70B TP=8 shard,
+// profiles/r5_wide_attn.jsonl -- removed in round 6)
 
 // K/V stream loads: plain (non-temporal measured slower: in-situ decode step 4.43 vs 4.45 ms,
 // tools/ab_decode.py)
@@ -236,7 +233,6 @@ template <int kPart, int NW>
 struct DecodeLds {
   float o_lds[NW][16][kHD + 4];
   float ml_lds[NW][16][2];
-  int last;
   int bt_s[kPart / 8 + 2];  // this partition's block-table window (LDS: lookups use lgkmcnt)
   // FROM_QKV, new token folded in (see below): its rotated k, its v and its G scores
   bf16_t kn_s[kHD] __attribute__((aligned(16)));
@@ -245,34 +241,20 @@ struct DecodeLds {
   bf16_t q_s[16][kHD] __attribute__((aligned(16)));
 };
 
-// bf16 store of the attention output; WT: write-through (sc1) -- the output is handed off in-launch
-// to the o-projection tiles of the same launch (decode_fused.hip), which read it with sc1 loads
-template <bool WT>
-__device__ __forceinline__ void st_out(bf16_t* base, int64_t idx, bf16_t v) {
-  if constexpr (WT)
-    __builtin_amdgcn_raw_buffer_store_b16(
-        v, __builtin_amdgcn_make_buffer_rsrc(base, static_cast<short>(0), 0x7ffffff0, 0x00020000),
-        static_cast<int>(idx * 2), 0, 16);
-  else
-    base[idx] = v;
-}
-
 // One decode-attention workgroup (seq = by, kv head = bx, partition = bz of gdz).  FL & 2: the
 // QKV slabs are handed over in-launch (decode_fused.hip): wait on kv head bx's tickets in fin
-// before reading them, and read them with sc1 loads.  FL & 1: the output is handed over in-launch
-// (to the o-projection tiles): write-through stores; the caller takes the tickets.
+// before reading them, and read them with sc1 loads.
 // PRE = 1 / 2 (fused launch): the first partition's first one / two K/V steps per wave are
 // requested before the hand-off wait, so they stream in while the QKV tiles finish.
 template <int kPart, int NW, bool FROM_QKV, int SS = 0, int FL = 0, int PRE = 0>
 __device__ __forceinline__ void decode_tile(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, bf16_t* __restrict__ kc,
     bf16_t* __restrict__ vc, const int* __restrict__ block_tables, const int* __restrict__ context_lens,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int* __restrict__ counters, int n_q, int n_kv, int bs,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int n_q, int n_kv, int bs,
     int max_blocks, int q_stride, int out_stride, int n_parts, float scale2, const QkvIn qi, const int bx,
     const int by, const int bz, const int gdz, DecodeLds<kPart, NW>& L, const Flow& fin) {
   auto& o_lds = L.o_lds;
   auto& ml_lds = L.ml_lds;
-  int& last = L.last;
   auto& bt_s = L.bt_s;
   auto& kn_s = L.kn_s;
   auto& vn_s = L.vn_s;
@@ -357,7 +339,7 @@ __device__ __forceinline__ void decode_tile(
   if (ctx <= 0) {
     if (bz == 0)  // a padded (graph) row -> zeros
       for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW)
-        st_out<(FL & 1) != 0>(out, static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD, 0);
+        out[static_cast<int64_t>(seq) * out_stride + (h * G + idx / kHD) * kHD + idx % kHD] = 0;
     return;
   }
   // n_parts comes from the launch's context bound; the clamp keeps a violated bound in-bounds
@@ -549,18 +531,7 @@ __device__ __forceinline__ void decode_tile(
     }
     const int hq = h * G + c;
     if (n_eff == 1) {
-      st_out<(FL & 1) != 0>(out, static_cast<int64_t>(seq) * out_stride + hq * kHD + d, f2bf(L > 0.f ? O / L : 0.f));
-    } else if (counters != nullptr) {
-      // merged in-launch: write-through (sc1) stores relative to this sequence's slab (< 2 GiB),
-      // read back by the merging workgroup with sc1 loads -- no release / acquire fences (an L2
-      // write-back / invalidate per workgroup measured +6.6 us per 70B TP=8 layer)
-      const int pl = hq * n_parts + bz;
-      stf_sc1(part_o + static_cast<int64_t>(seq) * n_q * n_parts * kHD, pl * kHD + d, O);
-      if (d == 0) {
-        float* ml = part_ml + static_cast<int64_t>(seq) * n_q * n_parts * 2;
-        stf_sc1(ml, 2 * pl, M);
-        stf_sc1(ml, 2 * pl + 1, L);
-      }
+      out[static_cast<int64_t>(seq) * out_stride + hq * kHD + d] = f2bf(L > 0.f ? O / L : 0.f);
     } else {
       const int64_t pi = (static_cast<int64_t>(seq) * n_q + hq) * n_parts + bz;
       part_o[pi * kHD + d] = O;
@@ -579,36 +550,6 @@ __device__ __forceinline__ void decode_tile(
       bf16_t* d = vc + (static_cast<int64_t>(slot / bs) * n_kv + h) * kHD * bs;
       d[vcache_off(slot % bs, t - kHD)] = f2bf(vn_s[t - kHD]);
     }
-  }
-  if (n_eff == 1 || counters == nullptr) return;
-  // ---- in-launch split-K merge: the last workgroup to arrive combines the partials
-  // (write-through partials, every wave drains them, one lane takes the ticket; the last arriver
-  // reads them back with sc1 loads, merges and re-arms the counter -- flow.h's hand-off rule).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int* ctr = counters + seq * n_kv + h;
-    const int t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == n_eff - 1);
-    if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!last) return;
-  const float* so = part_o + static_cast<int64_t>(seq) * n_q * n_parts * kHD;
-  const float* sml = part_ml + static_cast<int64_t>(seq) * n_q * n_parts * 2;
-  for (int idx = threadIdx.x; idx < G * kHD; idx += 64 * NW) {
-    const int c = idx / kHD, d = idx % kHD;
-    const int hq = h * G + c;
-    const int base = hq * n_parts;
-    float M = kNegBig;
-    for (int p = 0; p < n_eff; ++p) M = fmaxf(M, ldf_sc1(sml, sml + 2 * (base + p)));
-    float O = 0.f, L = 0.f;
-    for (int p = 0; p < n_eff; ++p) {
-      const float f = exp2f(ldf_sc1(sml, sml + 2 * (base + p)) - M);
-      O += f * ldf_sc1(so, so + (base + p) * kHD + d);
-      L += f * ldf_sc1(sml, sml + 2 * (base + p) + 1);
-    }
-    st_out<(FL & 1) != 0>(out, static_cast<int64_t>(seq) * out_stride + hq * kHD + d, f2bf(L > 0.f ? O / L : 0.f));
   }
 }
 

@@ -11,7 +11,6 @@
 // first two K/V steps of each wave before its hand-off wait (decode_tile PRE = 2): 37.5-38 vs
 // 39.5-40 us per 8B layer (tools/qa_stamps.py, profiles/r4_qa_fused_stamps.txt -- the QKV phase
 // stretches from ~16 to ~22 us while the attention after the hand-off shrinks from ~20 to ~13 us).
-#include "phase.h"
 #include "skinny_tile.h"
 #include "attn_decode.h"
 
@@ -33,29 +32,7 @@ struct AttnArgs {
   int n_q, n_kv, bs, max_blocks, out_stride, n_parts, n_seqs, z;
   float scale2;
   QkvIn qi;
-  int* counters;  // [n_seqs, n_kv] in-launch partition merge (the o-projection phase needs it)
 };
-
-// The o-projection phase (OPH): the o tiles' K slices are ranges of q heads, so a slice depends on
-// the attention tiles of its kv heads only.  Slice of kv head h: h / kvps (kvps kv heads per slice),
-// or slices h * spk .. h * spk + spk - 1 when a kv head's q heads span spk slices (70B TP=8: one kv
-// head, 2 slices).  Every attention workgroup -- empty partitions and padded rows too -- drains its
-// write-through output stores and takes ONE ticket per slice it completes.
-struct OSlices {
-  int kvps, spk;
-};
-
-__device__ __forceinline__ void o_signal(const Flow& f, const OSlices& os, int h) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (os.spk <= 1)
-      __hip_atomic_fetch_add(f.ready + kFlowPad * (h / os.kvps), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      for (int i = 0; i < os.spk; ++i)
-        __hip_atomic_fetch_add(f.ready + kFlowPad * (h * os.spk + i), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
 
 template <int MT, int P>
 union FusedLds {
@@ -63,39 +40,26 @@ union FusedLds {
   DecodeLds<P, kDecodeWaves> a;
 };
 
-// RES: phase 0 is the TP = 1 residual update of the previous layer's down slabs (phase.h), whose
-// residual and norm parts the QKV tiles take in-launch (skinny_tile FL & 4).
-// OPH: phase 3 is the o-projection's split-K slabs (64-row n-blocks, packed W): its tiles request
-// their first weight k-steps, wait for their K slice's attention tiles (OSlices) and read the
-// attention output with sc1 loads -- the o-projection's launch and weight ramp overlap the
-// attention tail (partitions are merged in-launch: aa.counters).
-template <int MT, int SS, int P, bool RES = false, bool OPH = false>
+// (Removed in round 6, both measured slower on the serving chain: the TP = 1 residual update of
+// the previous layer's down slabs as phase 0 of this launch, profiles/r5_phase_ab.jsonl; the
+// o-projection as its phase 3 with the partitions merged in-launch, +0.4 % / 70B TP=8 7.86 vs
+// 6.70 ms.)
+template <int MT, int SS, int P>
 __global__ void __launch_bounds__(256, 2) qkv_attn_fused_kernel(const GemmArgs qkv, const AttnArgs aa,
-                                                                const Flow fq, const Flow fa, int n_qkv, int n_attn,
-                                                                const ResArgs ra, const Flow fres, int n_res,
-                                                                const GemmArgs oa, const Flow fo, const OSlices os,
-                                                                int n_o) {
+                                                                const Flow fq, const Flow fa, int n_qkv, int n_attn) {
   __shared__ FusedLds<MT, P> lds;
   const int b = blockIdx.x;
-  if constexpr (RES)
-    if (b < n_res) res_phase(ra, b, fres);
   if (b < n_qkv) {
-    skinny_tile<MT, kPartial, true, false, false, true, 2, RES ? 5 : 1>(qkv, b, 0, n_qkv, lds.g, fq, fres);
+    skinny_tile<MT, kPartial, true, false, false, true, 2, 1>(qkv, b, 0, n_qkv, lds.g, fq);
     __syncthreads();  // the LDS is reused by the attention tile
   }
-  if (b < n_attn) {  // small batches: more QKV (or o) tiles than attention tiles
+  if (b < n_attn) {  // small batches: more QKV tiles than attention tiles
     const int x = b % aa.n_kv, y = (b / aa.n_kv) % aa.n_seqs, z = b / (aa.n_kv * aa.n_seqs);
-    decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 2>(
+    decode_tile<P, kDecodeWaves, true, SS, 2, 2>(
         aa.out, nullptr, aa.kc, aa.vc, aa.block_tables, aa.context_lens, aa.part_o, aa.part_ml,
-        aa.counters, aa.n_q, aa.n_kv, aa.bs, aa.max_blocks, 0, aa.out_stride, aa.n_parts, aa.scale2,
+        aa.n_q, aa.n_kv, aa.bs, aa.max_blocks, 0, aa.out_stride, aa.n_parts, aa.scale2,
         aa.qi, x, y, z, aa.z, lds.a, fa);
-    if constexpr (OPH) o_signal(fo, os, x);  // (its barrier also frees the LDS for the o tile)
   }
-  if constexpr (OPH)
-    if (b < n_o) {
-      __syncthreads();
-      skinny_tile<MT, kPartial, true, false, false, false, 1, 2>(oa, b, 0, n_o, lds.g, fo);
-    }
 }
 
 }  // namespace
@@ -107,17 +71,10 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
                                 const void* slots, void* k_cache, void* v_cache, const void* block_tables,
                                 const void* context_lens, void* part_o, void* part_ml, int n_q, int n_kv, int bs,
                                 int max_blocks, int out_stride, float scale, int max_ctx, int* flow,
-                                const ResArgs* res, const GemmArgs* o_in, int* flow_o, void* counters,
                                 hipStream_t stream) {
   GemmArgs g = *qkv_in;
   const int n_seqs = g.M;
   if (n_seqs <= 0) return 0;
-  // res (may be null): phase 0 updates the residual stream g.A and its norm parts g.nrm_parts
-  if (res != nullptr && (res->residual == nullptr || res->parts == nullptr || res->flow == nullptr ||
-                         res->M != g.M || res->H != g.K || res->H % kResCols || (res->slabs != nullptr && res->S < 1) ||
-                         static_cast<const void*>(res->residual) != static_cast<const void*>(g.A) ||
-                         res->parts != g.nrm_parts || g.nrm_nparts != res->H / kResCols || g.lda != res->H))
-    return -1;
   // up to 128 rows (one row tile; 128 rows take the MT = 8 tile, whose row scale reads <= 16 parts)
   if (n_seqs > 128 || (n_seqs > 64 && g.nrm_nparts > 16) || g.N != (n_q + 2 * n_kv) * kHD || g.N % 128 || g.S < 1 || g.K % (kKC * g.S) || !g.row_scale ||
       g.nrm_parts == nullptr || g.nrm_nparts < 1 || g.nrm_nparts > 64 || g.partial == nullptr || g.lda % 8 ||
@@ -137,7 +94,7 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   const AttnArgs aa{static_cast<bf16_t*>(out), static_cast<bf16_t*>(k_cache), static_cast<bf16_t*>(v_cache),
                     static_cast<const int*>(block_tables), static_cast<const int*>(context_lens),
                     static_cast<float*>(part_o), static_cast<float*>(part_ml), n_q, n_kv, bs, max_blocks, out_stride,
-                    n_parts, n_seqs, z, scale * 1.4426950408889634f, qi, static_cast<int*>(counters)};
+                    n_parts, n_seqs, z, scale * 1.4426950408889634f, qi};
   int* done = flow + 64 * kFlowPad;
   int* err = fused_err_word() != nullptr ? fused_err_word() : flow + 128 * kFlowPad;
   const int G = n_q / n_kv;
@@ -146,51 +103,13 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
   const Flow fa{flow, done, err, (G + 2) * g.S, n_seqs * z, 0, 2, n_q, n_kv, fused_spin_limit()};
   const int n_qkv = (g.N / 128) * g.S;
   const int n_attn = n_kv * n_seqs * z;
-  const ResArgs ra = res != nullptr ? *res : ResArgs{};
-  const int n_res = res != nullptr ? res_workgroups(ra) : 0;
-  const Flow fres = res != nullptr ? res_flow(ra, n_qkv, err, fused_spin_limit()) : Flow{};
-  // o_in (may be null): the o-projection phase -- its split-K slabs [o.S, M, o.N] of out @ Wo^T
-  // (packed W, 64-row n-blocks), out handed over in-launch (needs counters when partitioned).
-  // counters (may be null): [n_seqs, n_kv] zeroed -- partitions merged in-launch by the last
-  // partition workgroup to arrive instead of by a reduce kernel after the launch
-  const bool oph = o_in != nullptr;
-  GemmArgs oa = oph ? *o_in : GemmArgs{};
-  OSlices os{1, 1};
-  int n_o = 0;
-  Flow fo{};
-  if (oph) {
-    const int hps = oa.S > 0 && n_q % oa.S == 0 ? n_q / oa.S : 0;  // q heads per K slice
-    if (oa.M != n_seqs || oa.K != n_q * kHD || static_cast<const void*>(oa.A) != out || oa.lda != out_stride ||
-        oa.N % 64 || oa.S < 1 || oa.S > 64 || oa.K % (kKC * oa.S) || oa.partial == nullptr || oa.partial == g.partial ||
-        oa.row_scale || oa.row_offsets != nullptr || flow_o == nullptr || hps == 0 ||
-        (hps >= G ? hps % G : G % hps) || (n_parts > 1 && counters == nullptr))
-      return -1;
-    os = hps >= G ? OSlices{hps / G, 1} : OSlices{1, G / hps};
-    oa.row_tiles = 1;
-    oa.tile_rows = g.tile_rows;
-    oa.max_group_rows = 0;
-    n_o = (oa.N / 64) * oa.S;
-    // per slice: every attention workgroup of its kv heads; consumers: the slice's n-blocks
-    fo = Flow{flow_o, flow_o + 64 * kFlowPad, err, n_seqs * z * os.kvps, oa.N / 64, 0, 2, 0, 0, fused_spin_limit()};
-  }
-  int nwg = n_attn > n_qkv ? n_attn : n_qkv;
-  nwg = n_o > nwg ? n_o : nwg;
-  nwg = n_res > nwg ? n_res : nwg;  // (the residual workgroups come first and never wait)
-  const dim3 grid(nwg);
+  const dim3 grid(n_attn > n_qkv ? n_attn : n_qkv);
   auto go = [&](auto mt, auto ss) {
     constexpr int MT = decltype(mt)::value, SS = decltype(ss)::value;
-#define PK_QAF(PP, RR, OO)                                                                                     \
-  qkv_attn_fused_kernel<MT, SS, PP, RR, OO><<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv, n_attn, ra, fres, n_res, \
-                                                                      oa, fo, os, n_o)
-#define PK_QAF_O(PP, RR) \
-  if (oph) PK_QAF(PP, RR, true); else PK_QAF(PP, RR, false);
-    if (P == kDecodePartSmall) {
-      if (res != nullptr) { PK_QAF_O(kDecodePartSmall, true) } else { PK_QAF_O(kDecodePartSmall, false) }
-    } else {
-      if (res != nullptr) { PK_QAF_O(512, true) } else { PK_QAF_O(512, false) }
-    }
-#undef PK_QAF_O
-#undef PK_QAF
+    if (P == kDecodePartSmall)
+      qkv_attn_fused_kernel<MT, SS, kDecodePartSmall><<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv, n_attn);
+    else
+      qkv_attn_fused_kernel<MT, SS, 512><<<grid, 256, 0, stream>>>(g, aa, fq, fa, n_qkv, n_attn);
   };
   auto go_mt = [&](auto ss) {
     switch ((n_seqs + 15) / 16) {
@@ -210,7 +129,7 @@ PK_EXPORT int pk_qkv_attn_fused(const GemmArgs* qkv_in, void* out, const void* p
     default: go_mt(std::integral_constant<int, 0>{}); break;
   }
   int rc = PK_CHECK_LAUNCH();
-  if (rc || n_parts == 1 || counters != nullptr) return rc;  // (counters: partitions merged in-launch)
+  if (rc || n_parts == 1) return rc;
   if (P == kDecodePartSmall)
     paged_decode_reduce_kernel<kDecodePartSmall><<<dim3(n_q, n_seqs), 128, 0, stream>>>(
         static_cast<bf16_t*>(out), static_cast<const float*>(part_o), static_cast<const float*>(part_ml),

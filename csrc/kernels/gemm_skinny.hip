@@ -21,7 +21,6 @@
 //     (tools/gemm_lab.hip: LM head 5.1 -> 5.9 TB/s with non-temporal loads).
 #include <cstring>
 
-#include "phase.h"
 #include "skinny_tile.h"
 
 using namespace pk;
@@ -42,25 +41,18 @@ __global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const GemmArgs args
 // workgroup is resident at once (one per CU) and a gate_up tile never waits: no deadlock.
 // (A/B, tools/gpu/mlp_ab.sh: down tiles as workgroups of their own, dispatched after the gate_up
 // ones, put two down tiles on some CUs and lost 7 us per layer.)
-// SPLIT: gate_up split over K (gu.S > 1; kSiluSplit: write-through slabs, the last split of an
-// n-block sums them, applies SiLU and publishes h) -- for shapes whose gate_up n-blocks alone
-// cannot fill the chip (70B TP=8: 56).
 // DKR: the down projection's n-block height (2: 128 rows; 1: 64 rows -- twice the tiles at the
 // same split when 128-row tiles would leave CUs idle: 8B 32 x 4, 70B TP=8 64 x 2 -> 256).
 // DNT: non-temporal down weights (A/B builds: tools/lab/build_variant.py)
-// RES: the TP = 1 residual update of the o-projection's slabs runs as phase 0 (phase.h res_phase)
-// and the gate_up tiles take their A and row scale from it in-launch (skinny_tile FL & 4).
-template <int MT, bool SPLIT, int DKR, bool DNT = false, bool RES = false>
+// (Removed in round 6, measured slower: gate_up split over K inside this launch -- the 70B TP=8
+// shard, r4_tp_solo.md -- and the o-projection's residual update as phase 0, r5_phase_ab.jsonl.)
+template <int MT, int DKR, bool DNT = false>
 __global__ void __launch_bounds__(256, 2) mlp_fused_kernel(const GemmArgs gu, const GemmArgs dn, const Flow fgu,
-                                                           const Flow fdn, int n_gu, int n_dn, const ResArgs ra,
-                                                           const Flow fres, int n_res) {
+                                                           const Flow fdn, int n_gu, int n_dn) {
   __shared__ SkinnyLds<MT> lds;
   const int b = blockIdx.x;
-  if constexpr (RES)
-    if (b < n_res) res_phase(ra, b, fres);
   if (b < n_gu) {
-    skinny_tile<MT, SPLIT ? kSiluSplit : kSiluMul, true, false, true, true, 2, RES ? 5 : 1>(gu, b, 0, n_gu, lds, fgu,
-                                                                                          fres);
+    skinny_tile<MT, kSiluMul, true, false, true, true, 2, 1>(gu, b, 0, n_gu, lds, fgu);
     __syncthreads();  // the LDS tiles are reused by the down tile
   }
   if (b < n_dn) skinny_tile<MT, kPartial, true, false, DNT, false, DKR, 2>(dn, b, 0, n_dn, lds, fdn);
@@ -470,12 +462,6 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
                     : launch<kBF16, false, false, false, false, 1>(a, stream);
     }
     if (nt) return -1;
-    if ((mode & 7) == kSiluMul) {  // folded-norm gate_up + SiLU, no K split: N / 64 workgroups
-      if (!packed || !a.row_scale || a.S != 1 || a.row_tiles > 1 || a.nrm_parts == nullptr || a.nrm_nparts < 1 ||
-          a.nrm_nparts > 64)
-        return -1;
-      return launch<kSiluMul, true, false, false, true, 1>(a, stream);
-    }
     if (a.row_scale) {  // folded-norm QKV slabs (packed W only)
       if ((mode & 7) != kPartial || !packed || a.nrm_parts == nullptr || a.nrm_nparts < 1 || a.nrm_nparts > 64)
         return -1;
@@ -517,13 +503,6 @@ int dispatch(const GemmArgs& args, int mode, hipStream_t stream) {
     case kPush:
       if (norm || !push_ok(a, 128)) return -1;
       return packed ? launch<kPush, true, false, false>(a, stream) : launch<kPush, false, false, false>(a, stream);
-    case kSiluSplit:
-      // interleaved gate / up split over K, reduced in-launch by the last split of each n-block
-      // (SiLU applied there): folded-norm row scale, packed W, one 64-row tile, counters [N / 128]
-      if (norm || !packed || !a.row_scale || a.S < 2 || a.M > 64 || a.row_tiles > 1 || a.counters == nullptr ||
-          a.partial == nullptr || a.out == nullptr)
-        return -1;
-      return nt ? launch<kSiluSplit, true, false, true, true>(a, stream) : launch<kSiluSplit, true, false, false, true>(a, stream);
     default: return -1;
   }
 }
@@ -551,37 +530,27 @@ PK_EXPORT int pk_skinny_gemm_ex(const GemmArgs* args, int mode, hipStream_t stre
 }
 
 // Fused decode MLP (mlp_fused_kernel): gu = gate_up + SiLU (packed, non-temporal, folded norm:
-// row_scale + nrm_parts; gu.S > 1: split over K with fp32 slabs in gu.partial), dn = down split-K
-// slabs (packed) reading gu's output.  flow: a zeroed int buffer of >= kFlowWords words (64
-// tickets and 64 consumer counts, 64 words apart, the sticky error word, then the gate_up split
-// counters), left zeroed by every launch that completes.
-constexpr int kFlowCounters = 128 * kFlowPad + 64;  // gate_up n-block counters (kSiluSplit)
-constexpr int kFlowWords = kFlowCounters + 1024;
+// row_scale + nrm_parts; unsplit), dn = down split-K slabs (packed) reading gu's output.  flow: a
+// zeroed int buffer of >= kFlowWords words (64 tickets and 64 consumer counts, 64 words apart, the
+// sticky error word; ops/gemm.py FLOW_WORDS keeps 1024 spare words), left zeroed by every launch
+// that completes.
+constexpr int kFlowWords = 128 * kFlowPad + 64 + 1024;
 
 // n-block height of the fused MLP's down tiles (ops/gemm.py down_kr must agree): 64 rows when
 // 128-row tiles at split S would be fewer than 192 workgroups
 static int down_kr(int N, int S) { return (N / 128) * S < 192 ? 1 : 2; }
 
-// res (may be null): the residual update of the previous projection's slabs as phase 0 --
-// gu.A must be res->residual and gu.nrm_parts res->parts (ResArgs, phase.h).
-PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, const ResArgs* res,
-                           hipStream_t stream) {
+PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* flow, hipStream_t stream) {
   GemmArgs gu = *gu_in, dn = *dn_in;
   if (gu.M <= 0) return 0;
-  if (res != nullptr && (res->residual == nullptr || res->parts == nullptr || res->flow == nullptr || res->M != gu.M ||
-                         res->H != gu.K || res->H % kResCols || (res->slabs != nullptr && res->S < 1) ||
-                         static_cast<const void*>(res->residual) != static_cast<const void*>(gu.A) ||
-                         res->parts != gu.nrm_parts || gu.nrm_nparts != res->H / kResCols || gu.lda != res->H))
-    return -1;
   // up to 128 rows (one row tile; MT = 8 above 64 rows, whose row scale reads <= 16 parts)
-  if (gu.M > 128 || (gu.M > 64 && gu.nrm_nparts > 16) || dn.M != gu.M || gu.N % 128 || gu.S < 1 || gu.K % (kKC * gu.S) || !gu.row_scale ||
-      gu.nrm_parts == nullptr || gu.nrm_nparts < 1 || gu.nrm_nparts > 64 || gu.out == nullptr || dn.K != gu.N / 2 ||
-      dn.N % 128 || dn.S < 1 || dn.S > 64 || dn.K % (kKC * dn.S) || (dn.K / dn.S) % 64 || dn.partial == nullptr ||
-      dn.A != gu.out || dn.lda % 8 || gu.lda % 8 || gu.row_offsets != nullptr || dn.row_offsets != nullptr ||
-      flow == nullptr || (gu.S > 1 && (gu.partial == nullptr || gu.N / 128 > kFlowWords - kFlowCounters)))
+  if (gu.M > 128 || (gu.M > 64 && gu.nrm_nparts > 16) || dn.M != gu.M || gu.N % 128 || gu.S != 1 || gu.K % kKC ||
+      !gu.row_scale || gu.nrm_parts == nullptr || gu.nrm_nparts < 1 || gu.nrm_nparts > 64 || gu.out == nullptr ||
+      dn.K != gu.N / 2 || dn.N % 128 || dn.S < 1 || dn.S > 64 || dn.K % (kKC * dn.S) || (dn.K / dn.S) % 64 ||
+      dn.partial == nullptr || dn.A != gu.out || dn.lda % 8 || gu.lda % 8 || gu.row_offsets != nullptr ||
+      dn.row_offsets != nullptr || flow == nullptr)
     return -1;
-  const bool split = gu.S > 1;
-  gu.counters = split ? flow + kFlowCounters : nullptr;
+  gu.counters = nullptr;
   gu.row_tiles = dn.row_tiles = 1;
   gu.tile_rows = dn.tile_rows = gu.M > 64 ? 128 : 64;
   gu.max_group_rows = dn.max_group_rows = 0;
@@ -590,19 +559,11 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
   const int dkr = down_kr(dn.N, dn.S);
   Flow fgu{flow, done, err, 0, 0, dn.K / dn.S, 1, 0, 0, fused_spin_limit()};
   Flow fdn{flow, done, err, (dn.K / dn.S) / 64, dn.N / (64 * dkr), dn.K / dn.S, 2, 0, 0, fused_spin_limit()};
-  const int n_gu = (gu.N / 128) * gu.S, n_dn = (dn.N / (64 * dkr)) * dn.S;
-  const ResArgs ra = res != nullptr ? *res : ResArgs{};
-  const int n_res = res != nullptr ? res_workgroups(ra) : 0;
-  const Flow fres = res != nullptr ? res_flow(ra, n_gu, err, fused_spin_limit()) : Flow{};
-  int nwg = n_gu > n_dn ? n_gu : n_dn;
-  if (n_res > nwg) return -1;  // every residual producer is also a GEMM workgroup (resident anyway)
-  const dim3 grid(nwg);
-  auto go = [&](auto sp, auto kr, auto rs) {
-    constexpr bool SP = decltype(sp)::value;
+  const int n_gu = gu.N / 128, n_dn = (dn.N / (64 * dkr)) * dn.S;
+  const dim3 grid(n_gu > n_dn ? n_gu : n_dn);
+  auto go = [&](auto kr) {
     constexpr int KR = decltype(kr)::value;
-    constexpr bool RS = decltype(rs)::value;
-#define PK_MLPF(MT) \
-  mlp_fused_kernel<MT, SP, KR, false, RS><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn, ra, fres, n_res)
+#define PK_MLPF(MT) mlp_fused_kernel<MT, KR><<<grid, 256, 0, stream>>>(gu, dn, fgu, fdn, n_gu, n_dn)
     switch ((gu.M + 15) / 16) {
       case 1: PK_MLPF(1); break;
       case 2: PK_MLPF(2); break;
@@ -612,18 +573,10 @@ PK_EXPORT int pk_mlp_fused(const GemmArgs* gu_in, const GemmArgs* dn_in, int* fl
     }
 #undef PK_MLPF
   };
-  using K1 = std::integral_constant<int, 1>;
-  using K2 = std::integral_constant<int, 2>;
-  auto go_r = [&](auto sp, auto kr) {
-    if (res != nullptr)
-      go(sp, kr, std::true_type{});
-    else
-      go(sp, kr, std::false_type{});
-  };
-  if (split)
-    dkr == 1 ? go_r(std::true_type{}, K1{}) : go_r(std::true_type{}, K2{});
+  if (dkr == 1)
+    go(std::integral_constant<int, 1>{});
   else
-    dkr == 1 ? go_r(std::false_type{}, K1{}) : go_r(std::false_type{}, K2{});
+    go(std::integral_constant<int, 2>{});
   return PK_CHECK_LAUNCH();
 }
 

@@ -59,15 +59,13 @@ namespace {
 //                of the new residual, consumed by the next GEMM's RMSNorm prologue;
 //   kQkvRope:    128-column n-block = one head: RoPE (neox) for q / k heads, q -> out, k -> K
 //                cache, v -> transposed V cache at the token's slot (slot < 0: not cached).
-//   kSiluSplit:  interleaved gate / up split over K (the fused MLP's gate_up when N / 128 tiles
-//                alone cannot fill the chip, e.g. 70B TP=8: 56 n-blocks): silu(gate) * up of the
-//                summed slabs -> h, stored write-through for the in-launch hand-off.
 //   kPush:       a row-parallel TP projection whose epilogue drives its collective: bf16(sum) of
 //                the n-block is stored straight into the input slot of the rank that owns its
 //                256-column chunk (remote stores over xGMI while the other tiles still stream),
 //                then that rank's push flag [n-block][this rank] is stamped with the call's
 //                epoch (custom_allreduce.hip reduce_residual_pushed_kernel consumes them).
-enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4, kSiluSplit = 5, kPush = 6 };
+// (5 was kSiluSplit, the split gate_up reduced in-launch: removed in round 6, measured slower)
+enum Mode { kBF16 = 0, kPartial = 1, kSiluMul = 2, kAddResNorm = 3, kQkvRope = 4, kPush = 6 };
 constexpr int kMaxRows = 1024;  // decode batch bound of the row-tiled modes
 constexpr int kPartCols = 512;  // columns per sum-of-squares part (residual_parts_kernel)
 
@@ -126,39 +124,7 @@ __device__ void epilogue(const GemmArgs& args, int nb) {
   constexpr int NCOL = 64 * KR;  // columns of an n-block
   const int nbase = nb * NCOL;
   constexpr int RB = (SS == 0 || SS >= 16) ? 1 : (SS == 8 ? 2 : 4);  // rows per thread per batch
-  if constexpr (MODE == kSiluSplit) {
-    // 128 slab columns = 4 waves x (16 gate | 16 up) -> 64 h columns; 16 threads per row, each
-    // 4 gate columns and their 4 up columns (16 further), the same arithmetic as kSiluMul's
-    // single-pass epilogue on the summed slabs
-    static_assert(KR == 2, "gate / up pairs need 32-row wave tiles");
-    const int q = tid & 15, wv = q >> 2, j = (q & 3) * 4;
-    const int gc = nbase + wv * 32 + j;
-    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc(args.out, static_cast<short>(0), 0x7ffffff0, 0x00020000);
-    for (int m0 = tid >> 4; m0 < M; m0 += 16 * RB) {
-      float4 g[RB], u[RB];
-#pragma unroll
-      for (int i = 0; i < RB; ++i) {
-        const int m = min(m0 + 16 * i, M - 1);
-        const float* src = args.partial + static_cast<int64_t>(m) * N + gc;
-        g[i] = slab_sum<SS, true>(src, slab, S, args.partial);
-        u[i] = slab_sum<SS, true>(src + 16, slab, S, args.partial);
-      }
-#pragma unroll
-      for (int i = 0; i < RB; ++i) {
-        const int m = m0 + 16 * i;
-        if (m >= M) break;
-        const float gv[4] = {g[i].x, g[i].y, g[i].z, g[i].w}, uv[4] = {u[i].x, u[i].y, u[i].z, u[i].w};
-        float y[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = rbf(silu(rbf(gv[e]))) * rbf(uv[e]);
-        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-        const bf16_t* o = args.out + static_cast<int64_t>(m) * args.ldo + nb * 64 + wv * 16 + j;
-        // handed off in-launch to the down tiles: write-through (sc1) stores
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack2(y[0], y[1]), pack2(y[2], y[3])}, orsrc,
-                                              static_cast<int>((o - args.out) * 2), 0, 16);
-      }
-    }
-  } else if constexpr (MODE == kAddResNorm) {
+  if constexpr (MODE == kAddResNorm) {
     // TPR threads per row (4 columns each), RPP rows per pass of the workgroup
     constexpr int TPR = NCOL / 4, RPP = 256 / TPR;
     const int c = nbase + (tid % TPR) * 4;
@@ -334,17 +300,11 @@ struct SkinnyLds {
 //   1  producer: output stores write-through (sc1), one ticket per finished n-block on `fl`
 //   2  consumer of per-K-slice tickets on `fl` (slice = this tile's split): weights requested first,
 //      A (the producers' output) read with sc1 loads after the wait
-//   4  consumer of ONE all-to-all hand-off on `fw` (slice 0: the in-launch residual update of
-//      phase.h res_phase): weights requested first, then the wait, then A (the residual stream)
-//      and the row-scale parts, both with sc1 loads
 template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2, int FL = 0>
 __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_in, const int by, const int gdx,
-                                            SkinnyLds<MT>& L, const Flow& fl, const Flow& fw = Flow{}) {
+                                            SkinnyLds<MT>& L, const Flow& fl) {
   constexpr bool kProd = (FL & 1) != 0;
-  constexpr bool kWaitSlice = (FL & 2) != 0;
-  constexpr bool kWaitRes = (FL & 4) != 0;
-  constexpr bool kWait = kWaitSlice || kWaitRes;
-  static_assert(!(kWaitSlice && kWaitRes), "one wait per tile");
+  constexpr bool kWait = (FL & 2) != 0;
   constexpr int kR = KR;
   constexpr int kKA = SkinnyLds<MT>::kKA;  // k per staged A tile
   constexpr int kPPR = kKA / 8;             // 16-byte pieces per A row
@@ -410,21 +370,14 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       const int rr = min(64 * h + (tid >> 2), M - 1);
 #pragma unroll
       for (int q = 0; q < kRsLoads; ++q) {
-        const float* p = args.nrm_parts + min(sub + 4 * q, np - 1) * args.M + row0 + rr;
-        // parts written in this launch (res_phase): sc1 loads after the hand-off wait
-        rs_p[h * kRsLoads + q] = kWaitRes ? ldf_sc1(args.nrm_parts, p) : *p;
+        rs_p[h * kRsLoads + q] = args.nrm_parts[min(sub + 4 * q, np - 1) * args.M + row0 + rr];
       }
     }
   };
-  if constexpr (RS && !kWaitRes) load_rs();
-  // the consumer's wait (after its first weight k-steps are requested); the residual hand-off
-  // also makes the row-scale parts readable
+  if constexpr (RS) load_rs();
+  // the consumer's wait (after its first weight k-steps are requested)
   auto wait_in = [&](int split_) {
-    if constexpr (kWaitSlice) flow_wait(fl, split_);
-    if constexpr (kWaitRes) {
-      flow_wait(fw, 0);
-      if constexpr (RS) load_rs();
-    }
+    if constexpr (kWait) flow_wait(fl, split_);
   };
 
   const bf16_t* wp[kR];
@@ -588,44 +541,14 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   }
 
   // C^T tile: rows = W rows (n), cols = m:  acc[t][mt][i] = C[m = 16*mt + r][n = n0 + 16*t + 4*g + i]
-  if constexpr (MODE == kSiluMul && kR == 1) {
-    // 64-row n-blocks: wave w holds the 16 gate (w even) or up (w odd) rows of the same 16 h
-    // columns as its partner w ^ 1 (interleave block 16); the up waves hand their (row-scaled)
-    // accumulators to the gate waves through the LDS the A tiles no longer need
-    static_assert(!kProd, "KR = 1 SiLU: no in-launch hand-off");
-    __syncthreads();  // every wave is done reading the A tiles
-    float* xch = reinterpret_cast<float*>(&a_lds[0][0][0]) + (w >> 1) * MT * 256 + lane * 4;
-    if constexpr (RS)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[0][mt] *= rinv_s[min(16 * mt + r, M - 1)];
-    if (w & 1) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<f32x4*>(xch + mt * 256) = acc[0][mt];
-    }
-    __syncthreads();
-    if ((w & 1) == 0) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int m = 16 * mt + r;
-        if (m >= M) continue;
-        const f32x4 u = *reinterpret_cast<const f32x4*>(xch + mt * 256);
-        float y[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) y[i] = rbf(silu(rbf(acc[0][mt][i]))) * rbf(u[i]);
-        uint2 v;
-        v.x = pack2(y[0], y[1]);
-        v.y = pack2(y[2], y[3]);
-        *reinterpret_cast<uint2*>(args.out + static_cast<int64_t>(row0 + m) * args.ldo + (n0 >> 1) + 4 * g) = v;
-      }
-    }
-    return;
-  }
-  constexpr bool kSlab =
-      MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit || MODE == kPush;
+  // (kSiluMul with 64-row n-blocks, KR = 1 -- the unsplit 70B TP=8 gate_up -- measured slower and
+  // was removed in round 6: profiles/r5_kr1.jsonl)
+  static_assert(MODE != kSiluMul || kR == 2, "SiLU: gate and up of the same columns in one wave");
+  constexpr bool kSlab = MODE == kPartial || MODE == kAddResNorm || MODE == kQkvRope || MODE == kPush;
   // the in-launch residual update hands its slabs over write-through (measured faster than plain
   // stores + release: tools/gemm_lab.hip o_res / down_res); the plain split-K slabs are read by
   // the next kernel and stay plain (write-through made those slower)
-  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kSiluSplit || MODE == kPush || (MODE == kPartial && kProd);
+  constexpr bool kSlabSc1 = MODE == kAddResNorm || MODE == kPush || (MODE == kPartial && kProd);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = 16 * mt + r;
@@ -678,7 +601,7 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   }
   if constexpr ((MODE == kSiluMul || MODE == kPartial) && kProd)  // output columns of n-block nb
     flow_signal(fl, flow_slice(fl, nb, MODE == kSiluMul ? 64 * kR / 2 : 64 * kR));
-  if constexpr (MODE == kAddResNorm || MODE == kQkvRope || MODE == kSiluSplit || MODE == kPush) {
+  if constexpr (MODE == kAddResNorm || MODE == kQkvRope || MODE == kPush) {
     // ---- in-launch split-K reduction by the last split of this n-block to arrive
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -708,8 +631,6 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       case 16: epilogue<MODE, 16, KR>(args, nb); break;
       default: epilogue<MODE, 0, KR>(args, nb); break;
     }
-    if constexpr (MODE == kSiluSplit && kProd)  // h columns of n-block nb are out: one ticket
-      flow_signal(fl, flow_slice(fl, nb, 64));
   }
 }
 

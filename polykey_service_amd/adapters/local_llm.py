@@ -65,9 +65,9 @@ class LLMTool:
             raise ToolError("INVALID_ARGUMENT", str(e))
         return sp
 
-    def _summary(self, text: str, n_prompt: int, toks: List[int], last, t0: float) -> dict:
+    def _summary(self, text: str, n_prompt: int, toks: List[int], last, t0: float, with_ids: bool = False) -> dict:
         m = (last.metrics or {}) if last is not None else {}
-        return {
+        out = {
             "model": self.model_name,
             "text": text,
             "finish_reason": last.finish_reason if last is not None else "abort",
@@ -75,6 +75,9 @@ class LLMTool:
                       "total_tokens": n_prompt + len(toks)},
             "metrics": {k: v for k, v in {**m, "server_e2e_s": time.monotonic() - t0}.items() if v is not None},
         }
+        if with_ids:  # parameters.return_token_ids: the generated ids themselves (token-level clients, tests)
+            out["token_ids"] = list(toks)
+        return out
 
     @staticmethod
     def _stop_hit(text: str, stops) -> Optional[int]:
@@ -146,7 +149,7 @@ class LLMTool:
             text = self.tok.decode(toks)
         resp = proto.ExecuteToolResponse(status=_status())
         if params.get("return") == "struct":
-            resp.struct_output.update(self._summary(text, len(prompt), toks, last, t0))
+            resp.struct_output.update(self._summary(text, len(prompt), toks, last, t0, bool(params.get("return_token_ids"))))
         else:
             resp.string_output = text
         return resp
@@ -185,7 +188,7 @@ class LLMTool:
             await agen.aclose()
         text = detok.text
         final = proto.ExecuteToolResponse(status=_status())
-        final.struct_output.update(self._summary(text, len(prompt), toks, last, t0))
+        final.struct_output.update(self._summary(text, len(prompt), toks, last, t0, bool(params.get("return_token_ids"))))
         yield final
 
 

@@ -130,10 +130,6 @@ class ModelRunner:
         a0 = model.layers[0].attn
         self.part_o, self.part_ml = attn_ops.decode_workspace(cfg.max_num_seqs, a0.nq, self.max_blocks, self.bs, device,
                                                               kv_heads=a0.nkv)
-        # decode attention partitions merged in-launch by the last one to arrive (no reduce launch)
-        self.decode_counters = (torch.zeros((cfg.max_num_seqs, a0.nkv), dtype=torch.int32, device=device)
-                                if attn_ops.INLAUNCH_MERGE and self.part_o is not None and device.type == "cuda"
-                                else None)
         self.stats = {"steps": 0, "graph_steps": 0, "short_graph_steps": 0, "tokens": 0}
         self.keep_logits = False  # tests: keep the last eager step's logits
         self.last_logits = None
@@ -248,7 +244,6 @@ class ModelRunner:
             decode_block_tables=d["block_tables"][:nd] if nd else None,
             decode_context_lens=d["context_lens"][:nd] if nd else None,
             decode_part_o=self.part_o, decode_part_ml=self.part_ml,
-            decode_counters=self.decode_counters,
             decode_max_ctx=self.short_ctx if short else 0)
         if npf:
             md.prefill_block_tables = d["block_tables"][nd:n]

@@ -463,57 +463,19 @@ class LlamaForCausalLM(nn.Module):
         if self.st.tp_size > 1:
             parts = gemm.residual_parts(None, residual, buf)
             return self._forward_rowscale_tp(residual, parts, positions, md, kv_caches, ws, buf, buf2)
-        # every residual update (+ norm parts) is phase 0 of the fused launch that consumes it
-        # when that launch is taken (RES_PHASE: the 2 residual_parts launches per layer go)
         pending = None  # the previous layer's down slabs, not yet added to the residual
         for i, layer in enumerate(self.layers):
-            oph = self._o_phase(layer, residual, md)
-            if self._res_phase_attn(layer, residual, md):
-                a = self._decode_attn(layer, residual, None, positions, md, kv_caches[i], ws,
-                                      res=gemm.ResIn(pending, residual, buf, self._flow_res), o=oph)
-            else:
-                parts = gemm.residual_parts(pending, residual, buf)
-                a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws, o=oph)
+            parts = gemm.residual_parts(pending, residual, buf)
+            a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws)
             # o-projection slabs from 64-row n-blocks at half the split (-0.7..1.5 % decode step,
             # profiles/r2_decode_ab.txt: fewer fp32 slab bytes written and re-read); the residual
-            # update by the last split of each n-block inside the O launch measured 1 % slower
-            # (profiles/r4_o_inlaunch_ab.jsonl).  With the o phase the fused launch returned them.
-            o = a if isinstance(a, gemm.Partial) else gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p,
-                                                                          half=True)
-            if self._res_phase_mlp(layer, residual):
-                pending = self._decode_mlp(layer, residual, None, ws,
-                                           res=gemm.ResIn(o, residual, buf2, self._flow_res))
-            else:
-                parts = gemm.residual_parts(o, residual, buf2)
-                pending = self._decode_mlp(layer, residual, parts, ws)
+            # update inside the O launch (1 % slower, profiles/r4_o_inlaunch_ab.jsonl) and as phase 0
+            # of the fused launches (3 % slower, profiles/r5_phase_ab.jsonl) were removed in round 6
+            o = gemm.linear_partial(a, layer.attn.o, ws, packed=layer.attn.o_p, half=True)
+            parts = gemm.residual_parts(o, residual, buf2)
+            pending = self._decode_mlp(layer, residual, parts, ws)
         x, _ = gemm.partial_add_rms_norm(pending, residual, self.norm, self.cfg.rms_eps)
         return x
-
-    def _o_phase(self, layer, residual: torch.Tensor, md) -> Optional[gemm.OProj]:
-        """The o-projection as phase 3 of the fused QKV -> attention launch (gemm.O_PHASE): its slab
-        buffer, hand-off buffer and partition-merge counters -- used only if _decode_attn takes that
-        launch (it then returns the o slabs, a gemm.Partial)."""
-        T = residual.shape[0]
-        at = layer.attn
-        if not (gemm.O_PHASE and at.o_p is not None and md.num_prefill == 0 and T <= gemm.FUSED_MAX_M
-                and gemm.o_phase_ok(at.o.shape[0], at.nq, at.nkv, T) and getattr(self, "_ws_o", None) is not None):
-            return None
-        return gemm.OProj(at.o_p, self._ws_o, self._flow_o, self._attn_counters)
-
-    def _res_phase_attn(self, layer, residual: torch.Tensor, md) -> bool:
-        """The fused QKV -> attention launch is taken AND can run the residual update as its phase 0."""
-        T, H = residual.shape
-        at = layer.attn
-        return (gemm.RES_PHASE and self.st.tp_size == 1 and self._qkv_attn_fused_ok(at, T, H // gemm.PART_COLS, md)
-                and gemm.res_workgroups(T, H) <= max((at.qkv.shape[0] // 128) * gemm.choose_split(
-                    at.qkv.shape[0], H, T), T * at.nkv))
-
-    def _res_phase_mlp(self, layer, residual: torch.Tensor) -> bool:
-        T, H = residual.shape
-        mlp = layer.mlp
-        return (gemm.RES_PHASE and self.st.tp_size == 1 and not self.st.shared_device
-                and gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, H // gemm.PART_COLS)
-                and gemm.res_workgroups(T, H) <= gemm.mlp_fused_grid(residual, mlp.gate_up_pf, mlp.down_p))
 
     def _qkv_attn_fused_ok(self, at, T: int, nparts: int, md) -> bool:
         # (a TP rank sharing its GPU keeps the two launches: a hand-off lost to a co-tenant has a
@@ -522,46 +484,35 @@ class LlamaForCausalLM(nn.Module):
                 and gemm.fused_rows_ok(T, nparts) and md.num_decode == T
                 and not (self.st.shared_device and self.st.tp_size > 1))
 
-    def _decode_attn(self, layer, residual: torch.Tensor, parts: Optional[torch.Tensor], positions: torch.Tensor,
-                     md: attn_ops.AttnMetadata, kv: Tuple[torch.Tensor, torch.Tensor], ws: torch.Tensor,
-                     res: Optional[gemm.ResIn] = None, o: Optional[gemm.OProj] = None):
-        """Folded-norm QKV projection + RoPE + KV write + attention of one layer -> [T, nq * 128]
-        (``res``: the fused launch's phase 0 updates the residual and makes the norm parts; ``o``:
-        its phase 3 is the o-projection, whose slabs (a :class:`gemm.Partial`) are returned)."""
+    def _decode_attn(self, layer, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
+                     md: attn_ops.AttnMetadata, kv: Tuple[torch.Tensor, torch.Tensor], ws: torch.Tensor):
+        """Folded-norm QKV projection + RoPE + KV write + attention of one layer -> [T, nq * 128]."""
         at = layer.attn
         kc, vc = kv
         T = residual.shape[0]
-        if res is not None:
-            return gemm.qkv_attn_fused(residual, at.qkv_pf, None, ws, positions, self.cos_sin, kc, vc, md, at.scale,
-                                       at.nq, at.nkv, self._flow_qkv, res=res, eps=layer.eps, o=o)
         rs = gemm.RowScale(parts, layer.eps)
         if self._qkv_attn_fused_ok(at, T, parts.shape[0], md):
             # QKV slabs handed to the decode attention in-launch (one launch, csrc/kernels/decode_fused.hip);
             # deadlock-free on a shared GPU too: the QKV tiles never wait and dispatch first
             return gemm.qkv_attn_fused(residual, at.qkv_pf, rs, ws, positions, self.cos_sin, kc, vc, md, at.scale,
-                                       at.nq, at.nkv, self._flow_qkv, o=o)
+                                       at.nq, at.nkv, self._flow_qkv)
         # (64-row n-blocks at half the split: half the slabs the attention prologue sums -- the 70B
         # TP=8 shard's 10 n-blocks otherwise take split 16; one 64-row tile only: the row-tiled wide
         # batches keep 128-row n-blocks, 8B at 256 rows 34.5 vs 26 us, profiles/r5_wide_256_kgrid.md)
-        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, S=gemm.QKV_SPLIT or None, packed=at.qkv_pf,
+        p = gemm.linear_partial_rowscale(residual, at.qkv, ws, rs, packed=at.qkv_pf,
                                          half=gemm.QKV_HALF and T <= gemm.SKINNY_MAX_M)
         if md.num_prefill == 0:
             return attn_ops.paged_decode_from_qkv(p, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
         q = gemm.qkv_reduce_rope_cache(p, positions, self.cos_sin, kc, vc, md.slot_mapping, at.nq, at.nkv)
         return attn_ops.paged_attention(q, kc, vc, md, at.scale)
 
-    def _decode_mlp(self, layer, residual: torch.Tensor, parts: Optional[torch.Tensor], ws: torch.Tensor,
-                    res: Optional[gemm.ResIn] = None) -> gemm.Partial:
-        """Folded-norm gate_up + SiLU and the down projection of one layer -> down's split-K slabs
-        (``res``: the fused launch's phase 0 updates the residual and makes the norm parts)."""
+    def _decode_mlp(self, layer, residual: torch.Tensor, parts: torch.Tensor, ws: torch.Tensor) -> gemm.Partial:
+        """Folded-norm gate_up + SiLU and the down projection of one layer -> down's split-K slabs."""
         mlp = layer.mlp
-        if res is not None:
-            return gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, None, ws, self._flow, ws_gu=self._ws_gu,
-                                  res=res, eps=layer.eps)
         rs = gemm.RowScale(parts, layer.eps)
         if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, parts.shape[0]) and not self.st.shared_device:
             # gate_up + SiLU and the down slabs in one launch (down's launch ramp hidden)
-            return gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, rs, ws, self._flow, ws_gu=self._ws_gu)
+            return gemm.mlp_fused(residual, mlp.gate_up_pf, mlp.down_p, rs, ws, self._flow)
         h = self._decode_gate_up(layer, residual, parts)
         return gemm.linear_down(h, mlp.down, ws, mlp.down_p)  # tiled as the fused launch tiles it
 
@@ -576,8 +527,7 @@ class LlamaForCausalLM(nn.Module):
             x = gemm.norm_apply(residual, parts, layer.ln2, layer.eps)
             return gemm.silu_and_mul_interleaved(F.linear(x, mlp.gate_up))
         # split over K like the fused launch's gate_up when its n-blocks cannot fill the chip
-        return gemm.linear_silu(residual, mlp.gate_up, ws=self._ws_gu, packed=mlp.gate_up_pf, rowscale=rs,
-                                counters=self._gu_counters)
+        return gemm.linear_silu(residual, mlp.gate_up, ws=self._ws_gu, packed=mlp.gate_up_pf, rowscale=rs)
 
     def _forward_rowscale_tp(self, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
                              md: attn_ops.AttnMetadata, kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
@@ -593,17 +543,15 @@ class LlamaForCausalLM(nn.Module):
                     over K: 56 n-blocks at 70B TP=8) handed in-launch to the down slabs
                   -> fused collective
 
-        five launches per layer; each row-parallel projection costs its GEMM and ONE collective
-        launch (2 x 80 all-reduces per 70B TP=8 step)."""
+        Each row-parallel projection costs its GEMM and ONE collective launch (2 x 80
+        all-reduces per 70B TP=8 step).  Launches per layer: 6 with the fused QKV -> attention and MLP
+        launches (8B-like shards: >= 4 kv heads per rank), 8 at the 70B TP=8 shard (one kv head: QKV |
+        attention; gate_up split over K: gate_up | SiLU reduce | down), profiles/r5_decode_attention.md."""
         car = self.st.custom_ar
         for i, layer in enumerate(self.layers):
             at, mlp = layer.attn, layer.mlp
-            oph = None if at.fault_drop else self._o_phase(layer, residual, md)
-            a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws, o=oph)
-            if isinstance(a, gemm.Partial):
-                parts = car.reduce_residual(a, residual, buf2)
-            else:
-                parts = self._tp_row_collective(at.drop(a), at.o, at.o_p, ws, residual, buf2)
+            a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws)
+            parts = self._tp_row_collective(at.drop(a), at.o, at.o_p, ws, residual, buf2)
             if gemm.mlp_fused_ok(residual, mlp.gate_up_pf, mlp.down_p, parts.shape[0]) and not self.st.shared_device:
                 parts = car.reduce_residual(self._decode_mlp(layer, residual, parts, ws), residual, buf)
             else:
@@ -661,12 +609,17 @@ class LlamaForCausalLM(nn.Module):
         main.wait_stream(cs)
         return buf.view(-1)[: car.nparts(M, N) * M].view(-1, M)
 
+    # the chunked TP decode chain regardless of _overlap_streams_ok (tests: 8 ranks on one GPU)
+    force_overlap_streams = False
+
     def _overlap_streams_ok(self) -> bool:
-        """The overlapped TP chain forks a comm stream inside the captured decode graph.  Ranks
-        sharing one GPU (rehearsals) gain nothing from it, and under a single hardware queue per
-        process (GPU_MAX_HW_QUEUES=1, the rehearsals' setting) replaying such a graph crashed the
-        HIP runtime (profiles/r5_tp_overlap.md); POLYKEY_TP_OVERLAP_FORCE=1 lifts the check."""
-        if os.environ.get("POLYKEY_TP_OVERLAP_FORCE") == "1":
+        """The overlapped TP chain forks a comm stream inside the captured decode graph.  It can only
+        pay where the two streams really run concurrently: one rank per GPU and at least two hardware
+        queues per process.  (The round-5 crash in ``graph.replay`` under one hardware queue,
+        profiles/r5_tp_overlap.md §1, belonged to the removed design whose collective kernel spun
+        on flags of a GEMM queued behind it; the chunked design never waits in-kernel on a producer,
+        so one queue only serialises it -- gated off because it then only adds launches.)"""
+        if self.force_overlap_streams:
             return True
         return not self.st.shared_device and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 2
 
@@ -680,24 +633,9 @@ class LlamaForCausalLM(nn.Module):
             self._flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
             gemm.fused_err_word()  # before the first fused launch (engine polls gemm.check_fused)
             self._flow_qkv = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
-            # the residual phase's hand-off (gemm.ResIn: phase 0 of either fused launch)
-            self._flow_res = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
-            # the o-projection phase of the fused QKV -> attention launch (gemm.OProj): its own slab
-            # buffer, hand-off buffer and the attention's in-launch partition-merge counters
-            at = self.layers[0].attn
-            if at.o is not None and at.o.dim() == 2:
-                No, Ko = at.o.shape
-                n = max(gemm.o_phase_split(No, Ko, m) * m * No for m in range(1, gemm.FUSED_MAX_M + 1))
-                self._ws_o = torch.empty(n, dtype=torch.float32, device=self.device)
-                self._flow_o = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
-                self._attn_counters = torch.zeros((gemm.FUSED_MAX_M, at.nkv), dtype=torch.int32, device=self.device)
             # slabs of a gate_up split over K (gemm.gate_up_split > 1: the 70B TP=8 shard)
             n = self._gate_up_split_elems()
             self._ws_gu = torch.empty(n, dtype=torch.float32, device=self.device) if n else None
-            # arrival counters of that gate_up's in-launch split-K reduction (gemm.GATE_UP_INLAUNCH)
-            gu = self.layers[0].mlp.gate_up if hasattr(self.layers[0].mlp, "gate_up") else None
-            self._gu_counters = (torch.zeros(gu.shape[0] // 128, dtype=torch.int32, device=self.device)
-                                 if n and gu is not None else None)
             # split-K arrival counters of the push GEMMs (gemm.TP_PUSH: o / down, N = hidden)
             self._push_counters = (torch.zeros(self.cfg.hidden_size // 64, dtype=torch.int32, device=self.device)
                                    if self.st.tp_size > 1 else None)

@@ -32,7 +32,6 @@ class AttnMetadata:
     prefill_cu_q: Optional[torch.Tensor] = None          # [np+1] int32, relative to the first prefill token
     decode_part_o: Optional[torch.Tensor] = None         # split-K workspace
     decode_part_ml: Optional[torch.Tensor] = None
-    decode_counters: Optional[torch.Tensor] = None       # [n_seqs, n_kv] int32, zero-initialised
     decode_max_ctx: int = 0  # bound on every decode context of the step (0: block-table capacity)
 
     @property
@@ -41,26 +40,16 @@ class AttnMetadata:
 
 
 _PART = 512  # must match kDecodePart in csrc/kernels/attention.hip
-# decode: a sequence's partitions merged by its last partition workgroup (in-launch) instead of a
-# reduce launch after the attention (the engine passes AttnMetadata.decode_counters).  Measured
-# slower: 70B TP=8 per-rank step 7.21 vs 6.68 ms (the merge's release / acquire fences,
-# profiles/r5_tp_ab.jsonl) -- off by default
-INLAUNCH_MERGE = os.environ.get("POLYKEY_DECODE_INLAUNCH_MERGE", "0") == "1"
 _PART_MIN = 128  # kDecodePartSmall: launches whose (seq, kv head) pairs cannot fill the chip
 _FILL_SET = False
 
 
 def apply_decode_fill() -> None:
-    """A/B knobs of the decode attention launch, applied once per process:
-    POLYKEY_DECODE_FILL -- the workgroup count below which decode attention takes 128-key
-    partitions (csrc attention.hip decode_part; 0: always 512); POLYKEY_DECODE_WIDE=1 -- 8-wave
-    workgroups for launches of at most 128 workgroups."""
+    """POLYKEY_DECODE_FILL, applied once per process: the workgroup count below which decode
+    attention takes 128-key partitions (csrc attention.hip decode_part; 0: always 512)."""
     global _FILL_SET
-    if not _FILL_SET:
-        if os.environ.get("POLYKEY_DECODE_FILL") is not None:
-            native.call("pk_set_decode_fill", int(os.environ["POLYKEY_DECODE_FILL"]))
-        if os.environ.get("POLYKEY_DECODE_WIDE") is not None:
-            native.call("pk_set_decode_wide", int(os.environ["POLYKEY_DECODE_WIDE"]))
+    if not _FILL_SET and os.environ.get("POLYKEY_DECODE_FILL") is not None:
+        native.call("pk_set_decode_fill", int(os.environ["POLYKEY_DECODE_FILL"]))
     _FILL_SET = True
 
 
@@ -70,7 +59,7 @@ _DECODE_FILL = int(os.environ.get("POLYKEY_DECODE_FILL", "256"))
 
 def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, device, n_kv: int = 0,
                      kv_heads: Optional[int] = None) -> tuple:
-    """Partition slabs (+ arrival counters when ``n_kv``) for split-K decode attention.  A launch
+    """Partition slabs for split-K decode attention.  A launch
     strides the slabs by its OWN partition count, so they are sized for the largest launch:
     ``n_seqs`` sequences at 512-key partitions, or the few sequences that take 128-key ones
     (csrc attention.hip decode_part: fewer than 256 (seq, kv head) workgroups, i.e. at most
@@ -80,7 +69,7 @@ def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, de
     ctx = max_blocks * block_size
     n_small = (ctx + _PART_MIN - 1) // _PART_MIN
     if n_small <= 1:
-        return (None, None, None) if n_kv else (None, None)
+        return None, None
     kvh = kv_heads or n_kv
     if kvh:
         seqs_small = min(n_seqs, (_DECODE_FILL - 1) // kvh)
@@ -89,8 +78,6 @@ def decode_workspace(n_seqs: int, n_q: int, max_blocks: int, block_size: int, de
         rows = n_seqs * n_small
     o = torch.empty((rows * n_q, 128), dtype=torch.float32, device=device)
     ml = torch.empty((rows * n_q, 2), dtype=torch.float32, device=device)
-    if n_kv:
-        return o, ml, torch.zeros((n_seqs, n_kv), dtype=torch.int32, device=device)
     return o, ml
 
 
@@ -129,7 +116,7 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         native.call("pk_paged_decode", out.data_ptr(), q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                     bt.data_ptr(), md.decode_context_lens.data_ptr(),
                     native.ptr(md.decode_part_o) or 0, native.ptr(md.decode_part_ml) or 0,
-                    native.ptr(md.decode_counters) or 0, nd, nq, nkv, bs, bt.stride(0), q.stride(0), out.stride(0),
+                    nd, nq, nkv, bs, bt.stride(0), q.stride(0), out.stride(0),
                     float(scale), int(md.decode_max_ctx), stream)
     if md.num_prefill > 0:
         bt = md.prefill_block_tables
@@ -169,14 +156,6 @@ def paged_decode_from_qkv(p, positions: torch.Tensor, cos_sin: torch.Tensor, k_c
     T = p.M
     out = torch.empty((T, nq * 128), dtype=torch.bfloat16, device=p.buf.device)
     bt = md.decode_block_tables
-    if md.decode_counters is not None:  # partitions merged in-launch (no reduce kernel after)
-        native.call("pk_paged_decode_qkv2", out.data_ptr(), p.buf.data_ptr(), p.S, p.M, positions.data_ptr(),
-                    cos_sin.data_ptr(), md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
-                    bt.data_ptr(), md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,
-                    native.ptr(md.decode_part_ml) or 0, md.decode_counters.data_ptr(), md.num_decode, nq, nkv,
-                    k_cache.shape[2], bt.stride(0), out.stride(0), float(scale), int(md.decode_max_ctx),
-                    native.stream_ptr())
-        return out
     native.call("pk_paged_decode_qkv", out.data_ptr(), p.buf.data_ptr(), p.S, p.M, positions.data_ptr(),
                 cos_sin.data_ptr(), md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                 bt.data_ptr(), md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,

@@ -32,52 +32,40 @@ FUSED_MAX_M = 128
 FUSED_MT8_MAX_PARTS = 16
 SKINNY_TILE_M = 128  # rows per row tile above 64 (the kernel's MT = 8 variant)
 # measured best (tools/bench_gemm.py, cold weights): ~0.75-1 workgroup per CU
-_TARGET_WGS = int(os.environ.get("POLYKEY_SKINNY_TARGET", "192"))  # (A/B knob)
+_TARGET_WGS = 192
 _ROWS_PER_WG = 128
 _KCHUNK = 256
 # The hand-written decode GEMM is used when it beats hipBLASLt on the shape (see
 # tools/bench_gemm.py and profiles/); POLYKEY_SKINNY_GEMM=0/1 forces it off/on.
 SKINNY_ENABLED = os.environ.get("POLYKEY_SKINNY_GEMM", "1") == "1"
-# decode MLP as one launch (gate_up -> down hand-off in-kernel, mlp_fused); 0: two launches
+# decode MLP as one launch (gate_up -> down hand-off in-kernel, mlp_fused); 0: two launches.  Not
+# when its gate_up must be split over K (the 70B TP=8 shard's 56 n-blocks): measured 1.4 us / layer
+# slower than the two launches there (profiles/r4_tp_solo.md; that variant was removed in round 6)
 MLP_FUSED = os.environ.get("POLYKEY_MLP_FUSED", "1") == "1"
-# ... also when its gate_up must be split over K (kSiluSplit: the 70B TP=8 shard's 56 n-blocks):
-# measured 1.4 us / layer slower than the two launches there (profiles/r4_tp_solo.md), so off
-MLP_FUSED_SPLIT = os.environ.get("POLYKEY_MLP_FUSED_SPLIT", "0") == "1"
 # the QKV -> attention launch wins where each kv head's attention tiles wait on a slice of the QKV
 # tiles (8B: 8 kv heads); with one or two kv heads per rank (70B TP=8 / TP=4) every attention tile
 # waits for the whole projection and the launch measured slower (26.6 vs ~20 us per layer at
 # 70B TP=8, profiles/r4_tp_solo.md)
-QKV_ATTN_MIN_KV = int(os.environ.get("POLYKEY_QKV_MIN_KV", "4"))
+QKV_ATTN_MIN_KV = 4
 # the two-launch decode QKV (TP shards with few kv heads) as 64-row n-blocks at half the split:
 # half the fp32 slabs the attention prologue sums (70B TP=8: 6.66-6.67 vs 6.68 ms, neutral)
-QKV_HALF = os.environ.get("POLYKEY_QKV_HALF", "1") == "1"
-QKV_SPLIT = int(os.environ.get("POLYKEY_QKV_SPLIT", "0"))  # A/B: the decode QKV's K split (0: choose_split)
+QKV_HALF = True
 # bf16-out decode GEMMs whose 128-row n-blocks cannot fill the chip run as 64-row n-blocks (the 70B
-# TP=8 LM-head shard: 126 -> 252 workgroups; per-rank step 6.52 vs 6.54 ms, profiles/r5_lmhalf.jsonl)
-LINEAR_HALF = os.environ.get("POLYKEY_LINEAR_HALF", "1") == "1"
-# A/B: the half-split (64-row n-block) decode projections (the o-projection) at this multiple of
-# their split -- more, smaller workgroups, more slab bytes (x2: 8B 4.04-4.05 vs 3.98-3.99 ms, 70B
-# TP=8 6.54 vs 6.50, profiles/r5_osplit.jsonl)
-HALF_SPLIT_MUL = int(os.environ.get("POLYKEY_HALF_SPLIT_MUL", "1"))
+# TP=8 LM-head shard: 126 -> 252 workgroups; per-rank step 6.52 vs 6.54 ms, profiles/r5_lmhalf.jsonl).
+# Measured and removed in round 6: the half-split projections at 2x their split (profiles/r5_osplit.jsonl),
+# explicit QKV splits (r5_split_ab.jsonl)
 PACKED_BIT = 16
 
 
-MODE_BF16, MODE_PARTIAL, MODE_SILU, MODE_ADD_RES_NORM, MODE_QKV_ROPE, MODE_SILU_SPLIT, MODE_PUSH = 0, 1, 2, 3, 4, 5, 6
+MODE_BF16, MODE_PARTIAL, MODE_SILU, MODE_ADD_RES_NORM, MODE_QKV_ROPE, MODE_PUSH = 0, 1, 2, 3, 4, 6
 # TP decode: the row-parallel projections' GEMM epilogue pushes its finished tiles into the owner
 # ranks' IPC slots (MODE_PUSH, :func:`push_projection`) and the collective starts at the
 # reduce-scatter (custom_ar.reduce_residual_pushed).  Bit-identical to GEMM + fused collective; off
-# by default until an 8-GPU run has timed it (one GPU cannot show the xGMI traffic it hides)
+# by default until an 8-GPU run has timed it (one GPU cannot show the xGMI traffic it hides).
+# (Removed in round 6, measured slower in rounds 4-5: the split gate_up reduced + SiLU'd in-launch,
+# 6.78 vs 6.68 ms per 70B TP=8 rank step, r5_tp_ab.jsonl; the unsplit 64-row gate_up, 7.75 vs
+# 6.51 ms, r5_kr1.jsonl.)
 TP_PUSH = os.environ.get("POLYKEY_TP_PUSH", "0") == "1"
-# a decode gate_up split over K (70B TP=8: 56 n-blocks) reduced + SiLU'd in-launch by the last split
-# of each n-block (MODE_SILU_SPLIT) instead of by a splitk_reduce launch after it.  Measured slower
-# (70B TP=8 per-rank step 6.78 vs 6.68 ms, profiles/r5_tp_ab.jsonl): off by default
-GATE_UP_INLAUNCH = os.environ.get("POLYKEY_GATE_UP_INLAUNCH", "0") == "1"
-# a folded-norm gate_up whose 128-row n-blocks cannot fill the chip (70B TP=8: 56) as 64-row
-# n-blocks WITHOUT a K split (112 workgroups, SiLU in the epilogue: no slabs, no reduce launch)
-# instead of split over K + the SiLU reduce launch.  Measured slower: 45 us vs 26 + 5 us per layer,
-# per-rank step 7.75 vs 6.51-6.54 ms (profiles/r5_kr1.jsonl: 112 workgroups cannot stream the 117 MB
-# shard) -- off by default
-GATE_UP_KR1 = os.environ.get("POLYKEY_GATE_UP_KR1", "0") == "1"
 NORM_BIT = 32
 
 
@@ -99,37 +87,6 @@ class GemmArgs(ctypes.Structure):
 
 
 _ARGS_CHECKED = False
-
-
-class ResArgs(ctypes.Structure):
-    """Mirror of ``struct ResArgs`` in csrc/kernels/phase.h: the in-launch residual phase."""
-    _fields_ = [("residual", ctypes.c_void_p), ("slabs", ctypes.c_void_p), ("parts", ctypes.c_void_p),
-                ("S", ctypes.c_int), ("M", ctypes.c_int), ("H", ctypes.c_int), ("flow", ctypes.c_void_p)]
-
-
-class ResIn(NamedTuple):
-    """Phase 0 of a fused decode launch (TP = 1): ``residual`` += sum of ``pending``'s slabs (None:
-    unchanged) and ``parts`` [H / 512, M] = the new rows' sums of squares -- the work of
-    :func:`residual_parts`, done inside the launch whose first GEMM consumes both (its tiles wait on
-    ``flow``, an int32 hand-off buffer of its own: >= :data:`FLOW_WORDS`, zeroed once, left zeroed)."""
-    pending: Optional["Partial"]
-    residual: torch.Tensor
-    parts: torch.Tensor
-    flow: torch.Tensor
-
-    def args(self) -> "ResArgs":
-        M, H = self.residual.shape
-        assert self.residual.is_contiguous() and H % PART_COLS == 0 and self.parts.numel() >= (H // PART_COLS) * M
-        assert self.flow.numel() >= FLOW_WORDS and self.flow.dtype == torch.int32
-        p = self.pending
-        if p is not None:
-            assert p.M == M and p.N == H
-        return ResArgs(self.residual.data_ptr(), 0 if p is None else p.buf.data_ptr(), self.parts.data_ptr(),
-                       0 if p is None else p.S, M, H, self.flow.data_ptr())
-
-    def parts_view(self) -> torch.Tensor:
-        M, H = self.residual.shape
-        return self.parts.view(-1)[: (H // PART_COLS) * M].view(H // PART_COLS, M)
 
 
 class RowScale(NamedTuple):
@@ -332,7 +289,7 @@ def unpack_weight(wp: torch.Tensor) -> torch.Tensor:
 
 
 # weights at least this large are streamed with non-temporal loads (gate_up, MoE w13, LM head)
-NT_MIN_BYTES = int(os.environ.get("POLYKEY_NT_MIN_MB", "160")) << 20
+NT_MIN_BYTES = 160 << 20
 NT_BIT = 64
 
 
@@ -362,7 +319,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
         out = torch.empty((M, N), dtype=x.dtype, device=x.device)
     src = packed if packed is not None else w
     # too few 128-row n-blocks for the chip (the 70B TP=8 LM-head shard: 126): 64-row n-blocks
-    half = LINEAR_HALF and packed is not None and M <= SKINNY_MAX_M and N // _ROWS_PER_WG < _TARGET_WGS
+    half = packed is not None and M <= SKINNY_MAX_M and N // _ROWS_PER_WG < _TARGET_WGS
     native.call("pk_skinny_gemm", out.data_ptr(), 0, x.data_ptr(), src.data_ptr(), M, N, K, x.stride(0),
                 out.stride(0), 1, 0 | _wmode(packed) | (HALF_BIT if half else 0), native.stream_ptr())
     return out
@@ -383,11 +340,7 @@ def partial_tiling(N: int, K: int, M: int, packed: Optional[torch.Tensor], half:
     and :func:`push_projection`, whose slabs must be bit-identical."""
     half = half and packed is not None and packed.numel() * packed.element_size() < NT_MIN_BYTES
     S = choose_split(N, K, M)
-    if half:
-        S = max(1, S // 2)
-        if HALF_SPLIT_MUL > 1 and M <= SKINNY_MAX_M and K % (_KCHUNK * S * HALF_SPLIT_MUL) == 0:
-            S *= HALF_SPLIT_MUL
-    return S, half
+    return (max(1, S // 2) if half else S), half
 
 
 def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Optional[int] = None,
@@ -407,8 +360,7 @@ def linear_partial(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, S: Option
 
 def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[torch.Tensor] = None,
                 packed: Optional[torch.Tensor] = None, norm: Optional[NormIn] = None,
-                rowscale: Optional[RowScale] = None, max_m: int = SKINNY_MAX_M,
-                counters: Optional[torch.Tensor] = None) -> torch.Tensor:
+                rowscale: Optional[RowScale] = None, max_m: int = SKINNY_MAX_M) -> torch.Tensor:
     """silu(x @ Wg^T) * (x @ Wu^T) with interleaved gate/up rows → [M, I].  With ``norm``,
     ``x`` is the residual stream and the RMSNorm is applied in the kernel's prologue (S = 1);
     with ``rowscale`` the norm is folded (W pre-multiplied, rows scaled in the epilogue)."""
@@ -417,19 +369,9 @@ def linear_silu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, ws: Optional[to
         N = w_gu_interleaved.shape[0]
         out = torch.empty((M, N // 2), dtype=x.dtype, device=x.device)
         Sg = gate_up_split(N, K, M) if rowscale is not None and M <= FUSED_MAX_M else 1
-        if Sg > 1 and GATE_UP_KR1 and packed is not None and M <= SKINNY_MAX_M:
-            _launch_ex(MODE_SILU | HALF_BIT, x, w_gu_interleaved, packed, 1, out=out, rowscale=rowscale)
-            return out
         if Sg > 1 and ws is not None and ws.numel() >= Sg * M * N:
-            if (GATE_UP_INLAUNCH and counters is not None and packed is not None and M <= SKINNY_MAX_M
-                    and counters.numel() >= N // 128):
-                # the last split of each n-block sums the slabs and applies SiLU in the same launch
-                # (the fused MLP's kSiluSplit epilogue; bit-identical to the reduce launch)
-                _launch_ex(MODE_SILU_SPLIT, x, w_gu_interleaved, packed, Sg, out=out, ws=ws, counters=counters,
-                           rowscale=rowscale)
-                return out
-            # split over K like the fused MLP's gate_up (bit-identical: the same slabs, summed in
-            # split order, the same SiLU arithmetic)
+            # split over K when its n-blocks cannot fill the chip (the 70B TP=8 shard), then one
+            # SiLU reduce launch over the slabs
             p = linear_partial_rowscale(x, w_gu_interleaved, ws, rowscale, S=Sg, packed=packed)
             native.call("pk_splitk_reduce", out.data_ptr(), p.buf.data_ptr(), Sg, M, N, out.stride(0), 1,
                         native.stream_ptr())
@@ -588,7 +530,7 @@ def push_projection(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, packed: 
         half = down_kr(N, K, M) == 1 and M <= FUSED_MAX_M
     else:
         # the unpushed chain's o projection is linear_partial(half=True): the same helper picks
-        # both tilings, so no threshold (POLYKEY_NT_MIN_MB) can make them differ
+        # both tilings, so they cannot drift apart
         S, half = partial_tiling(N, K, M, packed, True)
     S = split or S  # (tools/push_probe.py: other splits, not bit-identical to the serving chain)
     nbc = 64 if half else 128
@@ -622,122 +564,53 @@ def mlp_fused_ok(x: torch.Tensor, gate_up_packed: Optional[torch.Tensor], down_p
         return False
     N2, I = gate_up_packed.shape[0], down_packed.shape[1]
     S = choose_split(down_packed.shape[0], I, M)
-    Sg = gate_up_split(N2, K, M)
-    if Sg > 1 and not MLP_FUSED_SPLIT:
+    if gate_up_split(N2, K, M) > 1:
         return False
     # one workgroup per CU, each a gate_up tile then a down tile: above 256 tiles (70B on one GPU:
     # 448 gate_up tiles) the fused launch measured 8 % slower end to end (profiles/r2_decode_ab.txt)
-    return (N2 == 2 * I and N2 % 128 == 0 and K % (_KCHUNK * Sg) == 0
+    return (N2 == 2 * I and N2 % 128 == 0 and K % _KCHUNK == 0
             and down_packed.shape[0] % 128 == 0 and I % (_KCHUNK * S) == 0 and (I // S) % 64 == 0 and S <= 64
-            and gate_up_packed.shape[1] == K and (N2 // 128) * Sg <= device_cus(x.device)
+            and gate_up_packed.shape[1] == K and N2 // 128 <= device_cus(x.device)
             and (down_packed.shape[0] // (64 * down_kr(down_packed.shape[0], I, M))) * S <= device_cus(x.device))
 
 
-# TP = 1 decode: every residual update runs as phase 0 of the fused launch that consumes it
-# (ResIn, csrc/kernels/phase.h) instead of a residual_parts launch of its own.  Measured SLOWER
-# (8B step 4.12-4.16 vs 4.00-4.02 ms, profiles/r5_phase_ab.jsonl): off by default
-RES_PHASE = os.environ.get("POLYKEY_RES_PHASE", "0") == "1"
-# decode: the o-projection as phase 3 of the fused QKV -> attention launch (OProj).  Measured
-# slower too (+0.4 % on top of the residual phase; 70B TP=8 with the fused launch 7.86 vs 6.70 ms)
-O_PHASE = os.environ.get("POLYKEY_O_PHASE", "0") == "1"
-
-
-def res_workgroups(M: int, H: int) -> int:
-    """Producer workgroups of the residual phase (phase.h res_workgroups: one wave per (row, part))."""
-    return (M * (H // PART_COLS) + 3) // 4
-
-
-def mlp_fused_grid(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor) -> int:
-    """Workgroups of a :func:`mlp_fused` launch (pk_mlp_fused: max of its gate_up and down tiles)."""
-    M, K = x.shape
-    N2, I = gate_up_packed.shape[0], down_packed.shape[1]
-    N = down_packed.shape[0]
-    S = choose_split(N, I, M)
-    return max((N2 // 128) * gate_up_split(N2, K, M), (N // (64 * down_kr(N, I, M))) * S)
-
-
-def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: Optional[RowScale],
-              ws: torch.Tensor, flow: torch.Tensor, ws_gu: Optional[torch.Tensor] = None,
-              res: Optional[ResIn] = None, eps: float = 1e-5) -> Partial:
+def mlp_fused(x: torch.Tensor, gate_up_packed: torch.Tensor, down_packed: torch.Tensor, rowscale: RowScale,
+              ws: torch.Tensor, flow: torch.Tensor) -> Partial:
     """Decode MLP in ONE launch (csrc/kernels/gemm_skinny.hip mlp_fused_kernel):
     h = silu/mul of rinv * (x @ Wgu'^T) (folded norm, interleaved packed gate/up), then the down
     projection's fp32 split-K slabs of h @ Wd^T in ``ws``.  Down workgroups stream their first
     weight k-steps while gate_up finishes and wait on per-K-slice tickets in ``flow`` (int32,
-    >= :data:`FLOW_WORDS`, zeroed once; every launch leaves it zeroed).  When gate_up is split
-    over K (:func:`gate_up_split` > 1) its slabs go to ``ws_gu`` and the last split of each
-    n-block applies SiLU.  ``res`` (TP = 1): phase 0 of the launch is the residual update of the
-    o-projection's slabs (:class:`ResIn`; ``x`` must be ``res.residual``), whose parts are the row
-    scale (``rowscale`` None, ``eps`` its epsilon).  Returns the down slabs."""
-    if res is not None:
-        assert x is res.residual and rowscale is None
-        rowscale = RowScale(res.parts_view(), eps)
+    >= :data:`FLOW_WORDS`, zeroed once; every launch leaves it zeroed).  Returns the down slabs."""
     M, K = x.shape
     N2, I = gate_up_packed.shape[0], down_packed.shape[1]
     N = down_packed.shape[0]
     S = choose_split(N, I, M)
-    Sg = gate_up_split(N2, K, M)
     assert ws.numel() >= S * M * N and flow.numel() >= FLOW_WORDS and flow.dtype == torch.int32
-    assert Sg == 1 or (ws_gu is not None and ws_gu.numel() >= Sg * M * N2), "split gate_up needs its slab workspace"
+    assert gate_up_split(N2, K, M) == 1, "the fused MLP takes unsplit gate_up shapes (mlp_fused_ok)"
     h = torch.empty((M, I), dtype=x.dtype, device=x.device)
     gu = GemmArgs()
     gu.out, gu.A, gu.W = h.data_ptr(), x.data_ptr(), gate_up_packed.data_ptr()
-    gu.M, gu.N, gu.K, gu.lda, gu.ldo, gu.S = M, N2, K, x.stride(0), h.stride(0), Sg
-    gu.partial = ws_gu.data_ptr() if Sg > 1 else None
+    gu.M, gu.N, gu.K, gu.lda, gu.ldo, gu.S = M, N2, K, x.stride(0), h.stride(0), 1
     gu.row_scale, gu.nrm_parts, gu.nrm_nparts, gu.eps = 1, rowscale.parts.data_ptr(), rowscale.parts.shape[0], \
         float(rowscale.eps)
     dn = GemmArgs()
     dn.partial, dn.A, dn.W = ws.data_ptr(), h.data_ptr(), down_packed.data_ptr()
     dn.M, dn.N, dn.K, dn.lda, dn.ldo, dn.S = M, N, I, h.stride(0), N, S
-    ra = res.args() if res is not None else None
-    native.call("pk_mlp_fused", ctypes.byref(gu), ctypes.byref(dn), flow.data_ptr(),
-                ctypes.byref(ra) if ra is not None else None, native.stream_ptr())
+    native.call("pk_mlp_fused", ctypes.byref(gu), ctypes.byref(dn), flow.data_ptr(), native.stream_ptr())
     return Partial(ws, S, M, N)
 
 
 QKV_ATTN_FUSED = os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1") == "1"
 
 
-class OProj(NamedTuple):
-    """The o-projection as phase 3 of :func:`qkv_attn_fused`: split-K slabs of attn @ Wo^T
-    (``packed`` = :func:`pack_weight` (Wo), 64-row n-blocks at half the default split, as
-    :func:`linear_partial` ``half=True``) into ``ws`` -- a buffer of its own (the QKV slabs are still
-    being read when the first o tiles store); ``flow`` its hand-off buffer (>= :data:`FLOW_WORDS`,
-    zeroed once, left zeroed); ``counters`` [M, n_kv] int32 zeroed (the attention partitions are
-    merged in-launch)."""
-    packed: torch.Tensor
-    ws: torch.Tensor
-    flow: torch.Tensor
-    counters: torch.Tensor
-
-
-def o_phase_split(N: int, K: int, M: int) -> int:
-    """K split of the o-projection phase: :func:`linear_partial` ``half=True``'s."""
-    return max(1, choose_split(N, K, M) // 2)
-
-
-def o_phase_ok(N: int, nq: int, nkv: int, M: int) -> bool:
-    """The o-projection phase's K slices must be whole kv heads or whole fractions of one."""
-    S = o_phase_split(N, nq * 128, M)
-    G = nq // nkv
-    hps = nq // S if nq % S == 0 else 0
-    return hps > 0 and (hps % G == 0 if hps >= G else G % hps == 0) and S <= 64
-
-
-def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: Optional[RowScale], ws: torch.Tensor,
+def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: RowScale, ws: torch.Tensor,
                    positions: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, md,
-                   scale: float, nq: int, nkv: int, flow: torch.Tensor, S: Optional[int] = None,
-                   res: Optional[ResIn] = None, eps: float = 1e-5, o: Optional[OProj] = None):
+                   scale: float, nq: int, nkv: int, flow: torch.Tensor, S: Optional[int] = None) -> torch.Tensor:
     """Decode layer front half in ONE launch (csrc/kernels/decode_fused.hip): the folded-norm
     QKV projection's split-K slabs (``ws``), handed in-launch to the decode attention that
     reduces them, applies RoPE, writes the new k / v to the paged cache and attends.  Same
     result as :func:`linear_partial_rowscale` + ``attention.paged_decode_from_qkv``.  ``flow``:
-    int32 >= :data:`FLOW_WORDS`, zeroed once, left zeroed.  ``res`` (TP = 1): phase 0 is the residual
-    update of the previous layer's down slabs (:class:`ResIn`, ``x`` is ``res.residual``; its parts
-    are the row scale, ``eps`` its epsilon).  Returns [M, nq * 128] bf16, or with ``o``
-    (:class:`OProj`) the o-projection's slabs (:class:`Partial`) computed in the same launch."""
-    if res is not None:
-        assert x is res.residual and rowscale is None
-        rowscale = RowScale(res.parts_view(), eps)
+    int32 >= :data:`FLOW_WORDS`, zeroed once, left zeroed.  Returns [M, nq * 128] bf16."""
     M, K = x.shape
     N = qkv_packed.shape[0]
     S = S or choose_split(N, K, M)
@@ -752,25 +625,12 @@ def qkv_attn_fused(x: torch.Tensor, qkv_packed: torch.Tensor, rowscale: Optional
     a.row_scale, a.nrm_parts, a.nrm_nparts, a.eps = 1, rowscale.parts.data_ptr(), rowscale.parts.shape[0], \
         float(rowscale.eps)
     bt = md.decode_block_tables
-    ra = res.args() if res is not None else None
-    oa, op = None, None
-    if o is not None:
-        No = o.packed.shape[0]
-        So = o_phase_split(No, nq * 128, M)
-        assert o.packed.shape[1] == nq * 128 and o.ws.numel() >= So * M * No and o.ws.data_ptr() != ws.data_ptr()
-        assert o.flow.numel() >= FLOW_WORDS and o.counters.numel() >= M * nkv and o.counters.dtype == torch.int32
-        oa = GemmArgs()
-        oa.partial, oa.A, oa.W = o.ws.data_ptr(), out.data_ptr(), o.packed.data_ptr()
-        oa.M, oa.N, oa.K, oa.lda, oa.ldo, oa.S = M, No, nq * 128, out.stride(0), No, So
-        op = Partial(o.ws, So, M, No)
     native.call("pk_qkv_attn_fused", ctypes.byref(a), out.data_ptr(), positions.data_ptr(), cos_sin.data_ptr(),
                 md.slot_mapping.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), bt.data_ptr(),
                 md.decode_context_lens.data_ptr(), native.ptr(md.decode_part_o) or 0,
                 native.ptr(md.decode_part_ml) or 0, nq, nkv, k_cache.shape[2], bt.stride(0), out.stride(0),
-                float(scale), int(md.decode_max_ctx), flow.data_ptr(), ctypes.byref(ra) if ra is not None else None,
-                ctypes.byref(oa) if oa is not None else None, o.flow.data_ptr() if o is not None else None,
-                o.counters.data_ptr() if o is not None else native.ptr(md.decode_counters), native.stream_ptr())
-    return op if op is not None else out
+                float(scale), int(md.decode_max_ctx), flow.data_ptr(), native.stream_ptr())
+    return out
 
 
 def fold_norm(w: torch.Tensor, norm_weight: torch.Tensor) -> torch.Tensor:

@@ -35,11 +35,9 @@ SIGNATURES = {
     "pk_fused_add_rmsnorm": [P, P, P, I32, I32, F32, P],
     "pk_silu_and_mul": [P, P, I32, I32, P],
     "pk_rope_and_cache": [P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, P],
-    "pk_paged_decode": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, F32, I32, P],
+    "pk_paged_decode": [P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, F32, I32, P],
     "pk_set_decode_z": [I32],
     "pk_set_decode_fill": [I32],
-    "pk_set_decode_wide": [I32],
-    "pk_paged_decode_qkv2": [P, P, I32, I32, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, I32, P],
     "pk_paged_decode_qkv": [P, P, I32, I32, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, I32, P],
     "pk_paged_prefill": [P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, I32, I32, F32, P],
     "pk_sample": [P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, P],
@@ -58,8 +56,8 @@ SIGNATURES = {
     "pk_splitk_add_rmsnorm_route": [P, P, P, P, I32, I32, I32, F32, P, I32, I32, I32, P, P, P],
     "pk_qkv_reduce_rope_cache": [P, P, I32, I32, I32, I32, P, P, P, P, P, I32, P],
     "pk_skinny_gemm_ex": [P, I32, P],
-    "pk_mlp_fused": [P, P, P, P, P],
-    "pk_qkv_attn_fused": [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, P, P, P, P, P],
+    "pk_mlp_fused": [P, P, P, P],
+    "pk_qkv_attn_fused": [P, P, P, P, P, P, P, P, P, P, P, I32, I32, I32, I32, I32, F32, I32, P, P],
     "pk_gemm_args_size": [],
     "pk_norm_apply": [P, P, P, I32, P, I32, I32, F32, P],
     "pk_copy_from_host": [P, P, I64, P],

@@ -223,6 +223,58 @@ def check_custom_ar_serving(car, rank: int, world: int, dev: torch.device, M: in
             "shape": [M, N], "calls": calls}
 
 
+def check_chunk_form(car, rank: int, world: int, dev: torch.device, M: int, N: int, chunks: int) -> Dict[str, bool]:
+    """The column-chunk form of the fused collective (``reduce_residual_chunk``, the overlapped TP
+    decode chain with POLYKEY_TP_DECODE_CHUNKS > 1): every chunk's own 2-slab operand,
+    back to back, against the exact whole-width result."""
+    if not (hasattr(car, "chunks_ok") and car.chunks_ok(M, N, chunks)):
+        return {}
+    Nc = N // chunks
+    full = _pattern(rank, M * N, dtype=torch.float32, salt=400).view(M, N)
+    res0 = _pattern(0, M * N, salt=401).view(M, N).to(torch.bfloat16)
+    residual = res0.to(dev).clone()
+    nparts = car.nparts(M, N)
+    parts = torch.zeros(nparts * M, dtype=torch.float32, device=dev)
+    for c in range(chunks):
+        sl = full[:, c * Nc:(c + 1) * Nc]
+        buf = torch.cat([(sl + 0.5).reshape(-1), torch.full((M * Nc,), -0.5)]).to(dev)
+        car.reduce_residual_chunk(_Slabs(buf, 2, M, Nc), residual, parts, c, chunks)
+    _sync(dev)
+    tot = res0.float() + sum(_pattern(r, M * N, dtype=torch.float32, salt=400).view(M, N) for r in range(world))
+    want_parts = tot.view(M, nparts, N // nparts).pow(2).sum(-1).t()
+    return {f"chunks_{chunks}": _close(residual, tot.to(torch.bfloat16))
+            and bool(torch.equal(parts.view(nparts, M).cpu(), want_parts))}
+
+
+def check_push_form(car, rank: int, world: int, dev: torch.device, M: int, N: int) -> Dict[str, bool]:
+    """The GEMM-epilogue push form (POLYKEY_TP_PUSH): a real MODE_PUSH decode GEMM at
+    [M, K=512] x [N, K]^T whose weight selects column n % K of the rank-seeded activations (an exact
+    product), its tiles pushed into the owners' slots, then ``reduce_residual_pushed``."""
+    from ..ops import gemm
+    if dev.type != "cuda" or not (hasattr(car, "push_ok") and car.push_ok(M, N, 64)):
+        return {}
+    K = 512
+    x = _pattern(rank, M * K, salt=500).view(M, K).to(torch.bfloat16).to(dev)
+    w = torch.zeros(N, K, dtype=torch.bfloat16)
+    w[torch.arange(N), torch.arange(N) % K] = 1.0
+    w = w.to(dev)
+    wp = gemm.pack_weight(w)
+    S, _ = gemm.partial_tiling(N, K, M, wp, True)
+    ws = torch.empty(S * M * N, dtype=torch.float32, device=dev)
+    counters = torch.zeros(N // 64, dtype=torch.int32, device=dev)
+    res0 = _pattern(0, M * N, salt=501).view(M, N).to(torch.bfloat16)
+    residual = res0.to(dev).clone()
+    parts = torch.zeros((N // 256) * M, dtype=torch.float32, device=dev)
+    nbc = gemm.push_projection(x, w, ws, wp, counters, car.push_target())
+    p = car.reduce_residual_pushed(residual, parts, nbc)
+    _sync(dev)
+    cols = torch.arange(N) % K
+    tot = res0.float() + sum(_pattern(r, M * K, salt=500).view(M, K).float()[:, cols] for r in range(world))
+    want_parts = tot.view(M, N // 256, 256).pow(2).sum(-1).t()
+    return {"push": _close(residual, tot.to(torch.bfloat16)) and bool(torch.equal(p.float().cpu(), want_parts))
+            and int(counters.abs().sum()) == 0}
+
+
 def check_ep_ipc(a2a, rank: int, world: int, dev: torch.device) -> Dict[str, bool]:
     """Dispatch + return of the IPC expert all-to-all: rank r sends (r + j) % 2 + 1 rows to rank j
     (expert id j + 10 * row), the owners return each row doubled."""
@@ -284,6 +336,8 @@ def _serving_check(st: ParallelState, serving: Tuple[int, int], report: dict, em
     if agreed or car.fenced or _car_mod.FENCED == "0":
         report["car_protocol"] = "fenced" if car.fenced else "fence-free"
         verdict(name, res, err, st.tp_cpu_group, st.tp_size, off_car)
+        if st.custom_ar is not None:
+            _optional_forms(st, car, M, N, report, emit, verdict)
         return
     # the fence-free form failed somewhere: record it, then retry fenced if every rank is still in step
     report["checks"][name] = {"ok": ok, "group_ok": False, **({"error": err} if err else {}), **res}
@@ -296,6 +350,28 @@ def _serving_check(st: ParallelState, serving: Tuple[int, int], report: dict, em
     report["car_protocol"] = "fenced"
     res, err = attempt("custom_ar_serving_fenced")
     verdict("custom_ar_serving_fenced", res, err, st.tp_cpu_group, st.tp_size, off_car)
+    if st.custom_ar is not None:
+        _optional_forms(st, car, M, N, report, emit, verdict)
+
+
+def _optional_forms(st: ParallelState, car, M: int, N: int, report: dict, emit, verdict) -> None:
+    """The opt-in forms of the TP decode collective, checked when switched on: the
+    column-chunk form (gemm.TP_DECODE_CHUNKS > 1) and the GEMM-epilogue push (gemm.TP_PUSH).  A
+    failure turns that form off on every rank; the plain fused collective stays."""
+    from ..ops import gemm
+    dev = st.device
+    M = min(M, 64)  # the push form takes one 64-row tile; the chunk form is row-agnostic
+    forms = []
+    if gemm.TP_DECODE_CHUNKS > 1:
+        forms.append(("tp_decode_chunks", lambda: check_chunk_form(car, st.tp_rank, st.tp_size, dev, M, N,
+                                                                   gemm.TP_DECODE_CHUNKS),
+                      lambda: setattr(gemm, "TP_DECODE_CHUNKS", 1)))
+    if gemm.TP_PUSH:
+        forms.append(("tp_push", lambda: check_push_form(car, st.tp_rank, st.tp_size, dev, M, N),
+                      lambda: setattr(gemm, "TP_PUSH", False)))
+    for name, fn, off in forms:
+        res, err = _guarded(name, fn, lambda: car.fail(), report, emit)
+        verdict(name, res, err, st.tp_cpu_group, st.tp_size, off)
 
 
 

@@ -57,6 +57,20 @@ def test_bench_json_line(tmp_path, gpus, client, frontend):
     assert out["value"] == pytest.approx(4 * 4 * gpus / (out["ms_per_step"] / 1000.0), rel=0.02)
 
 
+def test_bench_openai_chat_route():
+    """VERDICT r5 item 8 / BASELINE config 4's route: --mode openai drives POST /v1/chat/completions
+    (api/openai.py on the server's process) with templated prompts of exactly --prompt-len tokens;
+    the same JSON contract, the route named in config.rpc."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = _run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--mode", "openai"] + ARGS[:-1]
+             + ["--prompt-len", "160", "--no-graphs"], REPO, env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["config"]["rpc"].startswith("POST /v1/chat/completions") and out["config"]["seq_len"] == 160
+    assert out["config"]["prefix_cache_hit_tokens"] == 0
+    assert out["value"] == pytest.approx(4 * 4 / (out["ms_per_step"] / 1000.0), rel=0.02)
+
+
 def test_bench_dp_attention_expert_all_to_all():
     """Mixtral-shaped MoE with DP attention + EP=2 (expert all-to-all between the two ranks'
     engines, lockstep steps, coordinated shutdown) through the same torchrun child launch."""
@@ -78,9 +92,10 @@ def test_bench_world8_reports_tp_child():
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
     base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
             "--master-addr", "127.0.0.1", "--master-port", "0", os.path.join(REPO, "bench.py"), "--gpus", "8",
-            "--model", "tiny-llama-g8", "--steps", "1", "--warmup", "1", "--concurrency", "2", "--prompt-len", "8",
-            "--max-tokens", "3", "--no-graphs"]
-    r = _run(base + ["--tp-extra-model", "tiny-llama-g8"], REPO, env, timeout=600)
+            "--model", "tiny-llama-g8", "--steps", "1", "--warmup", "1", "--concurrency", "2", "--prompt-len", "128",
+            "--max-tokens", "3", "--no-graphs"]  # (128: the TP child's chat template alone is 100 byte tokens)
+    r = _run(base + ["--tp-extra-model", "tiny-llama-g8", "--ep-extra-model", "tiny-mixtral-e8"], REPO, env,
+             timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -90,12 +105,20 @@ def test_bench_world8_reports_tp_child():
     tp = out["tp8_tiny-llama-g8"]
     assert "error" not in tp, tp
     assert tp["parallelism"] == "tp8" and tp["global_batch"] == 2 and tp["scaling"] == "strong"
+    assert tp["rpc"].startswith("POST /v1/chat/completions"), tp  # config 4: the OpenAI chat route
     assert tp["value"] == pytest.approx(2 * 3 / (tp["ms_per_step"] / 1000.0), rel=0.02)
+    # BASELINE config 5 -- an 8-expert MoE with DP attention + EP = 8 (expert
+    # all-to-all over the 8 ranks) under ep8_<model>, 2 clients per replica
+    ep = out["ep8_tiny-mixtral-e8"]
+    assert "error" not in ep, ep
+    assert ep["parallelism"] == "dp8_ep8_a2a" and ep["global_batch"] == 16 and ep["scaling"] == "weak", ep
+    assert ep["value"] == pytest.approx(2 * 3 * 8 / (ep["ms_per_step"] / 1000.0), rel=0.02)
     # a TP child that cannot run (unknown model) is reported in its key, the main number stays
-    r = _run(base + ["--tp-extra-model", "no-such-model", "--tp-extra-timeout", "120"], REPO, env, timeout=600)
+    r = _run(base + ["--tp-extra-model", "no-such-model", "--tp-extra-timeout", "120", "--ep-extra-model",
+                     "no-such-moe", "--ep-extra-timeout", "120"], REPO, env, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
-    assert out["value"] > 0 and "error" in out["tp8_no-such-model"]
+    assert out["value"] > 0 and "error" in out["tp8_no-such-model"] and "error" in out["ep8_no-such-moe"]
 
 
 def test_bench_world8_hung_tp_child_meets_the_deadline():

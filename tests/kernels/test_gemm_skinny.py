@@ -310,13 +310,13 @@ def test_rowscale_half_blocks(M):
 
 
 @pytest.mark.parametrize("M", [1, 17, 64, 100, 128])
-@pytest.mark.parametrize("H,I", [(4096, 14336), (1024, 4096), (8192, 28672), (8192, 3584)])
+@pytest.mark.parametrize("H,I", [(4096, 14336), (8192, 28672), (8192, 3584)])
 def test_mlp_fused_matches_two_launches(M, H, I):
     """Fused decode MLP (gate_up + SiLU -> in-launch hand-off -> down slabs, one launch) is
     bit-identical to the two launches it replaces, on repeated launches (the hand-off tickets
     re-arm themselves), and never trips the wait timeout.  (8192, 3584) is the 70B TP=8 shard:
-    its 56 gate_up n-blocks are split over K (the last split of each n-block applies SiLU and
-    hands h over), the two-launch reference splits the same way."""
+    its 56 gate_up n-blocks are split over K, a shape the fused launch refuses (the split variant
+    measured slower and was removed in round 6) -- the policy and the launcher must agree."""
     res = rnd(M, H)
     nw = (1.0 + 0.1 * torch.randn(H, device="cuda")).to(torch.bfloat16)
     wgu = gemm.interleave_gate_up(rnd(I, H, scale=0.05), rnd(I, H, scale=0.05))
@@ -327,9 +327,16 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     # gate_up tiles -> two launches, measured faster)
     Sg = gemm.gate_up_split(2 * I, H, M)
     nparts = H // gemm.PART_COLS
-    # (a gate_up split over K takes the fused launch only with POLYKEY_MLP_FUSED_SPLIT=1: measured slower)
+    # (a gate_up split over K never takes the fused launch: measured slower, removed in round 6)
     assert (Sg > 1) == (2 * I // 128 < 192) and gemm.mlp_fused_ok(res, gup, dp, nparts) == (
-        2 * I // 128 * Sg <= 256 and (Sg == 1 or gemm.MLP_FUSED_SPLIT))
+        2 * I // 128 <= 256 and Sg == 1)
+    if Sg > 1:
+        with pytest.raises(AssertionError):
+            gemm.mlp_fused(res, gup, gemm.pack_weight(rnd(H, I, scale=0.02)), gemm.RowScale(
+                torch.ones((H // gemm.PART_COLS) * M, device="cuda").view(-1, M), 1e-5),
+                torch.empty(gemm.choose_split(H, I, M) * M * H, dtype=torch.float32, device="cuda"),
+                torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda"))
+        return
     ws_gu = torch.empty(Sg * M * 2 * I, dtype=torch.float32, device="cuda")
     parts = gemm.residual_parts(None, res.clone(), torch.empty((H // gemm.PART_COLS) * 128, device="cuda"))
     rs = gemm.RowScale(parts, 1e-5)
@@ -341,7 +348,7 @@ def test_mlp_fused_matches_two_launches(M, H, I):
     ws = torch.empty_like(ws0)
     for _ in range(4):
         ws.fill_(float("nan"))
-        p = gemm.mlp_fused(res, gup, dp, rs, ws, flow, ws_gu=ws_gu)
+        p = gemm.mlp_fused(res, gup, dp, rs, ws, flow)
         assert p.S == S
         torch.testing.assert_close(p.view(), ref_slabs, atol=0, rtol=0)
     # against the fp32 reference of the whole MLP
@@ -357,7 +364,7 @@ def test_mlp_fused_matches_two_launches(M, H, I):
         rs2 = gemm.RowScale(p2, 1e-5)
         h2 = gemm.linear_silu(r2, wgu, ws=ws_gu, packed=gup, rowscale=rs2)
         exp2 = gemm.linear_down(h2, wd, ws0, dp).view().clone()
-        got = gemm.mlp_fused(r2, gup, dp, rs2, ws, flow, ws_gu=ws_gu).view()
+        got = gemm.mlp_fused(r2, gup, dp, rs2, ws, flow).view()
         torch.testing.assert_close(got, exp2, atol=0, rtol=0)
     torch.cuda.synchronize()
     assert int(flow.abs().sum()) == 0, flow.tolist()
@@ -418,15 +425,15 @@ def test_fused_err_word_plumbing():
     import ctypes
     addr = gemm.fused_err_word()
     assert addr and gemm.fused_err_word() == addr
-    M, H, I = 64, 1024, 4096
+    M, H, I = 64, 1024, 12288  # 192 gate_up n-blocks: unsplit, the shape the fused launch takes
     res = rnd(M, H)
     gup = gemm.pack_weight(gemm.interleave_gate_up(rnd(I, H, scale=0.05), rnd(I, H, scale=0.05)))
     dp = gemm.pack_weight(rnd(H, I, scale=0.02))
     parts = gemm.residual_parts(None, res.clone(), torch.empty(2 * 64, device="cuda"))
     ws = torch.empty(gemm.choose_split(H, I, M) * M * H, dtype=torch.float32, device="cuda")
     flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device="cuda")
-    ws_gu = torch.empty(gemm.gate_up_split(2 * I, H, M) * M * 2 * I, dtype=torch.float32, device="cuda")
-    gemm.mlp_fused(res, gup, dp, gemm.RowScale(parts, 1e-5), ws, flow, ws_gu=ws_gu)
+    assert gemm.gate_up_split(2 * I, H, M) == 1
+    gemm.mlp_fused(res, gup, dp, gemm.RowScale(parts, 1e-5), ws, flow)
     torch.cuda.synchronize()
     gemm.check_fused()
     w = ctypes.c_int.from_address(addr)

@@ -209,6 +209,14 @@ def _serving_phase(car, rank, world, dev):
     r = preflight.check_custom_ar_serving(car, rank, world, dev, 64, 4096)
     assert r["checks"] and all(r["checks"].values()), (car.fenced, r)
     assert set(r["checks"]) == {"eager", "graph", "graph_timed"} and r["collective_us"] > 0, r
+    # the opt-in forms' preflight checks on the real kernels: column chunks, GEMM push
+    dist.barrier()
+    c = preflight.check_chunk_form(car, rank, world, dev, 64, 4096, 2)
+    assert c == ({"chunks_2": True} if car.chunks_ok(64, 4096, 2) else {}), c
+    if not car.fenced:
+        dist.barrier()
+        p = preflight.check_push_form(car, rank, world, dev, 64, 4096)
+        assert p == ({"push": True} if car.push_ok(64, 4096, 64) else {}), p
     assert car.error() == 0
 
 

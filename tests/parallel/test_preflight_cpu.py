@@ -318,3 +318,61 @@ def test_serving_preflight_catches_a_stale_slot_and_falls_back(tmp_path, stale_i
             assert rep["disabled"] == ["custom_ar_serving_fenced"]
     line = json.loads(torch.load(f"{out}.0", weights_only=True)["lines"][-1])
     assert line["event"] == "multi_gpu_preflight" and "collective_us" in line
+
+
+class ChunkCar(StaleCar):
+    """StaleCar plus the column-chunk form; ``bad_chunk`` >= 0 drops that chunk's peer sum on rank 1."""
+
+    def __init__(self, group, world, bad_chunk):
+        super().__init__(group, world, stale_rank=-1, stale_in=())
+        self.bad_chunk = bad_chunk
+
+    def chunks_ok(self, M, N, chunks):
+        return N % (1024 * chunks) == 0
+
+    def reduce_residual_chunk(self, pending, residual, parts, chunk, chunks):
+        M, N = residual.shape
+        Nc = N // chunks
+        s = pending.view().sum(0).float().clone()
+        dist.all_reduce(s, group=self.g)
+        if chunk == self.bad_chunk and dist.get_rank(self.g) == 1:
+            s.zero_()
+        cols = slice(chunk * Nc, (chunk + 1) * Nc)
+        residual[:, cols] = (residual[:, cols].float() + s.to(torch.bfloat16).float()).to(residual.dtype)
+        n = self.nparts(M, N)
+        w = N // n
+        pv = parts.view(-1)[: n * M].view(n, M)
+        pv[chunk * (Nc // w):(chunk + 1) * (Nc // w)] = residual[:, cols].float().view(M, Nc // w, w).pow(2).sum(-1).t()
+
+
+def _chunk_worker(rank, world, port, out, bad_chunk):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), POLYKEY_PREFLIGHT="0")
+    from polykey_service_amd.ops import gemm
+    from polykey_service_amd.parallel import preflight
+    from polykey_service_amd.parallel.state import destroy_parallel, init_parallel
+    gemm.TP_DECODE_CHUNKS = 2
+    st = init_parallel(tp=world, device="cpu", backend="gloo")
+    st.custom_ar = ChunkCar(st.tp_cpu_group, world, bad_chunk)
+    rep = preflight.run(st, paths=("custom_ar_serving",), emit=lambda s: None, serving=(8, 2048))
+    torch.save({"report": rep, "chunks": gemm.TP_DECODE_CHUNKS, "car": st.custom_ar is not None}, f"{out}.{rank}")
+    st.custom_ar = None
+    destroy_parallel()
+
+
+@pytest.mark.parametrize("bad_chunk", [-1, 1])
+def test_serving_preflight_checks_the_chunk_form(tmp_path, bad_chunk):
+    """with POLYKEY_TP_DECODE_CHUNKS > 1 the column-chunk collective is checked at serving
+    shape too; a wrong chunk on one rank turns the chunked chain off on both ranks and keeps the
+    plain fused collective."""
+    out = str(tmp_path / "pf")
+    mp.start_processes(_chunk_worker, args=(2, _port(), out, bad_chunk), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        d = torch.load(f"{out}.{r}", weights_only=True)
+        chk = d["report"]["checks"]["tp_decode_chunks"]
+        assert d["car"] and d["report"]["checks"]["custom_ar_serving"]["group_ok"]
+        if bad_chunk < 0:
+            assert chk["ok"] and chk["group_ok"] and d["chunks"] == 2, chk
+        else:
+            assert chk["ok"] == (r != 1) and not chk["group_ok"] and d["chunks"] == 1, chk
+            assert d["report"]["disabled"] == ["tp_decode_chunks"]

@@ -51,8 +51,8 @@ def test_llama3_70b_tp8_overlapped_collectives(tmp_path):
     GEMMs, chunk collectives forked to the comm stream inside the captured graph), forced on for the
     shared-GPU rehearsal with the box's default hardware queues: graphs equal eager, logits inside
     the TP=1 noise band."""
-    env = dict(os.environ, POLYKEY_TP_OVERLAP_FORCE="1", POLYKEY_TP_DECODE_CHUNKS="2")
-    res = _rehearse(str(tmp_path / "tp8o"), ["--hw-queues", "0"], env=env)
+    env = dict(os.environ, POLYKEY_TP_DECODE_CHUNKS="2")
+    res = _rehearse(str(tmp_path / "tp8o"), ["--hw-queues", "0", "--force-overlap"], env=env)
     assert res["fused_tp_decode"] and res["car_err"] == 0 and res["graph_steps"] > 0, res
     assert res["graph_equals_eager"] and res["ref_rows_outside_noise"] == [], res
 

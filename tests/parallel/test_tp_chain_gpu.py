@@ -69,9 +69,9 @@ def test_tp8_shard_fused_chain_bit_identical_to_two_launches(monkeypatch):
             return real_qkv(*a, **k)
         monkeypatch.setattr(gemm, "mlp_fused", mlp)
         monkeypatch.setattr(gemm, "qkv_attn_fused", qkv)
-        # the serving policy keeps both off at this shape (measured slower, gemm.MLP_FUSED_SPLIT /
-        # QKV_ATTN_MIN_KV); the launches must still be exact where they are allowed
-        monkeypatch.setattr(gemm, "MLP_FUSED_SPLIT", True)
+        # the serving policy keeps the QKV -> attention launch off at this shape (one kv head per
+        # rank: measured slower, gemm.QKV_ATTN_MIN_KV); it must still be exact where allowed.  The
+        # fused MLP never takes the shard's K-split gate_up (that variant was removed in round 6)
         monkeypatch.setattr(gemm, "QKV_ATTN_MIN_KV", 1)
         # the fused launch's QKV tiles are 128-row n-blocks at the full split: compare with the same
         # tiling (the two-launch chain's half-split QKV sums its slabs in another grouping)
@@ -81,7 +81,7 @@ def test_tp8_shard_fused_chain_bit_identical_to_two_launches(monkeypatch):
             gemm.MLP_FUSED = gemm.QKV_ATTN_FUSED = fused
             kv = [(k.clone(), v.clone()) for k, v in kv0]
             outs.append((_run(model, md, kv, ids, pos), kv))
-        assert calls == {"mlp": 2, "qkv": 2}, calls  # both layers took both fused launches
+        assert calls == {"mlp": 0, "qkv": 2}, calls  # both layers took the fused QKV -> attention launch
         (h0, kv_a), (h1, kv_b) = outs
         assert torch.equal(h0, h1)
         for (ka, va), (kb, vb) in zip(kv_a, kv_b):

@@ -18,14 +18,13 @@ for ctx in (128, 384, 1024, 4096):
     bt = torch.arange(B * maxb, dtype=torch.int32, device="cuda").view(B, maxb)
     cl = torch.full((B,), ctx, dtype=torch.int32, device="cuda")
     q = torch.randn(B, NQ, D, device="cuda").to(torch.bfloat16)
-    o, ml, ctr = A.decode_workspace(B, NQ, maxb, BS, "cuda", n_kv=NKV)
+    o, ml = A.decode_workspace(B, NQ, maxb, BS, "cuda")
     md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0,
                         slot_mapping=None, decode_block_tables=bt, decode_context_lens=cl,
-                        decode_part_o=o, decode_part_ml=ml, decode_counters=ctr)
+                        decode_part_o=o, decode_part_ml=ml)
     row = f"ctx {ctx:5d}:"
-    for z, merge in ((4, True), (16, True), (4, False), (16, False)):
+    for z in (4, 16):
         native.lib().pk_set_decode_z(z)
-        md.decode_counters = ctr if merge else None
         for i in range(4):
             A.paged_attention(q, *layers[i % 4], md, 0.088)
         torch.cuda.synchronize()
@@ -38,7 +37,7 @@ for ctx in (128, 384, 1024, 4096):
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n * 1000
         gb = B * ctx * NKV * D * 2 * 2 / 1e9
-        row += f" | z{z} {'merge' if merge else 'reduce'} {us:7.1f} us {gb / us * 1e3:5.2f} TB/s"
+        row += f" | z{z} {us:7.1f} us {gb / us * 1e3:5.2f} TB/s"
     native.lib().pk_set_decode_z(4)
     print(row, flush=True)
     del layers

@@ -18,21 +18,15 @@ sys.path.insert(0, REPO)
 from polykey_service_amd._native.build import HIP_FLAGS, HIPCC  # noqa: E402
 
 VARIANTS = {
-    # timing only (NOT coherent): the residual-phase consumers read A / the row-scale parts with
-    # plain loads instead of sc1 loads -- what the sc1 hand-off of a widely re-read A costs
-    "res_plain": [("skinny_tile.h", "      if constexpr (kWait)  // the producers' output, handed off in-launch: sc1 loads",
-                   "      if constexpr (kWaitSlice)  // the producers' output, handed off in-launch: sc1 loads"),
-                  ("skinny_tile.h", "rs_p[h * kRsLoads + q] = kWaitRes ? ldf_sc1(args.nrm_parts, p) : *p;",
-                   "rs_p[h * kRsLoads + q] = *p;")],
     # round 5, measured and removed: "push_nofence" / "push_nostore" (the TP push epilogue without
     # its system release / without its stores: the release was 3.2 us of the 6.5 us the epilogue
     # added to the 70B TP=8 o projection, the stores 1.1 us -- profiles/r5_push_probe.jsonl; the
     # epilogue now stores write-through at system scope and stamps the flag without a fence)
     # the fused QKV -> attention launch without the K/V prefetch before the hand-off wait
-    "pre0": [("decode_fused.hip", "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 2>(",
-              "decode_tile<P, kDecodeWaves, true, SS, OPH ? 3 : 2, 0>(")],
+    "pre0": [("decode_fused.hip", "decode_tile<P, kDecodeWaves, true, SS, 2, 2>(",
+              "decode_tile<P, kDecodeWaves, true, SS, 2, 0>(")],
     # the fused MLP's down tiles with non-temporal weight loads
-    "mlp_nt": [("gemm_skinny.hip", "mlp_fused_kernel<MT, SP, KR, false, RS><<<", "mlp_fused_kernel<MT, SP, KR, !SP, RS><<<")],
+    "mlp_nt": [("gemm_skinny.hip", "mlp_fused_kernel<MT, KR><<<", "mlp_fused_kernel<MT, KR, true><<<")],
     # the fused launches' hand-off pollers sleeping 4 instead of 16 (x 64 cycles) between polls
     "sleep4": [("flow.h", "__builtin_amdgcn_s_sleep(16);", "__builtin_amdgcn_s_sleep(4);")],
     # ablations of the 4-wave prefill GEMM measured this round (timing only, wrong results;

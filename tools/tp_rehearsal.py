@@ -267,7 +267,8 @@ def launch(a) -> int:
     me = [sys.executable, os.path.abspath(__file__)]
     common = ["--world", str(a.world), "--model", a.model, "--layers", str(a.layers), "--batch", str(a.batch),
               "--prompt", str(a.prompt), "--steps", str(a.steps), "--out", a.out, "--cmp-tokens", str(a.cmp_tokens),
-              "--max-batched", str(a.max_batched)] + (["--check-only"] if a.check_only else [])
+              "--max-batched", str(a.max_batched)] + (["--check-only"] if a.check_only else []) + (
+              ["--force-overlap"] if a.force_overlap else [])
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     if a.ref == "run":
         print(json.dumps({"phase": "ref"}), flush=True)
@@ -333,6 +334,9 @@ def main() -> int:
     # which then time-slices the ranks and every collective waits for a slice (4-layer 70B TP=8
     # rehearsal: 7.4 ms / step at 1 queue per rank, 128 ms at 2, ~500 ms at the default)
     ap.add_argument("--hw-queues", type=int, default=1, help="GPU_MAX_HW_QUEUES per rank (0: the box default)")
+    ap.add_argument("--force-overlap", action="store_true",
+                    help="take the chunked comm-stream TP chain (POLYKEY_TP_DECODE_CHUNKS) although the ranks share "
+                         "one GPU (models/llama.py force_overlap_streams)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "tp_rehearsal"))
     a = ap.parse_args()
     if a.role == "ref":
@@ -340,6 +344,9 @@ def main() -> int:
     if a.role == "noise":
         os.makedirs(a.out, exist_ok=True)
         return role_noise(a)
+    if a.force_overlap:
+        from polykey_service_amd.models.llama import LlamaForCausalLM
+        LlamaForCausalLM.force_overlap_streams = True
     if a.role == "rank":
         return role_rank(a)
     return launch(a)

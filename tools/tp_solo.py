@@ -115,11 +115,9 @@ def main():
     pos = cl - 1
     slots = bt[:, (a.ctx - 1) // BS] * BS + (a.ctx - 1) % BS
     po, pml = A.decode_workspace(B, at.nq, maxb, BS, dev, kv_heads=at.nkv)
-    # the engine's metadata (engine/model_runner.py): in-launch partition merge counters
-    ctr = torch.zeros((B, at.nkv), dtype=torch.int32, device=dev) if A.INLAUNCH_MERGE and po is not None else None
     md = A.AttnMetadata(num_decode=B, num_prefill=0, num_prefill_tokens=0, max_prefill_q_len=0, slot_mapping=slots,
                         decode_block_tables=bt, decode_context_lens=cl, decode_part_o=po, decode_part_ml=pml,
-                        decode_counters=ctr, decode_max_ctx=A._PART if a.ctx <= A._PART else 0)
+                        decode_max_ctx=A._PART if a.ctx <= A._PART else 0)
     ids = torch.randint(0, cfg.vocab_size, (B,), dtype=torch.int32, device=dev)
 
     def step():
