@@ -300,11 +300,17 @@ struct SkinnyLds {
 //   1  producer: output stores write-through (sc1), one ticket per finished n-block on `fl`
 //   2  consumer of per-K-slice tickets on `fl` (slice = this tile's split): weights requested first,
 //      A (the producers' output) read with sc1 loads after the wait
+//   4  consumer of a TP collective carried by the same launch (car_gemm.hip): `fl` slice g = the
+//      collective's chunk group g (fl.cols_per_slice columns of A, the residual stream); the tile
+//      waits for every group its K range overlaps after requesting its first weight k-steps, and
+//      for ALL groups (`fw`, one counter) before the row scale, whose norm parts the collective
+//      writes too -- A and the parts read with sc1 loads
 template <int MT, int MODE, bool PK, bool NORM, bool NT, bool RS = false, int KR = 2, int FL = 0>
 __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_in, const int by, const int gdx,
-                                            SkinnyLds<MT>& L, const Flow& fl) {
+                                            SkinnyLds<MT>& L, const Flow& fl, const Flow& fw = Flow{}) {
   constexpr bool kProd = (FL & 1) != 0;
-  constexpr bool kWait = (FL & 2) != 0;
+  constexpr bool kWaitCar = (FL & 4) != 0;
+  constexpr bool kWait = (FL & 2) != 0 || kWaitCar;
   constexpr int kR = KR;
   constexpr int kKA = SkinnyLds<MT>::kKA;  // k per staged A tile
   constexpr int kPPR = kKA / 8;             // 16-byte pieces per A row
@@ -370,14 +376,20 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
       const int rr = min(64 * h + (tid >> 2), M - 1);
 #pragma unroll
       for (int q = 0; q < kRsLoads; ++q) {
-        rs_p[h * kRsLoads + q] = args.nrm_parts[min(sub + 4 * q, np - 1) * args.M + row0 + rr];
+        const float* p = args.nrm_parts + min(sub + 4 * q, np - 1) * args.M + row0 + rr;
+        rs_p[h * kRsLoads + q] = kWaitCar ? ldf_sc1(args.nrm_parts, p) : *p;  // (parts written in-launch)
       }
     }
   };
-  if constexpr (RS) load_rs();
+  if constexpr (RS && !kWaitCar) load_rs();
   // the consumer's wait (after its first weight k-steps are requested)
   auto wait_in = [&](int split_) {
-    if constexpr (kWait) flow_wait(fl, split_);
+    if constexpr (kWaitCar) {
+      const int g0 = k0 / fl.cols_per_slice, g1 = (k0 + kper - 1) / fl.cols_per_slice;
+      for (int g = g0; g <= g1; ++g) flow_wait(fl, g);
+    } else if constexpr (kWait) {
+      flow_wait(fl, split_);
+    }
   };
 
   const bf16_t* wp[kR];
@@ -525,6 +537,10 @@ __device__ __forceinline__ void skinny_tile(const GemmArgs& args, const int bx_i
   }
   }
 
+  if constexpr (RS && kWaitCar) {  // every group's parts are final once the whole collective is
+    flow_wait(fw, 0);
+    load_rs();
+  }
   if constexpr (RS) {
     const int np = min(args.nrm_nparts, 4 * kRsLoads), sub = tid & 3;
 #pragma unroll

@@ -546,8 +546,11 @@ class LlamaForCausalLM(nn.Module):
         Each row-parallel projection costs its GEMM and ONE collective launch (2 x 80
         all-reduces per 70B TP=8 step).  Launches per layer: 6 with the fused QKV -> attention and MLP
         launches (8B-like shards: >= 4 kv heads per rank), 8 at the 70B TP=8 shard (one kv head: QKV |
-        attention; gate_up split over K: gate_up | SiLU reduce | down), profiles/r5_decode_attention.md."""
+        attention; gate_up split over K: gate_up | SiLU reduce | down), profiles/r5_decode_attention.md
+        -- 6 there too when the collectives ride in their consumers' launches (_forward_tp_carried)."""
         car = self.st.custom_ar
+        if self._carry_ok(residual, md):
+            return self._forward_tp_carried(residual, parts, positions, md, kv_caches, ws, buf, buf2)
         for i, layer in enumerate(self.layers):
             at, mlp = layer.attn, layer.mlp
             a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws)
@@ -557,6 +560,81 @@ class LlamaForCausalLM(nn.Module):
             else:
                 h = self._decode_gate_up(layer, residual, parts)
                 parts = self._tp_row_collective(h, mlp.down, mlp.down_p, ws, residual, buf, down=True)
+        return gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
+
+    # the TP decode collectives carried by the launch of the projection that consumes them
+    # (kernels/car_gemm.hip); None: POLYKEY_TP_CARRY, off on a shared GPU.  Default OFF: on the
+    # loopback group the carried chain is bit-identical but 0.12 ms per 70B TP=8 rank step slower
+    # (7.58 vs 7.45 ms, profiles/r6_carry.md): the consumer's A operand, written in-launch by other
+    # XCDs, must be read past the (per-XCD, non-coherent) L2 -- the 56 n-blocks of a split re-read it
+    # from the Infinity Cache instead of L2 -- which costs more than the launch boundary it saves.
+    # Kept for the 8-GPU A/B, where the xGMI exchange is longer than loopback's.
+    carry_collectives: Optional[bool] = None
+
+    def _carry_ok(self, residual: torch.Tensor, md) -> bool:
+        """The carried chain (:meth:`_forward_tp_carried`) takes pure-decode steps of one 64-row tile
+        on the two-shot collective (TP = 4 / 8), for shards whose gate_up is split over K (no fused
+        MLP launch) and whose QKV is not fused with the attention (70B TP=8: one kv head per rank).
+        Ranks sharing a GPU keep the plain chain: a rank's consumer tiles wait inside a launch for
+        its collective, whose peers' workgroups need slots on the same device."""
+        on = self.carry_collectives
+        if on is None:
+            on = os.environ.get("POLYKEY_TP_CARRY", "0") == "1" and not self.st.shared_device
+        car = self.st.custom_ar
+        M, H = residual.shape
+        l0 = self.layers[0]
+        return bool(on and residual.is_cuda and md.num_prefill == 0 and md.num_decode == M
+                    and hasattr(car, "carry_ok") and car.carry_ok(M, H) and not gemm.TP_PUSH
+                    and gemm.TP_DECODE_CHUNKS < 2 and isinstance(l0.mlp, LlamaMLP)
+                    and not gemm.mlp_fused_ok(residual, l0.mlp.gate_up_pf, l0.mlp.down_p, H // 256)
+                    and gemm.gate_up_split(l0.mlp.gate_up.shape[0], H, M) > 1
+                    and not self._qkv_attn_fused_ok(l0.attn, M, H // 256, md)
+                    and getattr(self, "_ws_gu", None) is not None)
+
+    def _forward_tp_carried(self, residual: torch.Tensor, parts: torch.Tensor, positions: torch.Tensor,
+                            md: attn_ops.AttnMetadata, kv_caches: List[Tuple[torch.Tensor, torch.Tensor]],
+                            ws: torch.Tensor, buf: torch.Tensor, buf2: torch.Tensor) -> torch.Tensor:
+        """The TP decode chain with every collective but the last carried by its consumer's launch
+        (gemm.linear_partial_rowscale_car), per layer:
+
+            attention from the QKV slabs (RoPE, KV write)            [QKV came with the last launch]
+            o     = split-K slabs of a @ Wo_local^T
+            [collective(o) -> residual, parts | gate_up slabs of rinv2 * residual @ Wgu'^T]  ONE launch
+            h     = SiLU reduce of the gate_up slabs
+            d     = split-K slabs of h @ Wdown_local^T
+            [collective(d) -> residual, parts | next layer's QKV slabs]                     ONE launch
+
+        6 launches per 70B TP=8 layer instead of 8; bit-identical to the plain chain (the same
+        collective, the same consumer tiling, the row scale applied after accumulation)."""
+        car = self.st.custom_ar
+        dev = car.device_ctx()
+        if getattr(self, "_flow_car", None) is None:
+            self._flow_car = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=self.device)
+        flow = self._flow_car
+        M, H = residual.shape
+        qkv_half = gemm.QKV_HALF and M <= gemm.SKINNY_MAX_M
+        L = len(self.layers)
+        qkv = None  # this layer's QKV slabs when the previous launch produced them
+        for i, layer in enumerate(self.layers):
+            at, mlp = layer.attn, layer.mlp
+            kc, vc = kv_caches[i]
+            if qkv is None:
+                a = self._decode_attn(layer, residual, parts, positions, md, kv_caches[i], ws)
+            else:
+                a = attn_ops.paged_decode_from_qkv(qkv, positions, self.cos_sin, kc, vc, md, at.scale, at.nq, at.nkv)
+            o = gemm.linear_partial(at.drop(a), at.o, ws, packed=at.o_p, half=True)
+            N2 = mlp.gate_up.shape[0]
+            parts, gu = gemm.linear_partial_rowscale_car(dev, o, residual, buf2, mlp.gate_up, self._ws_gu, layer.eps,
+                                                         flow, packed=mlp.gate_up_pf, S=gemm.gate_up_split(N2, H, M))
+            h = torch.empty((M, N2 // 2), dtype=residual.dtype, device=residual.device)
+            gemm.silu_reduce(gu, h)
+            d = gemm.linear_down(h, mlp.down, ws, mlp.down_p)
+            if i + 1 < L:
+                nxt = self.layers[i + 1]
+                parts, qkv = gemm.linear_partial_rowscale_car(dev, d, residual, buf, nxt.attn.qkv, ws, nxt.eps, flow,
+                                                              packed=nxt.attn.qkv_pf, half=qkv_half)
+            else:
+                parts = car.reduce_residual(d, residual, buf)
         return gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
 
     def _tp_row_collective(self, x: torch.Tensor, w: torch.Tensor, wp: Optional[torch.Tensor], ws: torch.Tensor,

@@ -404,14 +404,51 @@ def linear_partial_rowscale(x: torch.Tensor, w: torch.Tensor, ws: torch.Tensor, 
     ``half`` (packed W): 64-row n-blocks at half the default split."""
     M, K = x.shape
     N = w.shape[0]
+    S, half = _rowscale_tiling(N, K, M, packed, half, S)
+    assert ws.numel() >= S * M * N, "split-K workspace too small"
+    _launch_ex(MODE_PARTIAL | (HALF_BIT if half else 0), x, w, packed, S, ws=ws, rowscale=rowscale)
+    return Partial(ws, S, M, N)
+
+
+def _rowscale_tiling(N: int, K: int, M: int, packed: Optional[torch.Tensor], half: bool, S: Optional[int]):
+    """(split, half) of :func:`linear_partial_rowscale` (shared with its collective-carrying form)."""
     half = half and packed is not None and packed.numel() * packed.element_size() < NT_MIN_BYTES
     if S is None:
         S = choose_split(N, K, M)
         if half:
             S = max(1, S // 2)
-    assert ws.numel() >= S * M * N, "split-K workspace too small"
-    _launch_ex(MODE_PARTIAL | (HALF_BIT if half else 0), x, w, packed, S, ws=ws, rowscale=rowscale)
-    return Partial(ws, S, M, N)
+    return S, half
+
+
+# the carried launch with each workgroup running a collective item and then a consumer tile (A/B)
+CAR_PAIRED = os.environ.get("POLYKEY_CAR_PAIRED", "1") == "1"
+
+
+def linear_partial_rowscale_car(car_dev, pending: Partial, residual: torch.Tensor, parts: torch.Tensor,
+                                w: torch.Tensor, ws: torch.Tensor, eps: float, flow: torch.Tensor,
+                                packed: torch.Tensor, S: Optional[int] = None, half: bool = False):
+    """ONE launch (csrc/kernels/car_gemm.hip): the two-shot TP collective of ``pending`` (the
+    row-parallel projection's split-K slabs) into ``residual`` / ``parts`` -- exactly
+    ``custom_ar.reduce_residual`` -- and the folded-norm projection that consumes that residual --
+    exactly :func:`linear_partial_rowscale` (same tiling and split, bit-identical slabs) -- whose
+    tiles stream their weights while the collective runs and wait only for the chunk groups they
+    read.  ``car_dev``: ``CustomAllReduce.device_ctx()``; ``flow``: int32 >= :data:`FLOW_WORDS`,
+    zeroed once, left zeroed.  Returns (the parts view [N / 256, M], the consumer's slabs)."""
+    M, N = residual.shape
+    Nc, K = w.shape
+    assert K == N and pending.M == M and pending.N == N and residual.is_contiguous()
+    S, half = _rowscale_tiling(Nc, K, M, packed, half, S)
+    assert ws.numel() >= S * M * Nc and flow.numel() >= FLOW_WORDS and flow.dtype == torch.int32
+    # (ws may be pending's own buffer: a consumer tile stores its slabs only after the whole
+    # collective -- every slab read included -- has taken its tickets)
+    g = GemmArgs()
+    g.partial, g.A, g.W = ws.data_ptr(), residual.data_ptr(), packed.data_ptr()
+    g.M, g.N, g.K, g.lda, g.ldo, g.S = M, Nc, K, N, Nc, S
+    g.row_scale, g.nrm_parts, g.nrm_nparts, g.eps = 1, parts.data_ptr(), N // 256, float(eps)
+    native.call("pk_car_gemm", ctypes.cast(car_dev, ctypes.c_void_p), pending.buf.data_ptr(), pending.S,
+                residual.data_ptr(), parts.data_ptr(), M, N, ctypes.byref(g), 1 if half else 2, int(CAR_PAIRED),
+                flow.data_ptr(), native.stream_ptr())
+    return parts.view(-1)[: (N // 256) * M].view(N // 256, M), Partial(ws, S, M, Nc)
 
 
 _CUS: dict = {}
@@ -656,6 +693,14 @@ def residual_parts(p: Optional[Partial], residual: torch.Tensor, parts: torch.Te
     native.call("pk_residual_parts", residual.data_ptr(), 0 if p is None else p.buf.data_ptr(), 0 if p is None else p.S,
                 M, H, parts.data_ptr(), native.stream_ptr())
     return parts.view(-1)[: n * M].view(n, M)
+
+
+def silu_reduce(p: Partial, out: torch.Tensor) -> torch.Tensor:
+    """h = SiLU(gate) * up of the summed slabs of an interleaved gate/up projection (the split
+    gate_up's reduce launch, as :func:`linear_silu` runs it) into ``out`` [M, N / 2]."""
+    native.call("pk_splitk_reduce", out.data_ptr(), p.buf.data_ptr(), p.S, p.M, p.N, out.stride(0), 1,
+                native.stream_ptr())
+    return out
 
 
 def reduce_partial(p: Partial, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -62,6 +62,7 @@ SIGNATURES = {
     "pk_norm_apply": [P, P, P, I32, P, I32, I32, F32, P],
     "pk_copy_from_host": [P, P, I64, P],
     "pk_residual_parts": [P, P, I32, I32, I32, P, P],
+    "pk_car_gemm": [P, P, I32, P, P, I32, I32, P, I32, I32, P, P],
 }
 
 

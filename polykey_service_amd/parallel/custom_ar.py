@@ -61,6 +61,7 @@ def _lib() -> ctypes.CDLL:
         lib.pk_car_set_error.argtypes = [_P]
         lib.pk_car_set_timeout_ms.argtypes = [_P, _LL]
         lib.pk_car_set_fenced.argtypes = [_P, _I]
+        lib.pk_car_device_ctx.argtypes = [_P, _P, _I]
         lib.pk_car_get_fenced.argtypes = [_P]
         lib.pk_car_destroy.argtypes = [_P]
         lib.pk_car_destroy.restype = None
@@ -239,6 +240,22 @@ class CustomAllReduce:
             torch.cuda.current_stream(self.device).cuda_stream)
         if rc != 0:
             raise RuntimeError(f"fused TP reduce (chunk {chunk}) launch failed ({rc})")
+
+    def device_ctx(self):
+        """This rank's collective context as the kernels see it (csrc/comm/car_device.h CarDev, a
+        byte buffer): what a launch of the kernel library that carries the two-shot collective
+        takes (gemm.linear_partial_rowscale_car).  Re-read after :meth:`set_fenced`."""
+        n = int(self.lib.pk_car_device_ctx_size())
+        buf = ctypes.create_string_buffer(n)
+        if self.lib.pk_car_device_ctx(self.ctx, buf, n) != 0:
+            raise RuntimeError("pk_car_device_ctx failed")
+        return buf
+
+    def carry_ok(self, M: int, N: int) -> bool:
+        """Shapes a consumer launch can carry this collective for (the two-shot form at W = 4 / 8,
+        one 64-row tile): kernels/car_gemm.hip."""
+        return (self.world in (4, 8) and 0 < M <= 64 and N % (256 * self.world) == 0
+                and self.nparts(M, N) == N // 256 and M * (N // (256 * self.world)) <= 1024)
 
     def push_target(self):
         """Where a decode GEMM's push epilogue writes (gemm.push_projection)."""

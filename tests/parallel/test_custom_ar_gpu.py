@@ -75,6 +75,7 @@ def _worker(rank, world, port, q):
         car.set_fenced(False)
         dist.barrier()
         _overlap_phase(car, rank, world, dev)
+        _carry_phase(car, rank, world, dev)
         _push_phase(car, rank, world, dev)
         # a rank that skips a call: every rank that waits for it times out and fails loudly
         # (sticky error word, read without a GPU sync), and later calls return at once
@@ -218,6 +219,76 @@ def _serving_phase(car, rank, world, dev):
         p = preflight.check_push_form(car, rank, world, dev, 64, 4096)
         assert p == ({"push": True} if car.push_ok(64, 4096, 64) else {}), p
     assert car.error() == 0
+
+
+def _carry_phase(car, rank, world, dev):
+    """The collective carried by its consumer's launch (kernels/car_gemm.hip):
+    residual, norm parts and the consumer's split-K slabs bit-identical to reduce_residual + the
+    separate folded-norm projection, across real ranks (small shapes: every rank's grid resident on
+    the shared GPU), repeated and graph-replayed (the hand-off counters re-arm themselves)."""
+    from polykey_service_amd.ops import gemm
+    if not car.carry_ok(8, 256 * world):
+        return
+    g = torch.Generator().manual_seed(11)
+    gr = torch.Generator().manual_seed(200 + rank)
+    flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=dev)
+    dctx = car.device_ctx()
+    for M, N, Nc, S_o, S_c, half in ((8, 256 * world, 512, 2, 4, False), (5, 512 * world, 256, 1, 2, True)):
+        K = N
+        res0 = (torch.randn(M, N, generator=g) * 2).to(torch.bfloat16).to(dev)
+        slabs = torch.randn(S_o * M * N, generator=gr).to(dev)
+        w = (torch.randn(Nc, K, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+        wp = gemm.pack_weight(w)
+        pend = gemm.Partial(slabs, S_o, M, N)
+        # reference: the two launches
+        r_ref = res0.clone()
+        p_ref = torch.zeros((N // 256) * M, dtype=torch.float32, device=dev)
+        pv = car.reduce_residual(pend, r_ref, p_ref)
+        ws_ref = torch.empty(S_c * M * Nc, dtype=torch.float32, device=dev)
+        c_ref = gemm.linear_partial_rowscale(r_ref, w, ws_ref, gemm.RowScale(pv, 1e-5), S=S_c, packed=wp, half=half)
+        torch.cuda.synchronize()
+        for it in range(3):
+            r = res0.clone()
+            p = torch.zeros_like(p_ref)
+            ws = torch.full((S_c * M * Nc,), float("nan"), device=dev)
+            dist.barrier()
+            pv2, c = gemm.linear_partial_rowscale_car(dctx, pend, r, p, w, ws, 1e-5, flow, packed=wp, S=S_c, half=half)
+            torch.cuda.synchronize()
+            assert torch.equal(r, r_ref), ("residual", M, N, it, car.error())
+            assert torch.equal(pv2, pv), ("parts", M, N, it)
+            assert c.S == c_ref.S and torch.equal(c.view(), c_ref.view()), ("slabs", M, N, it)
+            assert int(flow.abs().sum()) == 0, flow.nonzero()[:8].tolist()
+    # graph replay of the carried launch
+    M, N, Nc = 8, 256 * world, 512
+    res0 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+    r = res0.clone()
+    slabs = torch.zeros(2 * M * N, device=dev)
+    pend = gemm.Partial(slabs, 2, M, N)
+    w = (torch.randn(Nc, N, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    wp = gemm.pack_weight(w)
+    p = torch.zeros((N // 256) * M, dtype=torch.float32, device=dev)
+    ws = torch.empty(4 * M * Nc, dtype=torch.float32, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gemm.linear_partial_rowscale_car(dctx, pend, r, p, w, ws, 1e-5, flow, packed=wp, S=4)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        _, cg = gemm.linear_partial_rowscale_car(dctx, pend, r, p, w, ws, 1e-5, flow, packed=wp, S=4)
+    for it in range(3):
+        slabs.fill_(float(rank + it))
+        r.copy_(res0)
+        dist.barrier()
+        graph.replay()
+        torch.cuda.synchronize()
+        inc = torch.tensor(2.0 * sum(r2 + it for r2 in range(world))).to(torch.bfloat16).float()
+        assert torch.equal(r, (res0.float() + inc).to(torch.bfloat16)), it
+        want = gemm.linear_partial_rowscale(r, w, torch.empty_like(ws), gemm.RowScale(p.view(N // 256, M), 1e-5),
+                                            S=4, packed=wp)
+        torch.cuda.synchronize()
+        assert torch.equal(cg.view(), want.view()), it
+    assert car.error() == 0 and int(flow.abs().sum()) == 0
 
 
 def _overlap_phase(car, rank, world, dev):
@@ -422,5 +493,47 @@ def test_loopback_group_runs_every_collective_without_blocking():
             g.replay()
         torch.cuda.synchronize()
         assert car.error() == 0 and int(ctr.abs().sum()) == 0
+    finally:
+        car.close()
+
+
+@pytest.mark.parametrize("consumer", ["gate_up", "qkv"])
+def test_carried_collective_at_70b_tp8_shapes_on_loopback(consumer):
+    """The carried launch at the 70B TP=8 rank's real shapes (64 rows, hidden 8192; gate_up 7168 x
+    8192 split 4 after o, QKV 1280 x 8192 half-split after down) on the one-process loopback group:
+    every workgroup of the real grid runs (256 collective items + 224 / 160 consumer tiles), the
+    results equal the two launches bit for bit, the hand-off counters re-arm."""
+    from polykey_service_amd.ops import gemm
+    from polykey_service_amd.parallel.custom_ar import CustomAllReduce
+    dev = torch.device("cuda:0")
+    car = CustomAllReduce.loopback(0, 8, dev)
+    car.set_timeout(5.0)
+    try:
+        M, N = 64, 8192
+        Nc, S_c, half = (7168, 4, False) if consumer == "gate_up" else (1280, None, True)
+        g = torch.Generator(device=dev).manual_seed(3)
+        res0 = (torch.randn(M, N, device=dev, generator=g) * 2).to(torch.bfloat16)
+        slabs = torch.randn(2 * M * N, device=dev, generator=g)
+        pend = gemm.Partial(slabs, 2, M, N)
+        w = (torch.randn(Nc, N, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        wp = gemm.pack_weight(w)
+        S_real, _ = gemm._rowscale_tiling(Nc, N, M, wp, half, S_c)
+        assert car.carry_ok(M, N)
+        r_ref = res0.clone()
+        p_ref = torch.zeros((N // 256) * M, dtype=torch.float32, device=dev)
+        pv = car.reduce_residual(pend, r_ref, p_ref)
+        c_ref = gemm.linear_partial_rowscale(r_ref, w, torch.empty(S_real * M * Nc, device=dev), gemm.RowScale(pv, 1e-5),
+                                             S=S_c, packed=wp, half=half)
+        flow = torch.zeros(gemm.FLOW_WORDS, dtype=torch.int32, device=dev)
+        dctx = car.device_ctx()
+        for _ in range(3):
+            r = res0.clone()
+            p = torch.zeros_like(p_ref)
+            pv2, c = gemm.linear_partial_rowscale_car(dctx, pend, r, p, w, torch.empty(S_real * M * Nc, device=dev),
+                                                      1e-5, flow, packed=wp, S=S_c, half=half)
+            torch.cuda.synchronize()
+            assert torch.equal(r, r_ref) and torch.equal(pv2, pv)
+            assert torch.equal(c.view(), c_ref.view())
+        assert car.error() == 0 and int(flow.abs().sum()) == 0
     finally:
         car.close()

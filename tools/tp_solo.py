@@ -149,11 +149,23 @@ def main():
         torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     gemm.check_fused()
+    carried = None
+    if a.car == "loopback" and getattr(model, "_flow_car", None) is not None:
+        # the carried chain (kernels/car_gemm.hip) against the plain one on the same inputs: the
+        # loopback peers make the values meaningless but deterministic -- they must match bit for bit
+        with torch.inference_mode():
+            model.carry_collectives = False
+            ref = step().clone()
+            model.carry_collectives = True
+            got = step()
+            torch.cuda.synchronize()
+            model.carry_collectives = None
+        carried = {"taken": True, "bit_identical": bool(torch.equal(ref, got))}
     if a.car == "loopback":
         assert st.custom_ar.error() == 0, "a loopback wait timed out"
     print(json.dumps({"model": a.model, "tp": a.tp, "layers": cfg.num_layers, "batch": B, "ctx": a.ctx,
                       "ms_per_step": round(ms, 3), "us_per_layer": round(ms * 1000 / cfg.num_layers, 2),
-                      "graph": not a.eager, "init_s": round(init_s, 1), "car": a.car,
+                      "graph": not a.eager, "init_s": round(init_s, 1), "car": a.car, "carried": carried,
                       "mlp_fused": os.environ.get("POLYKEY_MLP_FUSED", "1"),
                       "qkv_attn_fused": os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1"),
                       "env": {k: v for k, v in os.environ.items() if k.startswith("POLYKEY_")}}), flush=True)
