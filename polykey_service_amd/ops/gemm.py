@@ -421,7 +421,7 @@ def _rowscale_tiling(N: int, K: int, M: int, packed: Optional[torch.Tensor], hal
 
 
 # the carried launch with each workgroup running a collective item and then a consumer tile (A/B)
-CAR_PAIRED = os.environ.get("POLYKEY_CAR_PAIRED", "1") == "1"
+CAR_PAIRED = True  # (separate workgroups measured slower: profiles/r6_carry.md)
 
 
 def linear_partial_rowscale_car(car_dev, pending: Partial, residual: torch.Tensor, parts: torch.Tensor,
