@@ -568,8 +568,13 @@ class LlamaForCausalLM(nn.Module):
     # (7.58 vs 7.45 ms, profiles/r6_carry.md): the consumer's A operand, written in-launch by other
     # XCDs, must be read past the (per-XCD, non-coherent) L2 -- the 56 n-blocks of a split re-read it
     # from the Infinity Cache instead of L2 -- which costs more than the launch boundary it saves.
-    # Kept for the 8-GPU A/B, where the xGMI exchange is longer than loopback's.
+    # Kept for the 8-GPU A/B, where the xGMI exchange is longer than loopback's.  Per site
+    # (profiles/r6_carry.md kernel table): the o -> gate_up launch is at parity with its two plain
+    # launches (35.5 vs 35.8 us), the down -> QKV one 2 us slower (21.3 vs 19.3 us: 160 QKV tiles
+    # wait on the whole collective for the row scale) -- POLYKEY_TP_CARRY=gate_up carries only the
+    # first.  carry_qkv None: from that variable.
     carry_collectives: Optional[bool] = None
+    carry_qkv: Optional[bool] = None
 
     def _carry_ok(self, residual: torch.Tensor, md) -> bool:
         """The carried chain (:meth:`_forward_tp_carried`) takes pure-decode steps of one 64-row tile
@@ -579,7 +584,7 @@ class LlamaForCausalLM(nn.Module):
         its collective, whose peers' workgroups need slots on the same device."""
         on = self.carry_collectives
         if on is None:
-            on = os.environ.get("POLYKEY_TP_CARRY", "0") == "1" and not self.st.shared_device
+            on = os.environ.get("POLYKEY_TP_CARRY", "0") in ("1", "gate_up") and not self.st.shared_device
         car = self.st.custom_ar
         M, H = residual.shape
         l0 = self.layers[0]
@@ -613,6 +618,9 @@ class LlamaForCausalLM(nn.Module):
         flow = self._flow_car
         M, H = residual.shape
         qkv_half = gemm.QKV_HALF and M <= gemm.SKINNY_MAX_M
+        carry_qkv = self.carry_qkv
+        if carry_qkv is None:
+            carry_qkv = os.environ.get("POLYKEY_TP_CARRY", "0") != "gate_up"
         L = len(self.layers)
         qkv = None  # this layer's QKV slabs when the previous launch produced them
         for i, layer in enumerate(self.layers):
@@ -629,12 +637,12 @@ class LlamaForCausalLM(nn.Module):
             h = torch.empty((M, N2 // 2), dtype=residual.dtype, device=residual.device)
             gemm.silu_reduce(gu, h)
             d = gemm.linear_down(h, mlp.down, ws, mlp.down_p)
-            if i + 1 < L:
+            if i + 1 < L and carry_qkv:
                 nxt = self.layers[i + 1]
                 parts, qkv = gemm.linear_partial_rowscale_car(dev, d, residual, buf, nxt.attn.qkv, ws, nxt.eps, flow,
                                                               packed=nxt.attn.qkv_pf, half=qkv_half)
             else:
-                parts = car.reduce_residual(d, residual, buf)
+                parts, qkv = car.reduce_residual(d, residual, buf), None
         return gemm.norm_apply(residual, parts, self.norm, self.cfg.rms_eps)
 
     def _tp_row_collective(self, x: torch.Tensor, w: torch.Tensor, wp: Optional[torch.Tensor], ws: torch.Tensor,
