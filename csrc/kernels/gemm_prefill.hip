@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_deep_kernel(const Pr
 // fragments of u (register set u & 1) while the 16 ds_reads of u + 1 go to the other set; before
 // reading the first half of a new tile (u odd) each wave retires its own LDS-DMA (vmcnt(0)),
 // lgkmcnt(0) and one raw barrier, then issues the 16 LDS-DMA loads of tile (u + 3) / 2 into the
-// buffer the barrier just freed (2 per group of 8 MFMAs): two sub-steps of latency cover them.
+// buffer the barrier just freed (one per MFMA quad): two sub-steps of latency cover them.
 __device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8_t& w, const bf16x8_t& a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(a));
 }
@@ -304,6 +304,7 @@ __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const Pr
   Tile tl;
   if (!tile_of(args, tl)) return;
   const int K = args.K, U = K / 32;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // provably wave-uniform: M0 from SALU
 
   // LDS-DMA sources: instruction j (0..7) of an operand fills rows 32 j .. 32 j + 31; thread t row
   // 32 j + t / 8, physical chunk t % 8 = logical chunk ^ ((row >> 1) & 7) = ^ ((t >> 4) & 7).
@@ -323,13 +324,30 @@ __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const Pr
       wsrc[j] = tl.W + static_cast<long long>(tl.n0 + 32 * j + (tid >> 3)) * K + logical * 8;
     }
   }
-  auto stage_one = [&](int j, int T) {  // instruction j (0-7 A, 8-15 W) of k-tile T
-    bf16_t* base = lds + (T & 1) * kStage + w * 8 * BK;  // wave w's 1 KiB of the instruction
+  // The 16 loads are buffer_load ... lds: a per-instruction constant VGPR offset from the tile's
+  // base (the resource), the k advance in an SGPR and M0 from SALU, so a load costs no VALU.  The
+  // global_load_lds form (a 64-bit address add per load, a readfirstlane for M0) was 4.5-13 %
+  // slower on every shape (profiles/r6_prefill_gemm_buffer_lds.md).
+  const bf16_t* abase = args.A + static_cast<long long>(tl.row0 + tl.m0) * args.lda;
+  const bf16_t* wbase = PW ? tl.W + static_cast<long long>(tl.n0 >> 7) * 128 * K : tl.W + static_cast<long long>(tl.n0) * K;
+  const auto ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(abase), static_cast<short>(0), 0x7ffffff0, 0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(wbase), static_cast<short>(0), 0x7ffffff0, 0x00020000);
+  unsigned avo[8], wvo[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    avo[j] = static_cast<unsigned>(asrc[j] - abase) * 2u;
+    wvo[j] = static_cast<unsigned>(wsrc[j] - wbase) * 2u;
+  }
+  auto stage_one = [&](int j, int T) {  // instruction j (0-7 A, 8-15 W) of k-tile T: wave w's 1 KiB
+    bf16_t* base = lds + (T & 1) * kStage + wu * 8 * BK;
     if (j < 8) {
-      glds16(asrc[j] + T * BK, base + j * 32 * BK);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)(base + j * 32 * BK), 16,
+                                               avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 0);
     } else {
-      const long long wo = PW ? (T >> 1) * 16384LL + (T & 1) * 1024 : static_cast<long long>(T) * BK;
-      glds16(wsrc[j - 8] + wo, base + kPiece + (j - 8) * 32 * BK);
+      const unsigned wo = PW ? static_cast<unsigned>(T >> 1) * 32768u + static_cast<unsigned>(T & 1) * 2048u
+                             : static_cast<unsigned>(T) * BK * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wrs, (__attribute__((address_space(3))) void*)(base + kPiece + (j - 8) * 32 * BK), 16, wvo[j - 8], wo, 0, 0);
     }
   };
 
@@ -382,19 +400,28 @@ __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const Pr
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int mf = 0; mf < 8; ++mf) {
-      if constexpr (NEXT) {
-        fw[C ^ 1][mf] = ld8(nb + wo + mf * kWStride);
-        fa[C ^ 1][mf] = ld8(nb + ao + mf * 16 * BK);
-      }
-      if constexpr (LOAD) {
-        stage_one(2 * mf, (u + 3) >> 1);
-        stage_one(2 * mf + 1, (u + 3) >> 1);
-      }
-#pragma unroll
-      for (int nf = 0; nf < 8; ++nf) {
+      auto mm = [&](int nf) {
         if constexpr (Z) mfma_zero(acc[nf][mf], fw[C][nf], fa[C][mf]);
         else mfma_acc(acc[nf][mf], fw[C][nf], fa[C][mf]);
-      }
+      };
+      // one memory instruction per MFMA pair, pinned: ds_read W | 2 MFMA | load | 2 MFMA | ds_read A |
+      // 2 MFMA | load | 2 MFMA -- no two issue-heavy instructions back to back (vs both reads and
+      // both loads ahead of 8 MFMAs: -1 %)
+      if constexpr (NEXT) fw[C ^ 1][mf] = ld8(nb + wo + mf * kWStride);
+      mm(0);
+      mm(1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (LOAD) stage_one(2 * mf, (u + 3) >> 1);
+      mm(2);
+      mm(3);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NEXT) fa[C ^ 1][mf] = ld8(nb + ao + mf * 16 * BK);
+      mm(4);
+      mm(5);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (LOAD) stage_one(2 * mf + 1, (u + 3) >> 1);
+      mm(6);
+      mm(7);
       __builtin_amdgcn_sched_barrier(0);
     }
   };

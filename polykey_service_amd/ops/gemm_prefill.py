@@ -20,10 +20,11 @@ from . import native
 
 BM = 256
 BN = 256
-# 6: the 4-wave, one-wave-per-SIMD kernel (AGPR accumulators, BK 64; K % 128 == 0), 4: the 8-wave
-# ping-pong kernel (the fallback for K % 128 != 0) -- csrc/kernels/gemm_prefill.hip; same process
-# vs 4: QKV +8 %, gate_up +3.5 %, O +6 %, down 0, Mixtral w13 +2.5 %, w2 -2.6 %
-# (profiles/r4_prefill_gemm_4wave.md); hipBLASLt is still 17-23 % faster on the dense shapes
+# 6: the 4-wave, one-wave-per-SIMD kernel (AGPR accumulators, BK 64, buffer_load ... lds staging;
+# K % 128 == 0), 4: the 8-wave ping-pong kernel (the fallback for K % 128 != 0) --
+# csrc/kernels/gemm_prefill.hip.  Round 6: 4.5-13 % faster than its global_load_lds form; hipBLASLt
+# is still 7-16 % faster on the dense shapes, 8 % slower on the grouped w2
+# (profiles/r6_prefill_gemm_buffer_lds.md, r4_prefill_gemm_4wave.md)
 VARIANT = 6
 
 
@@ -56,7 +57,7 @@ def _launch(a: PrefillGemmArgs, variant: Optional[int] = None) -> None:
         _checked = True
     v = VARIANT if variant is None else variant
     if v >= 6 and a.K % 128:
-        v -= 2  # the 8-wave kernel needs only K % 64 == 0
+        v = 4 + v % 2  # the 8-wave kernel needs only K % 64 == 0
     native.check(lib.pk_prefill_gemm(ctypes.byref(a), v, native.stream_ptr()), "pk_prefill_gemm")
 
 

@@ -124,3 +124,4 @@ def test_four_wave_kernel(variant, silu):
 def test_native_library_has_prefill_gemm():
     from polykey_service_amd.ops import native
     assert native.has("pk_prefill_gemm")
+

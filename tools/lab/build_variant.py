@@ -37,6 +37,12 @@ VARIANTS = {
     # the 4-wave prefill GEMM's 16 LDS-DMA loads of a tile, measured at gate_up against 2 per group
     # (1,453 us): all right after the barrier ("pg_front") 1,535, 4 per group in the first 4 groups
     # ("pg_first4") 1,443 (noise) -- profiles/r4_prefill_gemm_4wave.md
+    # round 6 ablations of the 4-wave prefill GEMM's buffer_load ... lds staging (timing only, wrong
+    # results; profiles/r6_prefill_gemm_buffer_lds.md): no vmcnt wait before the tile barrier
+    # (gate_up 1,350 vs 1,393 us), no loads in the k-loop (1,151: 7 % under hipBLASLt)
+    "pb_novm": [("gemm_prefill.hip", "if constexpr (BAR) wait_vm<0>();", "")],
+    "pb_noload": [("gemm_prefill.hip", "if constexpr (LOAD) stage_one(2 * mf, (u + 3) >> 1);", ""),
+                  ("gemm_prefill.hip", "if constexpr (LOAD) stage_one(2 * mf + 1, (u + 3) >> 1);", "")],
     # round 5, measured and removed: "mt8_chunk256" (128-row decode tiles staging A per 256-deep chunk,
     # one workgroup per CU: 8B at 128 rows 6.36 vs 5.62-5.65 ms, 256 rows 10.07-10.09 vs 9.21-9.22,
     # profiles/r5_mt8.jsonl); "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
