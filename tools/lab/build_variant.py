@@ -43,6 +43,11 @@ VARIANTS = {
     "pb_novm": [("gemm_prefill.hip", "if constexpr (BAR) wait_vm<0>();", "")],
     "pb_noload": [("gemm_prefill.hip", "if constexpr (LOAD) stage_one(2 * mf, (u + 3) >> 1);", ""),
                   ("gemm_prefill.hip", "if constexpr (LOAD) stage_one(2 * mf + 1, (u + 3) >> 1);", "")],
+    # cache policy of the prefill GEMM's staging loads: sc0 (aux 1) on the W / A stream, nt (aux 2) on W
+    "pb_sc0_w": [("gemm_prefill.hip", "wvo[j - 8], wo, 0, 0);", "wvo[j - 8], wo, 0, 1);")],
+    "pb_sc0_a": [("gemm_prefill.hip", "avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 0);",
+                  "avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 1);")],
+    "pb_nt_w": [("gemm_prefill.hip", "wvo[j - 8], wo, 0, 0);", "wvo[j - 8], wo, 0, 2);")],
     # round 5, measured and removed: "mt8_chunk256" (128-row decode tiles staging A per 256-deep chunk,
     # one workgroup per CU: 8B at 128 rows 6.36 vs 5.62-5.65 ms, 256 rows 10.07-10.09 vs 9.21-9.22,
     # profiles/r5_mt8.jsonl); "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
