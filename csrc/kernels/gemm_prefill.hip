@@ -11,7 +11,7 @@
 //   * workgroup tile 256 (m) x 256 (n), 8 waves as 2 (m) x 4 (n), each wave 128 x 64 outputs
 //     = 8 x 4 MFMA 16x16x32 bf16 accumulators (128 fp32 registers per lane), two waves per SIMD
 //     in a ping-pong (one wave's MFMAs cover the other's LDS reads and load issue);
-//   * both operands are staged HBM/L2 -> LDS with 16-byte global_load_lds (no VGPR round trip)
+//   * both operands are staged HBM/L2 -> LDS with 16-byte buffer_load ... lds (no VGPR round trip)
 //     into two 64-deep k-tile buffers (128 KiB), raw s_barriers and counted vmcnt waits that keep
 //     three 16 KiB pieces in flight across the phases;
 //   * LDS rows are 64 bf16 (128 B); 16-byte chunks are XOR-swizzled by row (chunk ^ (row >> 1) & 7:
@@ -55,11 +55,6 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else static_assert(N == 0, "unsupported vmcnt");
 }
-
-// 16-byte LDS-DMA: lane l's 16 bytes land at lds + 16 l (lds wave-uniform).  Kept in a plain
-// (non-template) device function: called directly inside the kernel template, hipcc's host pass
-// silently drops the kernel's launch stub (undefined symbol at load time).
-__device__ __forceinline__ void glds16(const bf16_t* g, bf16_t* lds) { __builtin_amdgcn_global_load_lds(g, lds, 16, 0, 0); }
 
 __device__ __forceinline__ void barrier() { asm volatile("s_barrier" ::: "memory"); }
 
@@ -164,11 +159,27 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_deep_kernel(const Pr
         src[p][j] = tl.W + static_cast<long long>(tl.n0 + (p - 2) * 128 + row) * K + logical * 8;
       }
     }
+  // buffer_load ... lds as in the 4-wave kernel below: constant lane offsets from the tile's A / W
+  // base, the k advance in an SGPR, M0 from SALU (no per-load VALU)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const bf16_t* abase = args.A + static_cast<long long>(tl.row0 + tl.m0) * args.lda;
+  const bf16_t* wbase = PW ? tl.W + static_cast<long long>(tl.n0 >> 7) * 128 * K : tl.W + static_cast<long long>(tl.n0) * K;
+  const auto ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(abase), static_cast<short>(0), 0x7ffffff0, 0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(wbase), static_cast<short>(0), 0x7ffffff0, 0x00020000);
+  unsigned vo[4][2];
+#pragma unroll
+  for (int p = 0; p < 4; ++p)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) vo[p][j] = static_cast<unsigned>(src[p][j] - (p < 2 ? abase : wbase)) * 2u;
   auto stage_piece = [&](int p, int kt) {
-    bf16_t* base = lds + (kt & 1) * kStage + p * kPiece + w * 64 * 8;
-    const long long off = PW && p >= 2 ? (kt >> 1) * 16384LL + (kt & 1) * 1024 : static_cast<long long>(kt) * BK;
-    glds16(src[p][0] + off, base);
-    glds16(src[p][1] + off, base + kRowsPerInstr * BK);
+    bf16_t* base = lds + (kt & 1) * kStage + p * kPiece + wu * 64 * 8;
+    const unsigned off = PW && p >= 2 ? static_cast<unsigned>(kt >> 1) * 32768u + static_cast<unsigned>(kt & 1) * 2048u
+                                      : static_cast<unsigned>(kt) * BK * 2u;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(p < 2 ? ars : wrs,
+                                               (__attribute__((address_space(3))) void*)(base + j * kRowsPerInstr * BK), 16,
+                                               vo[p][j], off, 0, 0);
   };
 
   const int wr = w >> 2, wc = w & 3;

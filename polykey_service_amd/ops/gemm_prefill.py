@@ -28,6 +28,14 @@ BN = 256
 VARIANT = 6
 
 
+def default_variant(N: int, K: int) -> int:
+    """Row-major variant for an N x K weight (+1: block-packed).  Deep-K, narrow-N shapes (the
+    down projections, Mixtral w2: K >= 2 N) run faster on the 8-wave kernel since both stage by
+    buffer_load ... lds (round 6: 8B down 687 vs 702 us, Mixtral grouped w2 1,673 vs 1,829 us;
+    the 4-wave kernel 5-12 % ahead elsewhere -- profiles/r6_prefill_gemm_buffer_lds.md)."""
+    return 4 if K >= 2 * N else VARIANT
+
+
 class PrefillGemmArgs(ctypes.Structure):
     """Mirror of ``struct PrefillGemmArgs`` (checked against ``pk_prefill_gemm_args_size``)."""
     _fields_ = [("C", ctypes.c_void_p), ("A", ctypes.c_void_p), ("W", ctypes.c_void_p),
@@ -55,7 +63,7 @@ def _launch(a: PrefillGemmArgs, variant: Optional[int] = None) -> None:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         f.restype = ctypes.c_int
         _checked = True
-    v = VARIANT if variant is None else variant
+    v = default_variant(a.N, a.K) if variant is None else variant
     if v >= 6 and a.K % 128:
         v = 4 + v % 2  # the 8-wave kernel needs only K % 64 == 0
     native.check(lib.pk_prefill_gemm(ctypes.byref(a), v, native.stream_ptr()), "pk_prefill_gemm")
@@ -68,10 +76,6 @@ def _ref(x: torch.Tensor, w: torch.Tensor, silu: bool) -> torch.Tensor:
         g, u = v[:, :, 0].reshape(y.shape[0], -1), v[:, :, 1].reshape(y.shape[0], -1)
         y = torch.nn.functional.silu(g).to(torch.bfloat16).float() * u
     return y.to(x.dtype)
-
-
-# the same kernels reading the decode GEMM's block-packed W
-PACKED_VARIANT = 7
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, silu: bool = False,
@@ -100,7 +104,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
             or (packed is not None and (K % 128 or tuple(packed.shape) != (N, K)))):
         raise ValueError(f"prefill GEMM: unsupported shape/layout M={M} N={N} K={K}")
     if packed is not None and variant not in (5, 7):
-        variant = PACKED_VARIANT
+        variant = default_variant(N, K) + 1
     a = PrefillGemmArgs()
     a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), src.data_ptr()
     a.M, a.N, a.K, a.lda, a.ldc = M, N, K, x.stride(0), out.stride(0)
