@@ -291,13 +291,16 @@ __global__ void __launch_bounds__(kThreads, 1) prefill_gemm_deep_kernel(const Pr
 // accumulator in AGPRs next to the fragment registers on its own).  hipcc neither counts nor pads
 // inline asm (guide §5.7): the first k-step takes C = 0, each accumulator's next MFMA is 64 MFMAs
 // later, and the epilogue reads the AGPRs 32 wait states after the last MFMA.
-// Pipeline: two 64-deep k-tile buffers (A | W, 64 KiB each; 128-byte LDS rows = whole cache lines
-// per glds row -- the BK = 32 form of this kernel doubled the L1 -> L2 requests,
-// profiles/r4_prefill_gemm_pmc.md); the k-loop runs 32-deep sub-steps u: 64 MFMAs on the
-// fragments of u (register set u & 1) while the 16 ds_reads of u + 1 go to the other set; before
-// reading the first half of a new tile (u odd) each wave retires its own LDS-DMA (vmcnt(0)),
-// lgkmcnt(0) and one raw barrier, then issues the 16 LDS-DMA loads of tile (u + 3) / 2 into the
-// buffer the barrier just freed (one per MFMA quad): two sub-steps of latency cover them.
+// Pipeline: 64-deep k-tiles staged by LDS-DMA (128-byte LDS rows = whole cache lines per row --
+// the BK = 32 form of this kernel doubled the L1 -> L2 requests, profiles/r4_prefill_gemm_pmc.md)
+// into a 3-slot ring of A pieces and a 2-slot ring of W pieces (5 x 32 KiB = the whole LDS); the
+// k-loop runs 32-deep sub-steps u: 64 MFMAs on the fragments of u (register set u & 1) while the
+// 16 ds_reads of u + 1 go to the other set.  Before reading the first half of tile t (u odd) each
+// wave retires all but the 8 youngest LDS-DMA loads (tile t + 1's A piece stays in flight),
+// lgkmcnt(0), one raw barrier; that sub-step then stages tile t + 1's W piece and the next one
+// tile t + 2's A piece, one load per 8 MFMAs: W gets two sub-steps to land, A three.  Against all
+// 16 loads of tile t + 1 in the odd sub-step of a 2 x 64 KiB double buffer: down -9 %, Mixtral w2
+// -14 %, the K = 4096 shapes unchanged (profiles/r6_prefill_gemm_buffer_lds.md).
 __device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8_t& w, const bf16x8_t& a) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(w), "v"(a));
 }
@@ -309,12 +312,16 @@ constexpr int kW4Threads = 256;
 
 template <bool PW>
 __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const PrefillGemmArgs args) {
-  constexpr int BK = 64, kPiece = 256 * BK, kStage = 2 * kPiece;  // 32 KiB per operand per k-tile
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * kStage];
+  // LDS: a 3-slot ring of A pieces and a 2-slot ring of W pieces, 32 KiB each = 160 KiB (the whole
+  // LDS).  The A pieces of tile t + 2 go out one sub-step after the W pieces of tile t + 1, so both
+  // streams are spread over the whole tile (one load per 8 MFMAs) and the A loads get three
+  // sub-steps to land instead of two.
+  constexpr int BK = 64, kPiece = 256 * BK;  // 32 KiB per operand piece
+  __shared__ __attribute__((aligned(16))) bf16_t lds[5 * kPiece];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   Tile tl;
   if (!tile_of(args, tl)) return;
-  const int K = args.K, U = K / 32;
+  const int K = args.K, U = K / 32, NT = K / BK;
   const int wu = __builtin_amdgcn_readfirstlane(w);  // provably wave-uniform: M0 from SALU
 
   // LDS-DMA sources: instruction j (0..7) of an operand fills rows 32 j .. 32 j + 31; thread t row
@@ -322,44 +329,38 @@ __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const Pr
   // Packed W: slot 4 j + w of the W piece = (128-row half h, row tile t, k-block bb) with
   // slot = (8 h + t) * 2 + bb, copied lane-linearly from the packed 128 x 128 blocks.
   const int logical = (tid & 7) ^ ((tid >> 4) & 7);
-  const bf16_t* asrc[8];
-  const bf16_t* wsrc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int m = min(tl.m0 + 32 * j + (tid >> 3), tl.rows - 1);  // rows past the group: clamped, never stored
-    asrc[j] = args.A + static_cast<long long>(tl.row0 + m) * args.lda + logical * 8;
-    if constexpr (PW) {
-      const int slot = 4 * j + w, h = slot >> 4, t = (slot >> 1) & 7, bb = slot & 1;
-      wsrc[j] = tl.W + static_cast<long long>((tl.n0 >> 7) + h) * 128 * K + (t * 4 + bb) * 512 + lane * 8;
-    } else {
-      wsrc[j] = tl.W + static_cast<long long>(tl.n0 + 32 * j + (tid >> 3)) * K + logical * 8;
-    }
-  }
-  // The 16 loads are buffer_load ... lds: a per-instruction constant VGPR offset from the tile's
-  // base (the resource), the k advance in an SGPR and M0 from SALU, so a load costs no VALU.  The
-  // global_load_lds form (a 64-bit address add per load, a readfirstlane for M0) was 4.5-13 %
-  // slower on every shape (profiles/r6_prefill_gemm_buffer_lds.md).
   const bf16_t* abase = args.A + static_cast<long long>(tl.row0 + tl.m0) * args.lda;
   const bf16_t* wbase = PW ? tl.W + static_cast<long long>(tl.n0 >> 7) * 128 * K : tl.W + static_cast<long long>(tl.n0) * K;
-  const auto ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(abase), static_cast<short>(0), 0x7ffffff0, 0x00020000);
-  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(wbase), static_cast<short>(0), 0x7ffffff0, 0x00020000);
   unsigned avo[8], wvo[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    avo[j] = static_cast<unsigned>(asrc[j] - abase) * 2u;
-    wvo[j] = static_cast<unsigned>(wsrc[j] - wbase) * 2u;
-  }
-  auto stage_one = [&](int j, int T) {  // instruction j (0-7 A, 8-15 W) of k-tile T: wave w's 1 KiB
-    bf16_t* base = lds + (T & 1) * kStage + wu * 8 * BK;
-    if (j < 8) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ars, (__attribute__((address_space(3))) void*)(base + j * 32 * BK), 16,
-                                               avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 0);
+    const int m = min(tl.m0 + 32 * j + (tid >> 3), tl.rows - 1);  // rows past the group: clamped, never stored
+    avo[j] = static_cast<unsigned>((m - tl.m0) * args.lda + logical * 8) * 2u;
+    if constexpr (PW) {
+      const int slot = 4 * j + w, h = slot >> 4, t = (slot >> 1) & 7, bb = slot & 1;
+      wvo[j] = static_cast<unsigned>(h * 128 * K + (t * 4 + bb) * 512 + lane * 8) * 2u;
     } else {
-      const unsigned wo = PW ? static_cast<unsigned>(T >> 1) * 32768u + static_cast<unsigned>(T & 1) * 2048u
-                             : static_cast<unsigned>(T) * BK * 2u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          wrs, (__attribute__((address_space(3))) void*)(base + kPiece + (j - 8) * 32 * BK), 16, wvo[j - 8], wo, 0, 0);
+      wvo[j] = static_cast<unsigned>((32 * j + (tid >> 3)) * K + logical * 8) * 2u;
     }
+  }
+  // The loads are buffer_load ... lds: a per-instruction constant VGPR offset from the tile's base
+  // (the resource), the k advance in an SGPR and M0 from SALU, so a load costs no VALU.  The
+  // global_load_lds form (a 64-bit address add per load, a readfirstlane for M0) was 4.5-13 %
+  // slower on every shape (profiles/r6_prefill_gemm_buffer_lds.md).
+  const auto ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(abase), static_cast<short>(0), 0x7ffffff0, 0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(wbase), static_cast<short>(0), 0x7ffffff0, 0x00020000);
+  auto a_slot = [&](int t) { return lds + (t % 3) * kPiece; };
+  auto w_slot = [&](int t) { return lds + (3 + (t & 1)) * kPiece; };
+  auto stage_a = [&](int j, int t) {  // instruction j of tile t's A piece: wave w's 1 KiB
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        ars, (__attribute__((address_space(3))) void*)(a_slot(t) + wu * 8 * BK + j * 32 * BK), 16, avo[j],
+        static_cast<unsigned>(t) * BK * 2u, 0, 0);
+  };
+  auto stage_w = [&](int j, int t) {
+    const unsigned wo = PW ? static_cast<unsigned>(t >> 1) * 32768u + static_cast<unsigned>(t & 1) * 2048u
+                           : static_cast<unsigned>(t) * BK * 2u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        wrs, (__attribute__((address_space(3))) void*)(w_slot(t) + wu * 8 * BK + j * 32 * BK), 16, wvo[j], wo, 0, 0);
   };
 
   // fragment reads of sub-step u: tile u / 2, k-half s = u & 1 (chunk 4 s + g); the swizzle term of
@@ -368,8 +369,8 @@ __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const Pr
   const int r = lane & 15, g = lane >> 4;
   auto a_off = [&](int s) { return (wr * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8); };
   auto w_off = [&](int s) {
-    if constexpr (PW) return kPiece + (wc * 8 * 2 + s) * 512 + lane * 8;
-    return kPiece + (wc * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8);
+    if constexpr (PW) return (wc * 8 * 2 + s) * 512 + lane * 8;
+    return (wc * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8);
   };
   constexpr int kWStride = PW ? 2 * 512 : 16 * BK;  // between the W fragments of one sub-step
 
@@ -378,36 +379,41 @@ __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const Pr
 
   // prologue: tiles 0 and 1 in flight, tile 0 retired, sub-step 0's fragments read
 #pragma unroll
-  for (int j = 0; j < 16; ++j) stage_one(j, 0);
+  for (int j = 0; j < 8; ++j) stage_a(j, 0);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) stage_one(j, 1);
+  for (int j = 0; j < 8; ++j) stage_w(j, 0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) stage_a(j, 1);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) stage_w(j, 1);
   wait_vm<16>();
   barrier();
   {
-    const int ao = a_off(0), wo = w_off(0);
+    const bf16_t* ab = a_slot(0) + a_off(0);
+    const bf16_t* wb = w_slot(0) + w_off(0);
 #pragma unroll
     for (int f = 0; f < 8; ++f) {
-      fw[0][f] = ld8(lds + wo + f * kWStride);
-      fa[0][f] = ld8(lds + ao + f * 16 * BK);
+      fw[0][f] = ld8(wb + f * kWStride);
+      fa[0][f] = ld8(ab + f * 16 * BK);
     }
   }
 
-  // sub-step u on register set C.  Z: the first (C = 0); BAR: u odd, the next sub-step opens a new
-  // tile; NEXT: read sub-step u + 1; LOAD: stage tile (u + 3) / 2 (all 16 loads in the odd
-  // sub-step: splitting them over both sub-steps leaves the second half one sub-step to land and
-  // measured 6-11 % slower)
+  // sub-step u on register set C (= u & 1).  Z: the first (C = 0); BW >= 0: u odd, the next
+  // sub-step opens tile (u + 1) / 2 -- retire all but the BW youngest loads (tile t + 1's A pieces
+  // may stay in flight), lgkmcnt(0), one raw barrier; NEXT: read sub-step u + 1; LOAD: u odd -> the
+  // W piece of tile (u + 3) / 2, u even -> the A piece of tile u / 2 + 2, one load per 8 MFMAs
   auto step = [&](auto Cc, auto Zc, auto Bc, auto Nc, auto Lc, int u) {
-    constexpr int C = decltype(Cc)::value;
-    constexpr bool Z = decltype(Zc)::value, BAR = decltype(Bc)::value, NEXT = decltype(Nc)::value,
-                   LOAD = decltype(Lc)::value;
-    if constexpr (BAR) wait_vm<0>();
+    constexpr int C = decltype(Cc)::value, BW = decltype(Bc)::value;
+    constexpr bool Z = decltype(Zc)::value, NEXT = decltype(Nc)::value, LOAD = decltype(Lc)::value;
+    if constexpr (BW >= 0) wait_vm<BW>();
     // lgkmcnt(0) (visible to hipcc's own waitcnt bookkeeping): this sub-step's fragments, read
     // during the previous one, have long landed -- without it hipcc waits after the first new reads
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    if constexpr (BAR) barrier();
+    if constexpr (BW >= 0) barrier();
     const int un = u + 1;
-    const bf16_t* nb = lds + ((un >> 1) & 1) * kStage;
-    const int ao = a_off(un & 1), wo = w_off(un & 1);
+    const bf16_t* ab = a_slot(un >> 1) + a_off(un & 1);
+    const bf16_t* wb = w_slot(un >> 1) + w_off(un & 1);
+    const int lt = C == 1 ? (u + 3) >> 1 : (u >> 1) + 2;
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int mf = 0; mf < 8; ++mf) {
@@ -415,22 +421,22 @@ __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const Pr
         if constexpr (Z) mfma_zero(acc[nf][mf], fw[C][nf], fa[C][mf]);
         else mfma_acc(acc[nf][mf], fw[C][nf], fa[C][mf]);
       };
-      // one memory instruction per MFMA pair, pinned: ds_read W | 2 MFMA | load | 2 MFMA | ds_read A |
-      // 2 MFMA | load | 2 MFMA -- no two issue-heavy instructions back to back (vs both reads and
-      // both loads ahead of 8 MFMAs: -1 %)
-      if constexpr (NEXT) fw[C ^ 1][mf] = ld8(nb + wo + mf * kWStride);
+      // one memory instruction per MFMA pair at most, pinned: ds_read W | 2 MFMA | load | 2 MFMA |
+      // ds_read A | 4 MFMA
+      if constexpr (NEXT) fw[C ^ 1][mf] = ld8(wb + mf * kWStride);
       mm(0);
       mm(1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (LOAD) stage_one(2 * mf, (u + 3) >> 1);
+      if constexpr (LOAD) {
+        if constexpr (C == 1) stage_w(mf, lt);
+        else stage_a(mf, lt);
+      }
       mm(2);
       mm(3);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (NEXT) fa[C ^ 1][mf] = ld8(nb + ao + mf * 16 * BK);
+      if constexpr (NEXT) fa[C ^ 1][mf] = ld8(ab + mf * 16 * BK);
       mm(4);
       mm(5);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (LOAD) stage_one(2 * mf + 1, (u + 3) >> 1);
       mm(6);
       mm(7);
       __builtin_amdgcn_sched_barrier(0);
@@ -438,17 +444,27 @@ __global__ void __launch_bounds__(kW4Threads, 1) prefill_gemm_w4_kernel(const Pr
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
+  using W8 = std::integral_constant<int, 8>;
+  using W0 = std::integral_constant<int, 0>;
+  using NB = std::integral_constant<int, -1>;
   using T = std::true_type;
   using F = std::false_type;
-  // U = K / 32 is a multiple of 4 (launcher: K % 128 == 0)
-  step(I0{}, T{}, F{}, T{}, F{}, 0);
-  for (int u = 1; u < U - 3; u += 2) {
-    step(I1{}, F{}, T{}, T{}, T{}, u);
-    step(I0{}, F{}, F{}, T{}, F{}, u + 1);
+  // U = K / 32 is a multiple of 4 (launcher: K % 128 == 0), NT = U / 2 tiles.  Sub-step 0 stages
+  // A(2); each loop pair u, u + 1 stages W((u + 3) / 2) and A((u + 1) / 2 + 2); the pair at U - 5
+  // has no A left to stage, and the barrier at U - 3 retires everything.
+  if (NT > 2) step(I0{}, T{}, NB{}, T{}, T{}, 0);
+  else step(I0{}, T{}, NB{}, T{}, F{}, 0);
+  for (int u = 1; u < U - 5; u += 2) {
+    step(I1{}, F{}, W8{}, T{}, T{}, u);
+    step(I0{}, F{}, NB{}, T{}, T{}, u + 1);
   }
-  step(I1{}, F{}, T{}, T{}, F{}, U - 3);
-  step(I0{}, F{}, F{}, T{}, F{}, U - 2);
-  step(I1{}, F{}, F{}, F{}, F{}, U - 1);
+  if (U >= 8) {
+    step(I1{}, F{}, W8{}, T{}, T{}, U - 5);
+    step(I0{}, F{}, NB{}, T{}, F{}, U - 4);
+  }
+  step(I1{}, F{}, W0{}, T{}, F{}, U - 3);
+  step(I0{}, F{}, NB{}, T{}, F{}, U - 2);
+  step(I1{}, F{}, NB{}, F{}, F{}, U - 1);
 
   // the last MFMAs' results before any AGPR read (8-pass XDL: 12+ wait states)
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");

@@ -20,20 +20,12 @@ from . import native
 
 BM = 256
 BN = 256
-# 6: the 4-wave, one-wave-per-SIMD kernel (AGPR accumulators, BK 64, buffer_load ... lds staging;
-# K % 128 == 0), 4: the 8-wave ping-pong kernel (the fallback for K % 128 != 0) --
-# csrc/kernels/gemm_prefill.hip.  Round 6: 4.5-13 % faster than its global_load_lds form; hipBLASLt
-# is still 7-16 % faster on the dense shapes, 8 % slower on the grouped w2
+# 6: the 4-wave, one-wave-per-SIMD kernel (AGPR accumulators, BK 64, buffer_load ... lds staging
+# into a 3-slot A / 2-slot W ring; K % 128 == 0), 4: the 8-wave ping-pong kernel (the fallback for
+# K % 128 != 0) -- csrc/kernels/gemm_prefill.hip.  Round 6: 7-16 % faster than the round-5 kernel;
+# hipBLASLt 6-9 % ahead on the dense shapes, 21 % behind on the grouped w2
 # (profiles/r6_prefill_gemm_buffer_lds.md, r4_prefill_gemm_4wave.md)
 VARIANT = 6
-
-
-def default_variant(N: int, K: int) -> int:
-    """Row-major variant for an N x K weight (+1: block-packed).  Deep-K, narrow-N shapes (the
-    down projections, Mixtral w2: K >= 2 N) run faster on the 8-wave kernel since both stage by
-    buffer_load ... lds (round 6: 8B down 687 vs 702 us, Mixtral grouped w2 1,673 vs 1,829 us;
-    the 4-wave kernel 5-12 % ahead elsewhere -- profiles/r6_prefill_gemm_buffer_lds.md)."""
-    return 4 if K >= 2 * N else VARIANT
 
 
 class PrefillGemmArgs(ctypes.Structure):
@@ -63,7 +55,7 @@ def _launch(a: PrefillGemmArgs, variant: Optional[int] = None) -> None:
         f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         f.restype = ctypes.c_int
         _checked = True
-    v = default_variant(a.N, a.K) if variant is None else variant
+    v = VARIANT if variant is None else variant
     if v >= 6 and a.K % 128:
         v = 4 + v % 2  # the 8-wave kernel needs only K % 64 == 0
     native.check(lib.pk_prefill_gemm(ctypes.byref(a), v, native.stream_ptr()), "pk_prefill_gemm")
@@ -104,7 +96,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
             or (packed is not None and (K % 128 or tuple(packed.shape) != (N, K)))):
         raise ValueError(f"prefill GEMM: unsupported shape/layout M={M} N={N} K={K}")
     if packed is not None and variant not in (5, 7):
-        variant = default_variant(N, K) + 1
+        variant = VARIANT + 1  # the same kernels reading the decode GEMM's block-packed W
     a = PrefillGemmArgs()
     a.C, a.A, a.W = out.data_ptr(), x.data_ptr(), src.data_ptr()
     a.M, a.N, a.K, a.lda, a.ldc = M, N, K, x.stride(0), out.stride(0)

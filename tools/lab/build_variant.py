@@ -48,6 +48,7 @@ VARIANTS = {
     "pb_sc0_a": [("gemm_prefill.hip", "avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 0);",
                   "avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 1);")],
     "pb_nt_w": [("gemm_prefill.hip", "wvo[j - 8], wo, 0, 0);", "wvo[j - 8], wo, 0, 2);")],
+    "pb_split": [("gemm_prefill.hip", "constexpr bool kSplitLoads = false;", "constexpr bool kSplitLoads = true;")],
     # round 5, measured and removed: "mt8_chunk256" (128-row decode tiles staging A per 256-deep chunk,
     # one workgroup per CU: 8B at 128 rows 6.36 vs 5.62-5.65 ms, 256 rows 10.07-10.09 vs 9.21-9.22,
     # profiles/r5_mt8.jsonl); "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
