@@ -49,6 +49,13 @@ VARIANTS = {
                   "avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 1);")],
     "pb_nt_w": [("gemm_prefill.hip", "wvo[j - 8], wo, 0, 0);", "wvo[j - 8], wo, 0, 2);")],
     "pb_split": [("gemm_prefill.hip", "constexpr bool kSplitLoads = false;", "constexpr bool kSplitLoads = true;")],
+    # the 4-wave prefill GEMM without the XOR chunk swizzle (lanes of a row in natural order: whole
+    # 64-byte lane groups for the address unit, LDS bank conflicts on the fragment reads instead)
+    "pb_noswz": [("gemm_prefill.hip", "const int logical = (tid & 7) ^ ((tid >> 4) & 7);", "const int logical = tid & 7;"),
+                 ("gemm_prefill.hip", "auto a_off = [&](int s) { return (wr * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8); };",
+                  "auto a_off = [&](int s) { return (wr * 128 + r) * BK + ((4 * s + g) * 8); };"),
+                 ("gemm_prefill.hip", "    return (wc * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8);",
+                  "    return (wc * 128 + r) * BK + ((4 * s + g) * 8);")],
     # round 5, measured and removed: "mt8_chunk256" (128-row decode tiles staging A per 256-deep chunk,
     # one workgroup per CU: 8B at 128 rows 6.36 vs 5.62-5.65 ms, 256 rows 10.07-10.09 vs 9.21-9.22,
     # profiles/r5_mt8.jsonl); "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
