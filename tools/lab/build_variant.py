@@ -37,25 +37,17 @@ VARIANTS = {
     # the 4-wave prefill GEMM's 16 LDS-DMA loads of a tile, measured at gate_up against 2 per group
     # (1,453 us): all right after the barrier ("pg_front") 1,535, 4 per group in the first 4 groups
     # ("pg_first4") 1,443 (noise) -- profiles/r4_prefill_gemm_4wave.md
-    # round 6 ablations of the 4-wave prefill GEMM's buffer_load ... lds staging (timing only, wrong
-    # results; profiles/r6_prefill_gemm_buffer_lds.md): no vmcnt wait before the tile barrier
-    # (gate_up 1,350 vs 1,393 us), no loads in the k-loop (1,151: 7 % under hipBLASLt)
-    "pb_novm": [("gemm_prefill.hip", "if constexpr (BAR) wait_vm<0>();", "")],
-    "pb_noload": [("gemm_prefill.hip", "if constexpr (LOAD) stage_one(2 * mf, (u + 3) >> 1);", ""),
-                  ("gemm_prefill.hip", "if constexpr (LOAD) stage_one(2 * mf + 1, (u + 3) >> 1);", "")],
-    # cache policy of the prefill GEMM's staging loads: sc0 (aux 1) on the W / A stream, nt (aux 2) on W
-    "pb_sc0_w": [("gemm_prefill.hip", "wvo[j - 8], wo, 0, 0);", "wvo[j - 8], wo, 0, 1);")],
-    "pb_sc0_a": [("gemm_prefill.hip", "avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 0);",
-                  "avo[j], static_cast<unsigned>(T) * BK * 2u, 0, 1);")],
-    "pb_nt_w": [("gemm_prefill.hip", "wvo[j - 8], wo, 0, 0);", "wvo[j - 8], wo, 0, 2);")],
-    "pb_split": [("gemm_prefill.hip", "constexpr bool kSplitLoads = false;", "constexpr bool kSplitLoads = true;")],
-    # the 4-wave prefill GEMM without the XOR chunk swizzle (lanes of a row in natural order: whole
-    # 64-byte lane groups for the address unit, LDS bank conflicts on the fragment reads instead)
-    "pb_noswz": [("gemm_prefill.hip", "const int logical = (tid & 7) ^ ((tid >> 4) & 7);", "const int logical = tid & 7;"),
-                 ("gemm_prefill.hip", "auto a_off = [&](int s) { return (wr * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8); };",
-                  "auto a_off = [&](int s) { return (wr * 128 + r) * BK + ((4 * s + g) * 8); };"),
-                 ("gemm_prefill.hip", "    return (wc * 128 + r) * BK + (((4 * s + g) ^ ((r >> 1) & 7)) * 8);",
-                  "    return (wc * 128 + r) * BK + ((4 * s + g) * 8);")],
+    # round 6 ablations of the 4-wave prefill GEMM (timing only, wrong results;
+    # profiles/r6_prefill_gemm_buffer_lds.md): no vmcnt wait before the tile barrier, no staging
+    # loads in the k-loop (double-buffer form: gate_up 1,350 / 1,151 vs 1,393 us -- the loads' issue
+    # cost, not their latency)
+    "pb_novm": [("gemm_prefill.hip", "if constexpr (BW >= 0) wait_vm<BW>();", "")],
+    "pb_noload": [("gemm_prefill.hip", "if constexpr (C == 1) stage_w(mf, lt);\n        else stage_a(mf, lt);",
+                   "(void)lt;")],
+    # round 6, measured and removed (profiles/r6_prefill_gemm_buffer_lds.md): sc0 / nt cache policy on
+    # the staging loads ("pb_sc0_w", "pb_sc0_a": no change; "pb_nt_w": down -6 %, gate_up +4 %, O
+    # +7 %), W loads moved to the even sub-step of the double buffer ("pb_split": -6 to -13 %), no XOR
+    # chunk swizzle ("pb_noswz": 1,328 vs 1,330 us at gate_up)
     # round 5, measured and removed: "mt8_chunk256" (128-row decode tiles staging A per 256-deep chunk,
     # one workgroup per CU: 8B at 128 rows 6.36 vs 5.62-5.65 ms, 256 rows 10.07-10.09 vs 9.21-9.22,
     # profiles/r5_mt8.jsonl); "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
