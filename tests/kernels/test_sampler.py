@@ -65,3 +65,22 @@ def test_distribution_chi2():
     expct = probs * counts.sum()
     chi2 = ((counts - expct) ** 2 / expct).sum()
     assert chi2 < 30, (chi2, counts, expct)  # 7 dof, p≈1e-4
+
+
+@pytest.mark.parametrize("V", [40, 64, 4096 + 8, 128256])
+def test_greedy_ties_across_slices(V):
+    """Greedy ties: a maximum repeated far apart in the row (different threads' vectors, different
+    waves) resolves to its lowest index, at vocabularies below one vector per thread too; the
+    full sampler and the greedy entry agree on every row, an all -inf row included."""
+    x = torch.randn(16, V, device="cuda").to(torch.bfloat16)
+    x[0, V - 1] = 50.0
+    x[0, V // 2] = 50.0
+    x[0, 3] = 50.0  # three slices hold the max: index 3 wins
+    x[1, V - 1] = 60.0
+    x[1, V - 9] = 60.0
+    x[2, :] = -float("inf")
+    exp = torch.argmax(x.float(), -1)
+    exp[0], exp[1] = 3, V - 9
+    got = sampler.greedy(x).long().cpu()
+    assert torch.equal(got[:2], exp[:2].cpu()) and torch.equal(got[3:], exp[3:].cpu())
+    assert torch.equal(sampler.sample(x, *params(16)).long().cpu(), got)
