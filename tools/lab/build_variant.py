@@ -48,6 +48,9 @@ VARIANTS = {
     # the staging loads ("pb_sc0_w", "pb_sc0_a": no change; "pb_nt_w": down -6 %, gate_up +4 %, O
     # +7 %), W loads moved to the even sub-step of the double buffer ("pb_split": -6 to -13 %), no XOR
     # chunk swizzle ("pb_noswz": 1,328 vs 1,330 us at gate_up)
+    # round 6, measured and removed: a four-deep weight ring in the fused MLP's gate_up tiles only
+    # (one workgroup per CU there, so the extra registers cost no occupancy): 8B decode step
+    # 3.982-3.999 vs 3.984-3.986 ms -- the stream is not short of bytes in flight (r6_wdeep.jsonl)
     # round 5, measured and removed: "mt8_chunk256" (128-row decode tiles staging A per 256-deep chunk,
     # one workgroup per CU: 8B at 128 rows 6.36 vs 5.62-5.65 ms, 256 rows 10.07-10.09 vs 9.21-9.22,
     # profiles/r5_mt8.jsonl); "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
