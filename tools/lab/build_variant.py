@@ -51,6 +51,10 @@ VARIANTS = {
     # round 6, measured and removed: a four-deep weight ring in the fused MLP's gate_up tiles only
     # (one workgroup per CU there, so the extra registers cost no occupancy): 8B decode step
     # 3.982-3.999 vs 3.984-3.986 ms -- the stream is not short of bytes in flight (r6_wdeep.jsonl)
+    # round 6, measured and removed: the fused MLP's down tiles reading the in-launch h hand-off with
+    # plain loads ("h_plain", timing only, not coherent: 3.974 vs 3.973-3.984 ms per 8B step) or plain
+    # loads after one agent-scope acquire per wave ("h_acq", coherent: 4.18 ms) instead of sc1 loads
+    # -- the sc1 re-reads of h cost nothing measurable (profiles/r6_hload.jsonl)
     # round 5, measured and removed: "mt8_chunk256" (128-row decode tiles staging A per 256-deep chunk,
     # one workgroup per CU: 8B at 128 rows 6.36 vs 5.62-5.65 ms, 256 rows 10.07-10.09 vs 9.21-9.22,
     # profiles/r5_mt8.jsonl); "wdepth4" (decode GEMM tiles with four 128-deep weight k-steps
