@@ -90,6 +90,8 @@ def parse_args(argv=None):
                     help="N > 1 with --tp 1: after the TP child, measure this MoE model with DP attention + EP = N "
                          "(expert all-to-all over all N GPUs) under ep{N}_<model> (BASELINE config 5); auto: "
                          "mixtral-8x7b when --model is llama3-8b and N divides its experts, else none")
+    ap.add_argument("--extra-steps", type=int, default=5,
+                    help="timed waves of the tp{N} / ep{N} children (at most --steps)")
     ap.add_argument("--ep-extra-timeout", type=float, default=300.0,
                     help="seconds the EP child may take at most (never at the main number's expense)")
     ap.add_argument("--child-timeout", type=float, default=1500.0, help="seconds the main measurement child may take")
@@ -212,8 +214,12 @@ def orchestrate(args, argv) -> int:
             main_line[key] = {"error": f"child skipped: {max(budget, 0.0):.0f} s left of the "
                                        f"{args.deadline:.0f} s deadline"}
             return
-        trc, tl, wall = run_child(_strip(argv, strip) + cargs + ["--tp-extra-model", "none", "--ep-extra-model",
-                                                                 "none", "--child"], args.gpus, budget)
+        # the extra configs time at most --extra-steps whole waves (after at most 2 warm-up waves):
+        # enough for a stable number, and the 70B / Mixtral children then fit the one deadline
+        steps = ["--steps", str(min(args.steps, args.extra_steps)), "--warmup", str(min(args.warmup, 2))]
+        trc, tl, wall = run_child(_strip(argv, strip) + cargs + steps + ["--tp-extra-model", "none",
+                                                                         "--ep-extra-model", "none", "--child"],
+                                  args.gpus, budget)
         if tl is not None:
             main_line[key] = {k: tl.get(k) for k in ("value", "unit", "p50_e2e_latency_ms", "ms_per_step", "steps",
                                                      "warmup", "scaling")}
