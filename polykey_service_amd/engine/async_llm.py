@@ -13,6 +13,7 @@ from __future__ import annotations
 import asyncio
 import collections
 import contextlib
+import gc
 import os
 import sys
 import threading
@@ -87,7 +88,18 @@ class AsyncLLM:
         # switch interval lets a burst of RPC handling hold the engine thread off for whole
         # decode steps (the GPU idles meanwhile); a short interval hands the GIL over promptly.
         sys.setswitchinterval(0.002)
+        # Collector pauses: the engine, its weights' Python wrappers and the captured graphs are
+        # long-lived -- gc.freeze() moves them out of every later collection, and a larger
+        # generation-0 threshold keeps the per-step garbage (outputs, RPC messages) from
+        # triggering collections mid-wave.  A full collection of the serving heap stalled a bench
+        # wave by ~50 ms (profiles/r6_gc.md).  POLYKEY_GC_FREEZE=0 keeps CPython's defaults.
+        if os.environ.get("POLYKEY_GC_FREEZE", "1") != "0":
+            gc.collect()
+            gc.freeze()
+            gc.set_threshold(50000, 20, 100)
         self._fatal_sent = False
+        if os.environ.get("POLYKEY_DRAIN_BEFORE_SCHEDULE", "1") != "0":
+            engine.before_schedule = self._drain_cmds
         self._thread = threading.Thread(target=self._run, name="polykey-engine", daemon=True)
         self._thread.start()
         self._watchdog = threading.Thread(target=self._watch, name="polykey-watchdog", daemon=True)

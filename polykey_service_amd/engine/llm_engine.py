@@ -10,7 +10,7 @@ import dataclasses
 import os
 import time
 import uuid
-from typing import Dict, Iterable, List, Optional
+from typing import Callable, Dict, Iterable, List, Optional
 
 import torch
 
@@ -141,6 +141,9 @@ class LLMEngine:
         self.total_output_tokens = 0
         self.overlap = cfg.overlap
         self._inflight = None
+        # called between completing a step and scheduling the next (AsyncLLM: admit the requests
+        # that arrived meanwhile)
+        self.before_schedule: Optional[Callable[[], None]] = None
         self.continuation_steps = 0
 
     def _serving_preflight(self, mcfg: ModelConfig) -> None:
@@ -213,6 +216,11 @@ class LLMEngine:
                 self._inflight = (batch, batch.decodes, nxt)
                 self.continuation_steps += 1
                 return self._outputs(done)
+        if self.before_schedule is not None and done is not None:
+            # requests that landed while the completed step ran join the next one (a burst whose
+            # tail arrived during the first prefill step is prefilled in the second instead of a
+            # straggler third step that delays the whole cohort by a prefill, profiles/r6_gc.md)
+            self.before_schedule()
         batch = self.scheduler.schedule()
         if not batch.empty:
             sampling = batch.sampling_seqs()
