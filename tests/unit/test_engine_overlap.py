@@ -34,3 +34,31 @@ def test_overlap_outputs_lag_one_step_and_abort_in_flight():
     assert all(o.request_id == "r1" for o in seen)
     assert len(s1.output_ids) == 5 and seen[-1].finished
     assert e.bm.num_free == e.bm.num_blocks
+
+
+def test_before_schedule_admits_arrivals_into_the_next_step():
+    """A request that arrives while a step is in flight (AsyncLLM's queue, drained by the
+    before_schedule hook) joins the step scheduled right after that one completes."""
+    e = _engine(True)
+    e.add_request([1, 2, 3], SamplingParams(max_tokens=3, ignore_eos=True), "r1")
+    sizes = []
+    orig = e.scheduler.schedule
+
+    def schedule():
+        b = orig()
+        sizes.append(sorted(s.request_id for s, _ in b.prefills))
+        return b
+    e.scheduler.schedule = schedule
+    assert e.step() == []            # r1's prefill in flight
+    arrivals = [("r2", [1, 4, 5])]
+
+    def drain():
+        while arrivals:
+            rid, p = arrivals.pop()
+            e.add_request(p, SamplingParams(max_tokens=3, ignore_eos=True), rid)
+    e.before_schedule = drain
+    e.step()
+    assert sizes[:2] == [["r1"], ["r2"]], sizes
+    while e.has_unfinished():
+        e.step()
+    assert e.bm.num_free == e.bm.num_blocks
