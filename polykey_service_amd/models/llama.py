@@ -39,6 +39,7 @@ from torch import nn
 from .. import ops
 from ..ops import attention as attn_ops
 from ..ops import gemm
+from ..ops import gemm_prefill
 from ..ops import moe as moe_ops
 from ..ops import reference
 from ..parallel import comm
@@ -98,6 +99,22 @@ LM_HEAD_SKINNY_MAX_M = 128
 # above this many decode rows gate_up runs on hipBLASLt (+ the norm / SiLU kernels): 256 clients
 # 19,030-19,728 -> 20,177-20,218 tok/s with 192 instead of 384 (profiles/r4_gate_up_rows_ab.jsonl)
 GATE_UP_SKINNY_MAX_M = 192
+# wide decode on the hand-written MFMA GEMM of prefill (gemm_prefill.hip, 256 x 256 tiles) reading
+# the block-packed weights decode already holds, once its tiles can fill the chip
+# (tools/wide_gemm_probe.py, profiles/r6_wide_gemm_probe.jsonl, cold weights): Llama-3-8B gate_up
+# + SiLU 100 vs hipBLASLt 107 us at 384 rows, 105 vs 123 at 512, but 95 vs 92 at 256 (112 tiles);
+# the LM head 248 vs 306 us at 256 rows, 433 vs 509 at 512
+WIDE_MFMA_MIN_TILES = 224
+
+
+def _wide_mfma_ok(x: torch.Tensor, packed: Optional[torch.Tensor]) -> bool:
+    """Decode rows ``x`` times the block-packed ``packed`` on the prefill MFMA GEMM: a shape it
+    tiles, with at least WIDE_MFMA_MIN_TILES 256 x 256 tiles."""
+    if packed is None or x.stride(1) != 1:
+        return False
+    N, K = packed.shape
+    tiles = (N // gemm_prefill.BN) * -(-x.shape[0] // gemm_prefill.BM)
+    return gemm_prefill.supported(N, K) and K % 128 == 0 and tiles >= WIDE_MFMA_MIN_TILES
 
 
 def pack_folded(owner, name: str, norm_w: torch.Tensor, packed_only: bool) -> torch.Tensor:
@@ -520,6 +537,10 @@ class LlamaForCausalLM(nn.Module):
         """Folded-norm gate_up + SiLU of the two-launch decode MLP -> h [T, I] bf16."""
         mlp = layer.mlp
         rs = gemm.RowScale(parts, layer.eps)
+        if _wide_mfma_ok(residual, mlp.gate_up_pf):
+            # rows * folded block-packed weight (ln2 inside): normalise with unit weights
+            x = gemm.norm_apply(residual, parts, self._ones_h, layer.eps)
+            return gemm_prefill.linear(x, mlp.gate_up, silu=True, packed=mlp.gate_up_pf)
         if residual.shape[0] > GATE_UP_SKINNY_MAX_M and not mlp.gate_up.is_meta:
             # hipBLASLt's MFMA GEMM wins on the 235 MB gate_up above 192 rows (67 vs 85 us at 256,
             # 97 vs 155 at 512: profiles/r4_wide_decode_probe.jsonl) even with the norm and SiLU as
@@ -801,6 +822,7 @@ class LlamaForCausalLM(nn.Module):
         if self.lm_head.shape[0] % 128 == 0 and self.lm_head.shape[1] % 256 == 0:
             self.lm_head_p = gemm.pack_weight(self.lm_head)
         self.packed_only = packed_only
+        self._ones_h = torch.ones(self.cfg.hidden_size, dtype=self.lm_head.dtype, device=self.device)
         return True
 
     def _packed_prefill_ok(self) -> bool:
@@ -825,7 +847,9 @@ class LlamaForCausalLM(nn.Module):
         # above 128 rows hipBLASLt's MFMA GEMM is the faster one (tools/bench_gemm_rows.py, 8B:
         # 284 vs 358 us at 256 rows, 492 vs 668 at 512; profiles/r3_decode_rows.txt)
         wp = getattr(self, "lm_head_p", None)
-        if wp is not None and gemm.skinny_ok(hidden, self.lm_head, max_m=gemm.DECODE_MAX_M) and (
+        if hidden.shape[0] > LM_HEAD_SKINNY_MAX_M and _wide_mfma_ok(hidden, wp):
+            logits = gemm_prefill.linear(hidden, self.lm_head, packed=wp)
+        elif wp is not None and gemm.skinny_ok(hidden, self.lm_head, max_m=gemm.DECODE_MAX_M) and (
                 hidden.shape[0] <= LM_HEAD_SKINNY_MAX_M or self.lm_head.is_meta):
             logits = gemm.linear(hidden, self.lm_head, packed=wp, max_m=gemm.DECODE_MAX_M)
         else:

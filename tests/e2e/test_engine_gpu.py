@@ -208,11 +208,40 @@ def _decode_logits(gpu, prompts, graphs=False):
 @pytest.mark.parametrize("batch", [150, 200, 450])
 def test_large_decode_batches_match_small(batch):
     """Decode batches above 64 rows (128-row tiles of the skinny GEMM; above 192 rows gate_up on
-    hipBLASLt with the norm and SiLU as kernels of their own) give the same logits as the same
+    hipBLASLt with the norm and SiLU as kernels of their own -- tiny-llama's projections are too
+    narrow for the wide MFMA path) give the same logits as the same
     sequences decoded in a batch of 8 (the M <= 64 fused chain)."""
     _, gpu = _models("tiny-llama-gqa4")
     prompts = [[1] + [(7 * i + 3 * j) % 1000 + 3 for j in range(5)] for i in range(batch)]
     big, fbig = _decode_logits(gpu, prompts)
+    small, fsmall = _decode_logits(gpu, prompts[:8])
+    scale = small.abs().max().item()
+    same = [i for i in range(8) if fbig[i] == fsmall[i]]
+    assert len(same) >= 6, (fbig[:8], fsmall)
+    torch.testing.assert_close(big[same], small[same], atol=0.02 * scale, rtol=0.05)
+
+
+@pytest.mark.parametrize("batch", [200, 300])
+def test_wide_decode_on_mfma_gemm_matches_small(batch, monkeypatch):
+    """Wide decode rows on the hand-written prefill MFMA GEMM (gate_up + SiLU on the folded
+    block-packed weight, the LM head on its packed copy; at 8B shapes above 256 / 128 rows): the
+    tile threshold is lowered so tiny-llama's projections take it, and the logits match the
+    same sequences decoded in a batch of 8."""
+    from polykey_service_amd.models import llama
+    from polykey_service_amd.ops import gemm_prefill
+    monkeypatch.setattr(llama, "WIDE_MFMA_MIN_TILES", 1)
+    calls = []
+    orig = gemm_prefill.linear
+
+    def spy(x, w, *a, **k):
+        calls.append((x.shape[0], w.shape[0], bool(k.get("silu"))))
+        return orig(x, w, *a, **k)
+    monkeypatch.setattr(gemm_prefill, "linear", spy)
+    _, gpu = _models("tiny-llama-gqa4")
+    prompts = [[1] + [(7 * i + 3 * j) % 1000 + 3 for j in range(5)] for i in range(batch)]
+    big, fbig = _decode_logits(gpu, prompts)
+    assert any(m == batch and silu for m, _, silu in calls), calls
+    assert any(m == batch and n == gpu.lm_head.shape[0] for m, n, _ in calls), calls
     small, fsmall = _decode_logits(gpu, prompts[:8])
     scale = small.abs().max().item()
     same = [i for i in range(8) if fbig[i] == fsmall[i]]

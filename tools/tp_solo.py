@@ -85,7 +85,12 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no graph (for per-kernel traces with launch gaps)")
     ap.add_argument("--car", choices=["solo", "loopback"], default="solo",
                     help="collectives: their local half (SoloAR) or the real kernels on local stand-in peers")
+    ap.add_argument("--wide-min-tiles", type=int, default=None,
+                    help="override models.llama.WIDE_MFMA_MIN_TILES (wide decode on the prefill MFMA GEMM)")
     a = ap.parse_args()
+    if a.wide_min_tiles is not None:
+        from polykey_service_amd.models import llama
+        llama.WIDE_MFMA_MIN_TILES = a.wide_min_tiles
     cfg = get_config(a.model)
     if a.layers:
         import dataclasses
@@ -165,7 +170,7 @@ def main():
         assert st.custom_ar.error() == 0, "a loopback wait timed out"
     print(json.dumps({"model": a.model, "tp": a.tp, "layers": cfg.num_layers, "batch": B, "ctx": a.ctx,
                       "ms_per_step": round(ms, 3), "us_per_layer": round(ms * 1000 / cfg.num_layers, 2),
-                      "graph": not a.eager, "init_s": round(init_s, 1), "car": a.car, "carried": carried,
+                      "graph": not a.eager, "wide_min_tiles": a.wide_min_tiles, "init_s": round(init_s, 1), "car": a.car, "carried": carried,
                       "mlp_fused": os.environ.get("POLYKEY_MLP_FUSED", "1"),
                       "qkv_attn_fused": os.environ.get("POLYKEY_QKV_ATTN_FUSED", "1"),
                       "env": {k: v for k, v in os.environ.items() if k.startswith("POLYKEY_")}}), flush=True)
