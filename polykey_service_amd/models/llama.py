@@ -100,20 +100,22 @@ LM_HEAD_SKINNY_MAX_M = 128
 # 19,030-19,728 -> 20,177-20,218 tok/s with 192 instead of 384 (profiles/r4_gate_up_rows_ab.jsonl)
 GATE_UP_SKINNY_MAX_M = 192
 # wide decode on the hand-written MFMA GEMM of prefill (gemm_prefill.hip, 256 x 256 tiles) reading
-# the block-packed weights decode already holds, once its tiles can fill the chip
-# (tools/wide_gemm_probe.py, profiles/r6_wide_gemm_probe.jsonl, cold weights): Llama-3-8B gate_up
-# + SiLU 100 vs hipBLASLt 107 us at 384 rows, 105 vs 123 at 512, but 95 vs 92 at 256 (112 tiles);
-# the LM head 248 vs 306 us at 256 rows, 433 vs 509 at 512
-WIDE_MFMA_MIN_TILES = 224
+# the block-packed weights decode already holds, once its tiles -- counted by the rows they hold,
+# a half-full row tile as half -- can fill the chip.  Llama-3-8B, tools/wide_gemm_probe.py (cold
+# weights, profiles/r6_wide_gemm_probe.jsonl): gate_up + SiLU 105 vs hipBLASLt 123 us at 512 rows,
+# the LM head 248 vs 306 us at 256 rows; whole decode step (tools/tp_solo.py --wide-min-tiles,
+# r6_wide256/384.jsonl): gate_up on it at 448 / 512 rows 13.02 vs 13.42 / 13.82 vs 14.31 ms, but
+# slower at 384 (12.34 vs 12.24: 168 row-weighted tiles), 256 (9.22 vs 9.00) and 200 rows
+WIDE_MFMA_MIN_TILES = 180
 
 
 def _wide_mfma_ok(x: torch.Tensor, packed: Optional[torch.Tensor]) -> bool:
     """Decode rows ``x`` times the block-packed ``packed`` on the prefill MFMA GEMM: a shape it
-    tiles, with at least WIDE_MFMA_MIN_TILES 256 x 256 tiles."""
+    tiles, with at least WIDE_MFMA_MIN_TILES row-weighted 256 x 256 tiles."""
     if packed is None or x.stride(1) != 1:
         return False
     N, K = packed.shape
-    tiles = (N // gemm_prefill.BN) * -(-x.shape[0] // gemm_prefill.BM)
+    tiles = (N // gemm_prefill.BN) * x.shape[0] / gemm_prefill.BM
     return gemm_prefill.supported(N, K) and K % 128 == 0 and tiles >= WIDE_MFMA_MIN_TILES
 
 
