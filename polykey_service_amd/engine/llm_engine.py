@@ -221,6 +221,9 @@ class LLMEngine:
             # tail arrived during the first prefill step is prefilled in the second instead of a
             # straggler third step that delays the whole cohort by a prefill, profiles/r6_gc.md)
             self.before_schedule()
+            # a request aborted by it loses the completed step's output too (as an abort while
+            # a step is in flight does)
+            done = [d for d in done if d[2] is not None or d[0].finish_reason is not FinishReason.ABORT]
         batch = self.scheduler.schedule()
         if not batch.empty:
             sampling = batch.sampling_seqs()

@@ -62,3 +62,23 @@ def test_before_schedule_admits_arrivals_into_the_next_step():
     while e.has_unfinished():
         e.step()
     assert e.bm.num_free == e.bm.num_blocks
+
+
+def test_abort_in_before_schedule_drops_the_completed_output():
+    e = _engine(True)
+    e.add_request([1, 2, 3], SamplingParams(max_tokens=4, ignore_eos=True), "r1")
+    e.add_request([1, 4, 5], SamplingParams(max_tokens=4, ignore_eos=True), "r2")
+    assert e.step() == []
+    fired = []
+
+    def drain():
+        if not fired:
+            fired.append(e.abort("r2"))
+    e.before_schedule = drain
+    outs = e.step()
+    assert [o.request_id for o in outs] == ["r1"], outs
+    seen = []
+    while e.has_unfinished():
+        seen += e.step()
+    assert all(o.request_id == "r1" for o in seen) and seen[-1].finished
+    assert e.bm.num_free == e.bm.num_blocks
