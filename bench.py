@@ -367,11 +367,16 @@ async def run_waves(args, engine, st, leaders_group, llm=None, n_replicas=1):
             te = time.perf_counter()
             sub = max(m[0] for m in marks) - tw
             rpc = sorted((m[1] - m[0]) - m[2]["server_e2e_s"] for m in marks)
+            # the two legs (in-process clients share the server's monotonic clock)
+            rin = sorted(m[2]["server_t0"] - m[0] for m in marks if "server_t0" in m[2]) or [0.0]
+            rout = sorted(m[1] - m[2]["server_t0"] - m[2]["server_e2e_s"] for m in marks if "server_t0" in m[2]) or [0.0]
             ttft = sorted(m[2].get("ttft_s", 0.0) for m in marks)
             e2e = sorted(m[2].get("e2e_s", 0.0) for m in marks)
             print(f"[wave] wall {1e3 * (te - tw):.1f} ms | last submit +{1e3 * sub:.1f} ms | engine e2e "
                   f"min/max {1e3 * e2e[0]:.1f}/{1e3 * e2e[-1]:.1f} ms | ttft min/max {1e3 * ttft[0]:.1f}/"
-                  f"{1e3 * ttft[-1]:.1f} ms | rpc overhead p50/max {1e3 * rpc[len(rpc) // 2]:.2f}/{1e3 * rpc[-1]:.2f} ms | "
+                  f"{1e3 * ttft[-1]:.1f} ms | rpc overhead p50/max {1e3 * rpc[len(rpc) // 2]:.2f}/{1e3 * rpc[-1]:.2f} ms "
+                  f"(request leg {1e3 * rin[len(rin) // 2]:.2f}/{1e3 * rin[-1]:.2f}, response leg "
+                  f"{1e3 * rout[len(rout) // 2]:.2f}/{1e3 * rout[-1]:.2f}) | "
                   f"last response +{1e3 * (max(m[1] for m in marks) - tw):.1f} ms", file=sys.stderr, flush=True)
         return sum(r[0] for r in res), [r[1] for r in res]
 

@@ -73,7 +73,10 @@ class LLMTool:
             "finish_reason": last.finish_reason if last is not None else "abort",
             "usage": {"prompt_tokens": n_prompt, "completion_tokens": len(toks),
                       "total_tokens": n_prompt + len(toks)},
-            "metrics": {k: v for k, v in {**m, "server_e2e_s": time.monotonic() - t0}.items() if v is not None},
+            # server_t0: the handler's start on the monotonic clock (an in-process client can split
+            # its round trip into the request and response legs)
+            "metrics": {k: v for k, v in {**m, "server_e2e_s": time.monotonic() - t0, "server_t0": t0}.items()
+                        if v is not None},
         }
         if with_ids:  # parameters.return_token_ids: the generated ids themselves (token-level clients, tests)
             out["token_ids"] = list(toks)
