@@ -87,7 +87,7 @@ class AsyncLLM:
         # The engine thread and the asyncio (gRPC) thread share the GIL.  CPython's default 5 ms
         # switch interval lets a burst of RPC handling hold the engine thread off for whole
         # decode steps (the GPU idles meanwhile); a short interval hands the GIL over promptly.
-        sys.setswitchinterval(0.002)
+        sys.setswitchinterval(float(os.environ.get("POLYKEY_SWITCH_INTERVAL_MS", "2")) / 1e3)
         # Collector pauses: the engine, its weights' Python wrappers and the captured graphs are
         # long-lived -- gc.freeze() moves them out of every later collection, and a larger
         # generation-0 threshold keeps the per-step garbage (outputs, RPC messages) from
